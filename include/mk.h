@@ -1,0 +1,129 @@
+/* libmk -- MI355X-native meta-kriging hot path (C ABI, no torch / R types).
+ *
+ * Drop-in boundary for the data-parallel core of MetaKriging_BinaryResponse.R:
+ * the per-subset spMvGLM fits + spPredict kriging + 200-level quantile
+ * summaries (the `foreach(i=1:n.core) %dopar% partitioned_spMvGLM(...)` at
+ * MK.R:108, whose body is MK.R:46-96) and the quantile-average combine
+ * (MK.R:119-133).  Conventions are R's: column-major fp64 matrices, int32
+ * counts, location-major multivariate vectors (site i, outcome a at i*q + a),
+ * caller-allocated outputs.  Every call returns 0 on success or a negative
+ * MK_E* code; mk_last_error() gives the thread-local message.
+ * See INTEGRATION.md for the R .Call glue that binds these entry points.
+ */
+#ifndef MK_H
+#define MK_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MK_OK 0
+#define MK_E_ARG (-1)      /* invalid argument (R: stop()) */
+#define MK_E_HIP (-2)      /* HIP runtime failure */
+#define MK_E_NOMEM (-3)    /* device allocation failed */
+#define MK_E_NODEV (-4)    /* no HIP device */
+
+#define MK_COV_EXPONENTIAL 0
+#define MK_COV_MATERN 1
+#define MK_N_LEVELS 200    /* quantile(x, probs = seq(0.005, 1, 0.005)), MK.R:88 */
+
+/* Subset data.  Replaces the globals Y*.part / X*.part / coords.part the
+ * worker reads (MK.R:67-75) plus coords.test (MK.R:87, 108). */
+typedef struct mk_problem {
+  int32_t n_subsets;          /* subsets in this call (this GPU's shard)              */
+  int32_t subset_base;        /* global index of subset 0 (selects its RNG stream)    */
+  int32_t q;                  /* outcomes (MK.R:80: length of the formula list)       */
+  int32_t p;                  /* regression coefficients, sum over outcomes           */
+  const int32_t* n_part;      /* [n_subsets] sites per subset (MK.R:18)               */
+  const double* coords;       /* concatenated per subset: n_s x 2 column-major        */
+  const double* y;            /* concatenated per subset: n_s*q responses (counts)    */
+  const double* weights;      /* concatenated per subset: n_s*q binomial trials       */
+  const double* x;            /* concatenated per subset: (n_s*q) x p column-major    */
+  int32_t n_test;             /* held-out sites (coords.test rows)                    */
+  const double* coords_test;  /* n_test x 2 column-major                              */
+} mk_problem;
+
+/* spMvGLM arguments (MK.R:56-64, 80-85).  Tuning values are proposal
+ * VARIANCES (spBayes amcmc semantics); beta_tuning is length p (the diagonal
+ * of the t(chol(vcov)) matrix MK.R:55 builds). */
+typedef struct mk_config {
+  int32_t cov_model;          /* MK_COV_EXPONENTIAL (MK.R:84) or MK_COV_MATERN        */
+  int32_t n_batch;            /* MK.R:57 */
+  int32_t batch_length;       /* MK.R:58 */
+  double accept_rate;         /* MK.R:83 */
+  int32_t burn_in;            /* first kept sample, 1-based (MK.R:85-89: start = burn.in) */
+  const double* beta_starting;  /* [p]  MK.R:54 */
+  const double* beta_tuning;    /* [p]  MK.R:55 (diagonal) */
+  const double* phi_starting;   /* [q]  MK.R:60 */
+  const double* phi_tuning;     /* [q]  MK.R:61 */
+  const double* A_starting;     /* [q(q+1)/2] lower triangle of A, col-major (MK.R:56) */
+  const double* A_tuning;       /* [q(q+1)/2] MK.R:61 */
+  const double* nu_starting;    /* [q] Matern only, else NULL */
+  const double* nu_tuning;      /* [q] Matern only, else NULL */
+  double w_starting;            /* MK.R:60 */
+  double w_tuning;              /* MK.R:62 */
+  const double* phi_unif_a;     /* [q] MK.R:63 */
+  const double* phi_unif_b;     /* [q] */
+  const double* nu_unif_a;      /* [q] Matern only */
+  const double* nu_unif_b;      /* [q] Matern only */
+  double K_IW_df;               /* MK.R:64 */
+  const double* K_IW_S;         /* [q*q] col-major, MK.R:64 */
+  uint64_t seed;                /* Philox stream seed (the R glue draws it from R's RNG) */
+  int32_t record_samples;       /* keep p.beta.theta.samples (n_samples x P)            */
+  int32_t record_w;             /* keep p.w.samples ((n_s*q) x n_samples)               */
+  int32_t device;               /* HIP device ordinal                                    */
+} mk_config;
+
+/* Caller-allocated outputs; any pointer may be NULL to skip it.
+ * P = p + q(q+1)/2 + q (+ q for Matern); kept = n_batch*batch_length - burn_in + 1. */
+typedef struct mk_outputs {
+  double* parameters;   /* [n_subsets] x (200 x P) column-major: obj[[i]]$parameters (MK.R:89)  */
+  double* w_predict;    /* [n_subsets] x (200 x q*n_test) column-major: obj[[i]]$w.predict      */
+  double* samples;      /* [n_subsets] x (n_samples x P) column-major: m.1$p.beta.theta.samples  */
+  double* w_samples;    /* [n_subsets] x ((n_s*q) x n_samples) column-major: m.1$p.w.samples    */
+  double* w_pred_samples; /* [n_subsets] x ((q*n_test) x kept): m.s.pred$p.w.predictive.samples */
+  double* acceptance;   /* [n_subsets] x (n_batch x (p + n_theta + 1)): per-batch accept rates,
+                           last column = mean over the latent w                                  */
+} mk_outputs;
+
+typedef struct mk_session mk_session;
+
+/* ---- batched meta-kriging path (replaces foreach %dopar% at MK.R:108) ---- */
+/* Upload the shard to HBM and initialise every chain (no MCMC yet). */
+int mk_session_create(const mk_problem* prob, const mk_config* cfg, mk_session** out);
+/* Advance every chain by n_iter iterations (returns after the device is idle). */
+int mk_session_run(mk_session* s, int32_t n_iter);
+/* Iterations done so far. */
+int32_t mk_session_iteration(const mk_session* s);
+/* Quantile summaries + optional sample copies (requires all iterations done
+ * for parameters / w_predict). */
+int mk_session_outputs(mk_session* s, mk_outputs* out);
+/* Per-kernel timing (HIP events on the session stream) for the MFMA-bound
+ * Cholesky panel update: launches, total ms, algorithmic flops.  Enabled by
+ * mk_session_profile(s, 1) before mk_session_run. */
+int mk_session_profile(mk_session* s, int32_t enable);
+int mk_session_kernel_stats(const mk_session* s, int32_t which, int64_t* launches, double* total_ms, double* flops);
+void mk_session_destroy(mk_session* s);
+
+/* One-shot convenience: create, run n_batch*batch_length iterations, outputs, destroy. */
+int mk_fit_predict_batched(const mk_problem* prob, const mk_config* cfg, mk_outputs* out);
+
+/* ---- combine (MK.R:123-133): out = (grid_1 + ... + grid_K) / K, sequential order ---- */
+int mk_combine(const double* grids, int32_t K, int64_t grid_len, double* out, int32_t device);
+
+/* ---- exposed kernels for parity tests ---- */
+/* R_k = correlation(coords_k) (n x n column-major) for S point sets of n sites. */
+int mk_correlation_batched(const double* coords, int32_t S, int32_t n, const double* phi, const double* nu,
+                           int32_t cov_model, double* R_out, int32_t device);
+/* Cholesky (lower) + log-determinant (+ optional inverse) of S SPD n x n matrices. */
+int mk_cholesky_batched(const double* A, int32_t S, int32_t n, double* L_out, double* logdet_out,
+                        double* inv_out, int32_t device);
+
+const char* mk_last_error(void);
+int mk_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MK_H */

@@ -1,0 +1,109 @@
+"""ctypes binding of include/mk.h (libmk.so, built in-tree for gfx950).
+
+There is no fallback: if libmk.so is missing or cannot be loaded the import of
+any compute entry point raises MkError.  Structures mirror include/mk.h field
+for field.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from ._build import LIB_PATH
+
+MK_OK = 0
+MK_E_ARG = -1
+MK_E_HIP = -2
+MK_E_NOMEM = -3
+MK_E_NODEV = -4
+MK_COV_EXPONENTIAL = 0
+MK_COV_MATERN = 1
+N_LEVELS = 200
+
+_dp = ctypes.POINTER(ctypes.c_double)
+_ip = ctypes.POINTER(ctypes.c_int32)
+
+
+class MkError(RuntimeError):
+    """Raised for every non-zero libmk status (R glue: Rf_error)."""
+
+    def __init__(self, code, msg):
+        super().__init__(f"libmk error {code}: {msg}")
+        self.code = code
+
+
+class Problem(ctypes.Structure):
+    _fields_ = [("n_subsets", ctypes.c_int32), ("subset_base", ctypes.c_int32), ("q", ctypes.c_int32),
+                ("p", ctypes.c_int32), ("n_part", _ip), ("coords", _dp), ("y", _dp), ("weights", _dp),
+                ("x", _dp), ("n_test", ctypes.c_int32), ("coords_test", _dp)]
+
+
+class Config(ctypes.Structure):
+    _fields_ = [("cov_model", ctypes.c_int32), ("n_batch", ctypes.c_int32), ("batch_length", ctypes.c_int32),
+                ("accept_rate", ctypes.c_double), ("burn_in", ctypes.c_int32),
+                ("beta_starting", _dp), ("beta_tuning", _dp), ("phi_starting", _dp), ("phi_tuning", _dp),
+                ("A_starting", _dp), ("A_tuning", _dp), ("nu_starting", _dp), ("nu_tuning", _dp),
+                ("w_starting", ctypes.c_double), ("w_tuning", ctypes.c_double),
+                ("phi_unif_a", _dp), ("phi_unif_b", _dp), ("nu_unif_a", _dp), ("nu_unif_b", _dp),
+                ("K_IW_df", ctypes.c_double), ("K_IW_S", _dp), ("seed", ctypes.c_uint64),
+                ("record_samples", ctypes.c_int32), ("record_w", ctypes.c_int32), ("device", ctypes.c_int32)]
+
+
+class Outputs(ctypes.Structure):
+    _fields_ = [("parameters", _dp), ("w_predict", _dp), ("samples", _dp), ("w_samples", _dp),
+                ("w_pred_samples", _dp), ("acceptance", _dp)]
+
+
+EXPORTS = {
+    "mk_session_create": (ctypes.c_int, [ctypes.POINTER(Problem), ctypes.POINTER(Config), ctypes.POINTER(ctypes.c_void_p)]),
+    "mk_session_run": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32]),
+    "mk_session_iteration": (ctypes.c_int32, [ctypes.c_void_p]),
+    "mk_session_outputs": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Outputs)]),
+    "mk_session_profile": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32]),
+    "mk_session_kernel_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64),
+                                               _dp, _dp]),
+    "mk_session_destroy": (None, [ctypes.c_void_p]),
+    "mk_fit_predict_batched": (ctypes.c_int, [ctypes.POINTER(Problem), ctypes.POINTER(Config), ctypes.POINTER(Outputs)]),
+    "mk_combine": (ctypes.c_int, [_dp, ctypes.c_int32, ctypes.c_int64, _dp, ctypes.c_int32]),
+    "mk_correlation_batched": (ctypes.c_int, [_dp, ctypes.c_int32, ctypes.c_int32, _dp, _dp, ctypes.c_int32, _dp,
+                                              ctypes.c_int32]),
+    "mk_cholesky_batched": (ctypes.c_int, [_dp, ctypes.c_int32, ctypes.c_int32, _dp, _dp, _dp, ctypes.c_int32]),
+    "mk_last_error": (ctypes.c_char_p, []),
+    "mk_device_count": (ctypes.c_int, []),
+}
+
+_LIB = None
+
+
+def load():
+    """Load libmk.so (raises MkError if it is absent -- no CPU fallback exists)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise MkError(MK_E_ARG, f"{LIB_PATH} not built; run __graft_entry__.build()")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in EXPORTS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _LIB = lib
+    return lib
+
+
+def check(rc):
+    if rc != MK_OK:
+        raise MkError(rc, load().mk_last_error().decode())
+
+
+def dptr(a):
+    """Pointer to a C-contiguous float64 array (or NULL for None)."""
+    if a is None:
+        return None
+    assert a.dtype == np.float64 and a.flags.c_contiguous
+    return a.ctypes.data_as(_dp)
+
+
+def iptr(a):
+    assert a.dtype == np.int32 and a.flags.c_contiguous
+    return a.ctypes.data_as(_ip)

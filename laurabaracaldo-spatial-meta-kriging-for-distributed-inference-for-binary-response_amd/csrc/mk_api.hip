@@ -1,0 +1,717 @@
+// C ABI (include/mk.h) and the per-iteration launch schedule.
+//
+// One mk_session = one GPU's shard of subsets resident in HBM.  Each MCMC
+// iteration is a fixed sequence of stream-ordered launches with no host
+// synchronisation (data-dependent control -- which factors changed -- lives in
+// device work lists), so an iteration costs the host only launch overhead.
+#include <hip/hip_runtime.h>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+#include "../../include/mk.h"
+#include "mk_kernels.hpp"
+
+using namespace mk;
+
+static thread_local std::string g_err;
+
+static int set_err(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIPCHK(x)                                                                                   \
+  do {                                                                                              \
+    hipError_t e_ = (x);                                                                            \
+    if (e_ != hipSuccess) return set_err(MK_E_HIP, std::string(#x " -> ") + hipGetErrorString(e_)); \
+  } while (0)
+
+extern "C" const char* mk_last_error(void) { return g_err.c_str(); }
+
+extern "C" int mk_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+namespace {
+
+constexpr int NKSTAT = 8;
+enum { KS_CHOL_UPDATE = 0, KS_CHOL_DIAG, KS_CHOL_TRSM, KS_SWEEP, KS_LAUUM, KS_ITER };
+
+struct Stat {
+  long launches = 0;
+  double ms = 0.0, flops = 0.0;
+};
+
+struct Timed {
+  int which;
+  hipEvent_t a, b;
+  double flops;
+};
+
+}  // namespace
+
+struct mk_session {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  Model md{};
+  MatSet ms{};
+  int S = 0, q = 1, p = 0, n_pad = 0, nt = 0, P = 0;
+  int iter = 0;
+  bool matern = false, record_samples = true, record_w = false;
+  int* d_list = nullptr;
+  int* d_count = nullptr;
+  double* d_probs = nullptr;
+  std::vector<int> n_part;
+  std::vector<void*> allocs;
+  bool prof = false;
+  std::vector<Timed> pending;
+  std::vector<hipEvent_t> pool;
+  Stat stats[NKSTAT];
+
+  template <typename T>
+  int alloc(T** p_, size_t n) {
+    void* ptr = nullptr;
+    if (n == 0) n = 1;
+    hipError_t e = hipMalloc(&ptr, n * sizeof(T));
+    if (e != hipSuccess) return set_err(MK_E_NOMEM, std::string("hipMalloc ") + std::to_string(n * sizeof(T)) + " B");
+    allocs.push_back(ptr);
+    *p_ = (T*)ptr;
+    return 0;
+  }
+  ~mk_session() {
+    if (device >= 0) hipSetDevice(device);
+    for (auto& t : pending) { hipEventDestroy(t.a); hipEventDestroy(t.b); }
+    for (void* p_ : allocs) hipFree(p_);
+    if (stream) hipStreamDestroy(stream);
+  }
+};
+
+static hipEvent_t ev_new() {
+  hipEvent_t e;
+  hipEventCreate(&e);
+  return e;
+}
+
+// Launch helper that optionally brackets a kernel with events.
+template <typename F>
+static void timed(mk_session* s, int which, double flops, F&& launch) {
+  if (!s->prof) {
+    launch();
+    return;
+  }
+  Timed t{which, ev_new(), ev_new(), flops};
+  hipEventRecord(t.a, s->stream);
+  launch();
+  hipEventRecord(t.b, s->stream);
+  s->pending.push_back(t);
+}
+
+static void drain_timers(mk_session* s) {
+  for (auto& t : s->pending) {
+    hipEventSynchronize(t.b);
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, t.a, t.b);
+    s->stats[t.which].launches += 1;
+    s->stats[t.which].ms += ms;
+    s->stats[t.which].flops += t.flops;
+    hipEventDestroy(t.a);
+    hipEventDestroy(t.b);
+  }
+  s->pending.clear();
+}
+
+static inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
+
+// ------------------------------------------------------------------ Cholesky of all candidates of outcome h
+static void launch_cholesky(mk_session* s, int h, int S_launch) {
+  const int nt = s->nt;
+  const size_t diag_lds = (size_t)(MK_NB * 129 + 3 * MK_NB) * sizeof(double);
+  Model& md = s->md;
+  // valid extent (excludes padding) for the algorithmic flop count
+  const double nv = (double)s->n_part[0] + 1.0;
+  for (int k = 0; k < nt; ++k) {
+    if (k > 0) {
+      // algorithmic flops: rows below panel start x panel cols x K, clipped to the valid extent
+      const double rows = std::fmax(0.0, nv - k * MK_NB);
+      const double cols = std::fmin((double)MK_NB, std::fmax(0.0, nv - k * MK_NB));
+      const double kk = std::fmin((double)k * MK_NB, nv);
+      const double fl = 2.0 * rows * cols * kk * S_launch;
+      timed(s, KS_CHOL_UPDATE, fl, [&] {
+        hipLaunchKernelGGL(k_chol_update, dim3(S_launch * (nt - k)), dim3(256), 0, s->stream, s->ms, S_launch, h, k);
+      });
+    }
+    timed(s, KS_CHOL_DIAG, 0.0, [&] {
+      hipLaunchKernelGGL(k_chol_diag, dim3(S_launch), dim3(512), diag_lds, s->stream, s->ms, md.n_s, h, k, md.ld_part,
+                         md.quad_c, md.info);
+    });
+    if (k < nt - 1) {
+      const double rows = std::fmax(0.0, nv - (k + 1) * MK_NB);
+      const double fl = 2.0 * rows * MK_NB * MK_NB * S_launch;
+      timed(s, KS_CHOL_TRSM, fl, [&] {
+        hipLaunchKernelGGL(k_chol_trsm, dim3(S_launch * (nt - k - 1)), dim3(256), 0, s->stream, s->ms, S_launch, h, k);
+      });
+    }
+  }
+}
+
+// Inverse + g refresh (+ kriging variance on kept iterations) for the dirty list.
+static void launch_inverse(mk_session* s, int max_entries, bool pred) {
+  const int nt = s->nt;
+  Model& md = s->md;
+  hipLaunchKernelGGL(k_inv_copydiag, dim3(max_entries * nt), dim3(256), 0, s->stream, s->ms, s->d_list, s->d_count);
+  for (int d = 1; d < nt; ++d) {
+    hipLaunchKernelGGL(k_inv_T, dim3(max_entries * (nt - d)), dim3(256), 0, s->stream, s->ms, s->d_list, s->d_count, d);
+    hipLaunchKernelGGL(k_inv_D, dim3(max_entries * (nt - d)), dim3(256), 0, s->stream, s->ms, s->d_list, s->d_count, d);
+  }
+  timed(s, KS_LAUUM, 0.0, [&] {
+    hipLaunchKernelGGL(k_lauum, dim3(max_entries * nt * (nt + 1) / 2), dim3(256), 0, s->stream, s->ms, md.n_s,
+                       s->d_list, s->d_count);
+  });
+  hipLaunchKernelGGL(k_gemv_refresh, dim3(max_entries * (s->n_pad / 4)), dim3(256), 0, s->stream, md, s->ms,
+                     s->d_list, s->d_count);
+  if (pred && md.n_test > 0) {
+    hipLaunchKernelGGL(k_pred_var, dim3(max_entries * nt * md.ntt), dim3(256), 0, s->stream, md, s->ms, s->d_list,
+                       s->d_count);
+    hipLaunchKernelGGL(k_pred_var_reduce, dim3(max_entries * (md.n_test_pad / 256)), dim3(256), 0, s->stream, md, nt,
+                       s->d_list, s->d_count);
+  }
+}
+
+static int run_iteration(mk_session* s) {
+  Model& md = s->md;
+  const int it = s->iter;
+  const int S = s->S, q = s->q;
+  const bool kept = it >= md.kept0;
+  hipLaunchKernelGGL(k_beta, dim3(S), dim3(256), 0, s->stream, md, it);
+  if (q > 1)
+    hipLaunchKernelGGL(k_gemv_G, dim3(S * q * (s->n_pad / 4)), dim3(256), 0, s->stream, md, s->ms);
+  hipLaunchKernelGGL(k_Aphase, dim3(S), dim3(256), 0, s->stream, md, it);
+  const int nkinds = s->matern ? 2 : 1;
+  const int ntri_tiles = s->nt * (s->nt + 1) / 2;
+  for (int which = 0; which < nkinds; ++which)
+    for (int h = 0; h < q; ++h) {
+      hipLaunchKernelGGL(k_cov_candidate, dim3(S * ntri_tiles), dim3(256), 0, s->stream, md, s->ms, h, which, it);
+      launch_cholesky(s, h, S);
+      hipLaunchKernelGGL(k_theta_mh, dim3((S + 63) / 64), dim3(64), 0, s->stream, md, s->ms, h, which, it);
+    }
+  hipLaunchKernelGGL(k_dirty_list, dim3(1), dim3(256), 0, s->stream, md, (int)(it == md.kept0), s->d_list, s->d_count);
+  launch_inverse(s, S * q, kept);
+  const size_t sw_lds = (size_t)q * (64 * 64 + 64) * sizeof(double);
+  timed(s, KS_SWEEP, 0.0, [&] {
+    hipLaunchKernelGGL(k_sweep, dim3(S), dim3(256), sw_lds, s->stream, md, s->ms, it);
+  });
+  if (s->record_samples) hipLaunchKernelGGL(k_record, dim3((S + 63) / 64), dim3(64), 0, s->stream, md, it);
+  if (s->record_w) hipLaunchKernelGGL(k_record_w, dim3((md.Np + 255) / 256, S), dim3(256), 0, s->stream, md, it);
+  if (kept && md.n_test > 0) {
+    const int per = (md.n_test + 3) / 4;
+    hipLaunchKernelGGL(k_pred_draw, dim3(S * per), dim3(256), 0, s->stream, md, it, it - md.kept0);
+  }
+  if ((it + 1) % md.batch_length == 0)
+    hipLaunchKernelGGL(k_adapt, dim3(S), dim3(256), 0, s->stream, md, it / md.batch_length);
+  s->iter++;
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+static int check_cfg(const mk_problem* pr, const mk_config* c) {
+  if (!pr || !c) return set_err(MK_E_ARG, "null problem/config");
+  if (pr->n_subsets < 1) return set_err(MK_E_ARG, "n_subsets must be >= 1");
+  if (pr->q < 1 || pr->q > MK_QMAX) return set_err(MK_E_ARG, "q must be in [1, 4]");
+  if (pr->p < 1) return set_err(MK_E_ARG, "p must be >= 1");
+  if (!pr->n_part || !pr->coords || !pr->y || !pr->weights || !pr->x) return set_err(MK_E_ARG, "null data pointer");
+  if (pr->n_test < 0 || (pr->n_test > 0 && !pr->coords_test)) return set_err(MK_E_ARG, "bad coords_test");
+  if (c->cov_model != MK_COV_EXPONENTIAL && c->cov_model != MK_COV_MATERN) return set_err(MK_E_ARG, "cov.model must be exponential or matern");
+  if (c->n_batch < 1 || c->batch_length < 1) return set_err(MK_E_ARG, "n.batch and batch.length must be >= 1");
+  const int n_samples = c->n_batch * c->batch_length;
+  if (c->burn_in < 1 || c->burn_in > n_samples) return set_err(MK_E_ARG, "burn_in must be in [1, n.samples]");
+  if (n_samples - c->burn_in + 1 > 2048) return set_err(MK_E_ARG, "at most 2048 kept samples supported");
+  if (!c->beta_starting || !c->beta_tuning || !c->phi_starting || !c->phi_tuning || !c->A_starting || !c->A_tuning ||
+      !c->phi_unif_a || !c->phi_unif_b || !c->K_IW_S)
+    return set_err(MK_E_ARG, "null starting/tuning/prior array");
+  if (c->cov_model == MK_COV_MATERN && (!c->nu_starting || !c->nu_tuning || !c->nu_unif_a || !c->nu_unif_b))
+    return set_err(MK_E_ARG, "matern needs nu starting/tuning/prior");
+  for (int i = 0; i < pr->n_subsets; ++i)
+    if (pr->n_part[i] < 1) return set_err(MK_E_ARG, "every subset needs >= 1 site");
+  for (int h = 0; h < pr->q; ++h) {
+    if (!(c->phi_unif_a[h] < c->phi_starting[h] && c->phi_starting[h] < c->phi_unif_b[h]))
+      return set_err(MK_E_ARG, "phi starting value outside phi.Unif support");
+  }
+  return 0;
+}
+
+extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_session** out) {
+  if (!out) return set_err(MK_E_ARG, "null out");
+  *out = nullptr;
+  int rc = check_cfg(pr, c);
+  if (rc) return rc;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return set_err(MK_E_NODEV, "no HIP device");
+  if (c->device < 0 || c->device >= ndev) return set_err(MK_E_ARG, "bad device ordinal");
+  HIPCHK(hipSetDevice(c->device));
+  mk_session* s = new mk_session();
+  s->device = c->device;
+  auto fail = [&](int code) { delete s; return code; };
+  if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) return fail(set_err(MK_E_HIP, "stream"));
+
+  const int S = pr->n_subsets, q = pr->q, p = pr->p;
+  s->S = S; s->q = q; s->p = p;
+  s->matern = c->cov_model == MK_COV_MATERN;
+  s->n_part.assign(pr->n_part, pr->n_part + S);
+  int nmax = 0;
+  long tot_sites = 0;
+  for (int i = 0; i < S; ++i) { nmax = std::max(nmax, (int)pr->n_part[i]); tot_sites += pr->n_part[i]; }
+  const int n_pad = round_up(nmax + 1, MK_NB);
+  const int nt = n_pad / MK_NB;
+  s->n_pad = n_pad; s->nt = nt;
+  const int Np = n_pad * q;
+  const int ntri = q * (q + 1) / 2;
+  const int n_theta = ntri + q * (s->matern ? 2 : 1);
+  const int P = p + n_theta;
+  s->P = P;
+  const int o_w = p + n_theta;
+  const int n_mh_max = o_w + Np;
+  const int n_samples = c->n_batch * c->batch_length;
+  const int kept0 = c->burn_in - 1;
+  const int n_kept = n_samples - kept0;
+  const int n_test = pr->n_test;
+  const int n_test_pad = round_up(std::max(n_test, 1), 256);
+
+  Model& md = s->md;
+  md.S = S; md.q = q; md.p = p; md.n_pad = n_pad; md.Np = Np; md.nt = nt; md.ntri = ntri; md.n_theta = n_theta;
+  md.cov_model = c->cov_model;
+  md.o_A = p; md.o_phi = p + ntri; md.o_nu = p + ntri + q; md.o_w = o_w; md.n_mh_max = n_mh_max;
+  md.n_batch = c->n_batch; md.batch_length = c->batch_length; md.n_samples = n_samples;
+  md.kept0 = kept0; md.n_kept = n_kept;
+  md.n_test = n_test; md.n_test_pad = n_test_pad; md.ntt = n_test_pad / MK_NB;
+  md.subset_base = pr->subset_base;
+  md.seed = c->seed;
+  md.accept_rate = c->accept_rate;
+  md.P = P;
+  for (int h = 0; h < q; ++h) {
+    md.phi_a[h] = c->phi_unif_a[h]; md.phi_b[h] = c->phi_unif_b[h];
+    md.nu_a[h] = s->matern ? c->nu_unif_a[h] : 0.0;
+    md.nu_b[h] = s->matern ? c->nu_unif_b[h] : 1.0;
+  }
+  md.iw_df = c->K_IW_df;
+  for (int i = 0; i < q * q; ++i) md.iw_S[i] = c->K_IW_S[i];
+  s->record_samples = true;   // needed on device for the parameter quantiles
+  s->record_w = c->record_w != 0;
+
+  // ---------------- allocations
+  int* d_ns; double *d_coords, *d_y, *d_wt, *d_X, *d_ct;
+  if ((rc = s->alloc(&d_ns, S)) || (rc = s->alloc(&d_coords, (size_t)S * 2 * n_pad)) ||
+      (rc = s->alloc(&d_y, (size_t)S * Np)) || (rc = s->alloc(&d_wt, (size_t)S * Np)) ||
+      (rc = s->alloc(&d_X, (size_t)S * p * Np)) || (rc = s->alloc(&d_ct, (size_t)2 * n_test_pad)))
+    return fail(rc);
+  md.n_s = d_ns; md.coords = d_coords; md.y = d_y; md.wt = d_wt; md.X = d_X; md.coords_test = d_ct;
+  if ((rc = s->alloc(&md.beta, (size_t)S * p)) || (rc = s->alloc(&md.theta, (size_t)S * n_theta)) ||
+      (rc = s->alloc(&md.w, (size_t)S * Np)) || (rc = s->alloc(&md.eta, (size_t)S * Np)) ||
+      (rc = s->alloc(&md.tune, (size_t)S * n_mh_max)) || (rc = s->alloc(&md.acc, (size_t)S * n_mh_max)) ||
+      (rc = s->alloc(&md.u, (size_t)S * q * n_pad)) || (rc = s->alloc(&md.g, (size_t)S * q * n_pad)) ||
+      (rc = s->alloc(&md.G, (size_t)S * q * q * n_pad)) || (rc = s->alloc(&md.logdetR, (size_t)S * q)) ||
+      (rc = s->alloc(&md.quad, (size_t)S * q)) || (rc = s->alloc(&md.A_full, (size_t)S * q * q)) ||
+      (rc = s->alloc(&md.Ainv, (size_t)S * q * q)) || (rc = s->alloc(&md.dirty, (size_t)S * q)) ||
+      (rc = s->alloc(&md.ld_part, (size_t)S * nt)) || (rc = s->alloc(&md.quad_c, (size_t)S)) ||
+      (rc = s->alloc(&md.info, (size_t)S)) || (rc = s->alloc(&md.sw_delta, (size_t)S * Np)) ||
+      (rc = s->alloc(&md.sw_dll, (size_t)S * Np)) || (rc = s->alloc(&md.sw_logu, (size_t)S * Np)) ||
+      (rc = s->alloc(&md.sw_acc, (size_t)S * Np)) || (rc = s->alloc(&md.samples, (size_t)S * n_samples * P)) ||
+      (rc = s->alloc(&md.acc_hist, (size_t)S * c->n_batch * (o_w + 1))))
+    return fail(rc);
+  if (s->record_w && (rc = s->alloc(&md.w_samples, (size_t)S * n_samples * Np))) return fail(rc);
+  if ((rc = s->alloc(&md.s_pred, (size_t)S * q * n_test_pad)) ||
+      (rc = s->alloc(&md.s_part, (size_t)S * q * nt * n_test_pad)) ||
+      (rc = s->alloc(&md.w_pred, (size_t)S * n_kept * q * std::max(n_test, 1))))
+    return fail(rc);
+  MatSet& ms = s->ms;
+  ms.ld = n_pad; ms.nt = nt; ms.q = q;
+  if ((rc = s->alloc(&ms.L, (size_t)S * q * 2 * n_pad * n_pad)) ||
+      (rc = s->alloc(&ms.Winv, (size_t)S * q * 2 * nt * MK_NB * MK_NB)) ||
+      (rc = s->alloc(&ms.Q, (size_t)S * q * n_pad * n_pad)) || (rc = s->alloc(&ms.cur, (size_t)S * q)) ||
+      (rc = s->alloc(&s->d_list, (size_t)S * q)) || (rc = s->alloc(&s->d_count, 1)) ||
+      (rc = s->alloc(&s->d_probs, MK_N_LEVELS)))
+    return fail(rc);
+
+  // ---------------- host staging (R layout -> padded device layout)
+  std::vector<double> hc((size_t)S * 2 * n_pad, 0.0), hy((size_t)S * Np, 0.0), hw((size_t)S * Np, 0.0),
+      hX((size_t)S * p * Np, 0.0);
+  {
+    long off_site = 0;
+    for (int i = 0; i < S; ++i) {
+      const int ns = pr->n_part[i];
+      const double* cs = pr->coords + 2 * off_site;
+      for (int r = 0; r < ns; ++r) {
+        hc[(size_t)i * 2 * n_pad + r] = cs[r];
+        hc[(size_t)i * 2 * n_pad + n_pad + r] = cs[ns + r];
+      }
+      const double* ys = pr->y + off_site * q;
+      const double* ws = pr->weights + off_site * q;
+      for (int k = 0; k < ns * q; ++k) {
+        hy[(size_t)i * Np + k] = ys[k];
+        hw[(size_t)i * Np + k] = ws[k];
+      }
+      const double* xs = pr->x + off_site * q * p;
+      for (int j = 0; j < p; ++j)
+        for (int k = 0; k < ns * q; ++k) hX[((size_t)i * p + j) * Np + k] = xs[(size_t)j * ns * q + k];
+      off_site += ns;
+    }
+  }
+  std::vector<double> hct((size_t)2 * n_test_pad, 0.0);
+  for (int t = 0; t < n_test; ++t) {
+    hct[t] = pr->coords_test[t];
+    hct[n_test_pad + t] = pr->coords_test[n_test + t];
+  }
+  HIPCHK(hipMemcpy(d_ns, pr->n_part, S * sizeof(int), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(d_coords, hc.data(), hc.size() * 8, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(d_y, hy.data(), hy.size() * 8, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(d_wt, hw.data(), hw.size() * 8, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(d_X, hX.data(), hX.size() * 8, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(d_ct, hct.data(), hct.size() * 8, hipMemcpyHostToDevice));
+
+  // ---------------- starting values (identical for every subset, MK.R:54-62)
+  std::vector<double> hb((size_t)S * p), hth((size_t)S * n_theta), hwv((size_t)S * Np, 0.0),
+      htune((size_t)S * n_mh_max, 0.0), hA((size_t)S * q * q), hAi((size_t)S * q * q);
+  std::vector<double> th0(n_theta), A0(q * q, 0.0), Ai0(q * q, 0.0), tune0(o_w);
+  {
+    int k = 0;
+    for (int j = 0; j < q; ++j)
+      for (int i = j; i < q; ++i, ++k) {
+        const double a = c->A_starting[k];
+        if (i == j && !(a > 0.0)) { delete s; return set_err(MK_E_ARG, "A starting diagonal must be > 0"); }
+        th0[k] = (i == j) ? std::log(a) : a;
+        A0[i + j * q] = a;
+      }
+    for (int h = 0; h < q; ++h) {
+      const double ph = c->phi_starting[h];
+      th0[ntri + h] = std::log((ph - md.phi_a[h]) / (md.phi_b[h] - ph));
+      if (s->matern) {
+        const double nv = c->nu_starting[h];
+        if (!(md.nu_a[h] < nv && nv < md.nu_b[h])) { delete s; return set_err(MK_E_ARG, "nu starting value outside nu.Unif support"); }
+        th0[ntri + q + h] = std::log((nv - md.nu_a[h]) / (md.nu_b[h] - nv));
+      }
+    }
+    for (int cc = 0; cc < q; ++cc)
+      for (int r = 0; r < q; ++r) {
+        if (r < cc) continue;
+        double sum = (r == cc) ? 1.0 : 0.0;
+        for (int m = cc; m < r; ++m) sum -= A0[r + m * q] * Ai0[m + cc * q];
+        Ai0[r + cc * q] = sum / A0[r + r * q];
+      }
+    for (int j = 0; j < p; ++j) {
+      if (!(c->beta_tuning[j] > 0.0)) { delete s; return set_err(MK_E_ARG, "beta tuning must be > 0"); }
+      tune0[j] = std::log(std::sqrt(c->beta_tuning[j]));
+    }
+    for (int k2 = 0; k2 < ntri; ++k2) tune0[p + k2] = std::log(std::sqrt(c->A_tuning[k2]));
+    for (int h = 0; h < q; ++h) {
+      tune0[p + ntri + h] = std::log(std::sqrt(c->phi_tuning[h]));
+      if (s->matern) tune0[p + ntri + q + h] = std::log(std::sqrt(c->nu_tuning[h]));
+    }
+  }
+  const double tw = std::log(std::sqrt(c->w_tuning));
+  for (int i = 0; i < S; ++i) {
+    for (int j = 0; j < p; ++j) hb[(size_t)i * p + j] = c->beta_starting[j];
+    for (int k = 0; k < n_theta; ++k) hth[(size_t)i * n_theta + k] = th0[k];
+    for (int k = 0; k < pr->n_part[i] * q; ++k) {
+      hwv[(size_t)i * Np + k] = c->w_starting;
+      htune[(size_t)i * n_mh_max + o_w + k] = tw;
+    }
+    for (int k = 0; k < o_w; ++k) htune[(size_t)i * n_mh_max + k] = tune0[k];
+    for (int k = 0; k < q * q; ++k) { hA[(size_t)i * q * q + k] = A0[k]; hAi[(size_t)i * q * q + k] = Ai0[k]; }
+  }
+  HIPCHK(hipMemcpy(md.beta, hb.data(), hb.size() * 8, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(md.theta, hth.data(), hth.size() * 8, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(md.w, hwv.data(), hwv.size() * 8, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(md.tune, htune.data(), htune.size() * 8, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(md.A_full, hA.data(), hA.size() * 8, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(md.Ainv, hAi.data(), hAi.size() * 8, hipMemcpyHostToDevice));
+  HIPCHK(hipMemsetAsync(md.acc, 0, (size_t)S * n_mh_max * 8, s->stream));
+  HIPCHK(hipMemsetAsync(md.dirty, 0, (size_t)S * q * 4, s->stream));
+  HIPCHK(hipMemsetAsync(md.info, 0, (size_t)S * 4, s->stream));
+  HIPCHK(hipMemsetAsync(ms.cur, 0, (size_t)S * q * 4, s->stream));
+  HIPCHK(hipMemsetAsync(md.u, 0, (size_t)S * q * n_pad * 8, s->stream));
+  HIPCHK(hipMemsetAsync(md.g, 0, (size_t)S * q * n_pad * 8, s->stream));
+  HIPCHK(hipMemsetAsync(md.G, 0, (size_t)S * q * q * n_pad * 8, s->stream));
+  HIPCHK(hipMemsetAsync(md.s_pred, 0, (size_t)S * q * n_test_pad * 8, s->stream));
+  HIPCHK(hipMemsetAsync(ms.Q, 0, (size_t)S * q * n_pad * n_pad * 8, s->stream));
+  {
+    std::vector<double> probs(MK_N_LEVELS);
+    // seq(0.005, 1, 0.005): from + (0:n)*by, pmin(x, to)  (MK.R:88)
+    for (int i = 0; i < MK_N_LEVELS; ++i) probs[i] = std::fmin(0.005 + (double)i * 0.005, 1.0);
+    HIPCHK(hipMemcpy(s->d_probs, probs.data(), MK_N_LEVELS * 8, hipMemcpyHostToDevice));
+  }
+  HIPCHK(hipFuncSetAttribute((const void*)k_chol_diag, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (MK_NB * 129 + 3 * MK_NB) * 8));
+  HIPCHK(hipFuncSetAttribute((const void*)k_sweep, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             q * (64 * 64 + 64) * 8));
+
+  // ---------------- initial state: eta, u, factor every R_h at the starting values, Q, g
+  hipLaunchKernelGGL(k_init_state, dim3(S), dim3(256), 0, s->stream, md);
+  const int ntri_tiles = nt * (nt + 1) / 2;
+  for (int h = 0; h < q; ++h) {
+    hipLaunchKernelGGL(k_cov_candidate, dim3(S * ntri_tiles), dim3(256), 0, s->stream, md, ms, h, 2, 0);
+    launch_cholesky(s, h, S);
+    hipLaunchKernelGGL(k_theta_init, dim3((S + 63) / 64), dim3(64), 0, s->stream, md, ms, h);
+  }
+  hipLaunchKernelGGL(k_dirty_list, dim3(1), dim3(256), 0, s->stream, md, 0, s->d_list, s->d_count);
+  launch_inverse(s, S * q, false);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(s->stream));
+  s->stats[0] = Stat(); s->stats[1] = Stat(); s->stats[2] = Stat(); s->stats[4] = Stat();
+  drain_timers(s);
+  for (auto& st : s->stats) st = Stat();
+  *out = s;
+  return 0;
+}
+
+extern "C" int mk_session_run(mk_session* s, int32_t n_iter) {
+  if (!s) return set_err(MK_E_ARG, "null session");
+  HIPCHK(hipSetDevice(s->device));
+  if (n_iter < 0 || s->iter + n_iter > s->md.n_samples) return set_err(MK_E_ARG, "n_iter beyond n.samples");
+  hipEvent_t a = nullptr, b = nullptr;
+  if (s->prof) { a = ev_new(); b = ev_new(); hipEventRecord(a, s->stream); }
+  for (int i = 0; i < n_iter; ++i) {
+    int rc = run_iteration(s);
+    if (rc) return rc;
+  }
+  if (s->prof) hipEventRecord(b, s->stream);
+  HIPCHK(hipStreamSynchronize(s->stream));
+  if (s->prof) {
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, a, b);
+    s->stats[KS_ITER].launches += n_iter;
+    s->stats[KS_ITER].ms += ms;
+    hipEventDestroy(a);
+    hipEventDestroy(b);
+    drain_timers(s);
+  }
+  return 0;
+}
+
+extern "C" int32_t mk_session_iteration(const mk_session* s) { return s ? s->iter : -1; }
+
+extern "C" int mk_session_profile(mk_session* s, int32_t enable) {
+  if (!s) return set_err(MK_E_ARG, "null session");
+  s->prof = enable != 0;
+  return 0;
+}
+
+extern "C" int mk_session_kernel_stats(const mk_session* s, int32_t which, int64_t* launches, double* total_ms,
+                                       double* flops) {
+  if (!s || which < 0 || which >= NKSTAT) return set_err(MK_E_ARG, "bad stats query");
+  if (launches) *launches = s->stats[which].launches;
+  if (total_ms) *total_ms = s->stats[which].ms;
+  if (flops) *flops = s->stats[which].flops;
+  return 0;
+}
+
+extern "C" int mk_session_outputs(mk_session* s, mk_outputs* o) {
+  if (!s || !o) return set_err(MK_E_ARG, "null session/outputs");
+  HIPCHK(hipSetDevice(s->device));
+  Model& md = s->md;
+  const int S = s->S, P = s->P, q = s->q;
+  const int n_test = md.n_test;
+  const bool done = s->iter >= md.n_samples;
+  if ((o->parameters || o->w_predict || o->w_pred_samples) && !done)
+    return set_err(MK_E_ARG, "quantile/predictive outputs need all n.samples iterations");
+  if (o->parameters) {
+    double* dq;
+    int rc = s->alloc(&dq, (size_t)S * P * MK_N_LEVELS);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_quantiles, dim3(S * P), dim3(256), 0, s->stream, md.samples + (long)md.kept0 * P,
+                       (long)md.n_samples * P, (long)P, md.n_kept, P, s->d_probs, MK_N_LEVELS, dq);
+    HIPCHK(hipGetLastError());
+    // device layout [S][P][200] == R's 200 x P column-major per subset
+    HIPCHK(hipMemcpyAsync(o->parameters, dq, (size_t)S * P * MK_N_LEVELS * 8, hipMemcpyDeviceToHost, s->stream));
+  }
+  if (o->w_predict && n_test > 0) {
+    const int C = q * n_test;
+    double* dq;
+    int rc = s->alloc(&dq, (size_t)S * C * MK_N_LEVELS);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_quantiles, dim3(S * C), dim3(256), 0, s->stream, md.w_pred, (long)md.n_kept * C, (long)C,
+                       md.n_kept, C, s->d_probs, MK_N_LEVELS, dq);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(o->w_predict, dq, (size_t)S * C * MK_N_LEVELS * 8, hipMemcpyDeviceToHost, s->stream));
+  }
+  HIPCHK(hipStreamSynchronize(s->stream));
+  const int it = s->iter;
+  if (o->samples) {
+    std::vector<double> h((size_t)S * md.n_samples * P);
+    HIPCHK(hipMemcpy(h.data(), md.samples, h.size() * 8, hipMemcpyDeviceToHost));
+    // [S][iter][P] -> per subset n_samples x P column-major (rows beyond `it` are zero)
+    for (int i = 0; i < S; ++i)
+      for (int r = 0; r < md.n_samples; ++r)
+        for (int cc = 0; cc < P; ++cc)
+          o->samples[(size_t)i * md.n_samples * P + r + (size_t)cc * md.n_samples] =
+              (r < it) ? h[((size_t)i * md.n_samples + r) * P + cc] : 0.0;
+  }
+  if (o->w_samples) {
+    if (!md.w_samples) return set_err(MK_E_ARG, "w samples were not recorded (record_w = 0)");
+    std::vector<double> h((size_t)S * md.n_samples * md.Np);
+    HIPCHK(hipMemcpy(h.data(), md.w_samples, h.size() * 8, hipMemcpyDeviceToHost));
+    size_t off = 0;
+    for (int i = 0; i < S; ++i) {
+      const int N = s->n_part[i] * q;
+      for (int r = 0; r < md.n_samples; ++r)
+        for (int k = 0; k < N; ++k)
+          o->w_samples[off + k + (size_t)r * N] = (r < it) ? h[((size_t)i * md.n_samples + r) * md.Np + k] : 0.0;
+      off += (size_t)N * md.n_samples;
+    }
+  }
+  if (o->w_pred_samples && n_test > 0) {
+    const int C = q * n_test;
+    std::vector<double> h((size_t)S * md.n_kept * C);
+    HIPCHK(hipMemcpy(h.data(), md.w_pred, h.size() * 8, hipMemcpyDeviceToHost));
+    // [S][kept][C] -> per subset C x kept column-major (p.w.predictive.samples)
+    for (int i = 0; i < S; ++i)
+      for (int k = 0; k < md.n_kept; ++k)
+        for (int cc = 0; cc < C; ++cc)
+          o->w_pred_samples[(size_t)i * md.n_kept * C + cc + (size_t)k * C] = h[((size_t)i * md.n_kept + k) * C + cc];
+  }
+  if (o->acceptance) {
+    const int nrep = md.o_w + 1;
+    std::vector<double> h((size_t)S * md.n_batch * nrep);
+    HIPCHK(hipMemcpy(h.data(), md.acc_hist, h.size() * 8, hipMemcpyDeviceToHost));
+    for (int i = 0; i < S; ++i)
+      for (int b = 0; b < md.n_batch; ++b)
+        for (int j = 0; j < nrep; ++j)
+          o->acceptance[(size_t)i * md.n_batch * nrep + b + (size_t)j * md.n_batch] =
+              h[((size_t)i * md.n_batch + b) * nrep + j];
+  }
+  return 0;
+}
+
+extern "C" void mk_session_destroy(mk_session* s) { delete s; }
+
+extern "C" int mk_fit_predict_batched(const mk_problem* pr, const mk_config* c, mk_outputs* o) {
+  mk_session* s = nullptr;
+  int rc = mk_session_create(pr, c, &s);
+  if (rc) return rc;
+  rc = mk_session_run(s, c->n_batch * c->batch_length);
+  if (!rc) rc = mk_session_outputs(s, o);
+  mk_session_destroy(s);
+  return rc;
+}
+
+// ------------------------------------------------------------------ combine
+extern "C" int mk_combine(const double* grids, int32_t K, int64_t G, double* out, int32_t device) {
+  if (!grids || !out || K < 1 || G < 1) return set_err(MK_E_ARG, "bad combine arguments");
+  HIPCHK(hipSetDevice(device));
+  double *dg = nullptr, *dout = nullptr;
+  HIPCHK(hipMalloc(&dg, (size_t)K * G * 8));
+  if (hipMalloc(&dout, (size_t)G * 8) != hipSuccess) { hipFree(dg); return set_err(MK_E_NOMEM, "combine alloc"); }
+  hipError_t e = hipMemcpy(dg, grids, (size_t)K * G * 8, hipMemcpyHostToDevice);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(k_combine, dim3((unsigned)((G + 255) / 256)), dim3(256), 0, 0, dg, K, (long)G, dout);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpy(out, dout, (size_t)G * 8, hipMemcpyDeviceToHost);
+  hipFree(dg);
+  hipFree(dout);
+  if (e != hipSuccess) return set_err(MK_E_HIP, std::string("combine: ") + hipGetErrorString(e));
+  return 0;
+}
+
+// ------------------------------------------------------------------ parity-test entry points
+extern "C" int mk_correlation_batched(const double* coords, int32_t S, int32_t n, const double* phi, const double* nu,
+                                      int32_t cov_model, double* R_out, int32_t device) {
+  if (!coords || !phi || !R_out || S < 1 || n < 1) return set_err(MK_E_ARG, "bad correlation arguments");
+  HIPCHK(hipSetDevice(device));
+  double *dc, *dphi, *dnu = nullptr, *dr;
+  HIPCHK(hipMalloc(&dc, (size_t)S * 2 * n * 8));
+  HIPCHK(hipMalloc(&dphi, (size_t)S * 8));
+  HIPCHK(hipMalloc(&dr, (size_t)S * n * n * 8));
+  if (nu) HIPCHK(hipMalloc(&dnu, (size_t)S * 8));
+  HIPCHK(hipMemcpy(dc, coords, (size_t)S * 2 * n * 8, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dphi, phi, (size_t)S * 8, hipMemcpyHostToDevice));
+  if (nu) HIPCHK(hipMemcpy(dnu, nu, (size_t)S * 8, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(k_corr_plain, dim3(2048), dim3(256), 0, 0, dc, S, n, dphi, dnu, cov_model, dr);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpy(R_out, dr, (size_t)S * n * n * 8, hipMemcpyDeviceToHost));
+  hipFree(dc); hipFree(dphi); hipFree(dr);
+  if (dnu) hipFree(dnu);
+  return 0;
+}
+
+extern "C" int mk_cholesky_batched(const double* A, int32_t S, int32_t n, double* L_out, double* logdet_out,
+                                   double* inv_out, int32_t device) {
+  if (!A || S < 1 || n < 1) return set_err(MK_E_ARG, "bad cholesky arguments");
+  HIPCHK(hipSetDevice(device));
+  mk_session* s = new mk_session();
+  s->device = device;
+  auto fail = [&](int code) { delete s; return code; };
+  if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) return fail(set_err(MK_E_HIP, "stream"));
+  const int n_pad = round_up(n + 1, MK_NB), nt = n_pad / MK_NB;
+  s->S = S; s->q = 1; s->n_pad = n_pad; s->nt = nt;
+  s->n_part.assign(S, n);
+  Model& md = s->md;
+  md.S = S; md.q = 1; md.nt = nt; md.n_pad = n_pad;
+  MatSet& ms = s->ms;
+  ms.ld = n_pad; ms.nt = nt; ms.q = 1;
+  int rc;
+  int* d_ns;
+  double* dA;
+  if ((rc = s->alloc(&d_ns, S)) || (rc = s->alloc(&md.ld_part, (size_t)S * nt)) || (rc = s->alloc(&md.quad_c, S)) ||
+      (rc = s->alloc(&md.info, S)) || (rc = s->alloc(&md.dirty, S)) || (rc = s->alloc(&ms.cur, S)) ||
+      (rc = s->alloc(&md.logdetR, S)) || (rc = s->alloc(&md.quad, S)) ||
+      (rc = s->alloc(&ms.L, (size_t)S * 2 * n_pad * n_pad)) || (rc = s->alloc(&ms.Winv, (size_t)S * 2 * nt * MK_NB * MK_NB)) ||
+      (rc = s->alloc(&ms.Q, (size_t)S * n_pad * n_pad)) || (rc = s->alloc(&s->d_list, S)) ||
+      (rc = s->alloc(&s->d_count, 1)) || (rc = s->alloc(&dA, (size_t)S * n * n)))
+    return fail(rc);
+  md.n_s = d_ns;
+  std::vector<int> hn(S, n);
+  if (hipMemcpy(d_ns, hn.data(), S * 4, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(dA, A, (size_t)S * n * n * 8, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemset(ms.cur, 0, S * 4) != hipSuccess || hipMemset(md.info, 0, S * 4) != hipSuccess)
+    return fail(set_err(MK_E_HIP, "cholesky upload"));
+  if (hipFuncSetAttribute((const void*)k_chol_diag, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (MK_NB * 129 + 3 * MK_NB) * 8) != hipSuccess)
+    return fail(set_err(MK_E_HIP, "lds attribute"));
+  hipLaunchKernelGGL(k_load_plain, dim3(2048), dim3(256), 0, s->stream, ms, dA, n, S);
+  launch_cholesky(s, 0, S);
+  std::vector<double> part((size_t)S * nt);
+  std::vector<int> info(S);
+  if (hipStreamSynchronize(s->stream) != hipSuccess) return fail(set_err(MK_E_HIP, "cholesky run"));
+  if (hipMemcpy(info.data(), md.info, S * 4, hipMemcpyDeviceToHost) != hipSuccess)
+    return fail(set_err(MK_E_HIP, "info download"));
+  for (int i = 0; i < S; ++i)
+    if (info[i]) return fail(set_err(MK_E_ARG, "matrix " + std::to_string(i) + " is not positive definite"));
+  hipLaunchKernelGGL(k_theta_init, dim3((S + 63) / 64), dim3(64), 0, s->stream, md, ms, 0);
+  double* dL = nullptr;
+  if ((rc = s->alloc(&dL, (size_t)S * n * n))) return fail(rc);
+  if (L_out) {
+    hipLaunchKernelGGL(k_extract_L, dim3(2048), dim3(256), 0, s->stream, ms, n, S, dL, 0);
+    if (hipMemcpyAsync(L_out, dL, (size_t)S * n * n * 8, hipMemcpyDeviceToHost, s->stream) != hipSuccess)
+      return fail(set_err(MK_E_HIP, "L download"));
+  }
+  if (logdet_out) {
+    if (hipMemcpy(part.data(), md.ld_part, part.size() * 8, hipMemcpyDeviceToHost) != hipSuccess)
+      return fail(set_err(MK_E_HIP, "logdet download"));
+    for (int i = 0; i < S; ++i) {
+      double v = 0.0;
+      for (int k = 0; k < nt; ++k) v += part[(size_t)i * nt + k];
+      logdet_out[i] = v;
+    }
+  }
+  if (inv_out) {
+    hipLaunchKernelGGL(k_dirty_list, dim3(1), dim3(256), 0, s->stream, md, 1, s->d_list, s->d_count);
+    const int ntiles = nt * (nt + 1) / 2;
+    hipLaunchKernelGGL(k_inv_copydiag, dim3(S * nt), dim3(256), 0, s->stream, ms, s->d_list, s->d_count);
+    for (int d = 1; d < nt; ++d) {
+      hipLaunchKernelGGL(k_inv_T, dim3(S * (nt - d)), dim3(256), 0, s->stream, ms, s->d_list, s->d_count, d);
+      hipLaunchKernelGGL(k_inv_D, dim3(S * (nt - d)), dim3(256), 0, s->stream, ms, s->d_list, s->d_count, d);
+    }
+    hipLaunchKernelGGL(k_lauum, dim3(S * ntiles), dim3(256), 0, s->stream, ms, md.n_s, s->d_list, s->d_count);
+    hipLaunchKernelGGL(k_extract_L, dim3(2048), dim3(256), 0, s->stream, ms, n, S, dL, 1);
+    if (hipMemcpyAsync(inv_out, dL, (size_t)S * n * n * 8, hipMemcpyDeviceToHost, s->stream) != hipSuccess)
+      return fail(set_err(MK_E_HIP, "inverse download"));
+  }
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+  if (e != hipSuccess) return fail(set_err(MK_E_HIP, std::string("cholesky: ") + hipGetErrorString(e)));
+  delete s;
+  return 0;
+}

@@ -1,0 +1,92 @@
+// Shared device helpers for libmk (gfx950 / CDNA4 only).
+//
+// Philox4x32-10 is the bit-exact twin of oracle/philox.py; every random draw
+// of the sampler and of the kriging step is a pure function of
+// (seed, subset, index, iteration, tag) so the device chain can be replayed on
+// the host.  Stream layout documented in oracle/philox.py and DESIGN.md.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define MK_NB 128          // Cholesky / GEMM tile edge (fp64)
+#define MK_TAG_PROPOSAL 1u
+#define MK_TAG_PREDICT 2u
+#define MK_TAG_RESAMPLE 3u
+
+#define MK_TWO_PI 6.283185307179586
+#define MK_TWO_M52 2.220446049250313e-16   // 2^-52
+
+namespace mk {
+
+struct Key { uint32_t k0, k1; };
+
+__host__ __device__ inline Key make_key(uint64_t seed, uint32_t subset) {
+  Key k;
+  k.k0 = (uint32_t)(seed & 0xFFFFFFFFull);
+  k.k1 = (uint32_t)(seed >> 32) + subset;
+  return k;
+}
+
+__device__ inline uint4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, Key key) {
+  uint32_t k0 = key.k0, k1 = key.k1;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    if (r > 0) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+    const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+    const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+  }
+  return make_uint4(c0, c1, c2, c3);
+}
+
+__device__ inline double u01_open(uint32_t hi, uint32_t lo) {
+  const uint64_t top52 = ((((uint64_t)hi) << 32) | (uint64_t)lo) >> 12;
+  return ((double)top52 + 0.5) * MK_TWO_M52;
+}
+
+__device__ inline double normal_from(uint4 w) {
+  const double u1 = u01_open(w.x, w.y), u2 = u01_open(w.z, w.w);
+  return sqrt(-2.0 * log(u1)) * cos(MK_TWO_PI * u2);
+}
+
+// N(0,1) proposal for MH parameter j at iteration s.
+__device__ inline double proposal_normal(Key key, uint32_t j, uint32_t s) {
+  return normal_from(philox(j, s, MK_TAG_PROPOSAL, 0u, key));
+}
+// log U accept draw for MH parameter j at iteration s.
+__device__ inline double accept_log_uniform(Key key, uint32_t j, uint32_t s) {
+  const uint4 w = philox(j, s, MK_TAG_PROPOSAL, 1u, key);
+  return log(u01_open(w.x, w.y));
+}
+__device__ inline double predict_normal(Key key, uint32_t idx, uint32_t s) {
+  return normal_from(philox(idx, s, MK_TAG_PREDICT, 0u, key));
+}
+
+__device__ inline double softplus(double x) { return fmax(x, 0.0) + log1p(exp(-fabs(x))); }
+__device__ inline double loglik_term(double y, double wt, double eta) { return y * eta - wt * softplus(eta); }
+
+// spBayes util logitInv(z, a, b) = b - (b-a)/(1+exp(z))
+__device__ __host__ inline double logit_inv(double z, double a, double b) { return b - (b - a) / (1.0 + exp(z)); }
+__device__ inline double unif_jacobian(double v, double a, double b) { return log(v - a) + log(b - v); }
+
+// Deterministic block reduction (fixed tree, wave64 shuffles then LDS).
+template <int NT>
+__device__ inline double block_sum(double v, double* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  double t = 0.0;
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w) t += red[w];
+    red[NT / 64] = t;
+  }
+  __syncthreads();
+  return red[NT / 64];
+}
+
+}  // namespace mk

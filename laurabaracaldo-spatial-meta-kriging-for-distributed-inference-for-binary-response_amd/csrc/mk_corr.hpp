@@ -1,0 +1,121 @@
+// Spatial correlation functions (spBayes spCor semantics):
+//   exponential  rho(d) = exp(-phi d)
+//   Matern       rho(d) = (phi d)^nu / (2^(nu-1) Gamma(nu)) K_nu(phi d),  rho(0) = 1
+// K_nu for real nu >= 0 in fp64: nu = n + mu, |mu| <= 1/2; K_mu, K_mu+1 from
+// Temme's series (x <= 2) or Steed's continued fraction CF2 (x > 2) (Temme
+// 1975, J. Comput. Phys. 19; the bessik scheme), then forward recurrence in nu.
+// 1/Gamma(1 +- mu) differences use the reciprocal-gamma Taylor series
+// (Abramowitz & Stegun 6.1.34) for |mu| < 0.1 to avoid cancellation.
+#pragma once
+#include "mk_common.hpp"
+
+namespace mk {
+
+#define MK_COV_EXPONENTIAL 0
+#define MK_COV_MATERN 1
+
+__host__ __device__ inline void temme_gammas(double mu, double* gam1, double* gam2, double* gampl, double* gammi) {
+  // 1/Gamma(1+z) = sum_k a_k z^(k-1)  (A&S 6.1.34)
+  const double a[15] = {1.0, 0.5772156649015329, -0.6558780715202538, -0.0420026350340952,
+                        0.1665386113822915, -0.0421977345555443, -0.0096219715278770, 0.0072189432466630,
+                        -0.0011651675918591, -0.0002152416741149, 0.0001280502823882, -0.0000201348547807,
+                        -0.0000012504934821, 0.0000011330272320, -0.0000002056338417};
+  *gampl = 1.0 / tgamma(1.0 + mu);
+  *gammi = 1.0 / tgamma(1.0 - mu);
+  *gam2 = 0.5 * (*gammi + *gampl);
+  if (fabs(mu) < 0.1) {
+    const double m2 = mu * mu;
+    double s = 0.0, pw = 1.0;
+    for (int k = 1; k < 15; k += 2) {  // a_2, a_4, ... (0-based odd indices)
+      s += a[k] * pw;
+      pw *= m2;
+    }
+    *gam1 = -s;
+  } else {
+    *gam1 = (*gammi - *gampl) / (2.0 * mu);
+  }
+}
+
+__host__ __device__ inline double bessel_k(double x, double nu) {
+  const double EPS = 1e-16;
+  const double PI = 3.141592653589793;
+  const int nl = (int)(nu + 0.5);
+  const double mu = nu - nl, mu2 = mu * mu;
+  const double xi = 1.0 / x, xi2 = 2.0 * xi;
+  double rkmu, rk1;
+  if (x < 2.0) {
+    const double x2 = 0.5 * x, pimu = PI * mu;
+    const double fact = (fabs(pimu) < EPS) ? 1.0 : pimu / sin(pimu);
+    double d = -log(x2);
+    double e = mu * d;
+    const double fact2 = (fabs(e) < EPS) ? 1.0 : sinh(e) / e;
+    double gam1, gam2, gampl, gammi;
+    temme_gammas(mu, &gam1, &gam2, &gampl, &gammi);
+    double ff = fact * (gam1 * cosh(e) + gam2 * fact2 * d);
+    double sum = ff;
+    e = exp(e);
+    double p = 0.5 * e / gampl, q = 0.5 / (e * gammi);
+    double c = 1.0;
+    d = x2 * x2;
+    double sum1 = p;
+    for (int i = 1; i <= 500; ++i) {
+      ff = (i * ff + p + q) / (i * (double)i - mu2);
+      c *= d / i;
+      p /= (i - mu);
+      q /= (i + mu);
+      const double del = c * ff;
+      sum += del;
+      sum1 += c * (p - i * ff);
+      if (fabs(del) < fabs(sum) * EPS) break;
+    }
+    rkmu = sum;
+    rk1 = sum1 * xi2;
+  } else {
+    double b = 2.0 * (1.0 + x), d = 1.0 / b, h = d, delh = d;
+    double q1 = 0.0, q2 = 1.0;
+    const double a1 = 0.25 - mu2;
+    double q = a1, c = a1, a = -a1;
+    double s = 1.0 + q * delh;
+    for (int i = 2; i <= 500; ++i) {
+      a -= 2 * (i - 1);
+      c = -a * c / i;
+      const double qnew = (q1 - b * q2) / a;
+      q1 = q2;
+      q2 = qnew;
+      q += c * qnew;
+      b += 2.0;
+      d = 1.0 / (b + a * d);
+      delh = (b * d - 1.0) * delh;
+      h += delh;
+      const double dels = q * delh;
+      s += dels;
+      if (fabs(dels / s) < EPS) break;
+    }
+    h = a1 * h;
+    rkmu = sqrt(PI / (2.0 * x)) * exp(-x) / s;
+    rk1 = rkmu * (mu + x + 0.5 - h) * xi;
+  }
+  for (int i = 1; i <= nl; ++i) {
+    const double t = (mu + i) * xi2 * rk1 + rkmu;
+    rkmu = rk1;
+    rk1 = t;
+  }
+  return rkmu;
+}
+
+__host__ __device__ inline double matern_corr(double d, double phi, double nu) {
+  const double x = d * phi;
+  if (!(x > 0.0)) return 1.0;
+  return pow(x, nu) / (pow(2.0, nu - 1.0) * tgamma(nu)) * bessel_k(x, nu);
+}
+
+__host__ __device__ inline double correlation(double d, double phi, double nu, int model) {
+  return (model == MK_COV_EXPONENTIAL) ? exp(-phi * d) : matern_corr(d, phi, nu);
+}
+
+__host__ __device__ inline double dist2d(double x0, double y0, double x1, double y1) {
+  const double dx = x0 - x1, dy = y0 - y1;
+  return sqrt(dx * dx + dy * dy);
+}
+
+}  // namespace mk

@@ -1,0 +1,148 @@
+// Batched fp64 128x128 tile GEMM on CDNA4 MFMA (v_mfma_f64_16x16x4_f64).
+//
+// One 256-thread workgroup (4 waves, 2x2) owns one 128x128 output tile; each
+// wave owns a 64x64 quadrant = 4x4 MFMA blocks (64 fp64 accumulators/lane).
+// K is streamed in chunks of 16 through LDS ([k][m] images, row stride 144
+// doubles so the two 16-lane halves of a ds_read_b64 group land on disjoint
+// banks), register-prefetching chunk c+1 while chunk c is multiplied.
+//
+// Operands are described by strides so that every product the Cholesky /
+// inverse / kriging code needs (NT, NN, TN) is the same kernel body:
+//   op(A)(m,k) = A[m + k*sA]  (A_MU)   or  A[m*sA + k]  (!A_MU)
+//   op(B)(k,n) = B[k*sB + n]  (B_NU)   or  B[k + n*sB]  (!B_NU)
+// The MFMA is issued with (B-fragment, A-fragment) so the accumulator holds
+// C^T: lane l, register r of block (bm,bn) is C[m = 16bm + (l&15)][n = 16bn +
+// (l>>4) + 4r] -- consecutive lanes walk consecutive rows of a column-major C
+// (coalesced 128-B stores) instead of consecutive columns.
+#pragma once
+#include "mk_common.hpp"
+
+namespace mk {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+typedef double d2 __attribute__((ext_vector_type(2)));
+
+constexpr int GB_K = 16;       // K chunk
+constexpr int GB_SM = 144;     // LDS row stride (doubles)
+constexpr int GB_LDS_DOUBLES = 2 * GB_K * GB_SM;
+
+struct Acc {
+  d4 v[4][4];
+};
+
+__device__ inline void acc_zero(Acc& a) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) a.v[i][j] = (d4){0.0, 0.0, 0.0, 0.0};
+}
+
+// Load one 128 x 16 chunk of op(X) into registers (8 doubles per thread).
+// `kvalid`: elements with chunk-relative k >= kvalid are zero (K masking).
+template <bool MU>
+__device__ inline void load_chunk(const double* __restrict__ X, long s, int k0, int kvalid, d2 (&r)[4]) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int e = t + 256 * i;
+    if (MU) {
+      const int k = e >> 6, m = (e & 63) * 2;
+      r[i] = (k < kvalid) ? *reinterpret_cast<const d2*>(X + m + (long)(k0 + k) * s) : (d2){0.0, 0.0};
+    } else {
+      const int k = (e & 7) * 2, m = e >> 3;
+      d2 v = *reinterpret_cast<const d2*>(X + (long)m * s + k0 + k);
+      if (k >= kvalid) v.x = 0.0;
+      if (k + 1 >= kvalid) v.y = 0.0;
+      r[i] = v;
+    }
+  }
+}
+
+template <bool MU>
+__device__ inline void store_chunk(double* lds, const d2 (&r)[4]) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int e = t + 256 * i;
+    if (MU) {
+      const int k = e >> 6, m = (e & 63) * 2;
+      *reinterpret_cast<d2*>(lds + k * GB_SM + m) = r[i];
+    } else {
+      const int k = (e & 7) * 2, m = e >> 3;
+      lds[k * GB_SM + m] = r[i].x;
+      lds[(k + 1) * GB_SM + m] = r[i].y;
+    }
+  }
+}
+
+__device__ inline void mma_chunk(const double* As, const double* Bs, Acc& acc) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wm = w & 1, wn = w >> 1;
+  const int li = lane & 15, lk = lane >> 4;
+#pragma unroll
+  for (int ks = 0; ks < GB_K / 4; ++ks) {
+    double ya[4], xb[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      ya[b] = As[(ks * 4 + lk) * GB_SM + wm * 64 + b * 16 + li];
+      xb[b] = Bs[(ks * 4 + lk) * GB_SM + wn * 64 + b * 16 + li];
+    }
+#pragma unroll
+    for (int bm = 0; bm < 4; ++bm)
+#pragma unroll
+      for (int bn = 0; bn < 4; ++bn)
+        acc.v[bm][bn] = __builtin_amdgcn_mfma_f64_16x16x4f64(xb[bn], ya[bm], acc.v[bm][bn], 0, 0, 0);
+  }
+}
+
+// acc += op(A)[128 x K] * op(B)[K x 128], K % 16 == 0; rows/cols beyond kvalid_total zeroed.
+template <bool A_MU, bool B_NU>
+__device__ inline void gemm_128(const double* __restrict__ A, long sA, const double* __restrict__ B, long sB,
+                                int K, int kvalid_total, Acc& acc, double* lds) {
+  double* As = lds;
+  double* Bs = lds + GB_K * GB_SM;
+  d2 ra[4], rb[4];
+  if (K <= 0) return;
+  load_chunk<A_MU>(A, sA, 0, kvalid_total, ra);
+  load_chunk<B_NU>(B, sB, 0, kvalid_total, rb);
+  for (int kc = 0; kc < K; kc += GB_K) {
+    __syncthreads();
+    store_chunk<A_MU>(As, ra);
+    store_chunk<B_NU>(Bs, rb);
+    __syncthreads();
+    if (kc + GB_K < K) {
+      load_chunk<A_MU>(A, sA, kc + GB_K, kvalid_total - (kc + GB_K), ra);
+      load_chunk<B_NU>(B, sB, kc + GB_K, kvalid_total - (kc + GB_K), rb);
+    }
+    mma_chunk(As, Bs, acc);
+  }
+}
+
+// Element coordinates of accumulator (bm,bn,r) for this lane.
+__device__ inline int acc_row(int bm) {
+  const int lane = threadIdx.x & 63, wm = (threadIdx.x >> 6) & 1;
+  return wm * 64 + bm * 16 + (lane & 15);
+}
+__device__ inline int acc_col(int bn, int r) {
+  const int lane = threadIdx.x & 63, wn = threadIdx.x >> 7;
+  return wn * 64 + bn * 16 + (lane >> 4) + 4 * r;
+}
+
+// C = alpha*acc + beta*C (column-major, ldc); optional mirrored store C^T at Ct.
+__device__ inline void store_tile(double* C, long ldc, const Acc& acc, double alpha, double beta,
+                                  double* Ct = nullptr) {
+#pragma unroll
+  for (int bm = 0; bm < 4; ++bm)
+#pragma unroll
+    for (int bn = 0; bn < 4; ++bn)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = acc_row(bm), n = acc_col(bn, r);
+        double* p = C + m + (long)n * ldc;
+        const double v = (beta == 0.0) ? alpha * acc.v[bm][bn][r] : alpha * acc.v[bm][bn][r] + beta * (*p);
+        *p = v;
+        if (Ct) Ct[n + (long)m * ldc] = v;
+      }
+}
+
+}  // namespace mk

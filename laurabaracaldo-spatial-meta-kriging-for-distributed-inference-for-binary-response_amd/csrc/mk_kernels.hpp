@@ -1,0 +1,39 @@
+// Kernel declarations shared by the launch code (mk_api.hip).
+#pragma once
+#include "mk_types.hpp"
+
+namespace mk {
+// mk_linalg.hip
+__global__ void k_cov_candidate(Model md, MatSet ms, int h, int which, int iter);
+__global__ void k_chol_update(MatSet ms, int S, int h, int k);
+__global__ void k_chol_trsm(MatSet ms, int S, int h, int k);
+__global__ void k_chol_diag(MatSet ms, const int* n_s, int h, int k, double* ld_part, double* quad_c, int* info);
+__global__ void k_inv_copydiag(MatSet ms, const int* list, const int* count);
+__global__ void k_inv_T(MatSet ms, const int* list, const int* count, int d);
+__global__ void k_inv_D(MatSet ms, const int* list, const int* count, int d);
+__global__ void k_lauum(MatSet ms, const int* n_s, const int* list, const int* count);
+__global__ void k_gemv_refresh(Model md, MatSet ms, const int* list, const int* count);
+__global__ void k_gemv_G(Model md, MatSet ms);
+__global__ void k_pred_var(Model md, MatSet ms, const int* list, const int* count);
+__global__ void k_pred_var_reduce(Model md, int nt, const int* list, const int* count);
+// mk_mcmc.hip
+__global__ void k_beta(Model md, int iter);
+__global__ void k_Aphase(Model md, int iter);
+__global__ void k_theta_mh(Model md, MatSet ms, int h, int which, int iter);
+__global__ void k_dirty_list(Model md, int force, int* list, int* count);
+__global__ void k_sweep(Model md, MatSet ms, int iter);
+__global__ void k_record(Model md, int iter);
+__global__ void k_record_w(Model md, int iter);
+__global__ void k_adapt(Model md, int b);
+__global__ void k_pred_draw(Model md, int iter, int kidx);
+__global__ void k_quantiles(const double* data, long subset_stride, long row_stride, int n_rows, int n_cols,
+                            const double* probs, int n_probs, double* out);
+__global__ void k_combine(const double* grids, int K, long G, double* out);
+// mk_init.hip
+__global__ void k_init_state(Model md);
+__global__ void k_theta_init(Model md, MatSet ms, int h);
+__global__ void k_load_plain(MatSet ms, const double* A, int n, int S);
+__global__ void k_corr_plain(const double* coords, int S, int n, const double* phi, const double* nu, int model,
+                             double* out);
+__global__ void k_extract_L(MatSet ms, int n, int S, double* L, int inv_slot_mode);
+}  // namespace mk

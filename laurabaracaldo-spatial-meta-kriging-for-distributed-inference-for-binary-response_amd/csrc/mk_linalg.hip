@@ -1,0 +1,413 @@
+// Batched covariance assembly, blocked left-looking Cholesky and explicit
+// inverse for every (subset, outcome) correlation matrix on the GPU.
+//
+// Replaces the spBayes internals behind spMvGLM (MK.R:80-84): spCovLT-style
+// covariance assembly + LAPACK dpotrf/dpotri.
+//
+// Cholesky (lower, NB = 128, nt tiles per side), for panel k = 0..nt-1:
+//   k_chol_update : C(i,k) -= L(i,0:k) L(k,0:k)^T        for i >= k   (MFMA GEMM, K = 128k)
+//   k_chol_diag   : factor C(k,k) in LDS, invert it (Winv_k), logdet partial,
+//                   read the bordered row (quadratic form u' R^-1 u)
+//   k_chol_trsm   : L(i,k) = C(i,k) Winv_k^T                for i > k    (MFMA GEMM, K = 128)
+// Inverse of an accepted factor (X = L^-1 by diagonal distance d, then Q = X^T X):
+//   k_inv_copydiag (d=0), k_inv_T(d): X(k+d,k) = sum_j L(k+d,j) X(j,k);
+//   k_inv_D(d): X(k+d,k) = -Winv_{k+d} X(k+d,k);  k_lauum: Q(i,j) = sum_l X(l,i)^T X(l,j)
+#include "mk_gemm.hpp"
+#include "mk_types.hpp"
+#include "mk_corr.hpp"
+
+namespace mk {
+
+// ---------------------------------------------------------------- covariance
+// Candidate correlation matrix of outcome h for every subset, lower tiles only:
+//   R[i][j] = rho(|s_i - s_j|; phi', nu')  (i, j < n_s);  R[n_s][j] = u_h[j];  R[n_s][n_s] = 0;
+//   padding rows/cols: identity.  phi'/nu' = the Philox proposal of MH parameter j_mh.
+__device__ inline void candidate_theta(const Model& md, int s, int h, int which, int iter, double* phi, double* nu) {
+  const Key key = subset_key(md, s);
+  const double* th = md.theta + (long)s * md.n_theta;
+  const int idx_phi = md.ntri + h, idx_nu = md.ntri + md.q + h;
+  double tphi = th[idx_phi];
+  double tnu = (md.cov_model == MK_COV_MATERN) ? th[idx_nu] : 0.0;
+  if (which == 0 || which == 1) {   // which == 2: current values (initial factorisation)
+    const int j_mh = (which == 0) ? md.o_phi + h : md.o_nu + h;
+    const double z = proposal_normal(key, (uint32_t)j_mh, (uint32_t)iter);
+    const double step = exp(md.tune[(long)s * md.n_mh_max + j_mh]) * z;
+    if (which == 0) tphi += step; else tnu += step;
+  }
+  *phi = logit_inv(tphi, md.phi_a[h], md.phi_b[h]);
+  *nu = (md.cov_model == MK_COV_MATERN) ? logit_inv(tnu, md.nu_a[h], md.nu_b[h]) : 0.0;
+}
+
+__global__ __launch_bounds__(256) void k_cov_candidate(Model md, MatSet ms, int h, int which, int iter) {
+  const int ntiles = ms.nt * (ms.nt + 1) / 2;
+  const int s = blockIdx.x / ntiles;
+  int t = blockIdx.x % ntiles;
+  int ti = 0;
+  while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
+  const int tj = t - ti * (ti + 1) / 2;
+  const int sh = s * md.q + h;
+  const int ns = md.n_s[s];
+  double phi, nu;
+  candidate_theta(md, s, h, which, iter, &phi, &nu);
+  double* M = mat_slot(ms, sh, 1 - ms.cur[sh]);
+  const long ld = ms.ld;
+  const double* cx = md.coords + (long)s * 2 * md.n_pad;
+  const double* cy = cx + md.n_pad;
+  const double* uh = md.u + ((long)s * md.q + h) * md.n_pad;
+  const int r = threadIdx.x & 127;
+  const int R = ti * MK_NB + r;
+  const double xr = cx[R], yr = cy[R];
+  for (int cc = threadIdx.x >> 7; cc < MK_NB; cc += 2) {
+    const int C = tj * MK_NB + cc;
+    double v;
+    if (R < ns && C < ns) {
+      v = (R == C) ? 1.0 : correlation(dist2d(xr, yr, cx[C], cy[C]), phi, nu, md.cov_model);
+    } else if (R == ns && C < ns) {
+      v = uh[C];
+    } else {
+      v = (R == C && R != ns) ? 1.0 : 0.0;
+    }
+    M[R + (long)C * ld] = v;
+  }
+}
+
+// Plain matrix (no border) loaded by the host for the standalone Cholesky test path.
+
+// ---------------------------------------------------------------- Cholesky
+__global__ __launch_bounds__(256) void k_chol_update(MatSet ms, int S, int h, int k) {
+  __shared__ __attribute__((aligned(16))) double lds[GB_LDS_DOUBLES];
+  const int ntk = ms.nt - k;
+  const int s = blockIdx.x / ntk, i = k + blockIdx.x % ntk;
+  const int sh = s * ms.q + h;
+  double* M = mat_slot(ms, sh, 1 - ms.cur[sh]);
+  const long ld = ms.ld;
+  Acc acc;
+  acc_zero(acc);
+  gemm_128<true, true>(M + i * MK_NB, ld, M + k * MK_NB, ld, k * MK_NB, k * MK_NB, acc, lds);
+  store_tile(M + i * MK_NB + (long)k * MK_NB * ld, ld, acc, -1.0, 1.0);
+}
+
+__global__ __launch_bounds__(256) void k_chol_trsm(MatSet ms, int S, int h, int k) {
+  __shared__ __attribute__((aligned(16))) double lds[GB_LDS_DOUBLES];
+  const int ntk = ms.nt - k - 1;
+  const int s = blockIdx.x / ntk, i = k + 1 + blockIdx.x % ntk;
+  const int sh = s * ms.q + h;
+  const int slot = 1 - ms.cur[sh];
+  double* M = mat_slot(ms, sh, slot);
+  const double* W = winv_slot(ms, sh, slot, k);
+  const long ld = ms.ld;
+  double* C = M + i * MK_NB + (long)k * MK_NB * ld;
+  Acc acc;
+  acc_zero(acc);
+  gemm_128<true, true>(C, ld, W, MK_NB, MK_NB, MK_NB, acc, lds);
+  store_tile(C, ld, acc, 1.0, 0.0);
+}
+
+#define DLD 129
+// Factor + invert the 128x128 diagonal tile k of each candidate in LDS.
+// Row rb = n_s - 128k (if inside the tile) is the bordered row: its pivot is
+// -(u' R^-1 u) and it is not factored (pivot set to 1).
+__global__ __launch_bounds__(512) void k_chol_diag(MatSet ms, const int* __restrict__ n_s, int h, int k,
+                                                   double* ld_part, double* quad_c, int* info) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  double* T = sm;                    // [128 * DLD] col-major: T[r + c*DLD]
+  double* dg = sm + MK_NB * DLD;     // [128]
+  double* xd = dg + MK_NB;           // [128]
+  double* lg = xd + MK_NB;           // [128]
+  const int s = blockIdx.x, tid = threadIdx.x;
+  const int sh = s * ms.q + h;
+  const int slot = 1 - ms.cur[sh];
+  double* M = mat_slot(ms, sh, slot);
+  const long ld = ms.ld;
+  const int base = k * MK_NB;
+  const int ns = n_s[s];
+  const int rb = ns - base;
+  double* Mt = M + base + (long)base * ld;
+  for (int e = tid; e < MK_NB * MK_NB; e += 512) {
+    const int r = e & 127, c = e >> 7;
+    T[r + c * DLD] = (r >= c) ? Mt[r + (long)c * ld] : 0.0;
+  }
+  __syncthreads();
+  bool bad = false;
+  // ---- right-looking unblocked Cholesky
+  for (int j = 0; j < MK_NB; ++j) {
+    const double a = T[j + j * DLD];
+    const double d = (j == rb) ? 1.0 : sqrt(a);
+    if (tid == 0) {
+      dg[j] = d;
+      if (j == rb) quad_c[s] = -a;
+      else if (!(a > 0.0)) bad = true;
+    }
+    const double inv = 1.0 / d;
+    if (tid < MK_NB - 1 - j) T[(j + 1 + tid) + j * DLD] *= inv;
+    __syncthreads();
+    const int r = j + 1 + (tid & 127);
+    if (r < MK_NB) {
+      const double lr = T[r + j * DLD];
+      for (int c = j + 1 + (tid >> 7); c <= r; c += 4) T[r + c * DLD] -= lr * T[c + j * DLD];
+    }
+    __syncthreads();
+  }
+  // ---- logdet partial over valid rows
+  if (tid < MK_NB) lg[tid] = (base + tid < ns) ? 2.0 * log(dg[tid]) : 0.0;
+  __syncthreads();
+  if (tid == 0) {
+    double sum = 0.0;
+    for (int r = 0; r < MK_NB; ++r) sum += lg[r];
+    ld_part[(long)s * ms.nt + k] = sum;
+    if (bad) info[s] = 1;
+  }
+  // ---- X = L^-1: strictly-lower X[r][c] kept (transposed) in the upper triangle T[c + r*DLD]
+  for (int m = 0; m < MK_NB; ++m) {
+    const double im = 1.0 / dg[m];
+    if (tid == 0) xd[m] = im;
+    if (tid < m) T[tid + m * DLD] *= im;   // row m final: X[m][c] = cur[m][c] / L[m][m]
+    __syncthreads();
+    const int r = m + 1 + (tid & 127);
+    if (r < MK_NB) {
+      const double lrm = T[r + m * DLD];
+      for (int c = (tid >> 7); c <= m; c += 4) {
+        const double xmc = (c == m) ? im : T[c + m * DLD];
+        T[c + r * DLD] -= lrm * xmc;
+      }
+    }
+    __syncthreads();
+  }
+  // ---- write L tile (lower incl. diag) and Winv_k (lower, zero upper)
+  double* W = winv_slot(ms, sh, slot, k);
+  for (int e = tid; e < MK_NB * MK_NB; e += 512) {
+    const int r = e & 127, c = e >> 7;
+    if (r > c) {
+      Mt[r + (long)c * ld] = T[r + c * DLD];
+      W[r + c * MK_NB] = T[c + r * DLD];
+    } else if (r == c) {
+      Mt[r + (long)c * ld] = dg[r];
+      W[r + c * MK_NB] = xd[r];
+    } else {
+      W[r + c * MK_NB] = 0.0;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- inverse
+// Work lists: entries are sh = s*q + h of pairs whose factor changed.
+__global__ __launch_bounds__(256) void k_inv_copydiag(MatSet ms, const int* __restrict__ list, const int* __restrict__ count) {
+  const int e = blockIdx.x / ms.nt, k = blockIdx.x % ms.nt;
+  if (e >= *count) return;
+  const int sh = list[e];
+  const int cur = ms.cur[sh];
+  double* X = mat_slot(ms, sh, 1 - cur);
+  const double* W = winv_slot(ms, sh, cur, k);
+  const long ld = ms.ld;
+  double* Xt = X + k * MK_NB + (long)k * MK_NB * ld;
+  for (int t = threadIdx.x; t < MK_NB * MK_NB; t += 256) {
+    const int r = t & 127, c = t >> 7;
+    Xt[r + (long)c * ld] = W[r + c * MK_NB];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_inv_T(MatSet ms, const int* __restrict__ list, const int* __restrict__ count, int d) {
+  __shared__ __attribute__((aligned(16))) double lds[GB_LDS_DOUBLES];
+  const int ntd = ms.nt - d;
+  const int e = blockIdx.x / ntd, k = blockIdx.x % ntd;
+  if (e >= *count) return;
+  const int sh = list[e];
+  const int cur = ms.cur[sh];
+  const double* Lm = mat_slot(ms, sh, cur);
+  double* X = mat_slot(ms, sh, 1 - cur);
+  const long ld = ms.ld;
+  const int i = k + d;
+  Acc acc;
+  acc_zero(acc);
+  gemm_128<true, false>(Lm + i * MK_NB + (long)k * MK_NB * ld, ld, X + k * MK_NB + (long)k * MK_NB * ld, ld,
+                        d * MK_NB, d * MK_NB, acc, lds);
+  store_tile(X + i * MK_NB + (long)k * MK_NB * ld, ld, acc, 1.0, 0.0);
+}
+
+__global__ __launch_bounds__(256) void k_inv_D(MatSet ms, const int* __restrict__ list, const int* __restrict__ count, int d) {
+  __shared__ __attribute__((aligned(16))) double lds[GB_LDS_DOUBLES];
+  const int ntd = ms.nt - d;
+  const int e = blockIdx.x / ntd, k = blockIdx.x % ntd;
+  if (e >= *count) return;
+  const int sh = list[e];
+  const int cur = ms.cur[sh];
+  double* X = mat_slot(ms, sh, 1 - cur);
+  const long ld = ms.ld;
+  const int i = k + d;
+  double* C = X + i * MK_NB + (long)k * MK_NB * ld;
+  Acc acc;
+  acc_zero(acc);
+  gemm_128<true, false>(winv_slot(ms, sh, cur, i), MK_NB, C, ld, MK_NB, MK_NB, acc, lds);
+  store_tile(C, ld, acc, -1.0, 0.0);
+}
+
+// Q(i,j) = sum_{l >= i} X(l,i)^T X(l,j) over rows l < n_s only (drops the bordered row and padding).
+__global__ __launch_bounds__(256) void k_lauum(MatSet ms, const int* __restrict__ n_s, const int* __restrict__ list,
+                                               const int* __restrict__ count) {
+  __shared__ __attribute__((aligned(16))) double lds[GB_LDS_DOUBLES];
+  const int ntiles = ms.nt * (ms.nt + 1) / 2;
+  const int e = blockIdx.x / ntiles;
+  if (e >= *count) return;
+  int t = blockIdx.x % ntiles;
+  int i = 0;
+  while ((i + 1) * (i + 2) / 2 <= t) ++i;
+  const int j = t - i * (i + 1) / 2;
+  const int sh = list[e];
+  const int s = sh / ms.q;
+  const double* X = mat_slot(ms, sh, 1 - ms.cur[sh]);
+  double* Q = ms.Q + (long)sh * mat_elems(ms);
+  const long ld = ms.ld;
+  const int K = (ms.nt - i) * MK_NB;
+  const int kvalid = n_s[s] - i * MK_NB;
+  Acc acc;
+  acc_zero(acc);
+  if (kvalid > 0)
+    gemm_128<false, false>(X + i * MK_NB + (long)i * MK_NB * ld, ld, X + i * MK_NB + (long)j * MK_NB * ld, ld, K,
+                           kvalid, acc, lds);
+  double* C = Q + i * MK_NB + (long)j * MK_NB * ld;
+  double* Ct = (i != j) ? Q + j * MK_NB + (long)i * MK_NB * ld : nullptr;
+  store_tile(C, ld, acc, 1.0, 0.0, Ct);
+}
+
+// g_h = Q_h u_h for listed pairs (one wave per output row; Q symmetric so row i = column i).
+__global__ __launch_bounds__(256) void k_gemv_refresh(Model md, MatSet ms, const int* __restrict__ list,
+                                                      const int* __restrict__ count) {
+  const int rows_per_blk = 4;
+  const int nblk = md.n_pad / rows_per_blk;
+  const int e = blockIdx.x / nblk;
+  if (e >= *count) return;
+  const int sh = list[e];
+  const int s = sh / md.q, h = sh % md.q;
+  const int i = (blockIdx.x % nblk) * rows_per_blk + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const double* Qc = ms.Q + (long)sh * mat_elems(ms) + (long)i * ms.ld;
+  const double* uh = md.u + ((long)s * md.q + h) * md.n_pad;
+  const int ns = md.n_s[s];
+  double acc = 0.0;
+  for (int r = lane; r < ns; r += 64) acc += Qc[r] * uh[r];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if (lane == 0) md.g[((long)s * md.q + h) * md.n_pad + i] = (i < ns) ? acc : 0.0;
+}
+
+// G_{h,c} = Q_h u_c for every subset and every (h, c) (q > 1, start of the A phase).
+__global__ __launch_bounds__(256) void k_gemv_G(Model md, MatSet ms) {
+  const int rows_per_blk = 4;
+  const int nblk = md.n_pad / rows_per_blk;
+  const int sh = blockIdx.x / nblk;
+  const int s = sh / md.q, h = sh % md.q;
+  const int i = (blockIdx.x % nblk) * rows_per_blk + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const double* Qc = ms.Q + (long)sh * mat_elems(ms) + (long)i * ms.ld;
+  const int ns = md.n_s[s];
+  double acc[MK_QMAX] = {0.0, 0.0, 0.0, 0.0};
+  for (int r = lane; r < ns; r += 64) {
+    const double qv = Qc[r];
+    for (int c = 0; c < md.q; ++c) acc[c] += qv * md.u[((long)s * md.q + c) * md.n_pad + r];
+  }
+  for (int c = 0; c < md.q; ++c) {
+    double a = acc[c];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
+    if (lane == 0) md.G[(((long)s * md.q + h) * md.q + c) * md.n_pad + i] = (i < ns) ? a : 0.0;
+  }
+}
+
+// ---------------------------------------------------------------- kriging variance
+// For listed pairs: s_h(t) = || L_h^-1 rho_h(t) ||^2 over the n_s valid rows, with
+// X = L^-1 (free slot after the inverse) and rho generated on the fly.
+// Tile (row block i, test block tb): partial column sums of squares -> s_part[sh][i][t].
+__global__ __launch_bounds__(256) void k_pred_var(Model md, MatSet ms, const int* __restrict__ list,
+                                                  const int* __restrict__ count) {
+  __shared__ __attribute__((aligned(16))) double lds[GB_LDS_DOUBLES];
+  __shared__ double tx[MK_NB], ty[MK_NB], red[2][MK_NB];
+  const int per = ms.nt * md.ntt;
+  const int e = blockIdx.x / per;
+  if (e >= *count) return;
+  const int t_ = blockIdx.x % per;
+  const int i = t_ / md.ntt, tb = t_ % md.ntt;
+  const int sh = list[e];
+  const int s = sh / md.q, h = sh % md.q;
+  const int ns = md.n_s[s];
+  const double* X = mat_slot(ms, sh, 1 - ms.cur[sh]);
+  const long ld = ms.ld;
+  const double* th = md.theta + (long)s * md.n_theta;
+  const double phi = logit_inv(th[md.ntri + h], md.phi_a[h], md.phi_b[h]);
+  const double nu = (md.cov_model == MK_COV_MATERN) ? logit_inv(th[md.ntri + md.q + h], md.nu_a[h], md.nu_b[h]) : 0.0;
+  const double* cx = md.coords + (long)s * 2 * md.n_pad;
+  const double* cy = cx + md.n_pad;
+  if (threadIdx.x < MK_NB) {
+    tx[threadIdx.x] = md.coords_test[tb * MK_NB + threadIdx.x];
+    ty[threadIdx.x] = md.coords_test[md.n_test_pad + tb * MK_NB + threadIdx.x];
+  }
+  __syncthreads();
+  double* As = lds;
+  double* Bs = lds + GB_K * GB_SM;
+  Acc acc;
+  acc_zero(acc);
+  const int K = (i + 1) * MK_NB;   // X lower-triangular: columns > row block are zero
+  const double* A = X + i * MK_NB;
+  d2 ra[4];
+  load_chunk<true>(A, ld, 0, K, ra);
+  for (int kc = 0; kc < K; kc += GB_K) {
+    __syncthreads();
+    store_chunk<true>(As, ra);
+    // B chunk: op(B)(k, n) = rho(|obs_{kc+k} - test_n|), zero for obs >= n_s or test >= n_test
+    for (int q2 = threadIdx.x; q2 < GB_K * MK_NB; q2 += 256) {
+      const int k = q2 >> 7, n = q2 & 127;
+      const int o = kc + k;
+      const int tt = tb * MK_NB + n;
+      double v = 0.0;
+      if (o < ns && tt < md.n_test) v = correlation(dist2d(cx[o], cy[o], tx[n], ty[n]), phi, nu, md.cov_model);
+      Bs[k * GB_SM + n] = v;
+    }
+    __syncthreads();
+    if (kc + GB_K < K) load_chunk<true>(A, ld, kc + GB_K, K - (kc + GB_K), ra);
+    mma_chunk(As, Bs, acc);
+  }
+  // column sums of squares over valid rows
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w & 1;
+  double colsum[4][4];
+#pragma unroll
+  for (int bn = 0; bn < 4; ++bn)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      double v = 0.0;
+#pragma unroll
+      for (int bm = 0; bm < 4; ++bm) {
+        const int m = i * MK_NB + acc_row(bm);
+        const double x = acc.v[bm][bn][r];
+        v += (m < ns) ? x * x : 0.0;
+      }
+      // reduce over the 16 lanes sharing (lane >> 4)
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+      colsum[bn][r] = v;
+    }
+  __syncthreads();
+  if ((lane & 15) == 0) {
+#pragma unroll
+    for (int bn = 0; bn < 4; ++bn)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[wm][acc_col(bn, r)] = colsum[bn][r];
+  }
+  __syncthreads();
+  if (threadIdx.x < MK_NB) {
+    const int n = threadIdx.x;
+    md.s_part[((long)sh * ms.nt + i) * md.n_test_pad + tb * MK_NB + n] = red[0][n] + red[1][n];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_pred_var_reduce(Model md, int nt, const int* __restrict__ list,
+                                                         const int* __restrict__ count) {
+  const int per = md.n_test_pad / 256;
+  const int e = blockIdx.x / per;
+  if (e >= *count) return;
+  const int sh = list[e];
+  const int t = (blockIdx.x % per) * 256 + threadIdx.x;
+  double v = 0.0;
+  for (int i = 0; i < nt; ++i) v += md.s_part[((long)sh * nt + i) * md.n_test_pad + t];
+  md.s_pred[(long)sh * md.n_test_pad + t] = v;
+}
+
+}  // namespace mk

@@ -1,0 +1,92 @@
+// Device-resident state of one batch of subsets (one GPU's shard).
+//
+// HBM layout (S local subsets, q outcomes, n_pad = roundup(max n_s + 1, 128)):
+//   coords  [S][2][n_pad]            SoA x | y (padding 0)
+//   y, wt   [S][Np]                  Np = n_pad*q, location-major (i*q + a), padding 0
+//   X       [S][p][Np]               column-major design
+//   eta, w  [S][Np]
+//   L       [S*q][2][n_pad^2]        current / candidate lower Cholesky factors of R_h
+//                                    (row n_s of the candidate holds u_h: bordered solve)
+//   Winv    [S*q][2][nt][128^2]      inverses of the diagonal 128-tiles of each factor
+//   Q       [S*q][n_pad^2]           R_h^-1, full symmetric, column-major
+//   u, g    [S][q][n_pad]            u = (I (x) A^-1) w, g_h = Q_h u_h
+//   G       [S][q][q][n_pad]         G_{h,c} = Q_h u_c (q > 1 only)
+// All matrices of one (subset, outcome) pair are contiguous; every kernel finds
+// its pair from blockIdx and the cur[] slot table, so no host round trip is
+// needed between the steps of an iteration.
+#pragma once
+#include "mk_common.hpp"
+
+#define MK_QMAX 4
+
+namespace mk {
+
+struct Model {
+  int S, q, p, n_pad, Np, nt, ntri, n_theta, cov_model;
+  int o_A, o_phi, o_nu, o_w, n_mh_max;   // MH parameter offsets (spBayes order)
+  int n_batch, batch_length, n_samples, kept0, n_kept;
+  int n_test, n_test_pad, ntt;
+  int subset_base;                        // global index of local subset 0
+  uint64_t seed;
+  double accept_rate;
+  double phi_a[MK_QMAX], phi_b[MK_QMAX], nu_a[MK_QMAX], nu_b[MK_QMAX];
+  double iw_df, iw_S[MK_QMAX * MK_QMAX];
+  // data
+  const int* n_s;
+  const double* coords;
+  const double* y;
+  const double* wt;
+  const double* X;
+  const double* coords_test;   // [2][n_test_pad]
+  // state
+  double* beta;      // [S][p]
+  double* theta;     // [S][n_theta]: A lower-tri (log diag) | logit phi | logit nu
+  double* w;         // [S][Np]
+  double* eta;       // [S][Np]
+  double* tune;      // [S][n_mh_max]  log proposal sd
+  double* acc;       // [S][n_mh_max]  accept counts within the current batch
+  double* u;         // [S][q][n_pad]
+  double* g;         // [S][q][n_pad]
+  double* G;         // [S][q][q][n_pad]
+  double* logdetR;   // [S][q]
+  double* quad;      // [S][q]      u_h' R_h^-1 u_h at the current state
+  double* A_full;    // [S][q*q]    current A (col-major)
+  double* Ainv;      // [S][q*q]
+  int* dirty;        // [S*q]
+  // candidate scratch
+  double* ld_part;   // [S][nt]     logdet partials of the candidate factor
+  double* quad_c;    // [S]
+  int* info;         // [S]
+  // sweep scratch
+  double* sw_delta;  // [S][Np]
+  double* sw_dll;    // [S][Np]
+  double* sw_logu;   // [S][Np]
+  int* sw_acc;       // [S][Np]
+  // outputs
+  double* samples;     // [S][n_samples][P]   reported columns beta | K | phi | nu
+  double* acc_hist;    // [S][n_batch][p+n_theta+1]  per-batch accept rates (last = mean over w)
+  double* w_samples;   // [S][n_samples][Np] or null
+  double* s_pred;      // [S][q][n_test_pad]  kriging variance reduction for the current (phi, nu)
+  double* s_part;      // [S*q][nt][n_test_pad]
+  double* w_pred;      // [S][n_kept][q*n_test]
+  int P;               // reported columns
+};
+
+struct MatSet {
+  double* L;
+  double* Winv;
+  double* Q;
+  int* cur;    // [S*q]
+  int ld, nt, q;
+};
+
+__device__ inline long mat_elems(const MatSet& m) { return (long)m.ld * m.ld; }
+__device__ inline double* mat_slot(const MatSet& m, int sh, int slot) {
+  return m.L + ((long)sh * 2 + slot) * mat_elems(m);
+}
+__device__ inline double* winv_slot(const MatSet& m, int sh, int slot, int k) {
+  return m.Winv + (((long)sh * 2 + slot) * m.nt + k) * (MK_NB * MK_NB);
+}
+__device__ inline Key subset_key(const Model& md, int s) { return make_key(md.seed, (uint32_t)(md.subset_base + s)); }
+
+}  // namespace mk

@@ -1,0 +1,132 @@
+"""Meta-kriging workflow around the device path (MetaKriging_BinaryResponse.R).
+
+  partition            MK.R:15-41   random split into n.core subsets (last takes the remainder)
+  partitioned_spMvGLM  MK.R:46-96   one subset: glm start values -> spMvGLM -> spPredict -> quantiles
+  meta_fit             MK.R:100-114 every subset of a shard at once on one GPU (replaces foreach %dopar%)
+  combine              MK.R:119-133 mean of the subsets' 200-quantile grids (device kernel)
+  posterior_summary    MK.R:136-165 interpolate to the 996-level grid, resample, p(y=1), summaries
+"""
+import numpy as np
+
+from .glm import glm_binomial
+from .session import SamplerConfig, Session, combine
+
+PROBS200 = None
+
+
+def r_seq(frm, to, by):
+    n = int((to - frm) / by + 1e-10)
+    x = frm + np.arange(n + 1, dtype=np.float64) * by
+    return np.minimum(x, to)
+
+
+PROBS200 = r_seq(0.005, 1.0, 0.005)     # MK.R:88
+XOUT996 = r_seq(0.005, 1.0, 0.001)      # MK.R:140
+
+
+def partition(n, n_core, seed=20250114):
+    """MK.R:15-41: n.part = c(rep(floor(n/K), K-1), remainder); random indices without replacement.
+
+    Returns (n_part, index_part) with 0-based index arrays.  R's sample() stream is
+    not reproduced (documented; a seeded permutation gives the same distribution)."""
+    per = n // n_core
+    n_part = [per] * (n_core - 1) + [n - per * (n_core - 1)]
+    perm = np.random.default_rng(seed).permutation(n)
+    idx, off = [], 0
+    for m in n_part:
+        idx.append(perm[off:off + m])
+        off += m
+    return np.array(n_part, dtype=np.int32), idx
+
+
+def subset_data(y, x, weight, coords, q, index):
+    """Y*.part / X*.part / coords.part for one subset (MK.R:33-39), stacked location-major."""
+    rows = (np.asarray(index)[:, None] * q + np.arange(q)[None, :]).reshape(-1)
+    w = np.broadcast_to(np.asarray(weight, float), (len(y),))
+    return dict(coords=np.asarray(coords, float)[index], y=np.asarray(y, float)[rows],
+                weights=np.ascontiguousarray(w[rows]), x=np.asarray(x, float)[rows])
+
+
+def default_config(q, p, beta_starting, beta_tuning, cov_model="exponential", n_batch=100, batch_length=50,
+                   seed=20250114, **kw):
+    """The worker's literal settings (MK.R:56-64, 83, 85)."""
+    return SamplerConfig(q, p, beta_starting, beta_tuning, cov_model=cov_model, n_batch=n_batch,
+                         batch_length=batch_length, accept_rate=0.43, seed=seed, **kw)
+
+
+def start_values(y, x, weight, q):
+    """MK.R:53-55 on the full data: beta.starting and the diagonal of t(chol(vcov))."""
+    n_tot = len(y)
+    wt = np.broadcast_to(np.asarray(weight, float), (n_tot,))
+    coef, vcov, bt = glm_binomial(y, x, wt)
+    return coef, bt
+
+
+def meta_fit(y, x, weight, coords, q, index_part, coords_test=None, cfg=None, subset_base=0, device=0,
+             cov_model="exponential", n_batch=100, batch_length=50, seed=20250114):
+    """All subsets of one shard on one GPU; returns the list `obj` of MK.R:108 for those subsets:
+    [{'parameters': 200 x P, 'w.predict': 200 x (q n_test)}, ...]."""
+    p = np.asarray(x).shape[1]
+    if cfg is None:
+        beta0, bt = start_values(y, x, weight, q)
+        cfg = default_config(q, p, beta0, bt, cov_model=cov_model, n_batch=n_batch, batch_length=batch_length,
+                             seed=seed)
+    subsets = [subset_data(y, x, weight, coords, q, idx) for idx in index_part]
+    with Session(subsets, cfg, coords_test=coords_test, subset_base=subset_base, device=device) as ses:
+        ses.run(cfg.n_samples)
+        out = ses.outputs()
+    res = []
+    for i in range(len(subsets)):
+        d = {"parameters": out["parameters"][i]}
+        if "w_predict" in out:
+            d["w.predict"] = out["w_predict"][i]
+        res.append(d)
+    return res
+
+
+def partitioned_spMvGLM(i, y, x, weight, n, q, n_part, coords_test, x_test, index_part, coords,
+                        cov_model="exponential", n_batch=100, batch_length=50, seed=20250114, device=0):
+    """MK.R:46-96 for subset i (1-based, as the reference): list(parameters, w.predict)."""
+    return meta_fit(y, x, weight, coords, q, [index_part[i - 1]], coords_test=coords_test, subset_base=i - 1,
+                    device=device, cov_model=cov_model, n_batch=n_batch, batch_length=batch_length, seed=seed)[0]
+
+
+def combine_results(obj, device=0):
+    """MK.R:123-133: result (200 x P) and result2 (200 x q n_test)."""
+    result = combine([o["parameters"] for o in obj], device=device)
+    result2 = combine([o["w.predict"] for o in obj], device=device) if "w.predict" in obj[0] else None
+    return result, result2
+
+
+def r_approx(xg, y, xout):
+    """stats::approx linear interpolation (MK.R:142), vectorised over columns of y."""
+    xg = np.asarray(xg, float)
+    idx = np.searchsorted(xg, xout, side="right") - 1
+    idx = np.clip(idx, 0, len(xg) - 2)
+    x0, x1 = xg[idx], xg[idx + 1]
+    y0, y1 = y[idx], y[idx + 1]
+    frac = ((xout - x0) / (x1 - x0))[:, None]
+    out = y0 + (y1 - y0) * frac
+    exact0 = (xout == x0)
+    exact1 = (xout == x1)
+    out[exact0] = y0[exact0]
+    out[exact1] = y1[exact1]
+    return out
+
+
+def posterior_summary(result, result2, x_test, q, samplesize=1000, seed=20250114):
+    """MK.R:136-165: interpolate both combined grids to Xout (996 levels), draw one shared
+    resample index vector (comonotone draws, MK.R:141), p(y=1) = logistic(x.test B + w),
+    and the median / 2.5% / 97.5% summaries."""
+    rng = np.random.default_rng(seed)
+    idx = rng.integers(0, len(XOUT996), size=samplesize)
+    inter = r_approx(PROBS200, result, XOUT996)
+    inter2 = r_approx(PROBS200, result2, XOUT996)
+    sample_par = inter[idx]
+    sample_w = inter2[idx]
+    p = np.asarray(x_test).shape[1]
+    eta = sample_par[:, :p] @ np.asarray(x_test, float).T + sample_w
+    p_sample = 1.0 / (1.0 + np.exp(-eta))
+    probs = np.array([0.5, 0.025, 0.975])
+    return dict(SamplePar=sample_par, Samplew=sample_w, p_sample=p_sample,
+                w_quant=np.quantile(sample_w, probs, axis=0), param_quant=np.quantile(sample_par, probs, axis=0))

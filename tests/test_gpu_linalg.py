@@ -1,0 +1,58 @@
+"""Device covariance / Cholesky / inverse vs independent scipy references (SURVEY.md 8c:
+covariance and Cholesky within 1e-10 relative error)."""
+import numpy as np
+import pytest
+import scipy.linalg as sla
+
+from oracle import spmvglm as om
+
+pytestmark = pytest.mark.gpu
+
+REL = 1e-10
+
+
+def _coords(S, n, seed):
+    return np.random.default_rng(seed).uniform(size=(S, n, 2))
+
+
+@pytest.mark.parametrize("model,nu", [("exponential", None), ("matern", [0.5, 1.3, 0.21])])
+def test_correlation_matches_oracle(mk, model, nu):
+    S, n = 3, 200
+    c = _coords(S, n, 1)
+    phi = np.array([4.5, 7.0, 11.0])
+    R = mk.correlation_batched(c, phi, nu=nu, cov_model=model)
+    for s in range(S):
+        D = om.distance_matrix(c[s], c[s])
+        ref = om.correlation(D, phi[s], 0.0 if nu is None else nu[s], 1 if model == "matern" else 0)
+        np.fill_diagonal(ref, 1.0)
+        assert np.max(np.abs(R[s] - ref)) <= REL * np.max(np.abs(ref))
+
+
+@pytest.mark.parametrize("n", [1, 5, 127, 128, 200, 255, 256, 400, 700])
+def test_cholesky_logdet_inverse(mk, n):
+    S = 3
+    c = _coords(S, n, n)
+    A = np.stack([om.correlation(om.distance_matrix(c[s], c[s]), 4.0 + 3 * s, 0.0, 0) for s in range(S)])
+    L, ld, inv = mk.cholesky_batched(A, inverse=True)
+    for s in range(S):
+        Lr = sla.cholesky(A[s], lower=True)
+        assert np.linalg.norm(L[s] - Lr) <= REL * np.linalg.norm(Lr)
+        ldr = 2.0 * np.sum(np.log(np.diag(Lr)))
+        assert abs(ld[s] - ldr) <= REL * max(1.0, abs(ldr))
+        Ir = om.cho_inverse(Lr)
+        assert np.linalg.norm(inv[s] - Ir) <= 1e-9 * np.linalg.norm(Ir)
+
+
+def test_cholesky_rejects_non_pd(mk):
+    A = np.eye(4)[None].copy()
+    A[0, 3, 3] = -1.0
+    with pytest.raises(mk.MkError):
+        mk.cholesky_batched(A)
+
+
+def test_combine_is_sequential_mean(mk):
+    rng = np.random.default_rng(3)
+    grids = [rng.normal(size=(200, 7)) for _ in range(13)]
+    out = mk.combine(grids)
+    ref = om.combine_mean(grids)
+    assert np.array_equal(out, ref)          # same summation order -> bit identical

@@ -1,0 +1,71 @@
+"""Short-horizon replay: the device chain vs the CPU oracle on identical inputs and
+identical Philox draws.  Every accept/reject decision must agree (samples equal to
+fp rounding, tolerance 1e-8 absolute on O(1) parameters); kriging draws and the
+200-level quantile grids likewise.  Quantiles of identical inputs are bit-exact."""
+import numpy as np
+import pytest
+
+from oracle import spmvglm as om
+from oracle.rstats import PROBS200, r_quantile7
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-8
+
+
+def _run_both(mk, n, q, cov, n_test=12, n_batch=3, batch_length=4, burn_in=7, seed=9, subset_base=0, S=2):
+    d = mk.synthetic.generate(n * S, q=q, n_test=n_test, seed=seed + q, cov_model=cov)
+    p = 2 * q
+    kw = dict(n_batch=n_batch, batch_length=batch_length, burn_in=burn_in, seed=seed)
+    cfg = mk.SamplerConfig(q, p, beta_starting=np.zeros(p), beta_tuning=np.full(p, 0.05),
+                           cov_model="matern" if cov else "exponential", **kw)
+    ocfg = om.Config(q, p, beta_starting=np.zeros(p), beta_tuning=np.full(p, 0.05), cov_model=cov, **kw)
+    subs = []
+    for s in range(S):
+        sl = slice(s * n, (s + 1) * n)
+        rows = slice(s * n * q, (s + 1) * n * q)
+        subs.append(dict(coords=d["coords"][sl], y=d["y"][rows], weights=np.ones(n * q), x=d["x"][rows]))
+    with mk.Session(subs, cfg, coords_test=d["coords_test"], subset_base=subset_base, record_w=True) as ses:
+        ses.run(cfg.n_samples)
+        dev = ses.outputs(samples=True, w_samples=True, w_pred_samples=True, acceptance=True)
+    refs = [om.fit_subset(sb["coords"], sb["y"], sb["weights"], sb["x"], ocfg, subset=subset_base + s,
+                          coords_test=d["coords_test"], record_w=True) for s, sb in enumerate(subs)]
+    return dev, refs
+
+
+@pytest.mark.parametrize("n,q,cov", [(150, 1, 0), (300, 1, 0), (64, 2, 0), (100, 1, 1), (40, 3, 0)])
+def test_replay_matches_oracle(mk, n, q, cov):
+    dev, refs = _run_both(mk, n, q, cov)
+    for s, ref in enumerate(refs):
+        np.testing.assert_allclose(dev["samples"][s], ref["samples"], rtol=0, atol=TOL)
+        np.testing.assert_allclose(dev["w_samples"][s].T, ref["w_samples"], rtol=0, atol=TOL)
+        np.testing.assert_allclose(dev["w_pred_samples"][s].T, ref["w_pred"], rtol=0, atol=TOL)
+        np.testing.assert_allclose(dev["parameters"][s], ref["param_q"], rtol=0, atol=TOL)
+        np.testing.assert_allclose(dev["w_predict"][s], ref["w_q"], rtol=0, atol=TOL)
+        # accept rates of beta / A / phi per batch
+        nrep = ref["accept"].shape[1]
+        o_w = dev["acceptance"][s].shape[1] - 1
+        np.testing.assert_allclose(dev["acceptance"][s][:, :o_w], ref["accept"][:, :o_w], atol=1e-12)
+
+
+def test_quantiles_bit_exact_on_device_samples(mk):
+    dev, _ = _run_both(mk, 130, 1, 0, n_batch=4, batch_length=5, burn_in=3)
+    for s in range(len(dev["samples"])):
+        kept = dev["samples"][s][2:]
+        assert np.array_equal(dev["parameters"][s], r_quantile7(kept, PROBS200, axis=0))
+        assert np.array_equal(dev["w_predict"][s], r_quantile7(dev["w_pred_samples"][s].T, PROBS200, axis=0))
+
+
+def test_subset_streams_independent_of_sharding(mk):
+    """Subset k's chain depends only on (seed, global subset index): sharding-invariant."""
+    d = mk.synthetic.generate(240, q=1, n_test=4, seed=2)
+    cfg = mk.SamplerConfig(1, 2, beta_starting=[0, 0], beta_tuning=[0.05, 0.05], n_batch=2, batch_length=3, burn_in=4)
+    subs = [dict(coords=d["coords"][i * 80:(i + 1) * 80], y=d["y"][i * 80:(i + 1) * 80], weights=np.ones(80),
+                 x=d["x"][i * 80:(i + 1) * 80]) for i in range(3)]
+    with mk.Session(subs, cfg, coords_test=d["coords_test"]) as ses:
+        ses.run(cfg.n_samples)
+        allq = ses.outputs()
+    with mk.Session(subs[2:], cfg, coords_test=d["coords_test"], subset_base=2) as ses:
+        ses.run(cfg.n_samples)
+        oneq = ses.outputs()
+    assert np.array_equal(allq["parameters"][2], oneq["parameters"][0])
+    assert np.array_equal(allq["w_predict"][2], oneq["w_predict"][0])
