@@ -1,0 +1,179 @@
+#!/usr/bin/env python3
+"""Benchmark: MCMC subset-iterations/s (all subsets, whole node) on BASELINE.json's
+headline configuration -- n=500,000 binary sites split into K=250 subsets of 2,000,
+exponential covariance, q=1, 1,000 kriging sites (configs[2]).
+
+A step = one spMvGLM amcmc iteration of EVERY subset (beta, A, phi MH with a fresh
+2000x2000 Cholesky per subset, inverse where phi moved, single-site w sweep) plus
+the fused spPredict kriging draw of that iteration -- the timed steps are kept
+(post-burn-in) iterations, the costlier kind.  Subsets are sharded over ranks
+(contiguous blocks, strong scaling: K=250 fixed); no data-path collective.
+
+  python bench.py --gpus N --steps K --warmup W
+"""
+import argparse
+import importlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+PKG = "laurabaracaldo-spatial-meta-kriging-for-distributed-inference-for-binary-response_amd"
+
+FP64_PEAK_TFLOPS = 78.6     # MI355X dense fp64 (vector = MFMA), AMD datasheet
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n", type=int, default=500_000)
+    ap.add_argument("--subsets", type=int, default=250)
+    ap.add_argument("--n-test", type=int, default=1000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-iters", type=int, default=6)
+    return ap.parse_args()
+
+
+# ------------------------------------------------------------------ CPU baseline (oracle, rank 0, N=1)
+def _cpu_worker(args):
+    n_s, iters, seed, idx = args
+    os.environ["OPENBLAS_NUM_THREADS"] = "1"
+    sys.path.insert(0, ROOT)
+    from oracle import spmvglm as om
+    syn = importlib.import_module(PKG + ".synthetic")
+    d = syn.generate(n_s, q=1, n_test=1000, seed=seed + idx)
+    cfg = om.Config(1, 2, beta_starting=[0.9, -0.9], beta_tuning=[0.01, 0.01], n_batch=100, batch_length=50,
+                    burn_in=2, seed=seed)
+    r = om.fit_subset(d["coords"], d["y"], np.ones(n_s), d["x"], cfg, subset=idx, coords_test=d["coords_test"],
+                      max_iter=iters, quantiles=False)
+    return r["loop_seconds"]       # the MCMC iterations only (set-up excluded, as on the GPU side)
+
+
+def cpu_baseline(n_s, iters, workers):
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    saved = {k: os.environ.get(k) for k in ("OPENBLAS_NUM_THREADS", "OMP_NUM_THREADS")}
+    os.environ["OPENBLAS_NUM_THREADS"] = os.environ["OMP_NUM_THREADS"] = "1"   # inherited by the spawned workers
+    t0 = time.perf_counter()
+    try:
+        with ctx.Pool(workers) as pool:
+            per = pool.map(_cpu_worker, [(n_s, iters, 7, i) for i in range(workers)])
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    wall = time.perf_counter() - t0
+    # rate over the slowest worker's iteration loop (set-up and interpreter start-up excluded)
+    rate = workers * iters / max(per)
+    return dict(value=rate, unit="subset-iters/s", cores=workers, kind="port",
+                sample=f"{workers} subsets x {iters} kept iterations (n_s={n_s}, 1000 kriging sites) of the same "
+                       f"workload, oracle/spmvglm.py (NumPy + OpenBLAS dpotrf/dpotri), one process and one BLAS "
+                       f"thread per core; wall {wall:.1f}s incl. start-up")
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    K, n, n_test = a.subsets, a.n, a.n_test
+
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        workers = max(1, min(16, os.cpu_count() or 1))
+        cpu = cpu_baseline(n // K, a.cpu_iters, workers)   # before any GPU initialisation (spawn pool)
+
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", rank=rank, world_size=world)
+
+    mk = importlib.import_module(PKG)
+    d = mk.synthetic.generate(n, q=1, n_test=n_test, seed=20250114)
+    n_part, idx = mk.partition(n, K, seed=20250114)
+    beta0, bt = mk.start_values(d["y"], d["x"], 1.0, 1)
+    per = (K + world - 1) // world
+    lo, hi = rank * per, min(K, (rank + 1) * per)
+    W = max(1, a.warmup)
+    # amcmc batches of 50 as MK.R:57-58; the chain is long enough for warmup + timed steps and
+    # every timed step is a kept (kriging) iteration: burn_in = W (1-based) -> kept0 = W - 1
+    n_batch = (W + a.steps + 49) // 50
+    cfg = mk.SamplerConfig(1, 2, beta0, bt, n_batch=n_batch, batch_length=50, burn_in=W, seed=20250114)
+    subs = [mk.subset_data(d["y"], d["x"], 1.0, d["coords"], 1, idx[i]) for i in range(lo, hi)]
+    ses = mk.Session(subs, cfg, coords_test=d["coords_test"], subset_base=lo, device=local if world > 1 else 0)
+    ses.run(W)                                    # warmup (the last one refreshes every factor for kriging)
+    ses.profile(True)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+            import torch
+            torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    ses.run(a.steps)                              # returns after the device is idle
+    t1 = time.perf_counter()
+    barrier()
+    elapsed = t1 - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    st = ses.kernel_stats(mk.session.KS_CHOL_UPDATE)
+    kern = {name: ses.kernel_stats(i) for name, i in
+            [("chol_update", 0), ("chol_diag", 1), ("chol_trsm", 2), ("w_sweep", 3), ("lauum", 4)]}
+    ses.close()
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+    value = K * a.steps / elapsed
+    avg_ms = st["ms"] / max(1, st["launches"])
+    achieved = st["flops"] / (st["ms"] * 1e-3) / 1e12 if st["ms"] > 0 else 0.0
+    out = {
+        "metric": "MCMC iters/sec (all subsets, whole node) + end-to-end wall-clock, n=500k K=250",
+        "value": value,
+        "unit": "subset-iters/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": W,
+        "ms_per_step": elapsed / a.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (seeded binary GP field, RFF, SURVEY.md 8d generator)",
+        "config": {"workload": f"configs[2]: n={n}, K={K} subsets of {n // K}, exponential, q=1, "
+                               f"n_test={n_test}, amcmc 100x50, kept iterations with fused kriging",
+                   "subsets_per_gpu": per, "parallelism": f"subset-sharded x{world}"},
+        "roofline": {"bound": "mfma", "kernel": "k_chol_update (left-looking Cholesky panel GEMM, fp64 MFMA)",
+                     "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None,
+                     "avg_launch_ms": avg_ms, "launches": st["launches"]},
+        "kernels_ms_per_step": {k: v["ms"] / a.steps for k, v in kern.items()},
+        "end_to_end_estimate_s": elapsed / a.steps * 5000,
+    }
+    if cpu is not None:
+        out["cpu_baseline"] = cpu
+        out["gpu_over_cpu"] = value / cpu["value"]
+    print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -284,6 +284,8 @@ def fit_subset(coords, y, wt, X, cfg, subset=0, coords_test=None, record_w=False
     w_pred = np.zeros((max(0, n_iter - kept0), q * n_test)) if n_test else None
     accept = np.zeros(n_mh)
 
+    import time as _time
+    t_loop = _time.perf_counter()
     for s in range(n_iter):
         b = s // cfg.batch_length
         # all proposal normals / accept draws for this iteration (one Philox call each)
@@ -426,7 +428,7 @@ def fit_subset(coords, y, wt, X, cfg, subset=0, coords_test=None, record_w=False
             accept[:] = 0.0
 
     out = dict(samples=samples, accept=acc_hist, tuning=tune, w_pred=w_pred,
-               beta=beta, A=A, w=w, n_iter=n_iter)
+               beta=beta, A=A, w=w, n_iter=n_iter, loop_seconds=_time.perf_counter() - t_loop)
     if record_w:
         out["w_samples"] = w_samples
     if quantiles and n_iter >= cfg.n_samples:

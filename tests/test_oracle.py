@@ -1,0 +1,169 @@
+"""Pin the CPU oracle before trusting it (no reference fixtures exist: SURVEY.md 4, 8c).
+
+* Philox4x32-10 vs the Random123 known-answer vectors.
+* R semantics (seq, type-7 quantile, approx, glm) vs independent numpy / scipy /
+  scikit-learn implementations.
+* The incremental sampler vs the literal spBayes-structured restatement
+  (full dense log-posterior recompute per proposal) on identical draws.
+* Statistical sanity: the posterior recovers the generating parameters.
+"""
+import importlib
+
+import numpy as np
+import pytest
+import scipy.linalg as sla
+import scipy.special as ssp
+
+from oracle import literal, philox, rstats
+from oracle import spmvglm as om
+
+syn = importlib.import_module(
+    "laurabaracaldo-spatial-meta-kriging-for-distributed-inference-for-binary-response_amd.synthetic")
+
+KAT = [((0, 0, 0, 0), (0, 0), (0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8)),
+       ((0xffffffff,) * 4, (0xffffffff,) * 2, (0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd)),
+       ((0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344), (0xa4093822, 0x299f31d0),
+        (0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1))]
+
+
+@pytest.mark.parametrize("ctr,key,expect", KAT)
+def test_philox_known_answers(ctr, key, expect):
+    out = philox.philox4x32_10(np.array(ctr, dtype=np.uint32), np.array(key, dtype=np.uint32))
+    assert tuple(int(x) for x in out) == expect
+
+
+def test_philox_uniform_and_normal_moments():
+    key = philox.make_key(123, 4)
+    u = philox.u01_open(*philox.philox4x32_10(philox._ctr(np.arange(200000), 3, 9, 0), key)[..., :2].T)
+    assert 0.0 < u.min() and u.max() < 1.0
+    assert abs(u.mean() - 0.5) < 3e-3
+    z = philox.proposal_normal(key, np.arange(200000), 7)
+    assert abs(z.mean()) < 0.01 and abs(z.std() - 1.0) < 0.01
+
+
+def test_r_seq_grids():
+    assert rstats.PROBS200.shape == (200,) and rstats.PROBS200[-1] == 1.0
+    assert rstats.XOUT996.shape == (996,) and rstats.XOUT996[-1] == 1.0
+    np.testing.assert_allclose(rstats.PROBS200, np.arange(1, 201) * 0.005, rtol=1e-15)
+
+
+@pytest.mark.parametrize("n", [1, 2, 7, 251, 1251])
+def test_quantile7_matches_numpy_linear(n):
+    x = np.random.default_rng(n).normal(size=(n, 3))
+    ours = rstats.r_quantile7(x, rstats.PROBS200, axis=0)
+    ref = np.quantile(x, rstats.PROBS200, axis=0, method="linear")
+    np.testing.assert_allclose(ours, ref, rtol=0, atol=1e-14)
+
+
+def test_quantile7_ties_use_low_order_statistic():
+    x = np.array([1.0, 1.0, 1.0, 2.0])
+    q = rstats.r_quantile7(x, np.array([0.3, 0.5, 1.0]))
+    assert q[0] == 1.0 and q[1] == 1.0 and q[2] == 2.0
+
+
+def test_approx_matches_interp():
+    xg = rstats.PROBS200
+    y = np.cumsum(np.random.default_rng(1).uniform(size=(200, 2)), axis=0)
+    ours = rstats.r_approx(xg, y, rstats.XOUT996)
+    for c in range(2):
+        np.testing.assert_allclose(ours[:, c], np.interp(rstats.XOUT996, xg, y[:, c]), rtol=1e-14, atol=1e-14)
+
+
+def test_glm_matches_sklearn_unpenalised():
+    from sklearn.linear_model import LogisticRegression
+    d = syn.generate(3000, q=1, n_test=0, seed=4)
+    coef, vcov = rstats.glm_binomial(d["y"], d["x"], np.ones(3000))
+    lr = LogisticRegression(penalty=None, fit_intercept=False, tol=1e-12, max_iter=1000).fit(d["x"], d["y"])
+    np.testing.assert_allclose(coef, lr.coef_[0], rtol=1e-6)
+    # vcov = inverse Fisher information; R takes the working weights of the last IRLS
+    # step (one step before the MLE), hence agreement to the convergence tolerance only
+    mu = 1 / (1 + np.exp(-d["x"] @ coef))
+    fisher = d["x"].T @ (d["x"] * (mu * (1 - mu))[:, None])
+    np.testing.assert_allclose(vcov, np.linalg.inv(fisher), rtol=1e-4)
+
+
+@pytest.mark.parametrize("nu", [0.3, 0.5, 1.0, 1.7])
+def test_matern_correlation(nu):
+    d = np.linspace(0.0, 1.2, 50)
+    r = om.correlation(d, 6.0, nu, om.COV_MATERN)
+    assert r[0] == 1.0
+    if nu == 0.5:
+        np.testing.assert_allclose(r, np.exp(-6.0 * d), rtol=1e-13)
+    x = 6.0 * d[1:]
+    np.testing.assert_allclose(r[1:], x ** nu / (2 ** (nu - 1) * ssp.gamma(nu)) * ssp.kv(nu, x), rtol=1e-14)
+
+
+def test_lmc_covariance_is_kronecker_structure():
+    c = np.random.default_rng(0).uniform(size=(9, 2))
+    A = np.array([[1.0, 0, 0], [-0.5, 1.0, 0], [0.25, 0.3, 0.8]])
+    C = om.lmc_covariance(c, A, [6.0, 4.0, 9.0], None, 0)
+    D = om.distance_matrix(c, c)
+    for i in range(9):
+        for j in range(9):
+            blk = C[i * 3:(i + 1) * 3, j * 3:(j + 1) * 3]
+            ref = sum(np.outer(A[:, h], A[:, h]) * np.exp(-[6.0, 4.0, 9.0][h] * D[i, j]) for h in range(3))
+            np.testing.assert_allclose(blk, ref, rtol=1e-14)
+
+
+@pytest.mark.parametrize("q,cov,n", [(1, 0, 10), (2, 0, 8), (1, 1, 9), (3, 0, 5)])
+def test_incremental_sampler_reproduces_literal_spbayes_loop(q, cov, n):
+    d = syn.generate(n, q=q, n_test=3, seed=3 + q, cov_model=cov)
+    p = 2 * q
+    cfg = om.Config(q, p, beta_starting=np.zeros(p), beta_tuning=np.full(p, 0.1), n_batch=3, batch_length=4,
+                    cov_model=cov, seed=7, burn_in=5)
+    a = om.fit_subset(d["coords"], d["y"], np.ones(n * q), d["x"], cfg, subset=1, record_w=True)
+    b = literal.fit_subset_literal(d["coords"], d["y"], np.ones(n * q), d["x"], cfg, subset=1)
+    np.testing.assert_allclose(a["samples"], b["samples"], rtol=0, atol=1e-10)
+    np.testing.assert_allclose(a["w"], b["params"][-n * q:], rtol=0, atol=1e-10)
+
+
+def test_kriging_moments_match_dense_conditional():
+    """spPredict per-site conditional: mean c'C^-1 w, var K - c'C^-1 c, from the structured formulas."""
+    rng = np.random.default_rng(5)
+    n, q = 30, 2
+    c = rng.uniform(size=(n, 2))
+    ct = rng.uniform(size=(4, 2))
+    A = np.array([[1.2, 0.0], [-0.4, 0.7]])
+    phi = [5.0, 9.0]
+    w = rng.normal(size=n * q)
+    C = om.lmc_covariance(c, A, phi, None, 0)
+    allc = np.vstack([c, ct])
+    Call = om.lmc_covariance(allc, A, phi, None, 0)
+    cross = Call[n * q:, :n * q]
+    Kt = Call[n * q:n * q + q, n * q:n * q + q]
+    mean_ref = cross @ np.linalg.solve(C, w)
+    Ainv = np.linalg.inv(A)
+    U = (Ainv @ w.reshape(n, q).T).T
+    Dt = om.distance_matrix(ct, c)
+    D = om.distance_matrix(c, c)
+    for t in range(4):
+        m, v = np.zeros(q), np.zeros(q)
+        for h in range(q):
+            R = np.exp(-phi[h] * D)
+            rho = np.exp(-phi[h] * Dt[t])
+            g = np.linalg.solve(R, U[:, h])
+            m[h] = rho @ g
+            v[h] = 1.0 - rho @ np.linalg.solve(R, rho)
+        np.testing.assert_allclose(A @ m, mean_ref[t * q:(t + 1) * q], rtol=1e-10)
+        cov_ref = Kt - cross[t * q:(t + 1) * q] @ np.linalg.solve(C, cross[t * q:(t + 1) * q].T)
+        np.testing.assert_allclose(A @ np.diag(v) @ A.T, cov_ref, rtol=1e-9, atol=1e-12)
+        # A diag(sqrt v) is exactly the lower Cholesky factor of the conditional covariance
+        np.testing.assert_allclose(A @ np.diag(np.sqrt(v)), sla.cholesky(cov_ref, lower=True), rtol=1e-8)
+
+
+def test_posterior_recovers_truth():
+    d = syn.generate(300, q=1, n_test=0, seed=21)
+    coef, vcov = rstats.glm_binomial(d["y"], d["x"], np.ones(300))
+    cfg = om.Config(1, 2, beta_starting=coef, beta_tuning=np.linalg.cholesky(vcov), n_batch=40, batch_length=25,
+                    seed=3)
+    r = om.fit_subset(d["coords"], d["y"], np.ones(300), d["x"], cfg)
+    lo, hi = r["param_q"][4], r["param_q"][194]          # 2.5% / 97.5%
+    assert lo[1] <= -1.0 <= hi[1]                          # slope
+    assert cfg.phi_a[0] < r["samples"][:, 3].mean() < cfg.phi_b[0]
+    rate_w = r["accept"][-1, cfg.p + cfg.n_theta:].mean()
+    assert 0.25 < rate_w < 0.6                             # adaptation drives acceptance toward 0.43
+
+
+def test_combine_mean_sequential_order():
+    g = [np.full((2, 2), v) for v in (0.1, 0.2, 0.3)]
+    np.testing.assert_array_equal(om.combine_mean(g), ((g[0] + g[1]) + g[2]) / 3)
