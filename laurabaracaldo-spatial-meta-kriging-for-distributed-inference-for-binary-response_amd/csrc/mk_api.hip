@@ -62,8 +62,10 @@ struct mk_session {
   int S = 0, q = 1, p = 0, n_pad = 0, nt = 0, P = 0;
   int iter = 0;
   bool matern = false, record_samples = true, record_w = false;
-  int* d_list = nullptr;
+  int* d_list = nullptr;     // pairs whose factor changed (inverse work list)
   int* d_count = nullptr;
+  int* d_plist = nullptr;    // pairs needing a kriging refresh
+  int* d_pcount = nullptr;
   double* d_probs = nullptr;
   std::vector<int> n_part;
   std::vector<void*> allocs;
@@ -158,8 +160,8 @@ static void launch_cholesky(mk_session* s, int h, int S_launch) {
   }
 }
 
-// Inverse + g refresh (+ kriging variance on kept iterations) for the dirty list.
-static void launch_inverse(mk_session* s, int max_entries, bool pred) {
+// W = L^-1 for the changed factors, diagonal tiles of R^-1, z from the bordered row.
+static void launch_inverse(mk_session* s, int max_entries) {
   const int nt = s->nt;
   Model& md = s->md;
   hipLaunchKernelGGL(k_inv_copydiag, dim3(max_entries * nt), dim3(256), 0, s->stream, s->ms, s->d_list, s->d_count);
@@ -168,17 +170,23 @@ static void launch_inverse(mk_session* s, int max_entries, bool pred) {
     hipLaunchKernelGGL(k_inv_D, dim3(max_entries * (nt - d)), dim3(256), 0, s->stream, s->ms, s->d_list, s->d_count, d);
   }
   timed(s, KS_LAUUM, 0.0, [&] {
-    hipLaunchKernelGGL(k_lauum, dim3(max_entries * nt * (nt + 1) / 2), dim3(256), 0, s->stream, s->ms, md.n_s,
-                       s->d_list, s->d_count);
-  });
-  hipLaunchKernelGGL(k_gemv_refresh, dim3(max_entries * (s->n_pad / 4)), dim3(256), 0, s->stream, md, s->ms,
-                     s->d_list, s->d_count);
-  if (pred && md.n_test > 0) {
-    hipLaunchKernelGGL(k_pred_var, dim3(max_entries * nt * md.ntt), dim3(256), 0, s->stream, md, s->ms, s->d_list,
+    hipLaunchKernelGGL(k_qblocks, dim3(max_entries * nt), dim3(256), 0, s->stream, s->ms, md.n_s, s->d_list,
                        s->d_count);
-    hipLaunchKernelGGL(k_pred_var_reduce, dim3(max_entries * (md.n_test_pad / 256)), dim3(256), 0, s->stream, md, nt,
-                       s->d_list, s->d_count);
-  }
+  });
+  hipLaunchKernelGGL(k_take_border, dim3(max_entries * ((s->n_pad + 255) / 256)), dim3(256), 0, s->stream, md, s->ms,
+                     s->d_list, s->d_count);
+}
+
+// Kriging refresh (kept iterations): P^T, X = W P^T and s = |X_t|^2 for the pairs in the pred list.
+static void launch_pred_refresh(mk_session* s, int max_entries) {
+  Model& md = s->md;
+  if (md.n_test <= 0) return;
+  const int nt = s->nt;
+  hipLaunchKernelGGL(k_pred_PT, dim3(max_entries * md.n_pad), dim3(256), 0, s->stream, md, s->d_plist, s->d_pcount);
+  hipLaunchKernelGGL(k_pred_var, dim3(max_entries * nt * md.ntt), dim3(256), 0, s->stream, md, s->ms, s->d_plist,
+                     s->d_pcount);
+  hipLaunchKernelGGL(k_pred_var_reduce, dim3(max_entries * (md.n_test_pad / 256)), dim3(256), 0, s->stream, md, nt,
+                     s->d_plist, s->d_pcount);
 }
 
 static int run_iteration(mk_session* s) {
@@ -188,7 +196,7 @@ static int run_iteration(mk_session* s) {
   const bool kept = it >= md.kept0;
   hipLaunchKernelGGL(k_beta, dim3(S), dim3(256), 0, s->stream, md, it);
   if (q > 1)
-    hipLaunchKernelGGL(k_gemv_G, dim3(S * q * (s->n_pad / 4)), dim3(256), 0, s->stream, md, s->ms);
+    hipLaunchKernelGGL(k_trmv_Z, dim3(S * q * ((s->n_pad + 255) / 256)), dim3(256), 0, s->stream, md, s->ms);
   hipLaunchKernelGGL(k_Aphase, dim3(S), dim3(256), 0, s->stream, md, it);
   const int nkinds = s->matern ? 2 : 1;
   const int ntri_tiles = s->nt * (s->nt + 1) / 2;
@@ -198,11 +206,13 @@ static int run_iteration(mk_session* s) {
       launch_cholesky(s, h, S);
       hipLaunchKernelGGL(k_theta_mh, dim3((S + 63) / 64), dim3(64), 0, s->stream, md, s->ms, h, which, it);
     }
-  hipLaunchKernelGGL(k_dirty_list, dim3(1), dim3(256), 0, s->stream, md, (int)(it == md.kept0), s->d_list, s->d_count);
-  launch_inverse(s, S * q, kept);
-  const size_t sw_lds = (size_t)q * (64 * 64 + 64) * sizeof(double);
+  hipLaunchKernelGGL(k_dirty_list, dim3(1), dim3(256), 0, s->stream, md, (int)(it == md.kept0), s->d_list, s->d_count,
+                     s->d_plist, s->d_pcount);
+  launch_inverse(s, S * q);
+  if (kept) launch_pred_refresh(s, S * q);
+  const size_t sw_lds = (size_t)q * (64 * 64 + 2 * 64) * sizeof(double);
   timed(s, KS_SWEEP, 0.0, [&] {
-    hipLaunchKernelGGL(k_sweep, dim3(S), dim3(256), sw_lds, s->stream, md, s->ms, it);
+    hipLaunchKernelGGL(k_sweep, dim3(S), dim3(512), sw_lds, s->stream, md, s->ms, it);
   });
   if (s->record_samples) hipLaunchKernelGGL(k_record, dim3((S + 63) / 64), dim3(64), 0, s->stream, md, it);
   if (s->record_w) hipLaunchKernelGGL(k_record_w, dim3((md.Np + 255) / 256, S), dim3(256), 0, s->stream, md, it);
@@ -311,8 +321,8 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
   if ((rc = s->alloc(&md.beta, (size_t)S * p)) || (rc = s->alloc(&md.theta, (size_t)S * n_theta)) ||
       (rc = s->alloc(&md.w, (size_t)S * Np)) || (rc = s->alloc(&md.eta, (size_t)S * Np)) ||
       (rc = s->alloc(&md.tune, (size_t)S * n_mh_max)) || (rc = s->alloc(&md.acc, (size_t)S * n_mh_max)) ||
-      (rc = s->alloc(&md.u, (size_t)S * q * n_pad)) || (rc = s->alloc(&md.g, (size_t)S * q * n_pad)) ||
-      (rc = s->alloc(&md.G, (size_t)S * q * q * n_pad)) || (rc = s->alloc(&md.logdetR, (size_t)S * q)) ||
+      (rc = s->alloc(&md.u, (size_t)S * q * n_pad)) || (rc = s->alloc(&md.z, (size_t)S * q * n_pad)) ||
+      (rc = s->alloc(&md.Z, (size_t)S * q * q * n_pad)) || (rc = s->alloc(&md.logdetR, (size_t)S * q)) ||
       (rc = s->alloc(&md.quad, (size_t)S * q)) || (rc = s->alloc(&md.A_full, (size_t)S * q * q)) ||
       (rc = s->alloc(&md.Ainv, (size_t)S * q * q)) || (rc = s->alloc(&md.dirty, (size_t)S * q)) ||
       (rc = s->alloc(&md.ld_part, (size_t)S * nt)) || (rc = s->alloc(&md.quad_c, (size_t)S)) ||
@@ -324,14 +334,18 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
   if (s->record_w && (rc = s->alloc(&md.w_samples, (size_t)S * n_samples * Np))) return fail(rc);
   if ((rc = s->alloc(&md.s_pred, (size_t)S * q * n_test_pad)) ||
       (rc = s->alloc(&md.s_part, (size_t)S * q * nt * n_test_pad)) ||
+      (n_test > 0 && (rc = s->alloc(&md.PT, (size_t)S * q * n_pad * n_test_pad))) ||
+      (n_test > 0 && (rc = s->alloc(&md.XK, (size_t)S * q * n_pad * n_test_pad))) ||
       (rc = s->alloc(&md.w_pred, (size_t)S * n_kept * q * std::max(n_test, 1))))
     return fail(rc);
   MatSet& ms = s->ms;
   ms.ld = n_pad; ms.nt = nt; ms.q = q;
   if ((rc = s->alloc(&ms.L, (size_t)S * q * 2 * n_pad * n_pad)) ||
       (rc = s->alloc(&ms.Winv, (size_t)S * q * 2 * nt * MK_NB * MK_NB)) ||
-      (rc = s->alloc(&ms.Q, (size_t)S * q * n_pad * n_pad)) || (rc = s->alloc(&ms.cur, (size_t)S * q)) ||
+      (rc = s->alloc(&ms.W, (size_t)S * q * n_pad * n_pad)) ||
+      (rc = s->alloc(&ms.QB, (size_t)S * q * nt * MK_NB * MK_NB)) || (rc = s->alloc(&ms.cur, (size_t)S * q)) ||
       (rc = s->alloc(&s->d_list, (size_t)S * q)) || (rc = s->alloc(&s->d_count, 1)) ||
+      (rc = s->alloc(&s->d_plist, (size_t)S * q)) || (rc = s->alloc(&s->d_pcount, 1)) ||
       (rc = s->alloc(&s->d_probs, MK_N_LEVELS)))
     return fail(rc);
 
@@ -432,10 +446,10 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
   HIPCHK(hipMemsetAsync(md.info, 0, (size_t)S * 4, s->stream));
   HIPCHK(hipMemsetAsync(ms.cur, 0, (size_t)S * q * 4, s->stream));
   HIPCHK(hipMemsetAsync(md.u, 0, (size_t)S * q * n_pad * 8, s->stream));
-  HIPCHK(hipMemsetAsync(md.g, 0, (size_t)S * q * n_pad * 8, s->stream));
-  HIPCHK(hipMemsetAsync(md.G, 0, (size_t)S * q * q * n_pad * 8, s->stream));
+  HIPCHK(hipMemsetAsync(md.z, 0, (size_t)S * q * n_pad * 8, s->stream));
+  HIPCHK(hipMemsetAsync(md.Z, 0, (size_t)S * q * q * n_pad * 8, s->stream));
   HIPCHK(hipMemsetAsync(md.s_pred, 0, (size_t)S * q * n_test_pad * 8, s->stream));
-  HIPCHK(hipMemsetAsync(ms.Q, 0, (size_t)S * q * n_pad * n_pad * 8, s->stream));
+  HIPCHK(hipMemsetAsync(ms.W, 0, (size_t)S * q * n_pad * n_pad * 8, s->stream));
   {
     std::vector<double> probs(MK_N_LEVELS);
     // seq(0.005, 1, 0.005): from + (0:n)*by, pmin(x, to)  (MK.R:88)
@@ -445,7 +459,7 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
   HIPCHK(hipFuncSetAttribute((const void*)k_chol_diag, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (MK_NB * 129 + 3 * MK_NB) * 8));
   HIPCHK(hipFuncSetAttribute((const void*)k_sweep, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             q * (64 * 64 + 64) * 8));
+                             q * (64 * 64 + 2 * 64) * 8));
 
   // ---------------- initial state: eta, u, factor every R_h at the starting values, Q, g
   hipLaunchKernelGGL(k_init_state, dim3(S), dim3(256), 0, s->stream, md);
@@ -455,8 +469,9 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
     launch_cholesky(s, h, S);
     hipLaunchKernelGGL(k_theta_init, dim3((S + 63) / 64), dim3(64), 0, s->stream, md, ms, h);
   }
-  hipLaunchKernelGGL(k_dirty_list, dim3(1), dim3(256), 0, s->stream, md, 0, s->d_list, s->d_count);
-  launch_inverse(s, S * q, false);
+  hipLaunchKernelGGL(k_dirty_list, dim3(1), dim3(256), 0, s->stream, md, 0, s->d_list, s->d_count, s->d_plist,
+                     s->d_pcount);
+  launch_inverse(s, S * q);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(s->stream));
   s->stats[0] = Stat(); s->stats[1] = Stat(); s->stats[2] = Stat(); s->stats[4] = Stat();
@@ -658,8 +673,9 @@ extern "C" int mk_cholesky_batched(const double* A, int32_t S, int32_t n, double
       (rc = s->alloc(&md.info, S)) || (rc = s->alloc(&md.dirty, S)) || (rc = s->alloc(&ms.cur, S)) ||
       (rc = s->alloc(&md.logdetR, S)) || (rc = s->alloc(&md.quad, S)) ||
       (rc = s->alloc(&ms.L, (size_t)S * 2 * n_pad * n_pad)) || (rc = s->alloc(&ms.Winv, (size_t)S * 2 * nt * MK_NB * MK_NB)) ||
-      (rc = s->alloc(&ms.Q, (size_t)S * n_pad * n_pad)) || (rc = s->alloc(&s->d_list, S)) ||
-      (rc = s->alloc(&s->d_count, 1)) || (rc = s->alloc(&dA, (size_t)S * n * n)))
+      (rc = s->alloc(&ms.Q, (size_t)S * n_pad * n_pad)) || (rc = s->alloc(&ms.W, (size_t)S * n_pad * n_pad)) ||
+      (rc = s->alloc(&s->d_list, S)) || (rc = s->alloc(&s->d_count, 1)) || (rc = s->alloc(&s->d_plist, S)) ||
+      (rc = s->alloc(&s->d_pcount, 1)) || (rc = s->alloc(&dA, (size_t)S * n * n)))
     return fail(rc);
   md.n_s = d_ns;
   std::vector<int> hn(S, n);
@@ -697,7 +713,8 @@ extern "C" int mk_cholesky_batched(const double* A, int32_t S, int32_t n, double
     }
   }
   if (inv_out) {
-    hipLaunchKernelGGL(k_dirty_list, dim3(1), dim3(256), 0, s->stream, md, 1, s->d_list, s->d_count);
+    hipLaunchKernelGGL(k_dirty_list, dim3(1), dim3(256), 0, s->stream, md, 1, s->d_plist, s->d_pcount, s->d_list,
+                       s->d_count);
     const int ntiles = nt * (nt + 1) / 2;
     hipLaunchKernelGGL(k_inv_copydiag, dim3(S * nt), dim3(256), 0, s->stream, ms, s->d_list, s->d_count);
     for (int d = 1; d < nt; ++d) {

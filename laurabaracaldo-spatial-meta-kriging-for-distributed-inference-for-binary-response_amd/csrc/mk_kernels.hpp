@@ -12,15 +12,17 @@ __global__ void k_inv_copydiag(MatSet ms, const int* list, const int* count);
 __global__ void k_inv_T(MatSet ms, const int* list, const int* count, int d);
 __global__ void k_inv_D(MatSet ms, const int* list, const int* count, int d);
 __global__ void k_lauum(MatSet ms, const int* n_s, const int* list, const int* count);
-__global__ void k_gemv_refresh(Model md, MatSet ms, const int* list, const int* count);
-__global__ void k_gemv_G(Model md, MatSet ms);
+__global__ void k_qblocks(MatSet ms, const int* n_s, const int* list, const int* count);
+__global__ void k_take_border(Model md, MatSet ms, const int* list, const int* count);
+__global__ void k_trmv_Z(Model md, MatSet ms);
+__global__ void k_pred_PT(Model md, const int* list, const int* count);
 __global__ void k_pred_var(Model md, MatSet ms, const int* list, const int* count);
 __global__ void k_pred_var_reduce(Model md, int nt, const int* list, const int* count);
 // mk_mcmc.hip
 __global__ void k_beta(Model md, int iter);
 __global__ void k_Aphase(Model md, int iter);
 __global__ void k_theta_mh(Model md, MatSet ms, int h, int which, int iter);
-__global__ void k_dirty_list(Model md, int force, int* list, int* count);
+__global__ void k_dirty_list(Model md, int force, int* list_inv, int* count_inv, int* list_pred, int* count_pred);
 __global__ void k_sweep(Model md, MatSet ms, int iter);
 __global__ void k_record(Model md, int iter);
 __global__ void k_record_w(Model md, int iter);

@@ -9,9 +9,14 @@
 //   k_chol_diag   : factor C(k,k) in LDS, invert it (Winv_k), logdet partial,
 //                   read the bordered row (quadratic form u' R^-1 u)
 //   k_chol_trsm   : L(i,k) = C(i,k) Winv_k^T                for i > k    (MFMA GEMM, K = 128)
-// Inverse of an accepted factor (X = L^-1 by diagonal distance d, then Q = X^T X):
-//   k_inv_copydiag (d=0), k_inv_T(d): X(k+d,k) = sum_j L(k+d,j) X(j,k);
-//   k_inv_D(d): X(k+d,k) = -Winv_{k+d} X(k+d,k);  k_lauum: Q(i,j) = sum_l X(l,i)^T X(l,j)
+// Inverse of an accepted factor, W = L^-1 by diagonal distance d:
+//   k_inv_copydiag (d=0), k_inv_T(d): W(k+d,k) = sum_j L(k+d,j) W(j,k);
+//   k_inv_D(d): W(k+d,k) = -Winv_{k+d} W(k+d,k)
+// then the diagonal 128-tiles of R^-1 = W'W (k_qblocks) for the latent sweep;
+// the full W'W (k_lauum) only serves the parity-test entry point.
+// Kriging (kept iterations): P^T = rho(obs, test) materialised once per changed
+// (phi, nu) (k_pred_PT) and X = W P^T (k_pred_var, MFMA) give both the variance
+// reduction |X_t|^2 and, every kept iteration, the mean X_t . z.
 #include "mk_gemm.hpp"
 #include "mk_types.hpp"
 #include "mk_corr.hpp"
@@ -189,20 +194,19 @@ __global__ __launch_bounds__(512) void k_chol_diag(MatSet ms, const int* __restr
   }
 }
 
-// ---------------------------------------------------------------- inverse
-// Work lists: entries are sh = s*q + h of pairs whose factor changed.
+// ---------------------------------------------------------------- inverse (W = L^-1, persistent)
+__device__ inline double* wmat(const MatSet& ms, int sh) { return ms.W + (long)sh * mat_elems(ms); }
+
 __global__ __launch_bounds__(256) void k_inv_copydiag(MatSet ms, const int* __restrict__ list, const int* __restrict__ count) {
   const int e = blockIdx.x / ms.nt, k = blockIdx.x % ms.nt;
   if (e >= *count) return;
   const int sh = list[e];
-  const int cur = ms.cur[sh];
-  double* X = mat_slot(ms, sh, 1 - cur);
-  const double* W = winv_slot(ms, sh, cur, k);
+  const double* Wd = winv_slot(ms, sh, ms.cur[sh], k);
   const long ld = ms.ld;
-  double* Xt = X + k * MK_NB + (long)k * MK_NB * ld;
+  double* Wt = wmat(ms, sh) + k * MK_NB + (long)k * MK_NB * ld;
   for (int t = threadIdx.x; t < MK_NB * MK_NB; t += 256) {
     const int r = t & 127, c = t >> 7;
-    Xt[r + (long)c * ld] = W[r + c * MK_NB];
+    Wt[r + (long)c * ld] = Wd[r + c * MK_NB];
   }
 }
 
@@ -212,9 +216,8 @@ __global__ __launch_bounds__(256) void k_inv_T(MatSet ms, const int* __restrict_
   const int e = blockIdx.x / ntd, k = blockIdx.x % ntd;
   if (e >= *count) return;
   const int sh = list[e];
-  const int cur = ms.cur[sh];
-  const double* Lm = mat_slot(ms, sh, cur);
-  double* X = mat_slot(ms, sh, 1 - cur);
+  const double* Lm = mat_slot(ms, sh, ms.cur[sh]);
+  double* X = wmat(ms, sh);
   const long ld = ms.ld;
   const int i = k + d;
   Acc acc;
@@ -230,18 +233,29 @@ __global__ __launch_bounds__(256) void k_inv_D(MatSet ms, const int* __restrict_
   const int e = blockIdx.x / ntd, k = blockIdx.x % ntd;
   if (e >= *count) return;
   const int sh = list[e];
-  const int cur = ms.cur[sh];
-  double* X = mat_slot(ms, sh, 1 - cur);
+  double* X = wmat(ms, sh);
   const long ld = ms.ld;
   const int i = k + d;
   double* C = X + i * MK_NB + (long)k * MK_NB * ld;
   Acc acc;
   acc_zero(acc);
-  gemm_128<true, false>(winv_slot(ms, sh, cur, i), MK_NB, C, ld, MK_NB, MK_NB, acc, lds);
+  gemm_128<true, false>(winv_slot(ms, sh, ms.cur[sh], i), MK_NB, C, ld, MK_NB, MK_NB, acc, lds);
   store_tile(C, ld, acc, -1.0, 0.0);
 }
 
-// Q(i,j) = sum_{l >= i} X(l,i)^T X(l,j) over rows l < n_s only (drops the bordered row and padding).
+// Tiles (i,j), i >= j, of R^-1 = sum over rows l < n_s of W(l,i)^T W(l,j) (drops the bordered
+// row and the padding).  diag_only: tiles (i,i) into QB; otherwise the full symmetric Q.
+__device__ inline void wtw_tile(const MatSet& ms, int sh, int ns, int i, int j, Acc& acc, double* lds) {
+  const double* X = wmat(ms, sh);
+  const long ld = ms.ld;
+  const int K = (ms.nt - i) * MK_NB;
+  const int kvalid = ns - i * MK_NB;
+  acc_zero(acc);
+  if (kvalid > 0)
+    gemm_128<false, false>(X + i * MK_NB + (long)i * MK_NB * ld, ld, X + i * MK_NB + (long)j * MK_NB * ld, ld, K,
+                           kvalid, acc, lds);
+}
+
 __global__ __launch_bounds__(256) void k_lauum(MatSet ms, const int* __restrict__ n_s, const int* __restrict__ list,
                                                const int* __restrict__ count) {
   __shared__ __attribute__((aligned(16))) double lds[GB_LDS_DOUBLES];
@@ -253,119 +267,113 @@ __global__ __launch_bounds__(256) void k_lauum(MatSet ms, const int* __restrict_
   while ((i + 1) * (i + 2) / 2 <= t) ++i;
   const int j = t - i * (i + 1) / 2;
   const int sh = list[e];
-  const int s = sh / ms.q;
-  const double* X = mat_slot(ms, sh, 1 - ms.cur[sh]);
-  double* Q = ms.Q + (long)sh * mat_elems(ms);
-  const long ld = ms.ld;
-  const int K = (ms.nt - i) * MK_NB;
-  const int kvalid = n_s[s] - i * MK_NB;
   Acc acc;
-  acc_zero(acc);
-  if (kvalid > 0)
-    gemm_128<false, false>(X + i * MK_NB + (long)i * MK_NB * ld, ld, X + i * MK_NB + (long)j * MK_NB * ld, ld, K,
-                           kvalid, acc, lds);
-  double* C = Q + i * MK_NB + (long)j * MK_NB * ld;
+  wtw_tile(ms, sh, n_s[sh / ms.q], i, j, acc, lds);
+  const long ld = ms.ld;
+  double* Q = ms.Q + (long)sh * mat_elems(ms);
   double* Ct = (i != j) ? Q + j * MK_NB + (long)i * MK_NB * ld : nullptr;
-  store_tile(C, ld, acc, 1.0, 0.0, Ct);
+  store_tile(Q + i * MK_NB + (long)j * MK_NB * ld, ld, acc, 1.0, 0.0, Ct);
 }
 
-// g_h = Q_h u_h for listed pairs (one wave per output row; Q symmetric so row i = column i).
-__global__ __launch_bounds__(256) void k_gemv_refresh(Model md, MatSet ms, const int* __restrict__ list,
-                                                      const int* __restrict__ count) {
-  const int rows_per_blk = 4;
-  const int nblk = md.n_pad / rows_per_blk;
-  const int e = blockIdx.x / nblk;
+__global__ __launch_bounds__(256) void k_qblocks(MatSet ms, const int* __restrict__ n_s, const int* __restrict__ list,
+                                                 const int* __restrict__ count) {
+  __shared__ __attribute__((aligned(16))) double lds[GB_LDS_DOUBLES];
+  const int e = blockIdx.x / ms.nt, i = blockIdx.x % ms.nt;
+  if (e >= *count) return;
+  const int sh = list[e];
+  Acc acc;
+  wtw_tile(ms, sh, n_s[sh / ms.q], i, i, acc, lds);
+  store_tile(ms.QB + ((long)sh * ms.nt + i) * MK_NB * MK_NB, MK_NB, acc, 1.0, 0.0);
+}
+
+// z_h = border row of the accepted factor = L^-1 u_h (exact for the u_h the candidate was built with).
+__global__ __launch_bounds__(256) void k_take_border(Model md, MatSet ms, const int* __restrict__ list,
+                                                     const int* __restrict__ count) {
+  const int per = (md.n_pad + 255) / 256;
+  const int e = blockIdx.x / per;
   if (e >= *count) return;
   const int sh = list[e];
   const int s = sh / md.q, h = sh % md.q;
-  const int i = (blockIdx.x % nblk) * rows_per_blk + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  const double* Qc = ms.Q + (long)sh * mat_elems(ms) + (long)i * ms.ld;
-  const double* uh = md.u + ((long)s * md.q + h) * md.n_pad;
   const int ns = md.n_s[s];
-  double acc = 0.0;
-  for (int r = lane; r < ns; r += 64) acc += Qc[r] * uh[r];
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
-  if (lane == 0) md.g[((long)s * md.q + h) * md.n_pad + i] = (i < ns) ? acc : 0.0;
+  const int j = (blockIdx.x % per) * 256 + threadIdx.x;
+  if (j >= md.n_pad) return;
+  const double* M = mat_slot(ms, sh, ms.cur[sh]);
+  md.z[((long)s * md.q + h) * md.n_pad + j] = (j < ns) ? M[ns + (long)j * ms.ld] : 0.0;
 }
 
-// G_{h,c} = Q_h u_c for every subset and every (h, c) (q > 1, start of the A phase).
-__global__ __launch_bounds__(256) void k_gemv_G(Model md, MatSet ms) {
-  const int rows_per_blk = 4;
-  const int nblk = md.n_pad / rows_per_blk;
-  const int sh = blockIdx.x / nblk;
+// Z_{h,c} = W_h u_c for every subset, outcome h and c (q > 1, start of the A phase).
+__global__ __launch_bounds__(256) void k_trmv_Z(Model md, MatSet ms) {
+  const int per = (md.n_pad + 255) / 256;
+  const int sh = blockIdx.x / per;
   const int s = sh / md.q, h = sh % md.q;
-  const int i = (blockIdx.x % nblk) * rows_per_blk + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  const double* Qc = ms.Q + (long)sh * mat_elems(ms) + (long)i * ms.ld;
   const int ns = md.n_s[s];
+  const int r = (blockIdx.x % per) * 256 + threadIdx.x;
+  if (r >= md.n_pad) return;
+  const double* Wm = wmat(ms, sh);
+  const long ld = ms.ld;
+  const int q = md.q;
   double acc[MK_QMAX] = {0.0, 0.0, 0.0, 0.0};
-  for (int r = lane; r < ns; r += 64) {
-    const double qv = Qc[r];
-    for (int c = 0; c < md.q; ++c) acc[c] += qv * md.u[((long)s * md.q + c) * md.n_pad + r];
+  const int jmax = min(r + 1, ns);
+  for (int j = 0; j < jmax; ++j) {
+    const double wv = Wm[r + (long)j * ld];
+    for (int c = 0; c < q; ++c) acc[c] += wv * md.u[((long)s * q + c) * md.n_pad + j];
   }
-  for (int c = 0; c < md.q; ++c) {
-    double a = acc[c];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
-    if (lane == 0) md.G[(((long)s * md.q + h) * md.q + c) * md.n_pad + i] = (i < ns) ? a : 0.0;
+  for (int c = 0; c < q; ++c)
+    md.Z[(((long)s * q + h) * q + c) * md.n_pad + r] = (r < ns) ? acc[c] : 0.0;
+}
+
+// ---------------------------------------------------------------- kriging (kept iterations)
+__device__ inline void current_phi_nu(const Model& md, int s, int h, double* phi, double* nu) {
+  const double* th = md.theta + (long)s * md.n_theta;
+  *phi = logit_inv(th[md.ntri + h], md.phi_a[h], md.phi_b[h]);
+  *nu = (md.cov_model == MK_COV_MATERN) ? logit_inv(th[md.ntri + md.q + h], md.nu_a[h], md.nu_b[h]) : 0.0;
+}
+
+// P^T[k][t] = rho(|obs_k - test_t|) for the listed pairs (zero outside the valid block).
+__global__ __launch_bounds__(256) void k_pred_PT(Model md, const int* __restrict__ list, const int* __restrict__ count) {
+  const int per = md.n_pad;   // one block per observation row
+  const int e = blockIdx.x / per;
+  if (e >= *count) return;
+  const int k = blockIdx.x % per;
+  const int sh = list[e];
+  const int s = sh / md.q, h = sh % md.q;
+  const int ns = md.n_s[s];
+  double phi, nu;
+  current_phi_nu(md, s, h, &phi, &nu);
+  const double* cx = md.coords + (long)s * 2 * md.n_pad;
+  const double ox = cx[k], oy = cx[md.n_pad + k];
+  double* row = md.PT + ((long)sh * md.n_pad + k) * md.n_test_pad;
+  for (int t = threadIdx.x; t < md.n_test_pad; t += 256) {
+    double v = 0.0;
+    if (k < ns && t < md.n_test)
+      v = correlation(dist2d(ox, oy, md.coords_test[t], md.coords_test[md.n_test_pad + t]), phi, nu, md.cov_model);
+    row[t] = v;
   }
 }
 
-// ---------------------------------------------------------------- kriging variance
-// For listed pairs: s_h(t) = || L_h^-1 rho_h(t) ||^2 over the n_s valid rows, with
-// X = L^-1 (free slot after the inverse) and rho generated on the fly.
-// Tile (row block i, test block tb): partial column sums of squares -> s_part[sh][i][t].
+// X = W P^T (row tile i, test tile tb), stored column-major by test site (XK[t][row]);
+// partial column sums of squares over valid rows -> s_part[sh][i][t].
 __global__ __launch_bounds__(256) void k_pred_var(Model md, MatSet ms, const int* __restrict__ list,
                                                   const int* __restrict__ count) {
   __shared__ __attribute__((aligned(16))) double lds[GB_LDS_DOUBLES];
-  __shared__ double tx[MK_NB], ty[MK_NB], red[2][MK_NB];
+  __shared__ double red[2][MK_NB];
   const int per = ms.nt * md.ntt;
   const int e = blockIdx.x / per;
   if (e >= *count) return;
   const int t_ = blockIdx.x % per;
   const int i = t_ / md.ntt, tb = t_ % md.ntt;
   const int sh = list[e];
-  const int s = sh / md.q, h = sh % md.q;
+  const int s = sh / md.q;
   const int ns = md.n_s[s];
-  const double* X = mat_slot(ms, sh, 1 - ms.cur[sh]);
   const long ld = ms.ld;
-  const double* th = md.theta + (long)s * md.n_theta;
-  const double phi = logit_inv(th[md.ntri + h], md.phi_a[h], md.phi_b[h]);
-  const double nu = (md.cov_model == MK_COV_MATERN) ? logit_inv(th[md.ntri + md.q + h], md.nu_a[h], md.nu_b[h]) : 0.0;
-  const double* cx = md.coords + (long)s * 2 * md.n_pad;
-  const double* cy = cx + md.n_pad;
-  if (threadIdx.x < MK_NB) {
-    tx[threadIdx.x] = md.coords_test[tb * MK_NB + threadIdx.x];
-    ty[threadIdx.x] = md.coords_test[md.n_test_pad + tb * MK_NB + threadIdx.x];
-  }
-  __syncthreads();
-  double* As = lds;
-  double* Bs = lds + GB_K * GB_SM;
+  const double* Wm = wmat(ms, sh);
+  const double* PT = md.PT + (long)sh * md.n_pad * md.n_test_pad + tb * MK_NB;
   Acc acc;
   acc_zero(acc);
-  const int K = (i + 1) * MK_NB;   // X lower-triangular: columns > row block are zero
-  const double* A = X + i * MK_NB;
-  d2 ra[4];
-  load_chunk<true>(A, ld, 0, K, ra);
-  for (int kc = 0; kc < K; kc += GB_K) {
-    __syncthreads();
-    store_chunk<true>(As, ra);
-    // B chunk: op(B)(k, n) = rho(|obs_{kc+k} - test_n|), zero for obs >= n_s or test >= n_test
-    for (int q2 = threadIdx.x; q2 < GB_K * MK_NB; q2 += 256) {
-      const int k = q2 >> 7, n = q2 & 127;
-      const int o = kc + k;
-      const int tt = tb * MK_NB + n;
-      double v = 0.0;
-      if (o < ns && tt < md.n_test) v = correlation(dist2d(cx[o], cy[o], tx[n], ty[n]), phi, nu, md.cov_model);
-      Bs[k * GB_SM + n] = v;
-    }
-    __syncthreads();
-    if (kc + GB_K < K) load_chunk<true>(A, ld, kc + GB_K, K - (kc + GB_K), ra);
-    mma_chunk(As, Bs, acc);
-  }
-  // column sums of squares over valid rows
+  const int K = (i + 1) * MK_NB;   // W lower-triangular
+  gemm_128<true, true>(Wm + i * MK_NB, ld, PT, md.n_test_pad, K, K, acc, lds);
+  double* XK = md.XK + (long)sh * md.n_test_pad * md.n_pad + (long)tb * MK_NB * md.n_pad + i * MK_NB;
+  store_tile(XK, md.n_pad, acc, 1.0, 0.0);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w & 1;
   double colsum[4][4];
 #pragma unroll
@@ -379,7 +387,6 @@ __global__ __launch_bounds__(256) void k_pred_var(Model md, MatSet ms, const int
         const double x = acc.v[bm][bn][r];
         v += (m < ns) ? x * x : 0.0;
       }
-      // reduce over the 16 lanes sharing (lane >> 4)
 #pragma unroll
       for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
       colsum[bn][r] = v;

@@ -84,8 +84,8 @@ __global__ __launch_bounds__(256) void k_beta(Model md, int iter) {
 }
 
 // ---------------------------------------------------------------- 2. A entries
-// T[h][c][d] = u_c . G_{h,d}; every candidate's quadratic form is
-// sum_h sum_cd M_hc M_hd T_hcd with M = A'^-1 A_base (O(q^3) per proposal).
+// T[h][c][d] = u_c' R_h^-1 u_d = Z_{h,c} . Z_{h,d} (q = 1: |z|^2); every candidate's
+// quadratic form is sum_h sum_cd M_hc M_hd T_hcd with M = A'^-1 A_base (O(q^3) per proposal).
 __global__ __launch_bounds__(256) void k_Aphase(Model md, int iter) {
   __shared__ double red[8];
   __shared__ double T[MK_QMAX * MK_QMAX * MK_QMAX];
@@ -93,19 +93,18 @@ __global__ __launch_bounds__(256) void k_Aphase(Model md, int iter) {
   const int s = blockIdx.x, tid = threadIdx.x;
   const int q = md.q, ns = md.n_s[s];
   const Key key = subset_key(md, s);
-  const double* u = md.u + (long)s * q * md.n_pad;
-  double* g = md.g + (long)s * q * md.n_pad;
-  const double* G = md.G + (long)s * q * q * md.n_pad;
-  // ---- T
+  double* z = md.z + (long)s * q * md.n_pad;
+  const double* Z = md.Z + (long)s * q * q * md.n_pad;
+  // ---- T (symmetric in c,d)
   for (int h = 0; h < q; ++h)
     for (int c = 0; c < q; ++c)
-      for (int d = 0; d < q; ++d) {
-        const double* gv = (q == 1) ? g : G + ((long)h * q + d) * md.n_pad;
-        const double* uv = u + (long)c * md.n_pad;
+      for (int d = c; d < q; ++d) {
+        const double* zc = (q == 1) ? z : Z + ((long)h * q + c) * md.n_pad;
+        const double* zd = (q == 1) ? z : Z + ((long)h * q + d) * md.n_pad;
         double loc = 0.0;
-        for (int i = tid; i < ns; i += 256) loc += uv[i] * gv[i];
+        for (int i = tid; i < ns; i += 256) loc += zc[i] * zd[i];
         const double tot = block_sum<256>(loc, red);
-        if (tid == 0) T[(h * q + c) * q + d] = tot;
+        if (tid == 0) { T[(h * q + c) * q + d] = tot; T[(h * q + d) * q + c] = tot; }
       }
   __syncthreads();
   if (tid == 0) {
@@ -132,10 +131,10 @@ __global__ __launch_bounds__(256) void k_Aphase(Model md, int iter) {
     double f_cur = objective(Ab, Ai);
     for (int k = 0; k < md.ntri; ++k) {
       const int j = md.o_A + k;
-      const double z = proposal_normal(key, j, iter);
+      const double zz = proposal_normal(key, j, iter);
       const double lu = accept_log_uniform(key, j, iter);
       for (int m = 0; m < md.ntri; ++m) trc[m] = tri[m];
-      trc[k] += exp(md.tune[(long)s * md.n_mh_max + j]) * z;
+      trc[k] += exp(md.tune[(long)s * md.n_mh_max + j]) * zz;
       tri_to_A(trc, q, Ac);
       double Aic[16];
       const double f_c = objective(Ac, Aic);
@@ -162,7 +161,7 @@ __global__ __launch_bounds__(256) void k_Aphase(Model md, int iter) {
     }
   }
   __syncthreads();
-  // ---- u = A^-1 w, g_h = sum_c M_hc G_{h,c}
+  // ---- u = A^-1 w,  z_h = W_h u_h = sum_c M_hc Z_{h,c}
   const double* w = md.w + (long)s * md.Np;
   double* uw = md.u + (long)s * q * md.n_pad;
   for (int i = tid; i < ns; i += 256) {
@@ -171,19 +170,19 @@ __global__ __launch_bounds__(256) void k_Aphase(Model md, int iter) {
       for (int a = 0; a < q; ++a) uv += Aish[h + a * q] * w[i * q + a];
       uw[(long)h * md.n_pad + i] = uv;
       if (q == 1) {
-        g[i] = Msh[0] * g[i];
+        z[i] = Msh[0] * z[i];
       } else {
-        double gv = 0.0;
-        for (int c = 0; c < q; ++c) gv += Msh[h + c * q] * G[((long)h * q + c) * md.n_pad + i];
-        g[(long)h * md.n_pad + i] = gv;
+        double zv = 0.0;
+        for (int c = 0; c < q; ++c) zv += Msh[h + c * q] * Z[((long)h * q + c) * md.n_pad + i];
+        z[(long)h * md.n_pad + i] = zv;
       }
     }
   }
   __syncthreads();
-  // ---- current quadratic forms u_h . g_h for the phi / nu proposals
+  // ---- current quadratic forms |z_h|^2 = u_h' R_h^-1 u_h for the phi / nu proposals
   for (int h = 0; h < q; ++h) {
     double loc = 0.0;
-    for (int i = tid; i < ns; i += 256) loc += uw[(long)h * md.n_pad + i] * g[(long)h * md.n_pad + i];
+    for (int i = tid; i < ns; i += 256) loc += z[(long)h * md.n_pad + i] * z[(long)h * md.n_pad + i];
     const double tot = block_sum<256>(loc, red);
     if (tid == 0) md.quad[(long)s * q + h] = tot;
   }
@@ -220,40 +219,54 @@ __global__ __launch_bounds__(64) void k_theta_mh(Model md, MatSet ms, int h, int
   md.info[s] = 0;
 }
 
-// Compact list of (subset, outcome) pairs whose factor changed (deterministic order).
-__global__ __launch_bounds__(256) void k_dirty_list(Model md, int force, int* list, int* count) {
-  __shared__ int base;
-  if (threadIdx.x == 0) base = 0;
+// Compact lists (deterministic order) of (subset, outcome) pairs: list_inv = pairs whose
+// factor changed this iteration; list_pred = those, or every pair when `force` (first
+// kept iteration: kriging needs X for the current factors).
+__global__ __launch_bounds__(256) void k_dirty_list(Model md, int force, int* list_inv, int* count_inv,
+                                                    int* list_pred, int* count_pred) {
+  __shared__ int base[2];
+  __shared__ int wc[2][4];
+  if (threadIdx.x < 2) base[threadIdx.x] = 0;
   __syncthreads();
   const int n = md.S * md.q;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   for (int c0 = 0; c0 < n; c0 += 256) {
     const int e = c0 + threadIdx.x;
-    const int flag = (e < n) ? (force || md.dirty[e]) : 0;
-    // block prefix sum via ballot per wave + LDS
-    __shared__ int wc[4];
-    const unsigned long long bal = __ballot(flag);
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int before = __popcll(bal & ((1ull << lane) - 1ull));
-    if (lane == 0) wc[wv] = __popcll(bal);
+    const int d = (e < n) ? md.dirty[e] : 0;
+    const int flag[2] = {d, (e < n) ? (force || d) : 0};
+    int before[2];
+    for (int l = 0; l < 2; ++l) {
+      const unsigned long long bal = __ballot(flag[l]);
+      before[l] = __popcll(bal & ((1ull << lane) - 1ull));
+      if (lane == 0) wc[l][wv] = __popcll(bal);
+    }
     __syncthreads();
-    int off = base;
-    for (int k = 0; k < wv; ++k) off += wc[k];
-    if (flag) list[off + before] = e;
+    for (int l = 0; l < 2; ++l) {
+      int off = base[l];
+      for (int k = 0; k < wv; ++k) off += wc[l][k];
+      if (flag[l]) (l == 0 ? list_inv : list_pred)[off + before[l]] = e;
+    }
     if (e < n) md.dirty[e] = 0;
     __syncthreads();
-    if (threadIdx.x == 0) base += wc[0] + wc[1] + wc[2] + wc[3];
+    if (threadIdx.x < 2) base[threadIdx.x] += wc[threadIdx.x][0] + wc[threadIdx.x][1] + wc[threadIdx.x][2] + wc[threadIdx.x][3];
     __syncthreads();
   }
-  if (threadIdx.x == 0) *count = base;
+  if (threadIdx.x == 0) { *count_inv = base[0]; *count_pred = base[1]; }
 }
 
 // ---------------------------------------------------------------- 5. single-site w sweep
+// Sites in blocks of 64.  For block B: g_B = W[:,B]' z (dots over rows >= b0), then the
+// sequential MH steps inside the block use the 64x64 tile Q_BB of R^-1 (from QB) to carry
+// accepted moves forward (g_i += delta'_k Q_ik), then z += W[:,B] delta'_B (rows >= b0).
+// W panels are streamed twice per sweep (dots, update) -> n^2 doubles per subset per sweep.
 #define SW_B 64
-__global__ __launch_bounds__(256) void k_sweep(Model md, MatSet ms, int iter) {
+#define SW_T 512
+__global__ __launch_bounds__(SW_T) void k_sweep(Model md, MatSet ms, int iter) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int q = md.q;
-  double* Qb = smem;                              // [q][SW_B*SW_B] column-major blocks
-  double* dacc = smem + q * SW_B * SW_B;          // [q][SW_B]
+  double* Qb = smem;                              // [q][SW_B*SW_B] column-major
+  double* gb = smem + q * SW_B * SW_B;            // [q][SW_B]
+  double* dacc = gb + q * SW_B;                   // [q][SW_B]
   __shared__ int any_acc;
   __shared__ double Ai[MK_QMAX * MK_QMAX];
   const int s = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -268,35 +281,80 @@ __global__ __launch_bounds__(256) void k_sweep(Model md, MatSet ms, int iter) {
   double* dll = md.sw_dll + (long)s * md.Np;
   double* lgu = md.sw_logu + (long)s * md.Np;
   int* sacc = md.sw_acc + (long)s * md.Np;
-  double* g = md.g + (long)s * q * md.n_pad;
+  double* z = md.z + (long)s * q * md.n_pad;
   const double* tune = md.tune + (long)s * md.n_mh_max + md.o_w;
   if (tid < q * q) Ai[tid] = md.Ainv[(long)s * q * q + tid];
-  // ---- proposals, likelihood differences and accept draws: all independent of the sweep order
-  for (int k = tid; k < Ns; k += 256) {
+  // ---- proposals, likelihood differences and accept draws: independent of the sweep order
+  for (int k = tid; k < Ns; k += SW_T) {
     const int j = md.o_w + k;
-    const double z = proposal_normal(key, j, iter);
-    const double d = exp(tune[k]) * z;
+    const double zz = proposal_normal(key, j, iter);
+    const double d = exp(tune[k]) * zz;
     dl[k] = d;
     dll[k] = loglik_term(y[k], wt[k], eta[k] + d) - loglik_term(y[k], wt[k], eta[k]);
     lgu[k] = accept_log_uniform(key, j, iter);
     sacc[k] = 0;
   }
+  if (tid == 0) any_acc = 0;
   __syncthreads();
-  for (int b0 = 0; b0 < ns; b0 += SW_B) {
+  int p0 = 0, pnb = 0;
+  for (int b0 = 0; b0 < ns + SW_B; b0 += SW_B) {
     const int nb = min(SW_B, ns - b0);
+    // ---- (a) z += W[:, prev block] delta'_prev   (rows >= p0)
+    if (pnb > 0 && any_acc) {
+      for (int h = 0; h < q; ++h) {
+        const double* Wp = ms.W + ((long)s * q + h) * (ld * ld) + (long)p0 * ld;
+        const double* da = dacc + h * SW_B;
+        double* zh = z + (long)h * md.n_pad;
+        for (int r = p0 + tid; r < ns; r += SW_T) {
+          double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
+          int k = 0;
+          for (; k + 4 <= pnb; k += 4) {
+            v0 += Wp[r + (long)k * ld] * da[k];
+            v1 += Wp[r + (long)(k + 1) * ld] * da[k + 1];
+            v2 += Wp[r + (long)(k + 2) * ld] * da[k + 2];
+            v3 += Wp[r + (long)(k + 3) * ld] * da[k + 3];
+          }
+          for (; k < pnb; ++k) v0 += Wp[r + (long)k * ld] * da[k];
+          zh[r] += (v0 + v1) + (v2 + v3);
+        }
+      }
+    }
+    __syncthreads();
+    if (nb <= 0) break;
+    if (tid == 0) any_acc = 0;
+    // ---- (b) Q_BB tile into LDS, dots g_B = W[:,B]' z over rows >= b0
+    const int tile = b0 / MK_NB, off = b0 % MK_NB;
     for (int h = 0; h < q; ++h) {
-      const double* Qh = ms.Q + ((long)s * q + h) * (ld * ld);
-      for (int e = tid; e < SW_B * SW_B; e += 256) {
+      const double* QBt = ms.QB + (((long)s * q + h) * ms.nt + tile) * MK_NB * MK_NB;
+      for (int e = tid; e < SW_B * SW_B; e += SW_T) {
         const int r = e & (SW_B - 1), c = e / SW_B;
-        Qb[h * SW_B * SW_B + e] = (r < nb && c < nb) ? Qh[(b0 + r) + (long)(b0 + c) * ld] : 0.0;
+        Qb[h * SW_B * SW_B + e] = (r < nb && c < nb) ? QBt[(off + r) + (off + c) * MK_NB] : 0.0;
       }
       if (tid < SW_B) dacc[h * SW_B + tid] = 0.0;
+      const double* Wb = ms.W + ((long)s * q + h) * (ld * ld) + (long)b0 * ld;
+      const double* zh = z + (long)h * md.n_pad;
+      for (int i = wv; i < nb; i += SW_T / 64) {
+        const double* col = Wb + (long)i * ld;
+        double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+        int r = b0 + lane;
+        for (; r + 192 < ns; r += 256) {
+          a0 += col[r] * zh[r];
+          a1 += col[r + 64] * zh[r + 64];
+          a2 += col[r + 128] * zh[r + 128];
+          a3 += col[r + 192] * zh[r + 192];
+        }
+        for (; r < ns; r += 64) a0 += col[r] * zh[r];
+        double acc = (a0 + a1) + (a2 + a3);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+        if (lane == 0) gb[h * SW_B + i] = acc;
+      }
     }
-    if (tid == 0) any_acc = 0;
     __syncthreads();
+    // ---- (c) sequential Metropolis steps of the block (wave 0)
     if (wv == 0) {
       double gl[MK_QMAX];
-      for (int h = 0; h < q; ++h) gl[h] = (lane < nb) ? g[(long)h * md.n_pad + b0 + lane] : 0.0;
+      for (int h = 0; h < q; ++h) gl[h] = (lane < nb) ? gb[h * SW_B + lane] : 0.0;
       int anyl = 0;
       for (int i = 0; i < nb; ++i) {
         for (int a = 0; a < q; ++a) {
@@ -320,29 +378,16 @@ __global__ __launch_bounds__(256) void k_sweep(Model md, MatSet ms, int iter) {
           }
         }
       }
-      if (lane < nb)
-        for (int h = 0; h < q; ++h) g[(long)h * md.n_pad + b0 + lane] = gl[h];
       if (lane == 0) any_acc = anyl;
     }
     __syncthreads();
-    if (any_acc) {
-      for (int h = 0; h < q; ++h) {
-        const double* Qh = ms.Q + ((long)s * q + h) * (ld * ld) + (long)b0 * ld;
-        const double* da = dacc + h * SW_B;
-        for (int r = tid; r < ns; r += 256) {
-          if (r >= b0 && r < b0 + nb) continue;
-          double v = 0.0;
-          for (int i = 0; i < nb; ++i) v += Qh[r + (long)i * ld] * da[i];
-          g[(long)h * md.n_pad + r] += v;
-        }
-      }
-    }
-    __syncthreads();
+    p0 = b0;
+    pnb = nb;
   }
   // ---- apply accepted moves to w, eta, u and the batch accept counts
   double* u = md.u + (long)s * q * md.n_pad;
   double* acc = md.acc + (long)s * md.n_mh_max + md.o_w;
-  for (int i = tid; i < ns; i += 256) {
+  for (int i = tid; i < ns; i += SW_T) {
     for (int a = 0; a < q; ++a) {
       const int k = i * q + a;
       if (sacc[k]) {
@@ -405,7 +450,8 @@ __global__ __launch_bounds__(256) void k_adapt(Model md, int b) {
 }
 
 // ---------------------------------------------------------------- 7. kriging draw (kept iterations)
-// w*_t = A (m_t + diag(sqrt(1 - s_h(t))) z_t),  m_{t,h} = rho_h(t)' g_h  (spPredict, per-site marginal).
+// w*_t = A (m_t + diag(sqrt(1 - s_h(t))) z*_t),  m_{t,h} = rho_h(t)' R_h^-1 u_h = X_{h,t} . z_h
+// (spPredict per-site marginal; X_h = W_h P_h^T from the last (phi, nu) change).
 __global__ __launch_bounds__(256) void k_pred_draw(Model md, int iter, int kidx) {
   const int per = (md.n_test + 3) / 4;
   const int s = blockIdx.x / per;
@@ -413,21 +459,23 @@ __global__ __launch_bounds__(256) void k_pred_draw(Model md, int iter, int kidx)
   const int lane = threadIdx.x & 63;
   if (t >= md.n_test) return;
   const int q = md.q, ns = md.n_s[s];
-  const double* cx = md.coords + (long)s * 2 * md.n_pad;
-  const double* cy = cx + md.n_pad;
-  const double tx = md.coords_test[t], ty = md.coords_test[md.n_test_pad + t];
-  const double* th = md.theta + (long)s * md.n_theta;
   double mean[MK_QMAX], sd[MK_QMAX];
   for (int h = 0; h < q; ++h) {
-    const double phi = logit_inv(th[md.ntri + h], md.phi_a[h], md.phi_b[h]);
-    const double nu = (md.cov_model == MK_COV_MATERN) ? logit_inv(th[md.ntri + q + h], md.nu_a[h], md.nu_b[h]) : 0.0;
-    const double* gh = md.g + ((long)s * q + h) * md.n_pad;
-    double acc = 0.0;
-    for (int i = lane; i < ns; i += 64) acc += correlation(dist2d(tx, ty, cx[i], cy[i]), phi, nu, md.cov_model) * gh[i];
+    const long sh = (long)s * q + h;
+    const double* xk = md.XK + (sh * md.n_test_pad + t) * md.n_pad;
+    const double* zh = md.z + sh * md.n_pad;
+    double a0 = 0.0, a1 = 0.0;
+    int i = lane;
+    for (; i + 64 < ns; i += 128) {
+      a0 += xk[i] * zh[i];
+      a1 += xk[i + 64] * zh[i + 64];
+    }
+    for (; i < ns; i += 64) a0 += xk[i] * zh[i];
+    double acc = a0 + a1;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
     mean[h] = acc;
-    sd[h] = sqrt(fmax(1.0 - md.s_pred[((long)s * q + h) * md.n_test_pad + t], 0.0));
+    sd[h] = sqrt(fmax(1.0 - md.s_pred[sh * md.n_test_pad + t], 0.0));
   }
   if (lane == 0) {
     const Key key = subset_key(md, s);

@@ -5,12 +5,14 @@
 //   y, wt   [S][Np]                  Np = n_pad*q, location-major (i*q + a), padding 0
 //   X       [S][p][Np]               column-major design
 //   eta, w  [S][Np]
-//   L       [S*q][2][n_pad^2]        current / candidate lower Cholesky factors of R_h
-//                                    (row n_s of the candidate holds u_h: bordered solve)
+//   L       [S*q][2][n_pad^2]        accepted / candidate lower Cholesky factors of R_h
+//                                    (row n_s of a candidate holds u_h: bordered solve -> z)
 //   Winv    [S*q][2][nt][128^2]      inverses of the diagonal 128-tiles of each factor
-//   Q       [S*q][n_pad^2]           R_h^-1, full symmetric, column-major
-//   u, g    [S][q][n_pad]            u = (I (x) A^-1) w, g_h = Q_h u_h
-//   G       [S][q][q][n_pad]         G_{h,c} = Q_h u_c (q > 1 only)
+//   W       [S*q][n_pad^2]           W_h = L_h^-1 of the accepted factor (lower, column-major)
+//   QB      [S*q][nt][128^2]         diagonal 128-tiles of R_h^-1 = W'W (rows < n_s)
+//   u, z    [S][q][n_pad]            u = (I (x) A^-1) w, z_h = W_h u_h  (so u_h'R_h^-1 u_h = |z_h|^2)
+//   Z       [S][q][q][n_pad]         Z_{h,c} = W_h u_c (q > 1 only)
+//   PT, XK  [S*q][n_pad][n_test_pad] kriging: P^T = rho(obs, test) and X = W P^T
 // All matrices of one (subset, outcome) pair are contiguous; every kernel finds
 // its pair from blockIdx and the cur[] slot table, so no host round trip is
 // needed between the steps of an iteration.
@@ -46,8 +48,8 @@ struct Model {
   double* tune;      // [S][n_mh_max]  log proposal sd
   double* acc;       // [S][n_mh_max]  accept counts within the current batch
   double* u;         // [S][q][n_pad]
-  double* g;         // [S][q][n_pad]
-  double* G;         // [S][q][q][n_pad]
+  double* z;         // [S][q][n_pad]
+  double* Z;         // [S][q][q][n_pad]
   double* logdetR;   // [S][q]
   double* quad;      // [S][q]      u_h' R_h^-1 u_h at the current state
   double* A_full;    // [S][q*q]    current A (col-major)
@@ -68,6 +70,8 @@ struct Model {
   double* w_samples;   // [S][n_samples][Np] or null
   double* s_pred;      // [S][q][n_test_pad]  kriging variance reduction for the current (phi, nu)
   double* s_part;      // [S*q][nt][n_test_pad]
+  double* PT;          // [S*q][n_pad][n_test_pad]
+  double* XK;          // [S*q][n_test_pad][n_pad]  column t = W rho_t
   double* w_pred;      // [S][n_kept][q*n_test]
   int P;               // reported columns
 };
@@ -75,7 +79,9 @@ struct Model {
 struct MatSet {
   double* L;
   double* Winv;
-  double* Q;
+  double* W;   // [S*q][ld*ld] inverse factor (persistent)
+  double* Q;   // [S*q][ld*ld] full inverse (parity-test entry point only)
+  double* QB;  // [S*q][nt][128*128] diagonal tiles of the inverse
   int* cur;    // [S*q]
   int ld, nt, q;
 };
