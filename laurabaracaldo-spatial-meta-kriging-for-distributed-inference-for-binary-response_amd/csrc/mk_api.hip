@@ -131,7 +131,7 @@ static inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
 // ------------------------------------------------------------------ Cholesky of all candidates of outcome h
 static void launch_cholesky(mk_session* s, int h, int S_launch) {
   const int nt = s->nt;
-  const size_t diag_lds = (size_t)(MK_NB * 129 + 3 * MK_NB) * sizeof(double);
+  const size_t diag_lds = (size_t)(MK_NB * MK_NB + 2 * MK_NB + 4 * 256) * sizeof(double);
   Model& md = s->md;
   // valid extent (excludes padding) for the algorithmic flop count
   const double nv = (double)s->n_part[0] + 1.0;
@@ -147,7 +147,7 @@ static void launch_cholesky(mk_session* s, int h, int S_launch) {
       });
     }
     timed(s, KS_CHOL_DIAG, 0.0, [&] {
-      hipLaunchKernelGGL(k_chol_diag, dim3(S_launch), dim3(512), diag_lds, s->stream, s->ms, md.n_s, h, k, md.ld_part,
+      hipLaunchKernelGGL(k_chol_diag, dim3(S_launch), dim3(256), diag_lds, s->stream, s->ms, md.n_s, h, k, md.ld_part,
                          md.quad_c, md.info);
     });
     if (k < nt - 1) {
@@ -457,7 +457,7 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
     HIPCHK(hipMemcpy(s->d_probs, probs.data(), MK_N_LEVELS * 8, hipMemcpyHostToDevice));
   }
   HIPCHK(hipFuncSetAttribute((const void*)k_chol_diag, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (MK_NB * 129 + 3 * MK_NB) * 8));
+                             (MK_NB * MK_NB + 2 * MK_NB + 4 * 256) * 8));
   HIPCHK(hipFuncSetAttribute((const void*)k_sweep, hipFuncAttributeMaxDynamicSharedMemorySize,
                              q * (64 * 64 + 2 * 64) * 8));
 
@@ -684,7 +684,7 @@ extern "C" int mk_cholesky_batched(const double* A, int32_t S, int32_t n, double
       hipMemset(ms.cur, 0, S * 4) != hipSuccess || hipMemset(md.info, 0, S * 4) != hipSuccess)
     return fail(set_err(MK_E_HIP, "cholesky upload"));
   if (hipFuncSetAttribute((const void*)k_chol_diag, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (MK_NB * 129 + 3 * MK_NB) * 8) != hipSuccess)
+                          (MK_NB * MK_NB + 2 * MK_NB + 4 * 256) * 8) != hipSuccess)
     return fail(set_err(MK_E_HIP, "lds attribute"));
   hipLaunchKernelGGL(k_load_plain, dim3(2048), dim3(256), 0, s->stream, ms, dA, n, S);
   launch_cholesky(s, 0, S);

@@ -108,17 +108,168 @@ __global__ __launch_bounds__(256) void k_chol_trsm(MatSet ms, int S, int h, int 
   store_tile(C, ld, acc, 1.0, 0.0);
 }
 
-#define DLD 129
-// Factor + invert the 128x128 diagonal tile k of each candidate in LDS.
-// Row rb = n_s - 128k (if inside the tile) is the bordered row: its pivot is
-// -(u' R^-1 u) and it is not factored (pivot set to 1).
-__global__ __launch_bounds__(512) void k_chol_diag(MatSet ms, const int* __restrict__ n_s, int h, int k,
+// ---------------------------------------------------------------- diagonal tile: factor + invert in LDS
+// 128x128 tile T (column-major, ld 128) in LDS, 256 threads.  Blocked by 16:
+//   F1 (wave 0)  factor the 16x16 pivot block and invert it in registers (readlane only);
+//   F2 (MFMA)    panel below: P = C Dinv^T;   F3 (MFMA) trailing update T -= P P^T.
+// Inverse X = L^-1 by block rows: X_ij = -Dinv_i sum_k L_ik X_kj (MFMA, 16x16 blocks).
+// Storage: L in the lower triangle; X strictly-lower transposed into the upper triangle
+// (X[r][c] at T[c + r*128]); diag(L) in dg, diag(X) in xd.
+#define TLD 128
+
+__device__ inline double rlane(double v, int lane) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), lane);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+// D(16x16) += sum_k A(i,k) B(k,j); lane l, reg r holds D[(l>>4) + 4r][l&15].
+template <class FA, class FB>
+__device__ inline d4 mfma16(d4 acc, int K, FA fa, FB fb) {
+  const int l = threadIdx.x & 63;
+  for (int k0 = 0; k0 < K; k0 += 4) {
+    const double a = fa(l & 15, k0 + (l >> 4));
+    const double b = fb(k0 + (l >> 4), l & 15);
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+  }
+  return acc;
+}
+
+// X[r][c] (r >= c) of the inverse as stored during/after the inverse phase.
+__device__ inline double xget(const double* T, const double* xd, int r, int c) {
+  return (r > c) ? T[c + r * TLD] : ((r == c) ? xd[r] : 0.0);
+}
+
+__device__ void factor_invert_tile(double* T, double* dg, double* xd, double* Pb, int rb, double* quad_out,
+                                   bool* bad_out) {
+  const int tid = threadIdx.x, l = tid & 63, wv = tid >> 6;
+  bool bad = false;
+  // ================= factorisation
+  for (int p = 0; p < 8; ++p) {
+    const int b = 16 * p;
+    if (wv == 0) {
+      double row[16];
+#pragma unroll
+      for (int c = 0; c < 16; ++c) row[c] = (l < 16 && c <= l) ? T[(b + l) + (b + c) * TLD] : 0.0;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const double a = rlane(row[j], j);
+        double d;
+        if (b + j == rb) {
+          d = 1.0;
+          if (l == 0) *quad_out = -a;
+        } else {
+          d = sqrt(a);
+          bad |= !(a > 0.0);
+        }
+        const double inv = 1.0 / d;
+        row[j] = (l == j) ? d : ((l > j) ? row[j] * inv : row[j]);
+#pragma unroll
+        for (int c = j + 1; c < 16; ++c) {
+          const double lc = rlane(row[j], c);
+          if (l >= c) row[c] -= row[j] * lc;
+        }
+      }
+      // inverse of the pivot block, row l of Dinv in xr
+      double xr[16];
+#pragma unroll
+      for (int c = 0; c < 16; ++c) xr[c] = (c == l) ? 1.0 : 0.0;
+#pragma unroll
+      for (int m = 0; m < 16; ++m) {
+        const double dm = rlane(row[m], m);
+        const double idm = 1.0 / dm;
+        if (l == m) {
+#pragma unroll
+          for (int c = 0; c <= m; ++c) xr[c] *= idm;
+        }
+#pragma unroll
+        for (int c = 0; c <= m; ++c) {
+          const double xmc = rlane(xr[c], m);
+          if (l > m) xr[c] -= row[m] * xmc;
+        }
+      }
+      if (l < 16) {
+#pragma unroll
+        for (int c = 0; c < 16; ++c) {
+          if (c < l) {
+            T[(b + l) + (b + c) * TLD] = row[c];
+            T[(b + c) + (b + l) * TLD] = xr[c];     // Dinv strictly lower, transposed
+          }
+        }
+        dg[b + l] = row[l];
+        xd[b + l] = xr[l];
+      }
+    }
+    __syncthreads();
+    // ---- F2: panel rows below: P_R = C_R Dinv^T (in place), one 16-row block per wave round-robin
+    for (int R = p + 1 + wv; R < 8; R += 4) {
+      d4 acc = {0.0, 0.0, 0.0, 0.0};
+      acc = mfma16(acc, 16, [&](int i, int k) { return T[(16 * R + i) + (b + k) * TLD]; },
+                   [&](int k, int j) { return xget(T, xd, b + j, b + k); });
+#pragma unroll
+      for (int r = 0; r < 4; ++r) T[(16 * R + (l >> 4) + 4 * r) + (b + (l & 15)) * TLD] = acc[r];
+    }
+    __syncthreads();
+    // ---- F3: trailing blocks (R, C), p < C <= R: T_RC -= P_R P_C^T
+    {
+      const int nb = 7 - p;
+      const int nblk = nb * (nb + 1) / 2;
+      for (int t = wv; t < nblk; t += 4) {
+        int R = 0;
+        while ((R + 1) * (R + 2) / 2 <= t) ++R;
+        const int C = t - R * (R + 1) / 2;
+        const int RR = p + 1 + R, CC = p + 1 + C;
+        d4 acc;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[r] = T[(16 * RR + (l >> 4) + 4 * r) + (16 * CC + (l & 15)) * TLD];
+        acc = mfma16(acc, 16, [&](int i, int k) { return -T[(16 * RR + i) + (b + k) * TLD]; },
+                     [&](int k, int j) { return T[(16 * CC + j) + (b + k) * TLD]; });
+#pragma unroll
+        for (int r = 0; r < 4; ++r) T[(16 * RR + (l >> 4) + 4 * r) + (16 * CC + (l & 15)) * TLD] = acc[r];
+      }
+    }
+    __syncthreads();
+  }
+  if (l == 0 && wv == 0) *bad_out = bad;
+  // ================= inverse X = L^-1 (diagonal blocks = Dinv already in place)
+  for (int i = 1; i < 8; ++i) {
+    for (int Cb = wv; Cb < i; Cb += 4) {
+      d4 acc = {0.0, 0.0, 0.0, 0.0};
+      // S = sum_{K=Cb}^{i-1} L_iK X_K,Cb
+      acc = mfma16(acc, 16 * (i - Cb), [&](int r, int m) { return T[(16 * i + r) + (16 * Cb + m) * TLD]; },
+                   [&](int m, int c) { return xget(T, xd, 16 * Cb + m, 16 * Cb + c); });
+      double* S = Pb + wv * 256;       // wave-private 16x16 staging (column-major)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) S[((l >> 4) + 4 * r) + (l & 15) * 16] = acc[r];
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      d4 out = {0.0, 0.0, 0.0, 0.0};
+      out = mfma16(out, 16, [&](int r, int m) { return -xget(T, xd, 16 * i + r, 16 * i + m); },
+                   [&](int m, int c) { return S[m + c * 16]; });
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int rr = 16 * i + (l >> 4) + 4 * r, cc = 16 * Cb + (l & 15);
+        T[cc + rr * TLD] = out[r];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+  }
+}
+
+// Factor + invert the 128x128 diagonal tile k of each candidate.  Row rb = n_s - 128k
+// (if inside the tile) is the bordered row: its pivot is -(u' R^-1 u) and it is not
+// factored (pivot set to 1).
+__global__ __launch_bounds__(256) void k_chol_diag(MatSet ms, const int* __restrict__ n_s, int h, int k,
                                                    double* ld_part, double* quad_c, int* info) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
-  double* T = sm;                    // [128 * DLD] col-major: T[r + c*DLD]
-  double* dg = sm + MK_NB * DLD;     // [128]
-  double* xd = dg + MK_NB;           // [128]
-  double* lg = xd + MK_NB;           // [128]
+  double* T = sm;                      // [128*128]
+  double* dg = T + TLD * TLD;          // [128]
+  double* xd = dg + MK_NB;             // [128]
+  double* Pb = xd + MK_NB;             // [4][256]
+  __shared__ int badf;
   const int s = blockIdx.x, tid = threadIdx.x;
   const int sh = s * ms.q + h;
   const int slot = 1 - ms.cur[sh];
@@ -126,65 +277,33 @@ __global__ __launch_bounds__(512) void k_chol_diag(MatSet ms, const int* __restr
   const long ld = ms.ld;
   const int base = k * MK_NB;
   const int ns = n_s[s];
-  const int rb = ns - base;
   double* Mt = M + base + (long)base * ld;
-  for (int e = tid; e < MK_NB * MK_NB; e += 512) {
+  for (int e = tid; e < MK_NB * MK_NB; e += 256) {
     const int r = e & 127, c = e >> 7;
-    T[r + c * DLD] = (r >= c) ? Mt[r + (long)c * ld] : 0.0;
+    T[r + c * TLD] = (r >= c) ? Mt[r + (long)c * ld] : 0.0;
   }
+  if (tid == 0) badf = 0;
   __syncthreads();
   bool bad = false;
-  // ---- right-looking unblocked Cholesky
-  for (int j = 0; j < MK_NB; ++j) {
-    const double a = T[j + j * DLD];
-    const double d = (j == rb) ? 1.0 : sqrt(a);
-    if (tid == 0) {
-      dg[j] = d;
-      if (j == rb) quad_c[s] = -a;
-      else if (!(a > 0.0)) bad = true;
-    }
-    const double inv = 1.0 / d;
-    if (tid < MK_NB - 1 - j) T[(j + 1 + tid) + j * DLD] *= inv;
-    __syncthreads();
-    const int r = j + 1 + (tid & 127);
-    if (r < MK_NB) {
-      const double lr = T[r + j * DLD];
-      for (int c = j + 1 + (tid >> 7); c <= r; c += 4) T[r + c * DLD] -= lr * T[c + j * DLD];
-    }
-    __syncthreads();
-  }
-  // ---- logdet partial over valid rows
-  if (tid < MK_NB) lg[tid] = (base + tid < ns) ? 2.0 * log(dg[tid]) : 0.0;
+  factor_invert_tile(T, dg, xd, Pb, ns - base, quad_c + s, &bad);
+  if (bad) badf = 1;
   __syncthreads();
-  if (tid == 0) {
-    double sum = 0.0;
-    for (int r = 0; r < MK_NB; ++r) sum += lg[r];
-    ld_part[(long)s * ms.nt + k] = sum;
-    if (bad) info[s] = 1;
-  }
-  // ---- X = L^-1: strictly-lower X[r][c] kept (transposed) in the upper triangle T[c + r*DLD]
-  for (int m = 0; m < MK_NB; ++m) {
-    const double im = 1.0 / dg[m];
-    if (tid == 0) xd[m] = im;
-    if (tid < m) T[tid + m * DLD] *= im;   // row m final: X[m][c] = cur[m][c] / L[m][m]
-    __syncthreads();
-    const int r = m + 1 + (tid & 127);
-    if (r < MK_NB) {
-      const double lrm = T[r + m * DLD];
-      for (int c = (tid >> 7); c <= m; c += 4) {
-        const double xmc = (c == m) ? im : T[c + m * DLD];
-        T[c + r * DLD] -= lrm * xmc;
-      }
+  if (tid < 64) {
+    double v = 0.0;
+    for (int r = tid; r < MK_NB; r += 64) v += (base + r < ns) ? 2.0 * log(dg[r]) : 0.0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (tid == 0) {
+      ld_part[(long)s * ms.nt + k] = v;
+      if (badf) info[s] = 1;
     }
-    __syncthreads();
   }
-  // ---- write L tile (lower incl. diag) and Winv_k (lower, zero upper)
   double* W = winv_slot(ms, sh, slot, k);
-  for (int e = tid; e < MK_NB * MK_NB; e += 512) {
+  for (int e = tid; e < MK_NB * MK_NB; e += 256) {
     const int r = e & 127, c = e >> 7;
     if (r > c) {
-      Mt[r + (long)c * ld] = T[r + c * DLD];
-      W[r + c * MK_NB] = T[c + r * DLD];
+      Mt[r + (long)c * ld] = T[r + c * TLD];
+      W[r + c * MK_NB] = T[c + r * TLD];
     } else if (r == c) {
       Mt[r + (long)c * ld] = dg[r];
       W[r + c * MK_NB] = xd[r];
