@@ -79,20 +79,21 @@ __global__ __launch_bounds__(256) void k_cov_candidate(Model md, MatSet ms, int 
 // Plain matrix (no border) loaded by the host for the standalone Cholesky test path.
 
 // ---------------------------------------------------------------- Cholesky
-__global__ __launch_bounds__(256) void k_chol_update(MatSet ms, int S, int h, int k) {
+__global__ __launch_bounds__(256, 2) void k_chol_update(MatSet ms, int S, int h, int k) {
   __shared__ __attribute__((aligned(16))) double lds[GB_LDS_DOUBLES];
   const int ntk = ms.nt - k;
   const int s = blockIdx.x / ntk, i = k + blockIdx.x % ntk;
   const int sh = s * ms.q + h;
   double* M = mat_slot(ms, sh, 1 - ms.cur[sh]);
   const long ld = ms.ld;
+  double* C = M + i * MK_NB + (long)k * MK_NB * ld;
   Acc acc;
-  acc_zero(acc);
-  gemm_128<true, true>(M + i * MK_NB, ld, M + k * MK_NB, ld, k * MK_NB, k * MK_NB, acc, lds);
-  store_tile(M + i * MK_NB + (long)k * MK_NB * ld, ld, acc, -1.0, 1.0);
+  acc_load(acc, C, ld);
+  gemm_128<true, true, true>(M + i * MK_NB, ld, M + k * MK_NB, ld, k * MK_NB, k * MK_NB, acc, lds);
+  store_tile(C, ld, acc);
 }
 
-__global__ __launch_bounds__(256) void k_chol_trsm(MatSet ms, int S, int h, int k) {
+__global__ __launch_bounds__(256, 2) void k_chol_trsm(MatSet ms, int S, int h, int k) {
   __shared__ __attribute__((aligned(16))) double lds[GB_LDS_DOUBLES];
   const int ntk = ms.nt - k - 1;
   const int s = blockIdx.x / ntk, i = k + 1 + blockIdx.x % ntk;
@@ -105,7 +106,7 @@ __global__ __launch_bounds__(256) void k_chol_trsm(MatSet ms, int S, int h, int 
   Acc acc;
   acc_zero(acc);
   gemm_128<true, true>(C, ld, W, MK_NB, MK_NB, MK_NB, acc, lds);
-  store_tile(C, ld, acc, 1.0, 0.0);
+  store_tile(C, ld, acc);
 }
 
 // ---------------------------------------------------------------- diagonal tile: factor + invert in LDS
@@ -329,7 +330,7 @@ __global__ __launch_bounds__(256) void k_inv_copydiag(MatSet ms, const int* __re
   }
 }
 
-__global__ __launch_bounds__(256) void k_inv_T(MatSet ms, const int* __restrict__ list, const int* __restrict__ count, int d) {
+__global__ __launch_bounds__(256, 2) void k_inv_T(MatSet ms, const int* __restrict__ list, const int* __restrict__ count, int d) {
   __shared__ __attribute__((aligned(16))) double lds[GB_LDS_DOUBLES];
   const int ntd = ms.nt - d;
   const int e = blockIdx.x / ntd, k = blockIdx.x % ntd;
@@ -343,10 +344,10 @@ __global__ __launch_bounds__(256) void k_inv_T(MatSet ms, const int* __restrict_
   acc_zero(acc);
   gemm_128<true, false>(Lm + i * MK_NB + (long)k * MK_NB * ld, ld, X + k * MK_NB + (long)k * MK_NB * ld, ld,
                         d * MK_NB, d * MK_NB, acc, lds);
-  store_tile(X + i * MK_NB + (long)k * MK_NB * ld, ld, acc, 1.0, 0.0);
+  store_tile(X + i * MK_NB + (long)k * MK_NB * ld, ld, acc);
 }
 
-__global__ __launch_bounds__(256) void k_inv_D(MatSet ms, const int* __restrict__ list, const int* __restrict__ count, int d) {
+__global__ __launch_bounds__(256, 2) void k_inv_D(MatSet ms, const int* __restrict__ list, const int* __restrict__ count, int d) {
   __shared__ __attribute__((aligned(16))) double lds[GB_LDS_DOUBLES];
   const int ntd = ms.nt - d;
   const int e = blockIdx.x / ntd, k = blockIdx.x % ntd;
@@ -358,8 +359,8 @@ __global__ __launch_bounds__(256) void k_inv_D(MatSet ms, const int* __restrict_
   double* C = X + i * MK_NB + (long)k * MK_NB * ld;
   Acc acc;
   acc_zero(acc);
-  gemm_128<true, false>(winv_slot(ms, sh, ms.cur[sh], i), MK_NB, C, ld, MK_NB, MK_NB, acc, lds);
-  store_tile(C, ld, acc, -1.0, 0.0);
+  gemm_128<true, false, true>(winv_slot(ms, sh, ms.cur[sh], i), MK_NB, C, ld, MK_NB, MK_NB, acc, lds);
+  store_tile(C, ld, acc);
 }
 
 // Tiles (i,j), i >= j, of R^-1 = sum over rows l < n_s of W(l,i)^T W(l,j) (drops the bordered
@@ -375,7 +376,7 @@ __device__ inline void wtw_tile(const MatSet& ms, int sh, int ns, int i, int j, 
                            kvalid, acc, lds);
 }
 
-__global__ __launch_bounds__(256) void k_lauum(MatSet ms, const int* __restrict__ n_s, const int* __restrict__ list,
+__global__ __launch_bounds__(256, 2) void k_lauum(MatSet ms, const int* __restrict__ n_s, const int* __restrict__ list,
                                                const int* __restrict__ count) {
   __shared__ __attribute__((aligned(16))) double lds[GB_LDS_DOUBLES];
   const int ntiles = ms.nt * (ms.nt + 1) / 2;
@@ -391,10 +392,10 @@ __global__ __launch_bounds__(256) void k_lauum(MatSet ms, const int* __restrict_
   const long ld = ms.ld;
   double* Q = ms.Q + (long)sh * mat_elems(ms);
   double* Ct = (i != j) ? Q + j * MK_NB + (long)i * MK_NB * ld : nullptr;
-  store_tile(Q + i * MK_NB + (long)j * MK_NB * ld, ld, acc, 1.0, 0.0, Ct);
+  store_tile(Q + i * MK_NB + (long)j * MK_NB * ld, ld, acc, Ct);
 }
 
-__global__ __launch_bounds__(256) void k_qblocks(MatSet ms, const int* __restrict__ n_s, const int* __restrict__ list,
+__global__ __launch_bounds__(256, 2) void k_qblocks(MatSet ms, const int* __restrict__ n_s, const int* __restrict__ list,
                                                  const int* __restrict__ count) {
   __shared__ __attribute__((aligned(16))) double lds[GB_LDS_DOUBLES];
   const int e = blockIdx.x / ms.nt, i = blockIdx.x % ms.nt;
@@ -402,7 +403,7 @@ __global__ __launch_bounds__(256) void k_qblocks(MatSet ms, const int* __restric
   const int sh = list[e];
   Acc acc;
   wtw_tile(ms, sh, n_s[sh / ms.q], i, i, acc, lds);
-  store_tile(ms.QB + ((long)sh * ms.nt + i) * MK_NB * MK_NB, MK_NB, acc, 1.0, 0.0);
+  store_tile(ms.QB + ((long)sh * ms.nt + i) * MK_NB * MK_NB, MK_NB, acc);
 }
 
 // z_h = border row of the accepted factor = L^-1 u_h (exact for the u_h the candidate was built with).
@@ -472,7 +473,7 @@ __global__ __launch_bounds__(256) void k_pred_PT(Model md, const int* __restrict
 
 // X = W P^T (row tile i, test tile tb), stored column-major by test site (XK[t][row]);
 // partial column sums of squares over valid rows -> s_part[sh][i][t].
-__global__ __launch_bounds__(256) void k_pred_var(Model md, MatSet ms, const int* __restrict__ list,
+__global__ __launch_bounds__(256, 2) void k_pred_var(Model md, MatSet ms, const int* __restrict__ list,
                                                   const int* __restrict__ count) {
   __shared__ __attribute__((aligned(16))) double lds[GB_LDS_DOUBLES];
   __shared__ double red[2][MK_NB];
@@ -492,7 +493,7 @@ __global__ __launch_bounds__(256) void k_pred_var(Model md, MatSet ms, const int
   const int K = (i + 1) * MK_NB;   // W lower-triangular
   gemm_128<true, true>(Wm + i * MK_NB, ld, PT, md.n_test_pad, K, K, acc, lds);
   double* XK = md.XK + (long)sh * md.n_test_pad * md.n_pad + (long)tb * MK_NB * md.n_pad + i * MK_NB;
-  store_tile(XK, md.n_pad, acc, 1.0, 0.0);
+  store_tile(XK, md.n_pad, acc);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w & 1;
   double colsum[4][4];
 #pragma unroll

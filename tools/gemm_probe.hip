@@ -1,0 +1,92 @@
+// Micro-benchmark for the fp64 MFMA tile GEMM (development tool, not shipped).
+// 1) raw v_mfma_f64_16x16x4 throughput (registers only)
+// 2) mk::gemm_128 on batched 128 x K panels: operands from HBM (distinct per tile) vs L2 (shared)
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <vector>
+#include <cstdlib>
+#include "../laurabaracaldo-spatial-meta-kriging-for-distributed-inference-for-binary-response_amd/csrc/mk_gemm.hpp"
+using namespace mk;
+
+__global__ __launch_bounds__(256) void k_mfma_peak(double* out, int iters) {
+  d4 acc[16];
+  for (int i = 0; i < 16; ++i) acc[i] = (d4){0, 0, 0, 0};
+  double a = threadIdx.x * 1e-3, b = 1.0 + threadIdx.x * 1e-4;
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[i], 0, 0, 0);
+  }
+  double s = 0;
+  for (int i = 0; i < 16; ++i) s += acc[i][0] + acc[i][1] + acc[i][2] + acc[i][3];
+  if (s == 12345.0) out[threadIdx.x] = s;
+}
+
+__global__ void k_fill(double* p, long n) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256)
+    p[i] = 1e-3 * (double)((i * 2654435761ull) % 1000) - 0.5;
+}
+
+__global__ __launch_bounds__(256) void k_probe(const double* A, const double* B, double* C, int K, long strideA,
+                                               long strideB, int lda) {
+  __shared__ __attribute__((aligned(16))) double lds[GB_LDS_DOUBLES];
+  const double* a = A + blockIdx.x * strideA;
+  const double* b = B + blockIdx.x * strideB;
+  Acc acc;
+  acc_zero(acc);
+  gemm_128<true, true>(a, lda, b, lda, K, K, acc, lds);
+  store_tile(C + (long)blockIdx.x * 128 * 128, 128, acc, 1.0, 0.0);
+}
+
+int main() {
+  double* out;
+  hipMalloc(&out, 4096 * 8);
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  const int iters = 4000;
+  for (int rep = 0; rep < 2; ++rep) {
+    for (int blocks_per_cu : {1, 2}) {
+      int nb = 256 * blocks_per_cu;
+      hipLaunchKernelGGL(k_mfma_peak, dim3(nb), dim3(256), 0, 0, out, 10);
+      hipEventRecord(e0);
+      hipLaunchKernelGGL(k_mfma_peak, dim3(nb), dim3(256), 0, 0, out, iters);
+      hipEventRecord(e1);
+      hipEventSynchronize(e1);
+      float ms;
+      hipEventElapsedTime(&ms, e0, e1);
+      double fl = (double)nb * 4 * iters * 16 * 2048.0;
+      printf("mfma_peak blocks/CU=%d: %.2f TFLOP/s (%.3f ms)\n", blocks_per_cu, fl / ms / 1e9, ms);
+    }
+  }
+  // GEMM probe: ntile tiles of 128x128, K deep.  distinct: every tile streams its own
+  // 128 x K A panel from HBM (B shared, L2); shared: both operands shared (L2 resident).
+  for (int K : {256, 1024, 1920}) {
+    for (int shared : {0, 1}) {
+      const int ntile = 2000;
+      const long nA = shared ? (long)128 * K : (long)ntile * 128 * K;
+      double *A, *B, *C;
+      hipMalloc(&A, nA * 8);
+      hipMalloc(&B, (long)128 * K * 8);
+      hipMalloc(&C, (long)ntile * 128 * 128 * 8);
+      if (getenv("ZERO")) { hipMemset(A, 0, nA * 8); hipMemset(B, 0, (long)128 * K * 8); }
+      else {
+        hipLaunchKernelGGL(k_fill, dim3(2048), dim3(256), 0, 0, A, nA);
+        hipLaunchKernelGGL(k_fill, dim3(2048), dim3(256), 0, 0, B, (long)128 * K);
+      }
+      const long sA = shared ? 0 : (long)128 * K;
+      hipLaunchKernelGGL(k_probe, dim3(ntile), dim3(256), 0, 0, A, B, C, K, sA, 0L, 128);
+      hipEventRecord(e0);
+      for (int r = 0; r < 3; ++r) hipLaunchKernelGGL(k_probe, dim3(ntile), dim3(256), 0, 0, A, B, C, K, sA, 0L, 128);
+      hipEventRecord(e1);
+      hipEventSynchronize(e1);
+      float ms;
+      hipEventElapsedTime(&ms, e0, e1);
+      double fl = 3.0 * ntile * 2.0 * 128 * 128 * K;
+      double by = 3.0 * (shared ? 0.0 : (double)nA * 8);
+      printf("gemm K=%d shared=%d: %.2f TFLOP/s  A-stream %.2f TB/s (%.3f ms/launch)\n", K, shared,
+             fl / ms / 1e9, by / ms / 1e9, ms / 3);
+      hipFree(A); hipFree(B); hipFree(C);
+    }
+  }
+  return 0;
+}
