@@ -4,10 +4,12 @@ headline configuration -- n=500,000 binary sites split into K=250 subsets of 2,0
 exponential covariance, q=1, 1,000 kriging sites (configs[2]).
 
 A step = one spMvGLM amcmc iteration of EVERY subset (beta, A, phi MH with a fresh
-2000x2000 Cholesky per subset, inverse where phi moved, single-site w sweep) plus
-the fused spPredict kriging draw of that iteration -- the timed steps are kept
-(post-burn-in) iterations, the costlier kind.  Subsets are sharded over ranks
-(contiguous blocks, strong scaling: K=250 fixed); no data-path collective.
+2000x2000 Cholesky per subset, inverse where phi moved, single-site w sweep) plus,
+on kept iterations, the fused spPredict kriging draw.  The timed window follows the
+reference schedule (MK.R:57-59, 85): 3 burn-in iterations per kept one.  Subsets are
+sharded over ranks (contiguous blocks, strong scaling: K=250 fixed); no data-path
+collective.  roofline.traffic is the PMC-measured HBM traffic of the same kernel from
+profiles/ (rocprofv3 --pmc passes of this command, gfx950 FETCH_SIZE x2 correction).
 
   python bench.py --gpus N --steps K --warmup W
 """
@@ -80,6 +82,16 @@ def cpu_baseline(n_s, iters, workers):
                        f"thread per core; wall {wall:.1f}s incl. start-up")
 
 
+def _pmc_traffic():
+    """HBM bytes per k_chol_update launch from the committed rocprofv3 --pmc passes (or None)."""
+    path = os.path.join(ROOT, "profiles", "pmc_chol_update.json")
+    try:
+        with open(path) as f:
+            return json.load(f)["hbm_bytes_per_launch"]
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def main():
     a = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -103,16 +115,19 @@ def main():
     d = mk.synthetic.generate(n, q=1, n_test=n_test, seed=20250114)
     n_part, idx = mk.partition(n, K, seed=20250114)
     beta0, bt = mk.start_values(d["y"], d["x"], 1.0, 1)
+    dmod = importlib.import_module(PKG + ".distributed")
+    lo, hi = dmod.shard_range(K, world, rank)
     per = (K + world - 1) // world
-    lo, hi = rank * per, min(K, (rank + 1) * per)
     W = max(1, a.warmup)
-    # amcmc batches of 50 as MK.R:57-58; the chain is long enough for warmup + timed steps and
-    # every timed step is a kept (kriging) iteration: burn_in = W (1-based) -> kept0 = W - 1
+    # amcmc batches of 50 as MK.R:57-58; the timed window holds burn-in and kept (kriging)
+    # iterations in the reference's 3:1 ratio (burn.in = 0.75 n.samples, MK.R:85)
+    n_burn_timed = int(round(0.75 * a.steps))
+    burn_in = W + n_burn_timed + 1               # 1-based first kept iteration
     n_batch = (W + a.steps + 49) // 50
-    cfg = mk.SamplerConfig(1, 2, beta0, bt, n_batch=n_batch, batch_length=50, burn_in=W, seed=20250114)
+    cfg = mk.SamplerConfig(1, 2, beta0, bt, n_batch=n_batch, batch_length=50, burn_in=burn_in, seed=20250114)
     subs = [mk.subset_data(d["y"], d["x"], 1.0, d["coords"], 1, idx[i]) for i in range(lo, hi)]
     ses = mk.Session(subs, cfg, coords_test=d["coords_test"], subset_base=lo, device=local if world > 1 else 0)
-    ses.run(W)                                    # warmup (the last one refreshes every factor for kriging)
+    ses.run(W)                                    # warmup
     ses.profile(True)
 
     def barrier():
@@ -158,12 +173,14 @@ def main():
         "dtype": "f64",
         "data": "synthetic (seeded binary GP field, RFF, SURVEY.md 8d generator)",
         "config": {"workload": f"configs[2]: n={n}, K={K} subsets of {n // K}, exponential, q=1, "
-                               f"n_test={n_test}, amcmc 100x50, kept iterations with fused kriging",
+                               f"n_test={n_test}, amcmc batches of 50, timed window {n_burn_timed} burn-in + "
+                               f"{a.steps - n_burn_timed} kept (fused kriging) iterations",
                    "subsets_per_gpu": per, "parallelism": f"subset-sharded x{world}"},
         "roofline": {"bound": "mfma", "kernel": "k_chol_update (left-looking Cholesky panel GEMM, fp64 MFMA)",
                      "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None,
-                     "avg_launch_ms": avg_ms, "launches": st["launches"]},
+                     "frac": achieved / FP64_PEAK_TFLOPS, "traffic": _pmc_traffic(),
+                     "avg_launch_ms": avg_ms, "launches": st["launches"],
+                     "algorithmic_flops_per_launch": st["flops"] / max(1, st["launches"])},
         "kernels_ms_per_step": {k: v["ms"] / a.steps for k, v in kern.items()},
         "end_to_end_estimate_s": elapsed / a.steps * 5000,
     }

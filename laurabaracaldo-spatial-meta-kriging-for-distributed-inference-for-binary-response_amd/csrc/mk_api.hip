@@ -160,15 +160,23 @@ static void launch_cholesky(mk_session* s, int h, int S_launch) {
   }
 }
 
+// W = L^-1 of the listed pairs: diagonal tiles, then recursive doubling.
+static void launch_trinv(mk_session* s, int max_entries, const int* list, const int* count) {
+  const int nt = s->nt;
+  hipLaunchKernelGGL(k_inv_copydiag, dim3(max_entries * nt), dim3(256), 0, s->stream, s->ms, list, count);
+  for (int sz = 1; sz < nt; sz *= 2) {
+    const int npairs = (nt + 2 * sz - 1) / (2 * sz);
+    for (int phase = 0; phase < 2; ++phase)
+      hipLaunchKernelGGL(k_inv_level, dim3(max_entries * npairs * sz * sz), dim3(256), 0, s->stream, s->ms, list,
+                         count, sz, phase);
+  }
+}
+
 // W = L^-1 for the changed factors, diagonal tiles of R^-1, z from the bordered row.
 static void launch_inverse(mk_session* s, int max_entries) {
   const int nt = s->nt;
   Model& md = s->md;
-  hipLaunchKernelGGL(k_inv_copydiag, dim3(max_entries * nt), dim3(256), 0, s->stream, s->ms, s->d_list, s->d_count);
-  for (int d = 1; d < nt; ++d) {
-    hipLaunchKernelGGL(k_inv_T, dim3(max_entries * (nt - d)), dim3(256), 0, s->stream, s->ms, s->d_list, s->d_count, d);
-    hipLaunchKernelGGL(k_inv_D, dim3(max_entries * (nt - d)), dim3(256), 0, s->stream, s->ms, s->d_list, s->d_count, d);
-  }
+  launch_trinv(s, max_entries, s->d_list, s->d_count);
   timed(s, KS_LAUUM, 0.0, [&] {
     hipLaunchKernelGGL(k_qblocks, dim3(max_entries * nt), dim3(256), 0, s->stream, s->ms, md.n_s, s->d_list,
                        s->d_count);
@@ -716,11 +724,7 @@ extern "C" int mk_cholesky_batched(const double* A, int32_t S, int32_t n, double
     hipLaunchKernelGGL(k_dirty_list, dim3(1), dim3(256), 0, s->stream, md, 1, s->d_plist, s->d_pcount, s->d_list,
                        s->d_count);
     const int ntiles = nt * (nt + 1) / 2;
-    hipLaunchKernelGGL(k_inv_copydiag, dim3(S * nt), dim3(256), 0, s->stream, ms, s->d_list, s->d_count);
-    for (int d = 1; d < nt; ++d) {
-      hipLaunchKernelGGL(k_inv_T, dim3(S * (nt - d)), dim3(256), 0, s->stream, ms, s->d_list, s->d_count, d);
-      hipLaunchKernelGGL(k_inv_D, dim3(S * (nt - d)), dim3(256), 0, s->stream, ms, s->d_list, s->d_count, d);
-    }
+    launch_trinv(s, S, s->d_list, s->d_count);
     hipLaunchKernelGGL(k_lauum, dim3(S * ntiles), dim3(256), 0, s->stream, ms, md.n_s, s->d_list, s->d_count);
     hipLaunchKernelGGL(k_extract_L, dim3(2048), dim3(256), 0, s->stream, ms, n, S, dL, 1);
     if (hipMemcpyAsync(inv_out, dL, (size_t)S * n * n * 8, hipMemcpyDeviceToHost, s->stream) != hipSuccess)

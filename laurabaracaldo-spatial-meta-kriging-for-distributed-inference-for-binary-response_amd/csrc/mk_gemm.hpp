@@ -29,8 +29,12 @@ typedef double d2 __attribute__((ext_vector_type(2)));
 #define MK_GB_K 16
 #endif
 constexpr int GB_K = MK_GB_K;  // K chunk
-constexpr int GB_SM = 144;     // LDS row stride (doubles)
-constexpr int GB_LDS_DOUBLES = 2 * GB_K * GB_SM;
+constexpr int GB_SM = 144;     // LDS row stride (doubles) for m-contiguous operands
+// k-contiguous operands are transposed while stored to LDS; an odd stride spreads
+// the 8 k values a 16-lane ds_write group stores for one m over distinct banks.
+constexpr int GB_SMT = 145;
+template <bool MU> constexpr int sm_of() { return MU ? GB_SM : GB_SMT; }
+constexpr int GB_LDS_DOUBLES = 2 * GB_K * GB_SMT;
 constexpr int GB_PER = GB_K / 4;   // d2 loads per thread per operand per chunk
 
 struct Acc {
@@ -76,13 +80,13 @@ __device__ inline void store_chunk(double* lds, const d2 (&r)[GB_PER]) {
       *reinterpret_cast<d2*>(lds + k * GB_SM + m) = r[i];
     } else {
       const int k = (e % (GB_K / 2)) * 2, m = e / (GB_K / 2);
-      lds[k * GB_SM + m] = r[i].x;
-      lds[(k + 1) * GB_SM + m] = r[i].y;
+      lds[k * GB_SMT + m] = r[i].x;
+      lds[(k + 1) * GB_SMT + m] = r[i].y;
     }
   }
 }
 
-template <bool NEG = false>
+template <bool NEG = false, int SA = GB_SM, int SB = GB_SM>
 __device__ inline void mma_chunk(const double* As, const double* Bs, Acc& acc) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int wm = w & 1, wn = w >> 1;
@@ -92,8 +96,9 @@ __device__ inline void mma_chunk(const double* As, const double* Bs, Acc& acc) {
     double ya[4], xb[4];
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
-      ya[b] = NEG ? -As[(ks * 4 + lk) * GB_SM + wm * 64 + b * 16 + li] : As[(ks * 4 + lk) * GB_SM + wm * 64 + b * 16 + li];
-      xb[b] = Bs[(ks * 4 + lk) * GB_SM + wn * 64 + b * 16 + li];
+      const double av = As[(ks * 4 + lk) * SA + wm * 64 + b * 16 + li];
+      ya[b] = NEG ? -av : av;
+      xb[b] = Bs[(ks * 4 + lk) * SB + wn * 64 + b * 16 + li];
     }
 #pragma unroll
     for (int bm = 0; bm < 4; ++bm)
@@ -108,7 +113,7 @@ template <bool A_MU, bool B_NU, bool NEG = false>
 __device__ inline void gemm_128(const double* __restrict__ A, long sA, const double* __restrict__ B, long sB,
                                 int K, int kvalid_total, Acc& acc, double* lds) {
   double* As = lds;
-  double* Bs = lds + GB_K * GB_SM;
+  double* Bs = lds + GB_K * GB_SMT;
   d2 ra[GB_PER], rb[GB_PER];
   if (K <= 0) return;
   load_chunk<A_MU>(A, sA, 0, kvalid_total, ra);
@@ -122,7 +127,7 @@ __device__ inline void gemm_128(const double* __restrict__ A, long sA, const dou
       load_chunk<A_MU>(A, sA, kc + GB_K, kvalid_total - (kc + GB_K), ra);
       load_chunk<B_NU>(B, sB, kc + GB_K, kvalid_total - (kc + GB_K), rb);
     }
-    mma_chunk<NEG>(As, Bs, acc);
+    mma_chunk<NEG, sm_of<A_MU>(), sm_of<B_NU>()>(As, Bs, acc);
   }
 }
 

@@ -9,8 +9,7 @@ __global__ void k_chol_update(MatSet ms, int S, int h, int k);
 __global__ void k_chol_trsm(MatSet ms, int S, int h, int k);
 __global__ void k_chol_diag(MatSet ms, const int* n_s, int h, int k, double* ld_part, double* quad_c, int* info);
 __global__ void k_inv_copydiag(MatSet ms, const int* list, const int* count);
-__global__ void k_inv_T(MatSet ms, const int* list, const int* count, int d);
-__global__ void k_inv_D(MatSet ms, const int* list, const int* count, int d);
+__global__ void k_inv_level(MatSet ms, const int* list, const int* count, int sz, int phase);
 __global__ void k_lauum(MatSet ms, const int* n_s, const int* list, const int* count);
 __global__ void k_qblocks(MatSet ms, const int* n_s, const int* list, const int* count);
 __global__ void k_take_border(Model md, MatSet ms, const int* list, const int* count);

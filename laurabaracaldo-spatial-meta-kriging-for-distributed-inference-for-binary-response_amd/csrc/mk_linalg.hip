@@ -9,9 +9,9 @@
 //   k_chol_diag   : factor C(k,k) in LDS, invert it (Winv_k), logdet partial,
 //                   read the bordered row (quadratic form u' R^-1 u)
 //   k_chol_trsm   : L(i,k) = C(i,k) Winv_k^T                for i > k    (MFMA GEMM, K = 128)
-// Inverse of an accepted factor, W = L^-1 by diagonal distance d:
-//   k_inv_copydiag (d=0), k_inv_T(d): W(k+d,k) = sum_j L(k+d,j) W(j,k);
-//   k_inv_D(d): W(k+d,k) = -Winv_{k+d} W(k+d,k)
+// Inverse of an accepted factor, W = L^-1: diagonal tiles from the Winv of the
+//   factorisation (k_inv_copydiag), then recursive doubling over block pairs
+//   (k_inv_level: W_BT = -W_BB L_BT W_TT, log2(nt) levels x 2 MFMA GEMM launches)
 // then the diagonal 128-tiles of R^-1 = W'W (k_qblocks) for the latent sweep;
 // the full W'W (k_lauum) only serves the parity-test entry point.
 // Kriging (kept iterations): P^T = rho(obs, test) materialised once per changed
@@ -330,37 +330,43 @@ __global__ __launch_bounds__(256) void k_inv_copydiag(MatSet ms, const int* __re
   }
 }
 
-__global__ __launch_bounds__(256, 2) void k_inv_T(MatSet ms, const int* __restrict__ list, const int* __restrict__ count, int d) {
+// Recursive-doubling inverse.  At level sz (sz = 1, 2, 4, ... tiles) every pair of
+// consecutive diagonal blocks T = [T0, T0+sz), B = [T0+sz, T0+2sz) of the factor gets
+//   phase 0: Y_BT = L_BT W_TT        (Y kept in the free factor slot)
+//   phase 1: W_BT = -W_BB Y_BT
+// with W_TT, W_BB complete from the lower levels.  Triangularity bounds every K range.
+__global__ __launch_bounds__(256, 2) void k_inv_level(MatSet ms, const int* __restrict__ list,
+                                                      const int* __restrict__ count, int sz, int phase) {
   __shared__ __attribute__((aligned(16))) double lds[GB_LDS_DOUBLES];
-  const int ntd = ms.nt - d;
-  const int e = blockIdx.x / ntd, k = blockIdx.x % ntd;
+  const int npairs = (ms.nt + 2 * sz - 1) / (2 * sz);
+  const int per = npairs * sz * sz;
+  const int e = blockIdx.x / per;
   if (e >= *count) return;
+  int t = blockIdx.x % per;
+  const int p = t / (sz * sz);
+  t %= sz * sz;
+  const int T0 = 2 * p * sz, B0 = T0 + sz;
+  const int i = B0 + t / sz, j = T0 + t % sz;
+  if (i >= ms.nt) return;
   const int sh = list[e];
-  const double* Lm = mat_slot(ms, sh, ms.cur[sh]);
-  double* X = wmat(ms, sh);
+  const int cur = ms.cur[sh];
   const long ld = ms.ld;
-  const int i = k + d;
+  double* Wm = wmat(ms, sh);
+  double* Y = mat_slot(ms, sh, 1 - cur);
   Acc acc;
   acc_zero(acc);
-  gemm_128<true, false>(Lm + i * MK_NB + (long)k * MK_NB * ld, ld, X + k * MK_NB + (long)k * MK_NB * ld, ld,
-                        d * MK_NB, d * MK_NB, acc, lds);
-  store_tile(X + i * MK_NB + (long)k * MK_NB * ld, ld, acc);
-}
-
-__global__ __launch_bounds__(256, 2) void k_inv_D(MatSet ms, const int* __restrict__ list, const int* __restrict__ count, int d) {
-  __shared__ __attribute__((aligned(16))) double lds[GB_LDS_DOUBLES];
-  const int ntd = ms.nt - d;
-  const int e = blockIdx.x / ntd, k = blockIdx.x % ntd;
-  if (e >= *count) return;
-  const int sh = list[e];
-  double* X = wmat(ms, sh);
-  const long ld = ms.ld;
-  const int i = k + d;
-  double* C = X + i * MK_NB + (long)k * MK_NB * ld;
-  Acc acc;
-  acc_zero(acc);
-  gemm_128<true, false, true>(winv_slot(ms, sh, ms.cur[sh], i), MK_NB, C, ld, MK_NB, MK_NB, acc, lds);
-  store_tile(C, ld, acc);
+  if (phase == 0) {
+    const double* Lm = mat_slot(ms, sh, cur);
+    const int K = (B0 - j) * MK_NB;
+    gemm_128<true, false>(Lm + i * MK_NB + (long)j * MK_NB * ld, ld, Wm + j * MK_NB + (long)j * MK_NB * ld, ld, K, K,
+                          acc, lds);
+    store_tile(Y + i * MK_NB + (long)j * MK_NB * ld, ld, acc);
+  } else {
+    const int K = (i - B0 + 1) * MK_NB;
+    gemm_128<true, false, true>(Wm + i * MK_NB + (long)B0 * MK_NB * ld, ld, Y + B0 * MK_NB + (long)j * MK_NB * ld, ld,
+                                K, K, acc, lds);
+    store_tile(Wm + i * MK_NB + (long)j * MK_NB * ld, ld, acc);
+  }
 }
 
 // Tiles (i,j), i >= j, of R^-1 = sum over rows l < n_s of W(l,i)^T W(l,j) (drops the bordered

@@ -1,0 +1,120 @@
+"""CPU-side tests: the C ABI library loads and exports every symbol include/mk.h declares,
+host logic (partition, subset slicing, config validation, glm start values) mirrors the
+reference, and the ctypes structures match the header field for field."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from oracle import rstats
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "mk.h")
+
+
+def _declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(mk_[a-z_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol(mk):
+    lib = mk.load()
+    names = _declared_functions()
+    assert len(names) >= 13
+    for n in names:
+        assert hasattr(lib, n), f"libmk.so lacks {n}"
+    # ctypes binding covers the whole header
+    from importlib import import_module
+    binding = import_module(mk.__name__ + "._lib")
+    assert set(names) <= set(binding.EXPORTS)
+
+
+def test_struct_layouts_match_header(mk):
+    binding = __import__(mk.__name__ + "._lib", fromlist=["x"])
+    src = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    for cname, pyname in [("mk_problem", "Problem"), ("mk_config", "Config"), ("mk_outputs", "Outputs")]:
+        body = re.search(r"typedef struct %s \{(.*?)\} %s;" % (cname, cname), src, flags=re.S).group(1)
+        fields = re.findall(r"\b([A-Za-z_][A-Za-z0-9_]*)\s*;", body)
+        py = [f[0] for f in getattr(binding, pyname)._fields_]
+        assert fields == py, (cname, fields, py)
+
+
+def test_no_gpu_errors_cleanly(mk):
+    lib = mk.load()
+    if lib.mk_device_count() > 0:
+        pytest.skip("GPU present")
+    d = mk.synthetic.generate(20, q=1, n_test=2, seed=1)
+    cfg = mk.SamplerConfig(1, 2, [0, 0], [0.1, 0.1], n_batch=1, batch_length=2)
+    with pytest.raises(mk.MkError):
+        mk.Session([dict(coords=d["coords"], y=d["y"], weights=np.ones(20), x=d["x"])], cfg)
+
+
+def test_partition_sizes_follow_reference(mk):
+    n_part, idx = mk.partition(2003, 20, seed=3)
+    assert list(n_part[:-1]) == [100] * 19 and n_part[-1] == 2003 - 100 * 19      # MK.R:17-18
+    allidx = np.concatenate(idx)
+    assert np.array_equal(np.sort(allidx), np.arange(2003))                        # without replacement
+
+
+def test_subset_data_location_major(mk):
+    d = mk.synthetic.generate(30, q=2, n_test=0, seed=2)
+    idx = np.array([5, 2, 9])
+    sub = mk.subset_data(d["y"], d["x"], 1.0, d["coords"], 2, idx)
+    assert sub["y"].shape == (6,) and sub["x"].shape == (6, 4)
+    for k, i in enumerate(idx):
+        np.testing.assert_array_equal(sub["y"][2 * k:2 * k + 2], d["y"][2 * i:2 * i + 2])
+        np.testing.assert_array_equal(sub["coords"][k], d["coords"][i])
+
+
+def test_glm_start_values_match_oracle(mk):
+    d = mk.synthetic.generate(2500, q=2, n_test=0, seed=8)
+    coef, vcov, bt = mk.glm.glm_binomial(d["y"], d["x"], np.ones(5000))
+    rc, rv = rstats.glm_binomial(d["y"], d["x"], np.ones(5000))
+    np.testing.assert_allclose(coef, rc, rtol=1e-10)
+    np.testing.assert_allclose(vcov, rv, rtol=1e-8)
+    np.testing.assert_allclose(bt @ bt.T, vcov, rtol=1e-12)        # t(chol(vcov)) is lower
+
+
+def test_sampler_config_mirrors_reference_defaults(mk):
+    cfg = mk.SamplerConfig(2, 4, np.zeros(4), np.eye(4) * 0.3)
+    assert cfg.n_samples == 5000 and cfg.burn_in == 3750 and cfg.kept == 1251        # MK.R:57-59, 85
+    np.testing.assert_array_equal(cfg.phi_starting, [6.0, 6.0])                      # MK.R:60
+    np.testing.assert_array_equal(cfg.phi_a, [4.0, 4.0])
+    np.testing.assert_array_equal(cfg.phi_b, [12.0, 12.0])                           # MK.R:63
+    np.testing.assert_array_equal(cfg.A_starting, [1.0, 0.0, 1.0])                   # MK.R:56
+    np.testing.assert_array_equal(cfg.A_tuning, [0.1, 0.1, 0.1])                     # MK.R:61
+    np.testing.assert_array_equal(cfg.beta_tuning, [0.3] * 4)                        # diag of MK.R:55
+    assert cfg.K_IW_df == 2 and np.array_equal(cfg.K_IW_S, np.eye(2) * 0.1)           # MK.R:64
+    assert cfg.P == 4 + 3 + 2
+
+
+def test_spmvglm_argument_errors(mk):
+    d = mk.synthetic.generate(10, q=1, n_test=0, seed=1)
+    f = [(d["y"], d["x"])]
+    ok = dict(starting={"beta": [0, 0], "phi": 6, "A": [1.0], "w": 0},
+              tuning={"beta": [0.1, 0.1], "phi": 1, "A": [0.1], "w": 0.5},
+              priors={"beta.Flat": True, "phi.Unif": (4, 12), "K.IW": (1, [[0.1]])},
+              amcmc={"n.batch": 1, "batch.length": 2, "accept.rate": 0.43})
+    with pytest.raises(ValueError):
+        mk.spMvGLM(f, d["coords"], np.ones((10, 1)), cov_model="gaussian", **ok)
+    bad = dict(ok, starting={"beta": [0, 0], "A": [1.0], "w": 0})
+    with pytest.raises(ValueError):
+        mk.spMvGLM(f, d["coords"], np.ones((10, 1)), **bad)
+    with pytest.raises(ValueError):
+        mk.spMvGLM(f, d["coords"], np.ones((10, 1)), family="poisson", **ok)
+
+
+def test_posterior_summary_shapes(mk):
+    rng = np.random.default_rng(0)
+    result = np.sort(rng.normal(size=(200, 4)), axis=0)
+    result2 = np.sort(rng.normal(size=(200, 7)), axis=0)
+    x_test = np.column_stack([np.ones(7), rng.normal(size=7)])
+    out = mk.posterior_summary(result, result2, np.hstack([x_test, np.zeros((7, 2))]), 1)
+    assert out["p_sample"].shape == (1000, 7)
+    assert out["w_quant"].shape == (3, 7) and out["param_quant"].shape == (3, 4)
+    # the interpolation the reference applies (MK.R:142) vs the oracle's approx
+    np.testing.assert_allclose(mk.metakriging.r_approx(rstats.PROBS200, result, rstats.XOUT996),
+                               rstats.r_approx(rstats.PROBS200, result, rstats.XOUT996), rtol=1e-14)

@@ -26,15 +26,16 @@ __global__ void k_fill(double* p, long n) {
     p[i] = 1e-3 * (double)((i * 2654435761ull) % 1000) - 0.5;
 }
 
-__global__ __launch_bounds__(256) void k_probe(const double* A, const double* B, double* C, int K, long strideA,
+template <bool BNU>
+__global__ __launch_bounds__(256, 2) void k_probe(const double* A, const double* B, double* C, int K, long strideA,
                                                long strideB, int lda) {
   __shared__ __attribute__((aligned(16))) double lds[GB_LDS_DOUBLES];
   const double* a = A + blockIdx.x * strideA;
   const double* b = B + blockIdx.x * strideB;
   Acc acc;
   acc_zero(acc);
-  gemm_128<true, true>(a, lda, b, lda, K, K, acc, lds);
-  store_tile(C + (long)blockIdx.x * 128 * 128, 128, acc, 1.0, 0.0);
+  gemm_128<true, BNU>(a, lda, b, BNU ? 128 : K, K, K, acc, lds);
+  store_tile(C + (long)blockIdx.x * 128 * 128, 128, acc);
 }
 
 int main() {
@@ -44,23 +45,10 @@ int main() {
   hipEventCreate(&e0);
   hipEventCreate(&e1);
   const int iters = 4000;
-  for (int rep = 0; rep < 2; ++rep) {
-    for (int blocks_per_cu : {1, 2}) {
-      int nb = 256 * blocks_per_cu;
-      hipLaunchKernelGGL(k_mfma_peak, dim3(nb), dim3(256), 0, 0, out, 10);
-      hipEventRecord(e0);
-      hipLaunchKernelGGL(k_mfma_peak, dim3(nb), dim3(256), 0, 0, out, iters);
-      hipEventRecord(e1);
-      hipEventSynchronize(e1);
-      float ms;
-      hipEventElapsedTime(&ms, e0, e1);
-      double fl = (double)nb * 4 * iters * 16 * 2048.0;
-      printf("mfma_peak blocks/CU=%d: %.2f TFLOP/s (%.3f ms)\n", blocks_per_cu, fl / ms / 1e9, ms);
-    }
-  }
   // GEMM probe: ntile tiles of 128x128, K deep.  distinct: every tile streams its own
   // 128 x K A panel from HBM (B shared, L2); shared: both operands shared (L2 resident).
-  for (int K : {256, 1024, 1920}) {
+  for (int bnu : {1, 0})
+  for (int K : {256, 1024}) {
     for (int shared : {0, 1}) {
       const int ntile = 2000;
       const long nA = shared ? (long)128 * K : (long)ntile * 128 * K;
@@ -74,16 +62,17 @@ int main() {
         hipLaunchKernelGGL(k_fill, dim3(2048), dim3(256), 0, 0, B, (long)128 * K);
       }
       const long sA = shared ? 0 : (long)128 * K;
-      hipLaunchKernelGGL(k_probe, dim3(ntile), dim3(256), 0, 0, A, B, C, K, sA, 0L, 128);
+      auto kern = bnu ? k_probe<true> : k_probe<false>;
+      hipLaunchKernelGGL(kern, dim3(ntile), dim3(256), 0, 0, A, B, C, K, sA, 0L, 128);
       hipEventRecord(e0);
-      for (int r = 0; r < 3; ++r) hipLaunchKernelGGL(k_probe, dim3(ntile), dim3(256), 0, 0, A, B, C, K, sA, 0L, 128);
+      for (int r = 0; r < 3; ++r) hipLaunchKernelGGL(kern, dim3(ntile), dim3(256), 0, 0, A, B, C, K, sA, 0L, 128);
       hipEventRecord(e1);
       hipEventSynchronize(e1);
       float ms;
       hipEventElapsedTime(&ms, e0, e1);
       double fl = 3.0 * ntile * 2.0 * 128 * 128 * K;
       double by = 3.0 * (shared ? 0.0 : (double)nA * 8);
-      printf("gemm K=%d shared=%d: %.2f TFLOP/s  A-stream %.2f TB/s (%.3f ms/launch)\n", K, shared,
+      printf("B_NU=%d gemm K=%d shared=%d: %.2f TFLOP/s  A-stream %.2f TB/s (%.3f ms/launch)\n", bnu, K, shared,
              fl / ms / 1e9, by / ms / 1e9, ms / 3);
       hipFree(A); hipFree(B); hipFree(C);
     }
