@@ -129,7 +129,8 @@ static void drain_timers(mk_session* s) {
 static inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
 
 // ------------------------------------------------------------------ Cholesky of all candidates of outcome h
-static void launch_cholesky(mk_session* s, int h, int S_launch) {
+// gen: candidate tiles generated from coordinates (session); otherwise preloaded (test entry).
+static void launch_cholesky(mk_session* s, int h, int S_launch, int which, int iter, bool gen) {
   const int nt = s->nt;
   const size_t diag_lds = (size_t)(MK_NB * MK_NB + 2 * MK_NB + 4 * 256) * sizeof(double);
   Model& md = s->md;
@@ -143,7 +144,8 @@ static void launch_cholesky(mk_session* s, int h, int S_launch) {
       const double kk = std::fmin((double)k * MK_NB, nv);
       const double fl = 2.0 * rows * cols * kk * S_launch;
       timed(s, KS_CHOL_UPDATE, fl, [&] {
-        hipLaunchKernelGGL(k_chol_update, dim3(S_launch * (nt - k)), dim3(256), 0, s->stream, s->ms, S_launch, h, k);
+        hipLaunchKernelGGL(k_chol_update, dim3(xcd_grid_h(S_launch, nt - k)), dim3(256), 0, s->stream, md, s->ms,
+                           S_launch, h, k, which, iter, (int)gen);
       });
     }
     timed(s, KS_CHOL_DIAG, 0.0, [&] {
@@ -154,7 +156,8 @@ static void launch_cholesky(mk_session* s, int h, int S_launch) {
       const double rows = std::fmax(0.0, nv - (k + 1) * MK_NB);
       const double fl = 2.0 * rows * MK_NB * MK_NB * S_launch;
       timed(s, KS_CHOL_TRSM, fl, [&] {
-        hipLaunchKernelGGL(k_chol_trsm, dim3(S_launch * (nt - k - 1)), dim3(256), 0, s->stream, s->ms, S_launch, h, k);
+        hipLaunchKernelGGL(k_chol_trsm, dim3(xcd_grid_h(S_launch, nt - k - 1)), dim3(256), 0, s->stream, s->ms,
+                           S_launch, h, k);
       });
     }
   }
@@ -210,8 +213,9 @@ static int run_iteration(mk_session* s) {
   const int ntri_tiles = s->nt * (s->nt + 1) / 2;
   for (int which = 0; which < nkinds; ++which)
     for (int h = 0; h < q; ++h) {
-      hipLaunchKernelGGL(k_cov_candidate, dim3(S * ntri_tiles), dim3(256), 0, s->stream, md, s->ms, h, which, it);
-      launch_cholesky(s, h, S);
+      hipLaunchKernelGGL(k_cov_candidate, dim3(xcd_grid_h(S, ntri_tiles)), dim3(256), 0, s->stream, md, s->ms, h,
+                         which, it);
+      launch_cholesky(s, h, S, which, it, false);
       hipLaunchKernelGGL(k_theta_mh, dim3((S + 63) / 64), dim3(64), 0, s->stream, md, s->ms, h, which, it);
     }
   hipLaunchKernelGGL(k_dirty_list, dim3(1), dim3(256), 0, s->stream, md, (int)(it == md.kept0), s->d_list, s->d_count,
@@ -473,8 +477,8 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
   hipLaunchKernelGGL(k_init_state, dim3(S), dim3(256), 0, s->stream, md);
   const int ntri_tiles = nt * (nt + 1) / 2;
   for (int h = 0; h < q; ++h) {
-    hipLaunchKernelGGL(k_cov_candidate, dim3(S * ntri_tiles), dim3(256), 0, s->stream, md, ms, h, 2, 0);
-    launch_cholesky(s, h, S);
+    hipLaunchKernelGGL(k_cov_candidate, dim3(xcd_grid_h(S, ntri_tiles)), dim3(256), 0, s->stream, md, ms, h, 2, 0);
+    launch_cholesky(s, h, S, 2, 0, false);
     hipLaunchKernelGGL(k_theta_init, dim3((S + 63) / 64), dim3(64), 0, s->stream, md, ms, h);
   }
   hipLaunchKernelGGL(k_dirty_list, dim3(1), dim3(256), 0, s->stream, md, 0, s->d_list, s->d_count, s->d_plist,
@@ -695,7 +699,7 @@ extern "C" int mk_cholesky_batched(const double* A, int32_t S, int32_t n, double
                           (MK_NB * MK_NB + 2 * MK_NB + 4 * 256) * 8) != hipSuccess)
     return fail(set_err(MK_E_HIP, "lds attribute"));
   hipLaunchKernelGGL(k_load_plain, dim3(2048), dim3(256), 0, s->stream, ms, dA, n, S);
-  launch_cholesky(s, 0, S);
+  launch_cholesky(s, 0, S, 2, 0, false);
   std::vector<double> part((size_t)S * nt);
   std::vector<int> info(S);
   if (hipStreamSynchronize(s->stream) != hipSuccess) return fail(set_err(MK_E_HIP, "cholesky run"));

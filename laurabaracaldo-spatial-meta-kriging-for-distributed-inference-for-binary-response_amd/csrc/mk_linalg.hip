@@ -43,52 +43,90 @@ __device__ inline void candidate_theta(const Model& md, int s, int h, int which,
   *nu = (md.cov_model == MK_COV_MATERN) ? logit_inv(tnu, md.nu_a[h], md.nu_b[h]) : 0.0;
 }
 
+// Element (R, C) of the candidate matrix of one (subset, outcome).
+struct CandGen {
+  const double* cx;
+  const double* cy;
+  const double* uh;
+  int ns, model;
+  double phi, nu;
+  __device__ inline double operator()(int R, int C) const {
+    if (R < ns && C < ns) return (R == C) ? 1.0 : correlation(dist2d(cx[R], cy[R], cx[C], cy[C]), phi, nu, model);
+    if (R == ns && C < ns) return uh[C];
+    return (R == C && R != ns) ? 1.0 : 0.0;
+  }
+};
+
+__device__ inline CandGen make_gen(const Model& md, int s, int h, int which, int iter) {
+  CandGen g;
+  candidate_theta(md, s, h, which, iter, &g.phi, &g.nu);
+  g.cx = md.coords + (long)s * 2 * md.n_pad;
+  g.cy = g.cx + md.n_pad;
+  g.uh = md.u + ((long)s * md.q + h) * md.n_pad;
+  g.ns = md.n_s[s];
+  g.model = md.cov_model;
+  return g;
+}
+
+// XCD-aware block -> (subset, tile) map: subsets s with s % 8 == x are served by blocks
+// b with b % 8 == x (blocks are dealt round-robin over the 8 XCDs), so a subset's tiles
+// share one L2 and its shared panel is fetched once.  Speed only; any placement is correct.
+__device__ inline bool xcd_map(int S, int T, int* s, int* t) {
+  const int x = blockIdx.x & 7, j = blockIdx.x >> 3;
+  *s = x + 8 * (j / T);
+  *t = j % T;
+  return *s < S;
+}
+__host__ inline int xcd_grid(int S, int T) { return 8 * ((S + 7) / 8) * T; }
+
+// Lower tiles (i >= j) of every candidate of outcome h (tiles with j < jmin are skipped).
+// Generating tiles inside k_chol_update at their first touch (gen = 1) was measured
+// slower on cfg3 (+3.5 ms of exp work at 2 waves/SIMD vs 1.7 ms for this pass).
 __global__ __launch_bounds__(256) void k_cov_candidate(Model md, MatSet ms, int h, int which, int iter) {
   const int ntiles = ms.nt * (ms.nt + 1) / 2;
-  const int s = blockIdx.x / ntiles;
-  int t = blockIdx.x % ntiles;
+  int s, t;
+  if (!xcd_map(md.S, ntiles, &s, &t)) return;
   int ti = 0;
   while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
   const int tj = t - ti * (ti + 1) / 2;
   const int sh = s * md.q + h;
-  const int ns = md.n_s[s];
-  double phi, nu;
-  candidate_theta(md, s, h, which, iter, &phi, &nu);
+  const CandGen g = make_gen(md, s, h, which, iter);
   double* M = mat_slot(ms, sh, 1 - ms.cur[sh]);
   const long ld = ms.ld;
-  const double* cx = md.coords + (long)s * 2 * md.n_pad;
-  const double* cy = cx + md.n_pad;
-  const double* uh = md.u + ((long)s * md.q + h) * md.n_pad;
-  const int r = threadIdx.x & 127;
-  const int R = ti * MK_NB + r;
-  const double xr = cx[R], yr = cy[R];
+  const int R = ti * MK_NB + (threadIdx.x & 127);
   for (int cc = threadIdx.x >> 7; cc < MK_NB; cc += 2) {
     const int C = tj * MK_NB + cc;
-    double v;
-    if (R < ns && C < ns) {
-      v = (R == C) ? 1.0 : correlation(dist2d(xr, yr, cx[C], cy[C]), phi, nu, md.cov_model);
-    } else if (R == ns && C < ns) {
-      v = uh[C];
-    } else {
-      v = (R == C && R != ns) ? 1.0 : 0.0;
-    }
-    M[R + (long)C * ld] = v;
+    M[R + (long)C * ld] = g(R, C);
   }
 }
 
 // Plain matrix (no border) loaded by the host for the standalone Cholesky test path.
 
 // ---------------------------------------------------------------- Cholesky
-__global__ __launch_bounds__(256, 2) void k_chol_update(MatSet ms, int S, int h, int k) {
+// gen: C(i,k) is generated from coordinates (first touch of the tile); otherwise read.
+__global__ __launch_bounds__(256, 2) void k_chol_update(Model md, MatSet ms, int S, int h, int k, int which, int iter,
+                                                       int gen) {
   __shared__ __attribute__((aligned(16))) double lds[GB_LDS_DOUBLES];
   const int ntk = ms.nt - k;
-  const int s = blockIdx.x / ntk, i = k + blockIdx.x % ntk;
+  int s, t;
+  if (!xcd_map(S, ntk, &s, &t)) return;
+  const int i = k + t;
   const int sh = s * ms.q + h;
   double* M = mat_slot(ms, sh, 1 - ms.cur[sh]);
   const long ld = ms.ld;
   double* C = M + i * MK_NB + (long)k * MK_NB * ld;
   Acc acc;
-  acc_load(acc, C, ld);
+  if (gen) {
+    const CandGen g = make_gen(md, s, h, which, iter);
+#pragma unroll
+    for (int bm = 0; bm < 4; ++bm)
+#pragma unroll
+      for (int bn = 0; bn < 4; ++bn)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc.v[bm][bn][r] = g(i * MK_NB + acc_row(bm), k * MK_NB + acc_col(bn, r));
+  } else {
+    acc_load(acc, C, ld);
+  }
   gemm_128<true, true, true>(M + i * MK_NB, ld, M + k * MK_NB, ld, k * MK_NB, k * MK_NB, acc, lds);
   store_tile(C, ld, acc);
 }
@@ -96,7 +134,9 @@ __global__ __launch_bounds__(256, 2) void k_chol_update(MatSet ms, int S, int h,
 __global__ __launch_bounds__(256, 2) void k_chol_trsm(MatSet ms, int S, int h, int k) {
   __shared__ __attribute__((aligned(16))) double lds[GB_LDS_DOUBLES];
   const int ntk = ms.nt - k - 1;
-  const int s = blockIdx.x / ntk, i = k + 1 + blockIdx.x % ntk;
+  int s, t;
+  if (!xcd_map(S, ntk, &s, &t)) return;
+  const int i = k + 1 + t;
   const int sh = s * ms.q + h;
   const int slot = 1 - ms.cur[sh];
   double* M = mat_slot(ms, sh, slot);
