@@ -170,7 +170,7 @@ static void launch_trinv(mk_session* s, int max_entries, const int* list, const 
   for (int sz = 1; sz < nt; sz *= 2) {
     const int npairs = (nt + 2 * sz - 1) / (2 * sz);
     for (int phase = 0; phase < 2; ++phase)
-      hipLaunchKernelGGL(k_inv_level, dim3(max_entries * npairs * sz * sz), dim3(256), 0, s->stream, s->ms, list,
+      hipLaunchKernelGGL(k_inv_level, dim3(xcd_grid_h(max_entries, npairs * sz * sz)), dim3(256), 0, s->stream, s->ms, list,
                          count, sz, phase);
   }
 }
@@ -181,7 +181,7 @@ static void launch_inverse(mk_session* s, int max_entries) {
   Model& md = s->md;
   launch_trinv(s, max_entries, s->d_list, s->d_count);
   timed(s, KS_LAUUM, 0.0, [&] {
-    hipLaunchKernelGGL(k_qblocks, dim3(max_entries * nt), dim3(256), 0, s->stream, s->ms, md.n_s, s->d_list,
+    hipLaunchKernelGGL(k_qblocks, dim3(xcd_grid_h(max_entries, nt)), dim3(256), 0, s->stream, s->ms, md.n_s, s->d_list,
                        s->d_count);
   });
   hipLaunchKernelGGL(k_take_border, dim3(max_entries * ((s->n_pad + 255) / 256)), dim3(256), 0, s->stream, md, s->ms,
@@ -194,7 +194,7 @@ static void launch_pred_refresh(mk_session* s, int max_entries) {
   if (md.n_test <= 0) return;
   const int nt = s->nt;
   hipLaunchKernelGGL(k_pred_PT, dim3(max_entries * md.n_pad), dim3(256), 0, s->stream, md, s->d_plist, s->d_pcount);
-  hipLaunchKernelGGL(k_pred_var, dim3(max_entries * nt * md.ntt), dim3(256), 0, s->stream, md, s->ms, s->d_plist,
+  hipLaunchKernelGGL(k_pred_var, dim3(xcd_grid_h(max_entries, nt * md.ntt)), dim3(256), 0, s->stream, md, s->ms, s->d_plist,
                      s->d_pcount);
   hipLaunchKernelGGL(k_pred_var_reduce, dim3(max_entries * (md.n_test_pad / 256)), dim3(256), 0, s->stream, md, nt,
                      s->d_plist, s->d_pcount);

@@ -380,9 +380,8 @@ __global__ __launch_bounds__(256, 2) void k_inv_level(MatSet ms, const int* __re
   __shared__ __attribute__((aligned(16))) double lds[GB_LDS_DOUBLES];
   const int npairs = (ms.nt + 2 * sz - 1) / (2 * sz);
   const int per = npairs * sz * sz;
-  const int e = blockIdx.x / per;
-  if (e >= *count) return;
-  int t = blockIdx.x % per;
+  int e, t;
+  if (!xcd_map(*count, per, &e, &t)) return;
   const int p = t / (sz * sz);
   t %= sz * sz;
   const int T0 = 2 * p * sz, B0 = T0 + sz;
@@ -444,8 +443,8 @@ __global__ __launch_bounds__(256, 2) void k_lauum(MatSet ms, const int* __restri
 __global__ __launch_bounds__(256, 2) void k_qblocks(MatSet ms, const int* __restrict__ n_s, const int* __restrict__ list,
                                                  const int* __restrict__ count) {
   __shared__ __attribute__((aligned(16))) double lds[GB_LDS_DOUBLES];
-  const int e = blockIdx.x / ms.nt, i = blockIdx.x % ms.nt;
-  if (e >= *count) return;
+  int e, i;
+  if (!xcd_map(*count, ms.nt, &e, &i)) return;
   const int sh = list[e];
   Acc acc;
   wtw_tile(ms, sh, n_s[sh / ms.q], i, i, acc, lds);
@@ -524,9 +523,8 @@ __global__ __launch_bounds__(256, 2) void k_pred_var(Model md, MatSet ms, const 
   __shared__ __attribute__((aligned(16))) double lds[GB_LDS_DOUBLES];
   __shared__ double red[2][MK_NB];
   const int per = ms.nt * md.ntt;
-  const int e = blockIdx.x / per;
-  if (e >= *count) return;
-  const int t_ = blockIdx.x % per;
+  int e, t_;
+  if (!xcd_map(*count, per, &e, &t_)) return;
   const int i = t_ / md.ntt, tb = t_ % md.ntt;
   const int sh = list[e];
   const int s = sh / md.q;
