@@ -39,7 +39,8 @@ def parse():
     ap.add_argument("--subsets", type=int, default=250)
     ap.add_argument("--n-test", type=int, default=1000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-iters", type=int, default=6)
+    ap.add_argument("--cpu-iters", type=int, default=40)
+    ap.add_argument("--streams", type=int, default=0, help="HIP streams per GPU for subset groups (0: library default)")
     return ap.parse_args()
 
 
@@ -124,7 +125,8 @@ def main():
     n_burn_timed = int(round(0.75 * a.steps))
     burn_in = W + n_burn_timed + 1               # 1-based first kept iteration
     n_batch = (W + a.steps + 49) // 50
-    cfg = mk.SamplerConfig(1, 2, beta0, bt, n_batch=n_batch, batch_length=50, burn_in=burn_in, seed=20250114)
+    cfg = mk.SamplerConfig(1, 2, beta0, bt, n_batch=n_batch, batch_length=50, burn_in=burn_in, seed=20250114,
+                           n_streams=a.streams)
     subs = [mk.subset_data(d["y"], d["x"], 1.0, d["coords"], 1, idx[i]) for i in range(lo, hi)]
     ses = mk.Session(subs, cfg, coords_test=d["coords_test"], subset_base=lo, device=local if world > 1 else 0)
     ses.run(W)                                    # warmup
@@ -150,7 +152,7 @@ def main():
 
     st = ses.kernel_stats(mk.session.KS_CHOL_UPDATE)
     kern = {name: ses.kernel_stats(i) for name, i in
-            [("chol_update", 0), ("chol_diag", 1), ("chol_trsm", 2), ("w_sweep", 3), ("lauum", 4)]}
+            [("chol_update", 0), ("chol_diag", 1), ("chol_trsm", 2), ("w_sweep", 3), ("qblocks", 4), ("inverse", 6)]}
     ses.close()
     if rank != 0:
         if dist is not None:
@@ -175,7 +177,8 @@ def main():
         "config": {"workload": f"configs[2]: n={n}, K={K} subsets of {n // K}, exponential, q=1, "
                                f"n_test={n_test}, amcmc batches of 50, timed window {n_burn_timed} burn-in + "
                                f"{a.steps - n_burn_timed} kept (fused kriging) iterations",
-                   "subsets_per_gpu": per, "parallelism": f"subset-sharded x{world}"},
+                   "subsets_per_gpu": per, "streams_per_gpu": a.streams or 1,
+                   "parallelism": f"subset-sharded x{world}"},
         "roofline": {"bound": "mfma", "kernel": "k_chol_update (left-looking Cholesky panel GEMM, fp64 MFMA)",
                      "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP64_PEAK_TFLOPS, "traffic": _pmc_traffic(),

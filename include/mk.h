@@ -73,6 +73,8 @@ typedef struct mk_config {
   int32_t record_samples;       /* keep p.beta.theta.samples (n_samples x P)            */
   int32_t record_w;             /* keep p.w.samples ((n_s*q) x n_samples)               */
   int32_t device;               /* HIP device ordinal                                    */
+  int32_t n_streams;            /* subset groups run on this many HIP streams (0: default 1);
+                                   results do not depend on it                          */
 } mk_config;
 
 /* Caller-allocated outputs; any pointer may be NULL to skip it.
@@ -111,6 +113,37 @@ int mk_fit_predict_batched(const mk_problem* prob, const mk_config* cfg, mk_outp
 
 /* ---- combine (MK.R:123-133): out = (grid_1 + ... + grid_K) / K, sequential order ---- */
 int mk_combine(const double* grids, int32_t K, int64_t grid_len, double* out, int32_t device);
+
+/* ---- combine extension (north star; not in the reference, which averages at MK.R:123-133):
+ * per column, the Weiszfeld geometric median of the K subset quantile functions in the
+ * Wasserstein-2 metric, started from the mean.  grids: K x (n_levels x n_cols) column-major;
+ * out: n_levels x n_cols; iters (optional): [n_cols] iterations used.  n_levels <= 256. ---- */
+int mk_combine_median(const double* grids, int32_t K, int32_t n_levels, int64_t n_cols, int32_t max_iter,
+                      double tol, double* out, int32_t* iters, int32_t device);
+
+/* ---- post-combine steps (MK.R:136-165) ---- */
+typedef struct mk_summary {
+  double* sample_par;    /* samplesize x P   SamplePar  (MK.R:145)                 */
+  double* sample_w;      /* samplesize x C   Samplew    (MK.R:146)                 */
+  double* p_sample;      /* samplesize x C   p.sample   (MK.R:156-161)             */
+  double* w_quant;       /* 3 x C            w.quant    (MK.R:164)                 */
+  double* param_quant;   /* 3 x P            param.quant (MK.R:165)                */
+  double* p_quant;       /* 3 x C            quantiles of p.sample (extension)     */
+  int32_t* index;        /* samplesize       sampleparIndex - 1 (MK.R:141)         */
+} mk_summary;
+/* result: 200 x P combined parameter grid (betas first, MK.R:159); result2: 200 x C combined
+ * w.predict grid; x_test: C x p (p <= P).  Any output pointer may be NULL. */
+int mk_posterior_summary(const double* result, int32_t P, const double* result2, int64_t C,
+                         const double* x_test, int32_t p, int32_t samplesize, uint64_t seed,
+                         mk_summary* out, int32_t device);
+
+/* ---- glm start values (MK.R:53-55), once on the full data: binomial-logit IRLS with
+ * glm.fit's rules (mustart init, |dev - devold|/(|dev| + 0.1) < epsilon, maxit).
+ * y: counts, weights: trials (n each), x: n x p column-major (p <= 8).
+ * coef: [p]; vcov: p x p (dispersion 1); iters (optional). ---- */
+int mk_glm_binomial(const double* y, const double* weights, const double* x, int64_t n, int32_t p,
+                    double epsilon, int32_t maxit, double* coef, double* vcov, int32_t* iters,
+                    int32_t device);
 
 /* ---- exposed kernels for parity tests ---- */
 /* R_k = correlation(coords_k) (n x n column-major) for S point sets of n sites. */

@@ -46,12 +46,18 @@ class Config(ctypes.Structure):
                 ("w_starting", ctypes.c_double), ("w_tuning", ctypes.c_double),
                 ("phi_unif_a", _dp), ("phi_unif_b", _dp), ("nu_unif_a", _dp), ("nu_unif_b", _dp),
                 ("K_IW_df", ctypes.c_double), ("K_IW_S", _dp), ("seed", ctypes.c_uint64),
-                ("record_samples", ctypes.c_int32), ("record_w", ctypes.c_int32), ("device", ctypes.c_int32)]
+                ("record_samples", ctypes.c_int32), ("record_w", ctypes.c_int32), ("device", ctypes.c_int32),
+                ("n_streams", ctypes.c_int32)]
 
 
 class Outputs(ctypes.Structure):
     _fields_ = [("parameters", _dp), ("w_predict", _dp), ("samples", _dp), ("w_samples", _dp),
                 ("w_pred_samples", _dp), ("acceptance", _dp)]
+
+
+class Summary(ctypes.Structure):
+    _fields_ = [("sample_par", _dp), ("sample_w", _dp), ("p_sample", _dp), ("w_quant", _dp),
+                ("param_quant", _dp), ("p_quant", _dp), ("index", _ip)]
 
 
 EXPORTS = {
@@ -65,6 +71,13 @@ EXPORTS = {
     "mk_session_destroy": (None, [ctypes.c_void_p]),
     "mk_fit_predict_batched": (ctypes.c_int, [ctypes.POINTER(Problem), ctypes.POINTER(Config), ctypes.POINTER(Outputs)]),
     "mk_combine": (ctypes.c_int, [_dp, ctypes.c_int32, ctypes.c_int64, _dp, ctypes.c_int32]),
+    "mk_combine_median": (ctypes.c_int, [_dp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32,
+                                         ctypes.c_double, _dp, _ip, ctypes.c_int32]),
+    "mk_posterior_summary": (ctypes.c_int, [_dp, ctypes.c_int32, _dp, ctypes.c_int64, _dp, ctypes.c_int32,
+                                            ctypes.c_int32, ctypes.c_uint64, ctypes.POINTER(Summary),
+                                            ctypes.c_int32]),
+    "mk_glm_binomial": (ctypes.c_int, [_dp, _dp, _dp, ctypes.c_int64, ctypes.c_int32, ctypes.c_double,
+                                       ctypes.c_int32, _dp, _dp, _ip, ctypes.c_int32]),
     "mk_correlation_batched": (ctypes.c_int, [_dp, ctypes.c_int32, ctypes.c_int32, _dp, _dp, ctypes.c_int32, _dp,
                                               ctypes.c_int32]),
     "mk_cholesky_batched": (ctypes.c_int, [_dp, ctypes.c_int32, ctypes.c_int32, _dp, _dp, _dp, ctypes.c_int32]),

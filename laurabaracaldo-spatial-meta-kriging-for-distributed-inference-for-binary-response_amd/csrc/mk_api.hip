@@ -1,10 +1,15 @@
 // C ABI (include/mk.h) and the per-iteration launch schedule.
 //
-// One mk_session = one GPU's shard of subsets resident in HBM.  Each MCMC
-// iteration is a fixed sequence of stream-ordered launches with no host
-// synchronisation (data-dependent control -- which factors changed -- lives in
-// device work lists), so an iteration costs the host only launch overhead.
+// One mk_session = one GPU's shard of subsets resident in HBM.  The shard is split into
+// contiguous subset groups, each advanced by its own HIP stream: a group's iteration is a
+// fixed sequence of stream-ordered launches with no host synchronisation (data-dependent
+// control -- which factors changed -- lives in device work lists), and the groups' streams
+// overlap on the GPU, so one group's latency-bound steps (diagonal-tile factorisations,
+// the MH decisions, launch tails) run beside another group's MFMA panel updates.  A group
+// is a pointer view into the shard's arrays (every array is [subset][...]); the chains do
+// not depend on the grouping (RNG streams are keyed by global subset index).
 #include <hip/hip_runtime.h>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -39,7 +44,7 @@ extern "C" int mk_device_count(void) {
 namespace {
 
 constexpr int NKSTAT = 8;
-enum { KS_CHOL_UPDATE = 0, KS_CHOL_DIAG, KS_CHOL_TRSM, KS_SWEEP, KS_LAUUM, KS_ITER };
+enum { KS_CHOL_UPDATE = 0, KS_CHOL_DIAG, KS_CHOL_TRSM, KS_SWEEP, KS_LAUUM, KS_ITER, KS_INV };
 
 struct Stat {
   long launches = 0;
@@ -52,26 +57,89 @@ struct Timed {
   double flops;
 };
 
+// One stream's share of the shard: views of the shard arrays starting at subset s0.
+struct Group {
+  Model md{};
+  MatSet ms{};
+  hipStream_t stream = nullptr;
+  int S = 0, s0 = 0;
+  int* d_list = nullptr;   // pairs whose factor changed (inverse work list)
+  int* d_count = nullptr;
+  int* d_plist = nullptr;  // pairs needing a kriging refresh
+  int* d_pcount = nullptr;
+};
+
+Model model_view(const Model& m, int s0, int S) {
+  Model v = m;
+  v.S = S;
+  v.subset_base = m.subset_base + s0;
+  const long q = m.q, np = m.n_pad, Np = m.Np, s = s0;
+  v.n_s = m.n_s + s;
+  v.coords = m.coords + s * 2 * np;
+  v.y = m.y + s * Np;
+  v.wt = m.wt + s * Np;
+  v.X = m.X + s * m.p * Np;
+  v.beta = m.beta + s * m.p;
+  v.theta = m.theta + s * m.n_theta;
+  v.w = m.w + s * Np;
+  v.eta = m.eta + s * Np;
+  v.tune = m.tune + s * m.n_mh_max;
+  v.acc = m.acc + s * m.n_mh_max;
+  v.u = m.u + s * q * np;
+  v.z = m.z + s * q * np;
+  v.Z = m.Z + s * q * q * np;
+  v.logdetR = m.logdetR + s * q;
+  v.quad = m.quad + s * q;
+  v.A_full = m.A_full + s * q * q;
+  v.Ainv = m.Ainv + s * q * q;
+  v.dirty = m.dirty + s * q;
+  v.ld_part = m.ld_part + s * m.nt;
+  v.quad_c = m.quad_c + s;
+  v.info = m.info + s;
+  v.sw_delta = m.sw_delta + s * Np;
+  v.sw_dll = m.sw_dll + s * Np;
+  v.sw_logu = m.sw_logu + s * Np;
+  v.sw_acc = m.sw_acc + s * Np;
+  v.samples = m.samples + s * m.n_samples * m.P;
+  v.acc_hist = m.acc_hist + s * m.n_batch * (m.o_w + 1);
+  if (m.w_samples) v.w_samples = m.w_samples + s * m.n_samples * Np;
+  v.s_pred = m.s_pred + s * q * m.n_test_pad;
+  v.s_part = m.s_part + s * q * m.nt * m.n_test_pad;
+  if (m.PT) v.PT = m.PT + s * q * np * m.n_test_pad;
+  if (m.XK) v.XK = m.XK + s * q * np * m.n_test_pad;
+  v.w_pred = m.w_pred + s * m.n_kept * q * (long)std::max(m.n_test, 1);
+  return v;
+}
+
+MatSet matset_view(const MatSet& m, int s0) {
+  MatSet v = m;
+  const long sq = (long)s0 * m.q, e = (long)m.ld * m.ld, wt = (long)m.nt * MK_NB * MK_NB;
+  v.L = m.L + sq * 2 * e;
+  v.Winv = m.Winv + sq * 2 * wt;
+  v.W = m.W + sq * e;
+  if (m.Q) v.Q = m.Q + sq * e;
+  if (m.QB) v.QB = m.QB + sq * wt;
+  v.cur = m.cur + sq;
+  return v;
+}
+
 }  // namespace
 
 struct mk_session {
   int device = 0;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;   // set-up, outputs and the one-group paths
   Model md{};
   MatSet ms{};
   int S = 0, q = 1, p = 0, n_pad = 0, nt = 0, P = 0;
   int iter = 0;
   bool matern = false, record_samples = true, record_w = false;
-  int* d_list = nullptr;     // pairs whose factor changed (inverse work list)
-  int* d_count = nullptr;
-  int* d_plist = nullptr;    // pairs needing a kriging refresh
-  int* d_pcount = nullptr;
+  Group all;                      // the whole shard on `stream`
+  std::vector<Group> groups;      // the run-time split, one stream each
   double* d_probs = nullptr;
   std::vector<int> n_part;
   std::vector<void*> allocs;
   bool prof = false;
   std::vector<Timed> pending;
-  std::vector<hipEvent_t> pool;
   Stat stats[NKSTAT];
 
   template <typename T>
@@ -87,6 +155,8 @@ struct mk_session {
   ~mk_session() {
     if (device >= 0) hipSetDevice(device);
     for (auto& t : pending) { hipEventDestroy(t.a); hipEventDestroy(t.b); }
+    for (auto& g : groups)
+      if (g.stream && g.stream != stream) hipStreamDestroy(g.stream);
     for (void* p_ : allocs) hipFree(p_);
     if (stream) hipStreamDestroy(stream);
   }
@@ -98,17 +168,17 @@ static hipEvent_t ev_new() {
   return e;
 }
 
-// Launch helper that optionally brackets a kernel with events.
+// Launch helper that optionally brackets a kernel with events on its stream.
 template <typename F>
-static void timed(mk_session* s, int which, double flops, F&& launch) {
+static void timed(mk_session* s, hipStream_t st, int which, double flops, F&& launch) {
   if (!s->prof) {
     launch();
     return;
   }
   Timed t{which, ev_new(), ev_new(), flops};
-  hipEventRecord(t.a, s->stream);
+  hipEventRecord(t.a, st);
   launch();
-  hipEventRecord(t.b, s->stream);
+  hipEventRecord(t.b, st);
   s->pending.push_back(t);
 }
 
@@ -130,113 +200,104 @@ static inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
 
 // ------------------------------------------------------------------ Cholesky of all candidates of outcome h
 // gen: candidate tiles generated from coordinates (session); otherwise preloaded (test entry).
-static void launch_cholesky(mk_session* s, int h, int S_launch, int which, int iter, bool gen) {
-  const int nt = s->nt;
+static void launch_cholesky(mk_session* s, Group& g, int h, int which, int iter, bool gen) {
+  const int nt = s->nt, S = g.S;
   const size_t diag_lds = (size_t)(MK_NB * MK_NB + 2 * MK_NB + 4 * 256) * sizeof(double);
-  Model& md = s->md;
   // valid extent (excludes padding) for the algorithmic flop count
-  const double nv = (double)s->n_part[0] + 1.0;
+  const double nv = (double)s->n_part[g.s0] + 1.0;
   for (int k = 0; k < nt; ++k) {
     if (k > 0) {
       // algorithmic flops: rows below panel start x panel cols x K, clipped to the valid extent
       const double rows = std::fmax(0.0, nv - k * MK_NB);
       const double cols = std::fmin((double)MK_NB, std::fmax(0.0, nv - k * MK_NB));
       const double kk = std::fmin((double)k * MK_NB, nv);
-      const double fl = 2.0 * rows * cols * kk * S_launch;
-      timed(s, KS_CHOL_UPDATE, fl, [&] {
-        hipLaunchKernelGGL(k_chol_update, dim3(xcd_grid_h(S_launch, nt - k)), dim3(256), 0, s->stream, md, s->ms,
-                           S_launch, h, k, which, iter, (int)gen);
+      const double fl = 2.0 * rows * cols * kk * S;
+      timed(s, g.stream, KS_CHOL_UPDATE, fl, [&] {
+        hipLaunchKernelGGL(k_chol_update, dim3(xcd_grid_h(S, nt - k)), dim3(256), 0, g.stream, g.md, g.ms, S, h, k,
+                           which, iter, (int)gen);
       });
     }
-    timed(s, KS_CHOL_DIAG, 0.0, [&] {
-      hipLaunchKernelGGL(k_chol_diag, dim3(S_launch), dim3(256), diag_lds, s->stream, s->ms, md.n_s, h, k, md.ld_part,
-                         md.quad_c, md.info);
+    timed(s, g.stream, KS_CHOL_DIAG, 0.0, [&] {
+      hipLaunchKernelGGL(k_chol_diag, dim3(S), dim3(256), diag_lds, g.stream, g.ms, g.md.n_s, h, k, g.md.ld_part,
+                         g.md.quad_c, g.md.info);
     });
     if (k < nt - 1) {
       const double rows = std::fmax(0.0, nv - (k + 1) * MK_NB);
-      const double fl = 2.0 * rows * MK_NB * MK_NB * S_launch;
-      timed(s, KS_CHOL_TRSM, fl, [&] {
-        hipLaunchKernelGGL(k_chol_trsm, dim3(xcd_grid_h(S_launch, nt - k - 1)), dim3(256), 0, s->stream, s->ms,
-                           S_launch, h, k);
+      const double fl = 2.0 * rows * MK_NB * MK_NB * S;
+      timed(s, g.stream, KS_CHOL_TRSM, fl, [&] {
+        hipLaunchKernelGGL(k_chol_trsm, dim3(xcd_grid_h(S, nt - k - 1)), dim3(256), 0, g.stream, g.ms, S, h, k);
       });
     }
   }
 }
 
 // W = L^-1 of the listed pairs: diagonal tiles, then recursive doubling.
-static void launch_trinv(mk_session* s, int max_entries, const int* list, const int* count) {
+static void launch_trinv(mk_session* s, Group& g, int max_entries, const int* list, const int* count) {
   const int nt = s->nt;
-  hipLaunchKernelGGL(k_inv_copydiag, dim3(max_entries * nt), dim3(256), 0, s->stream, s->ms, list, count);
+  hipLaunchKernelGGL(k_inv_copydiag, dim3(max_entries * nt), dim3(256), 0, g.stream, g.ms, list, count);
   for (int sz = 1; sz < nt; sz *= 2) {
     const int npairs = (nt + 2 * sz - 1) / (2 * sz);
     for (int phase = 0; phase < 2; ++phase)
-      hipLaunchKernelGGL(k_inv_level, dim3(xcd_grid_h(max_entries, npairs * sz * sz)), dim3(256), 0, s->stream, s->ms, list,
-                         count, sz, phase);
+      timed(s, g.stream, KS_INV, 0.0, [&] {
+        hipLaunchKernelGGL(k_inv_level, dim3(xcd_grid_h(max_entries, npairs * sz * sz)), dim3(256), 0, g.stream, g.ms,
+                           list, count, sz, phase);
+      });
   }
 }
 
 // W = L^-1 for the changed factors, diagonal tiles of R^-1, z from the bordered row.
-static void launch_inverse(mk_session* s, int max_entries) {
-  const int nt = s->nt;
-  Model& md = s->md;
-  launch_trinv(s, max_entries, s->d_list, s->d_count);
-  timed(s, KS_LAUUM, 0.0, [&] {
-    hipLaunchKernelGGL(k_qblocks, dim3(xcd_grid_h(max_entries, nt)), dim3(256), 0, s->stream, s->ms, md.n_s, s->d_list,
-                       s->d_count);
+static void launch_inverse(mk_session* s, Group& g) {
+  const int nt = s->nt, max_entries = g.S * s->q;
+  launch_trinv(s, g, max_entries, g.d_list, g.d_count);
+  timed(s, g.stream, KS_LAUUM, 0.0, [&] {
+    hipLaunchKernelGGL(k_qblocks, dim3(xcd_grid_h(max_entries, nt)), dim3(256), 0, g.stream, g.ms, g.md.n_s, g.d_list,
+                       g.d_count);
   });
-  hipLaunchKernelGGL(k_take_border, dim3(max_entries * ((s->n_pad + 255) / 256)), dim3(256), 0, s->stream, md, s->ms,
-                     s->d_list, s->d_count);
+  hipLaunchKernelGGL(k_take_border, dim3(max_entries * ((s->n_pad + 255) / 256)), dim3(256), 0, g.stream, g.md, g.ms,
+                     g.d_list, g.d_count);
 }
 
 // Kriging refresh (kept iterations): P^T, X = W P^T and s = |X_t|^2 for the pairs in the pred list.
-static void launch_pred_refresh(mk_session* s, int max_entries) {
-  Model& md = s->md;
+static void launch_pred_refresh(mk_session* s, Group& g) {
+  Model& md = g.md;
   if (md.n_test <= 0) return;
-  const int nt = s->nt;
-  hipLaunchKernelGGL(k_pred_PT, dim3(max_entries * md.n_pad), dim3(256), 0, s->stream, md, s->d_plist, s->d_pcount);
-  hipLaunchKernelGGL(k_pred_var, dim3(xcd_grid_h(max_entries, nt * md.ntt)), dim3(256), 0, s->stream, md, s->ms, s->d_plist,
-                     s->d_pcount);
-  hipLaunchKernelGGL(k_pred_var_reduce, dim3(max_entries * (md.n_test_pad / 256)), dim3(256), 0, s->stream, md, nt,
-                     s->d_plist, s->d_pcount);
+  const int nt = s->nt, max_entries = g.S * s->q;
+  hipLaunchKernelGGL(k_pred_PT, dim3(max_entries * md.n_pad), dim3(256), 0, g.stream, md, g.d_plist, g.d_pcount);
+  hipLaunchKernelGGL(k_pred_var, dim3(xcd_grid_h(max_entries, nt * md.ntt)), dim3(256), 0, g.stream, md, g.ms,
+                     g.d_plist, g.d_pcount);
+  hipLaunchKernelGGL(k_pred_var_reduce, dim3(max_entries * (md.n_test_pad / 256)), dim3(256), 0, g.stream, md, nt,
+                     g.d_plist, g.d_pcount);
 }
 
-static int run_iteration(mk_session* s) {
-  Model& md = s->md;
-  const int it = s->iter;
-  const int S = s->S, q = s->q;
+static void run_iteration(mk_session* s, Group& g, int it) {
+  Model& md = g.md;
+  const int S = g.S, q = s->q;
   const bool kept = it >= md.kept0;
-  hipLaunchKernelGGL(k_beta, dim3(S), dim3(256), 0, s->stream, md, it);
-  if (q > 1)
-    hipLaunchKernelGGL(k_trmv_Z, dim3(S * q * ((s->n_pad + 255) / 256)), dim3(256), 0, s->stream, md, s->ms);
-  hipLaunchKernelGGL(k_Aphase, dim3(S), dim3(256), 0, s->stream, md, it);
+  hipStream_t st = g.stream;
+  hipLaunchKernelGGL(k_beta, dim3(S), dim3(256), 0, st, md, it);
+  if (q > 1) hipLaunchKernelGGL(k_trmv_Z, dim3(S * q * ((s->n_pad + 255) / 256)), dim3(256), 0, st, md, g.ms);
+  hipLaunchKernelGGL(k_Aphase, dim3(S), dim3(256), 0, st, md, it);
   const int nkinds = s->matern ? 2 : 1;
   const int ntri_tiles = s->nt * (s->nt + 1) / 2;
   for (int which = 0; which < nkinds; ++which)
     for (int h = 0; h < q; ++h) {
-      hipLaunchKernelGGL(k_cov_candidate, dim3(xcd_grid_h(S, ntri_tiles)), dim3(256), 0, s->stream, md, s->ms, h,
-                         which, it);
-      launch_cholesky(s, h, S, which, it, false);
-      hipLaunchKernelGGL(k_theta_mh, dim3((S + 63) / 64), dim3(64), 0, s->stream, md, s->ms, h, which, it);
+      hipLaunchKernelGGL(k_cov_candidate, dim3(xcd_grid_h(S, ntri_tiles)), dim3(256), 0, st, md, g.ms, h, which, it);
+      launch_cholesky(s, g, h, which, it, false);
+      hipLaunchKernelGGL(k_theta_mh, dim3((S + 63) / 64), dim3(64), 0, st, md, g.ms, h, which, it);
     }
-  hipLaunchKernelGGL(k_dirty_list, dim3(1), dim3(256), 0, s->stream, md, (int)(it == md.kept0), s->d_list, s->d_count,
-                     s->d_plist, s->d_pcount);
-  launch_inverse(s, S * q);
-  if (kept) launch_pred_refresh(s, S * q);
+  hipLaunchKernelGGL(k_dirty_list, dim3(1), dim3(256), 0, st, md, (int)(it == md.kept0), g.d_list, g.d_count,
+                     g.d_plist, g.d_pcount);
+  launch_inverse(s, g);
+  if (kept) launch_pred_refresh(s, g);
   const size_t sw_lds = (size_t)q * (64 * 64 + 2 * 64) * sizeof(double);
-  timed(s, KS_SWEEP, 0.0, [&] {
-    hipLaunchKernelGGL(k_sweep, dim3(S), dim3(512), sw_lds, s->stream, md, s->ms, it);
-  });
-  if (s->record_samples) hipLaunchKernelGGL(k_record, dim3((S + 63) / 64), dim3(64), 0, s->stream, md, it);
-  if (s->record_w) hipLaunchKernelGGL(k_record_w, dim3((md.Np + 255) / 256, S), dim3(256), 0, s->stream, md, it);
+  timed(s, st, KS_SWEEP, 0.0, [&] { hipLaunchKernelGGL(k_sweep, dim3(S), dim3(512), sw_lds, st, md, g.ms, it); });
+  if (s->record_samples) hipLaunchKernelGGL(k_record, dim3((S + 63) / 64), dim3(64), 0, st, md, it);
+  if (s->record_w) hipLaunchKernelGGL(k_record_w, dim3((md.Np + 255) / 256, S), dim3(256), 0, st, md, it);
   if (kept && md.n_test > 0) {
     const int per = (md.n_test + 3) / 4;
-    hipLaunchKernelGGL(k_pred_draw, dim3(S * per), dim3(256), 0, s->stream, md, it, it - md.kept0);
+    hipLaunchKernelGGL(k_pred_draw, dim3(S * per), dim3(256), 0, st, md, it, it - md.kept0);
   }
-  if ((it + 1) % md.batch_length == 0)
-    hipLaunchKernelGGL(k_adapt, dim3(S), dim3(256), 0, s->stream, md, it / md.batch_length);
-  s->iter++;
-  HIPCHK(hipGetLastError());
-  return 0;
+  if ((it + 1) % md.batch_length == 0) hipLaunchKernelGGL(k_adapt, dim3(S), dim3(256), 0, st, md, it / md.batch_length);
 }
 
 static int check_cfg(const mk_problem* pr, const mk_config* c) {
@@ -251,6 +312,7 @@ static int check_cfg(const mk_problem* pr, const mk_config* c) {
   const int n_samples = c->n_batch * c->batch_length;
   if (c->burn_in < 1 || c->burn_in > n_samples) return set_err(MK_E_ARG, "burn_in must be in [1, n.samples]");
   if (n_samples - c->burn_in + 1 > 2048) return set_err(MK_E_ARG, "at most 2048 kept samples supported");
+  if (c->n_streams < 0 || c->n_streams > 8) return set_err(MK_E_ARG, "n_streams must be in [0, 8]");
   if (!c->beta_starting || !c->beta_tuning || !c->phi_starting || !c->phi_tuning || !c->A_starting || !c->A_tuning ||
       !c->phi_unif_a || !c->phi_unif_b || !c->K_IW_S)
     return set_err(MK_E_ARG, "null starting/tuning/prior array");
@@ -261,6 +323,45 @@ static int check_cfg(const mk_problem* pr, const mk_config* c) {
   for (int h = 0; h < pr->q; ++h) {
     if (!(c->phi_unif_a[h] < c->phi_starting[h] && c->phi_starting[h] < c->phi_unif_b[h]))
       return set_err(MK_E_ARG, "phi starting value outside phi.Unif support");
+  }
+  return 0;
+}
+
+// Work lists for `ng` run groups + the whole-shard view (last): list/plist per pair, 2 counts per view.
+static int setup_groups(mk_session* s, int n_groups) {
+  const int S = s->S, q = s->q;
+  const int G = std::max(1, std::min(n_groups, S));
+  int *lists = nullptr, *counts = nullptr;
+  int rc;
+  if ((rc = s->alloc(&lists, (size_t)4 * S * q)) || (rc = s->alloc(&counts, (size_t)2 * (G + 1)))) return rc;
+  s->all.md = s->md;
+  s->all.ms = s->ms;
+  s->all.stream = s->stream;
+  s->all.S = S;
+  s->all.s0 = 0;
+  s->all.d_list = lists;
+  s->all.d_plist = lists + S * q;
+  s->all.d_count = counts + 2 * G;
+  s->all.d_pcount = counts + 2 * G + 1;
+  const int per = (S + G - 1) / G;
+  for (int gi = 0; gi < G; ++gi) {
+    const int s0 = gi * per, Sg = std::min(per, S - s0);
+    if (Sg <= 0) break;
+    Group g;
+    g.S = Sg;
+    g.s0 = s0;
+    g.md = model_view(s->md, s0, Sg);
+    g.ms = matset_view(s->ms, s0);
+    g.d_list = lists + 2 * S * q + s0 * q;
+    g.d_plist = lists + 3 * S * q + s0 * q;
+    g.d_count = counts + 2 * gi;
+    g.d_pcount = counts + 2 * gi + 1;
+    if (G == 1) {
+      g.stream = s->stream;
+    } else if (hipStreamCreateWithFlags(&g.stream, hipStreamNonBlocking) != hipSuccess) {
+      return set_err(MK_E_HIP, "group stream");
+    }
+    s->groups.push_back(g);
   }
   return 0;
 }
@@ -284,8 +385,7 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
   s->matern = c->cov_model == MK_COV_MATERN;
   s->n_part.assign(pr->n_part, pr->n_part + S);
   int nmax = 0;
-  long tot_sites = 0;
-  for (int i = 0; i < S; ++i) { nmax = std::max(nmax, (int)pr->n_part[i]); tot_sites += pr->n_part[i]; }
+  for (int i = 0; i < S; ++i) nmax = std::max(nmax, (int)pr->n_part[i]);
   const int n_pad = round_up(nmax + 1, MK_NB);
   const int nt = n_pad / MK_NB;
   s->n_pad = n_pad; s->nt = nt;
@@ -356,10 +456,9 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
       (rc = s->alloc(&ms.Winv, (size_t)S * q * 2 * nt * MK_NB * MK_NB)) ||
       (rc = s->alloc(&ms.W, (size_t)S * q * n_pad * n_pad)) ||
       (rc = s->alloc(&ms.QB, (size_t)S * q * nt * MK_NB * MK_NB)) || (rc = s->alloc(&ms.cur, (size_t)S * q)) ||
-      (rc = s->alloc(&s->d_list, (size_t)S * q)) || (rc = s->alloc(&s->d_count, 1)) ||
-      (rc = s->alloc(&s->d_plist, (size_t)S * q)) || (rc = s->alloc(&s->d_pcount, 1)) ||
       (rc = s->alloc(&s->d_probs, MK_N_LEVELS)))
     return fail(rc);
+  if ((rc = setup_groups(s, c->n_streams > 0 ? c->n_streams : 1))) return fail(rc);
 
   // ---------------- host staging (R layout -> padded device layout)
   std::vector<double> hc((size_t)S * 2 * n_pad, 0.0), hy((size_t)S * Np, 0.0), hw((size_t)S * Np, 0.0),
@@ -473,20 +572,19 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
   HIPCHK(hipFuncSetAttribute((const void*)k_sweep, hipFuncAttributeMaxDynamicSharedMemorySize,
                              q * (64 * 64 + 2 * 64) * 8));
 
-  // ---------------- initial state: eta, u, factor every R_h at the starting values, Q, g
+  // ---------------- initial state: eta, u, factor every R_h at the starting values, W, z (whole shard)
+  Group& a = s->all;
   hipLaunchKernelGGL(k_init_state, dim3(S), dim3(256), 0, s->stream, md);
   const int ntri_tiles = nt * (nt + 1) / 2;
   for (int h = 0; h < q; ++h) {
     hipLaunchKernelGGL(k_cov_candidate, dim3(xcd_grid_h(S, ntri_tiles)), dim3(256), 0, s->stream, md, ms, h, 2, 0);
-    launch_cholesky(s, h, S, 2, 0, false);
+    launch_cholesky(s, a, h, 2, 0, false);
     hipLaunchKernelGGL(k_theta_init, dim3((S + 63) / 64), dim3(64), 0, s->stream, md, ms, h);
   }
-  hipLaunchKernelGGL(k_dirty_list, dim3(1), dim3(256), 0, s->stream, md, 0, s->d_list, s->d_count, s->d_plist,
-                     s->d_pcount);
-  launch_inverse(s, S * q);
+  hipLaunchKernelGGL(k_dirty_list, dim3(1), dim3(256), 0, s->stream, md, 0, a.d_list, a.d_count, a.d_plist, a.d_pcount);
+  launch_inverse(s, a);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(s->stream));
-  s->stats[0] = Stat(); s->stats[1] = Stat(); s->stats[2] = Stat(); s->stats[4] = Stat();
   drain_timers(s);
   for (auto& st : s->stats) st = Stat();
   *out = s;
@@ -497,21 +595,16 @@ extern "C" int mk_session_run(mk_session* s, int32_t n_iter) {
   if (!s) return set_err(MK_E_ARG, "null session");
   HIPCHK(hipSetDevice(s->device));
   if (n_iter < 0 || s->iter + n_iter > s->md.n_samples) return set_err(MK_E_ARG, "n_iter beyond n.samples");
-  hipEvent_t a = nullptr, b = nullptr;
-  if (s->prof) { a = ev_new(); b = ev_new(); hipEventRecord(a, s->stream); }
+  const auto t0 = std::chrono::steady_clock::now();
   for (int i = 0; i < n_iter; ++i) {
-    int rc = run_iteration(s);
-    if (rc) return rc;
+    for (auto& g : s->groups) run_iteration(s, g, s->iter);
+    s->iter++;
+    HIPCHK(hipGetLastError());
   }
-  if (s->prof) hipEventRecord(b, s->stream);
-  HIPCHK(hipStreamSynchronize(s->stream));
+  for (auto& g : s->groups) HIPCHK(hipStreamSynchronize(g.stream));
   if (s->prof) {
-    float ms = 0.f;
-    hipEventElapsedTime(&ms, a, b);
     s->stats[KS_ITER].launches += n_iter;
-    s->stats[KS_ITER].ms += ms;
-    hipEventDestroy(a);
-    hipEventDestroy(b);
+    s->stats[KS_ITER].ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     drain_timers(s);
   }
   return 0;
@@ -623,22 +716,245 @@ extern "C" int mk_fit_predict_batched(const mk_problem* pr, const mk_config* c, 
   return rc;
 }
 
+// ------------------------------------------------------------------ device scratch for the one-shot entry points
+namespace {
+struct DevBufs {
+  std::vector<void*> p;
+  ~DevBufs() {
+    for (void* x : p) hipFree(x);
+  }
+  template <typename T>
+  T* get(size_t n) {
+    void* x = nullptr;
+    if (hipMalloc(&x, std::max<size_t>(n, 1) * sizeof(T)) != hipSuccess) return nullptr;
+    p.push_back(x);
+    return (T*)x;
+  }
+};
+
+// R's seq.default(from, to, by) for by > 0: from + (0:n)*by, n = as.integer(del/by + 1e-10), pmin(x, to).
+std::vector<double> r_seq(double from, double to, double by) {
+  const int n = (int)((to - from) / by + 1e-10);
+  std::vector<double> x(n + 1);
+  for (int i = 0; i <= n; ++i) x[i] = std::fmin(from + (double)i * by, to);
+  return x;
+}
+}  // namespace
+
 // ------------------------------------------------------------------ combine
 extern "C" int mk_combine(const double* grids, int32_t K, int64_t G, double* out, int32_t device) {
   if (!grids || !out || K < 1 || G < 1) return set_err(MK_E_ARG, "bad combine arguments");
   HIPCHK(hipSetDevice(device));
-  double *dg = nullptr, *dout = nullptr;
-  HIPCHK(hipMalloc(&dg, (size_t)K * G * 8));
-  if (hipMalloc(&dout, (size_t)G * 8) != hipSuccess) { hipFree(dg); return set_err(MK_E_NOMEM, "combine alloc"); }
-  hipError_t e = hipMemcpy(dg, grids, (size_t)K * G * 8, hipMemcpyHostToDevice);
-  if (e == hipSuccess) {
-    hipLaunchKernelGGL(k_combine, dim3((unsigned)((G + 255) / 256)), dim3(256), 0, 0, dg, K, (long)G, dout);
-    e = hipGetLastError();
+  DevBufs b;
+  double* dg = b.get<double>((size_t)K * G);
+  double* dout = b.get<double>((size_t)G);
+  if (!dg || !dout) return set_err(MK_E_NOMEM, "combine alloc");
+  HIPCHK(hipMemcpy(dg, grids, (size_t)K * G * 8, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(k_combine, dim3((unsigned)((G + 255) / 256)), dim3(256), 0, 0, dg, K, (long)G, dout);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpy(out, dout, (size_t)G * 8, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+extern "C" int mk_combine_median(const double* grids, int32_t K, int32_t L, int64_t C, int32_t max_iter, double tol,
+                                 double* out, int32_t* iters, int32_t device) {
+  if (!grids || !out || K < 1 || L < 1 || L > 256 || C < 1 || max_iter < 1 || !(tol >= 0.0))
+    return set_err(MK_E_ARG, "bad combine_median arguments (1 <= n_levels <= 256, max_iter >= 1, tol >= 0)");
+  HIPCHK(hipSetDevice(device));
+  DevBufs b;
+  const size_t G = (size_t)L * C;
+  double* dg = b.get<double>((size_t)K * G);
+  double* dout = b.get<double>(G);
+  int* dit = b.get<int>((size_t)C);
+  if (!dg || !dout || !dit) return set_err(MK_E_NOMEM, "combine_median alloc");
+  HIPCHK(hipMemcpy(dg, grids, (size_t)K * G * 8, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(k_weiszfeld, dim3((unsigned)((C + 3) / 4)), dim3(256), 0, 0, dg, K, L, (long)C, max_iter, tol, dout,
+                     dit);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpy(out, dout, G * 8, hipMemcpyDeviceToHost));
+  if (iters) HIPCHK(hipMemcpy(iters, dit, (size_t)C * 4, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+// ------------------------------------------------------------------ post-combine steps (MK.R:136-165)
+extern "C" int mk_posterior_summary(const double* result, int32_t P, const double* result2, int64_t C,
+                                    const double* x_test, int32_t p, int32_t S, uint64_t seed, mk_summary* o,
+                                    int32_t device) {
+  if (!result || !o || P < 1 || C < 0 || p < 0 || p > P || S < 1 || S > 2048)
+    return set_err(MK_E_ARG, "bad posterior_summary arguments (P >= 1, 0 <= p <= P, 1 <= samplesize <= 2048)");
+  if (C > 0 && (!result2 || (p > 0 && !x_test))) return set_err(MK_E_ARG, "result2 / x_test missing");
+  HIPCHK(hipSetDevice(device));
+  const int L = MK_N_LEVELS;
+  const std::vector<double> xg = r_seq(0.005, 1.0, 0.005);   // allquant levels (MK.R:88)
+  const std::vector<double> xo = r_seq(0.005, 1.0, 0.001);   // Xout (MK.R:140)
+  const int n = (int)xg.size(), NL = (int)xo.size();
+  if (n != L) return set_err(MK_E_ARG, "internal: probs grid");
+  // stats/src/approx.c approx1: bisection to x[i] <= v <= x[j], exact hits return y
+  std::vector<int> lo(NL), hi(NL), mode(NL);
+  std::vector<double> tt(NL, 0.0);
+  for (int k = 0; k < NL; ++k) {
+    const double v = xo[k];
+    int i = 0, j = n - 1;
+    while (i < j - 1) {
+      const int ij = (i + j) / 2;
+      if (v < xg[ij]) j = ij; else i = ij;
+    }
+    lo[k] = i;
+    hi[k] = j;
+    if (v == xg[j]) mode[k] = 0;
+    else if (v == xg[i]) mode[k] = 1;
+    else { mode[k] = 2; tt[k] = (v - xg[i]) / (xg[j] - xg[i]); }
   }
-  if (e == hipSuccess) e = hipMemcpy(out, dout, (size_t)G * 8, hipMemcpyDeviceToHost);
-  hipFree(dg);
-  hipFree(dout);
-  if (e != hipSuccess) return set_err(MK_E_HIP, std::string("combine: ") + hipGetErrorString(e));
+  const double probs3[3] = {0.5, 0.025, 0.975};   // quant.pred (MK.R:163)
+  DevBufs b;
+  const size_t Cs = (size_t)std::max<int64_t>(C, 1);
+  double* d_res = b.get<double>((size_t)L * P);
+  double* d_res2 = b.get<double>((size_t)L * Cs);
+  double* d_xt = b.get<double>(Cs * std::max(p, 1));
+  int* d_idx = b.get<int>(S);
+  int* d_lo = b.get<int>(NL);
+  int* d_hi = b.get<int>(NL);
+  int* d_mode = b.get<int>(NL);
+  double* d_t = b.get<double>(NL);
+  double* d_spar = b.get<double>((size_t)S * P);
+  double* d_sw = b.get<double>((size_t)S * Cs);
+  double* d_p = b.get<double>((size_t)S * Cs);
+  double* d_q = b.get<double>((size_t)3 * std::max<size_t>(Cs, P));
+  double* d_pr = b.get<double>(3);
+  if (!d_res || !d_res2 || !d_xt || !d_idx || !d_lo || !d_hi || !d_mode || !d_t || !d_spar || !d_sw || !d_p || !d_q ||
+      !d_pr)
+    return set_err(MK_E_NOMEM, "posterior_summary alloc");
+  hipStream_t st = 0;
+  HIPCHK(hipMemcpy(d_res, result, (size_t)L * P * 8, hipMemcpyHostToDevice));
+  if (C > 0) HIPCHK(hipMemcpy(d_res2, result2, (size_t)L * C * 8, hipMemcpyHostToDevice));
+  if (C > 0 && p > 0) HIPCHK(hipMemcpy(d_xt, x_test, (size_t)C * p * 8, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(d_lo, lo.data(), NL * 4, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(d_hi, hi.data(), NL * 4, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(d_mode, mode.data(), NL * 4, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(d_t, tt.data(), NL * 8, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(d_pr, probs3, 3 * 8, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(k_post_index, dim3((S + 255) / 256), dim3(256), 0, st, seed, S, NL, d_idx);
+  hipLaunchKernelGGL(k_post_interp, dim3((unsigned)(((long)S * P + 255) / 256)), dim3(256), 0, st, d_res, L, (long)P,
+                     d_idx, S, d_lo, d_hi, d_mode, d_t, d_spar);
+  if (C > 0) {
+    const unsigned nb = (unsigned)(((long)S * C + 255) / 256);
+    hipLaunchKernelGGL(k_post_interp, dim3(nb), dim3(256), 0, st, d_res2, L, (long)C, d_idx, S, d_lo, d_hi, d_mode, d_t,
+                       d_sw);
+    hipLaunchKernelGGL(k_post_prob, dim3(nb), dim3(256), 0, st, d_spar, S, d_xt, (long)C, p, d_sw, d_p);
+  }
+  HIPCHK(hipGetLastError());
+  if (o->index) HIPCHK(hipMemcpy(o->index, d_idx, (size_t)S * 4, hipMemcpyDeviceToHost));
+  if (o->sample_par) HIPCHK(hipMemcpy(o->sample_par, d_spar, (size_t)S * P * 8, hipMemcpyDeviceToHost));
+  if (C > 0 && o->sample_w) HIPCHK(hipMemcpy(o->sample_w, d_sw, (size_t)S * C * 8, hipMemcpyDeviceToHost));
+  if (C > 0 && o->p_sample) HIPCHK(hipMemcpy(o->p_sample, d_p, (size_t)S * C * 8, hipMemcpyDeviceToHost));
+  // type-7 (0.5, 0.025, 0.975) per column: each column is S contiguous rows -> 3 x ncol column-major
+  auto quant = [&](const double* src, long ncol, double* dst) -> int {
+    hipLaunchKernelGGL(k_quantiles, dim3((unsigned)ncol), dim3(256), 0, st, src, (long)S, 1L, S, 1, d_pr, 3, d_q);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpy(dst, d_q, (size_t)ncol * 3 * 8, hipMemcpyDeviceToHost));
+    return 0;
+  };
+  int rc;
+  if (o->param_quant && (rc = quant(d_spar, P, o->param_quant))) return rc;
+  if (C > 0 && o->w_quant && (rc = quant(d_sw, C, o->w_quant))) return rc;
+  if (C > 0 && o->p_quant && (rc = quant(d_p, C, o->p_quant))) return rc;
+  return 0;
+}
+
+// ------------------------------------------------------------------ glm start values (MK.R:53-55)
+// p x p symmetric positive definite solve / inverse through a host Cholesky (p <= 8).
+static bool chol_small(const std::vector<double>& A, int p, std::vector<double>& Lc) {
+  Lc.assign((size_t)p * p, 0.0);
+  for (int j = 0; j < p; ++j) {
+    double d = A[j + j * p];
+    for (int k = 0; k < j; ++k) d -= Lc[j + k * p] * Lc[j + k * p];
+    if (!(d > 0.0)) return false;
+    d = std::sqrt(d);
+    Lc[j + j * p] = d;
+    for (int i = j + 1; i < p; ++i) {
+      double v = A[i + j * p];
+      for (int k = 0; k < j; ++k) v -= Lc[i + k * p] * Lc[j + k * p];
+      Lc[i + j * p] = v / d;
+    }
+  }
+  return true;
+}
+static void chol_solve_small(const std::vector<double>& Lc, int p, const double* b, double* x) {
+  std::vector<double> y(p);
+  for (int i = 0; i < p; ++i) {
+    double v = b[i];
+    for (int k = 0; k < i; ++k) v -= Lc[i + k * p] * y[k];
+    y[i] = v / Lc[i + i * p];
+  }
+  for (int i = p - 1; i >= 0; --i) {
+    double v = y[i];
+    for (int k = i + 1; k < p; ++k) v -= Lc[k + i * p] * x[k];
+    x[i] = v / Lc[i + i * p];
+  }
+}
+
+extern "C" int mk_glm_binomial(const double* y, const double* weights, const double* x, int64_t n, int32_t p,
+                               double epsilon, int32_t maxit, double* coef, double* vcov, int32_t* iters,
+                               int32_t device) {
+  if (!y || !weights || !x || !coef || n < 1 || p < 1 || p > 8 || maxit < 1)
+    return set_err(MK_E_ARG, "bad glm arguments (n >= 1, 1 <= p <= 8, maxit >= 1)");
+  HIPCHK(hipSetDevice(device));
+  std::vector<double> yp((size_t)n);
+  for (int64_t i = 0; i < n; ++i) yp[i] = y[i] / weights[i];     // glm((y/weight) ~ x - 1, ...)  MK.R:53
+  const int ntri = p * (p + 1) / 2, NP = 1 + ntri + p;
+  const int nblk = (int)std::min<int64_t>(1024, (n + 255) / 256);
+  DevBufs b;
+  double* d_y = b.get<double>((size_t)n);
+  double* d_w = b.get<double>((size_t)n);
+  double* d_x = b.get<double>((size_t)n * p);
+  double* d_c = b.get<double>(p);
+  double* d_part = b.get<double>((size_t)nblk * NP);
+  if (!d_y || !d_w || !d_x || !d_c || !d_part) return set_err(MK_E_NOMEM, "glm alloc");
+  HIPCHK(hipMemcpy(d_y, yp.data(), (size_t)n * 8, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(d_w, weights, (size_t)n * 8, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(d_x, x, (size_t)n * p * 8, hipMemcpyHostToDevice));
+  std::vector<double> part((size_t)nblk * NP), A((size_t)p * p), rhs(p), Lc, c(p, 0.0), A_used;
+  double dev = 0.0;
+  auto pass = [&](int mode) -> int {
+    if (mode == 1) HIPCHK(hipMemcpy(d_c, c.data(), (size_t)p * 8, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_glm_pass, dim3(nblk), dim3(256), 0, 0, d_y, d_w, d_x, (long)n, p, d_c, mode, d_part);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpy(part.data(), d_part, part.size() * 8, hipMemcpyDeviceToHost));
+    std::vector<double> tot(NP, 0.0);
+    for (int bk = 0; bk < nblk; ++bk)
+      for (int i = 0; i < NP; ++i) tot[i] += part[(size_t)bk * NP + i];
+    dev = tot[0];
+    int k = 1;
+    for (int a = 0; a < p; ++a)
+      for (int bb = a; bb < p; ++bb, ++k) A[a + bb * p] = A[bb + a * p] = tot[k];
+    for (int a = 0; a < p; ++a) rhs[a] = tot[1 + ntri + a];
+    return 0;
+  };
+  int rc = pass(0);
+  if (rc) return rc;
+  double devold = dev;
+  int it = 0;
+  for (it = 1; it <= maxit; ++it) {
+    if (!chol_small(A, p, Lc)) return set_err(MK_E_ARG, "glm: singular weighted design");
+    A_used = A;
+    chol_solve_small(Lc, p, rhs.data(), c.data());
+    if ((rc = pass(1))) return rc;
+    if (std::fabs(dev - devold) / (std::fabs(dev) + 0.1) < epsilon) break;
+    devold = dev;
+  }
+  if (it > maxit) it = maxit;
+  for (int j = 0; j < p; ++j) coef[j] = c[j];
+  if (vcov) {   // chol2inv of the final fit's weighted design = (X'WX)^-1 at the weights that produced coef
+    if (!chol_small(A_used, p, Lc)) return set_err(MK_E_ARG, "glm: singular weighted design");
+    std::vector<double> e(p), col(p);
+    for (int j = 0; j < p; ++j) {
+      std::fill(e.begin(), e.end(), 0.0);
+      e[j] = 1.0;
+      chol_solve_small(Lc, p, e.data(), col.data());
+      for (int i = 0; i < p; ++i) vcov[i + j * p] = col[i];
+    }
+  }
+  if (iters) *iters = it;
   return 0;
 }
 
@@ -647,19 +963,18 @@ extern "C" int mk_correlation_batched(const double* coords, int32_t S, int32_t n
                                       int32_t cov_model, double* R_out, int32_t device) {
   if (!coords || !phi || !R_out || S < 1 || n < 1) return set_err(MK_E_ARG, "bad correlation arguments");
   HIPCHK(hipSetDevice(device));
-  double *dc, *dphi, *dnu = nullptr, *dr;
-  HIPCHK(hipMalloc(&dc, (size_t)S * 2 * n * 8));
-  HIPCHK(hipMalloc(&dphi, (size_t)S * 8));
-  HIPCHK(hipMalloc(&dr, (size_t)S * n * n * 8));
-  if (nu) HIPCHK(hipMalloc(&dnu, (size_t)S * 8));
+  DevBufs b;
+  double* dc = b.get<double>((size_t)S * 2 * n);
+  double* dphi = b.get<double>(S);
+  double* dr = b.get<double>((size_t)S * n * n);
+  double* dnu = nu ? b.get<double>(S) : nullptr;
+  if (!dc || !dphi || !dr || (nu && !dnu)) return set_err(MK_E_NOMEM, "correlation alloc");
   HIPCHK(hipMemcpy(dc, coords, (size_t)S * 2 * n * 8, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(dphi, phi, (size_t)S * 8, hipMemcpyHostToDevice));
   if (nu) HIPCHK(hipMemcpy(dnu, nu, (size_t)S * 8, hipMemcpyHostToDevice));
   hipLaunchKernelGGL(k_corr_plain, dim3(2048), dim3(256), 0, 0, dc, S, n, dphi, dnu, cov_model, dr);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpy(R_out, dr, (size_t)S * n * n * 8, hipMemcpyDeviceToHost));
-  hipFree(dc); hipFree(dphi); hipFree(dr);
-  if (dnu) hipFree(dnu);
   return 0;
 }
 
@@ -686,10 +1001,11 @@ extern "C" int mk_cholesky_batched(const double* A, int32_t S, int32_t n, double
       (rc = s->alloc(&md.logdetR, S)) || (rc = s->alloc(&md.quad, S)) ||
       (rc = s->alloc(&ms.L, (size_t)S * 2 * n_pad * n_pad)) || (rc = s->alloc(&ms.Winv, (size_t)S * 2 * nt * MK_NB * MK_NB)) ||
       (rc = s->alloc(&ms.Q, (size_t)S * n_pad * n_pad)) || (rc = s->alloc(&ms.W, (size_t)S * n_pad * n_pad)) ||
-      (rc = s->alloc(&s->d_list, S)) || (rc = s->alloc(&s->d_count, 1)) || (rc = s->alloc(&s->d_plist, S)) ||
-      (rc = s->alloc(&s->d_pcount, 1)) || (rc = s->alloc(&dA, (size_t)S * n * n)))
+      (rc = s->alloc(&dA, (size_t)S * n * n)))
     return fail(rc);
   md.n_s = d_ns;
+  if ((rc = setup_groups(s, 1))) return fail(rc);
+  Group& a = s->all;
   std::vector<int> hn(S, n);
   if (hipMemcpy(d_ns, hn.data(), S * 4, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(dA, A, (size_t)S * n * n * 8, hipMemcpyHostToDevice) != hipSuccess ||
@@ -699,7 +1015,7 @@ extern "C" int mk_cholesky_batched(const double* A, int32_t S, int32_t n, double
                           (MK_NB * MK_NB + 2 * MK_NB + 4 * 256) * 8) != hipSuccess)
     return fail(set_err(MK_E_HIP, "lds attribute"));
   hipLaunchKernelGGL(k_load_plain, dim3(2048), dim3(256), 0, s->stream, ms, dA, n, S);
-  launch_cholesky(s, 0, S, 2, 0, false);
+  launch_cholesky(s, a, 0, 2, 0, false);
   std::vector<double> part((size_t)S * nt);
   std::vector<int> info(S);
   if (hipStreamSynchronize(s->stream) != hipSuccess) return fail(set_err(MK_E_HIP, "cholesky run"));
@@ -725,11 +1041,11 @@ extern "C" int mk_cholesky_batched(const double* A, int32_t S, int32_t n, double
     }
   }
   if (inv_out) {
-    hipLaunchKernelGGL(k_dirty_list, dim3(1), dim3(256), 0, s->stream, md, 1, s->d_plist, s->d_pcount, s->d_list,
-                       s->d_count);
+    hipLaunchKernelGGL(k_dirty_list, dim3(1), dim3(256), 0, s->stream, md, 1, a.d_plist, a.d_pcount, a.d_list,
+                       a.d_count);
     const int ntiles = nt * (nt + 1) / 2;
-    launch_trinv(s, S, s->d_list, s->d_count);
-    hipLaunchKernelGGL(k_lauum, dim3(S * ntiles), dim3(256), 0, s->stream, ms, md.n_s, s->d_list, s->d_count);
+    launch_trinv(s, a, S, a.d_list, a.d_count);
+    hipLaunchKernelGGL(k_lauum, dim3(S * ntiles), dim3(256), 0, s->stream, ms, md.n_s, a.d_list, a.d_count);
     hipLaunchKernelGGL(k_extract_L, dim3(2048), dim3(256), 0, s->stream, ms, n, S, dL, 1);
     if (hipMemcpyAsync(inv_out, dL, (size_t)S * n * n * 8, hipMemcpyDeviceToHost, s->stream) != hipSuccess)
       return fail(set_err(MK_E_HIP, "inverse download"));

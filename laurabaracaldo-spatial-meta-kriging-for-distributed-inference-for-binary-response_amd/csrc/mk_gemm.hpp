@@ -109,23 +109,29 @@ __device__ inline void mma_chunk(const double* As, const double* Bs, Acc& acc) {
 }
 
 // acc += (NEG ? -1 : 1) op(A)[128 x K] * op(B)[K x 128], K % GB_K == 0; k >= kvalid_total zeroed.
-template <bool A_MU, bool B_NU, bool NEG = false>
+// REV: K chunks in descending order -- tiles of one launch whose K ranges share their END
+// (triangular operands) then stream the same chunks at the same time, so an XCD's L2
+// serves the shared panels once.  SAME: op(B) = op(A)^T read from the same memory (A'A
+// products): one load and one LDS image serve both fragments.
+template <bool A_MU, bool B_NU, bool NEG = false, bool REV = false, bool SAME = false>
 __device__ inline void gemm_128(const double* __restrict__ A, long sA, const double* __restrict__ B, long sB,
                                 int K, int kvalid_total, Acc& acc, double* lds) {
   double* As = lds;
-  double* Bs = lds + GB_K * GB_SMT;
+  double* Bs = SAME ? lds : lds + GB_K * GB_SMT;
   d2 ra[GB_PER], rb[GB_PER];
   if (K <= 0) return;
-  load_chunk<A_MU>(A, sA, 0, kvalid_total, ra);
-  load_chunk<B_NU>(B, sB, 0, kvalid_total, rb);
+  const int k_first = REV ? K - GB_K : 0;
+  load_chunk<A_MU>(A, sA, k_first, kvalid_total - k_first, ra);
+  if (!SAME) load_chunk<B_NU>(B, sB, k_first, kvalid_total - k_first, rb);
   for (int kc = 0; kc < K; kc += GB_K) {
     __syncthreads();
     store_chunk<A_MU>(As, ra);
-    store_chunk<B_NU>(Bs, rb);
+    if (!SAME) store_chunk<B_NU>(Bs, rb);
     __syncthreads();
     if (kc + GB_K < K) {
-      load_chunk<A_MU>(A, sA, kc + GB_K, kvalid_total - (kc + GB_K), ra);
-      load_chunk<B_NU>(B, sB, kc + GB_K, kvalid_total - (kc + GB_K), rb);
+      const int k1 = REV ? K - 2 * GB_K - kc : kc + GB_K;
+      load_chunk<A_MU>(A, sA, k1, kvalid_total - k1, ra);
+      if (!SAME) load_chunk<B_NU>(B, sB, k1, kvalid_total - k1, rb);
     }
     mma_chunk<NEG, sm_of<A_MU>(), sm_of<B_NU>()>(As, Bs, acc);
   }

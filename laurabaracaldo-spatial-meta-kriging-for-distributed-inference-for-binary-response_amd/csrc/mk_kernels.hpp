@@ -31,6 +31,15 @@ __global__ void k_pred_draw(Model md, int iter, int kidx);
 __global__ void k_quantiles(const double* data, long subset_stride, long row_stride, int n_rows, int n_cols,
                             const double* probs, int n_probs, double* out);
 __global__ void k_combine(const double* grids, int K, long G, double* out);
+// mk_post.hip
+__global__ void k_weiszfeld(const double* grids, int K, int L, long C, int max_iter, double tol, double* out, int* iters);
+__global__ void k_post_index(uint64_t seed, int samplesize, int n_levels, int* idx);
+__global__ void k_post_interp(const double* grid, int L, long C, const int* idx, int S, const int* lo, const int* hi,
+                              const int* mode, const double* t, double* out);
+__global__ void k_post_prob(const double* sample_par, int S, const double* x_test, long C, int p, const double* sample_w,
+                            double* pout);
+__global__ void k_glm_pass(const double* yprop, const double* wt, const double* X, long n, int p, const double* coef,
+                           int mode, double* part);
 // mk_init.hip
 __global__ void k_init_state(Model md);
 __global__ void k_theta_init(Model md, MatSet ms, int h);

@@ -397,8 +397,9 @@ __global__ __launch_bounds__(256, 2) void k_inv_level(MatSet ms, const int* __re
   if (phase == 0) {
     const double* Lm = mat_slot(ms, sh, cur);
     const int K = (B0 - j) * MK_NB;
-    gemm_128<true, false>(Lm + i * MK_NB + (long)j * MK_NB * ld, ld, Wm + j * MK_NB + (long)j * MK_NB * ld, ld, K, K,
-                          acc, lds);
+    // K ranges [j, B0) share their end: descending chunks keep the tiles of a subset in step (L2 reuse)
+    gemm_128<true, false, false, true>(Lm + i * MK_NB + (long)j * MK_NB * ld, ld, Wm + j * MK_NB + (long)j * MK_NB * ld,
+                                       ld, K, K, acc, lds);
     store_tile(Y + i * MK_NB + (long)j * MK_NB * ld, ld, acc);
   } else {
     const int K = (i - B0 + 1) * MK_NB;
@@ -410,15 +411,17 @@ __global__ __launch_bounds__(256, 2) void k_inv_level(MatSet ms, const int* __re
 
 // Tiles (i,j), i >= j, of R^-1 = sum over rows l < n_s of W(l,i)^T W(l,j) (drops the bordered
 // row and the padding).  diag_only: tiles (i,i) into QB; otherwise the full symmetric Q.
+template <bool DIAG>
 __device__ inline void wtw_tile(const MatSet& ms, int sh, int ns, int i, int j, Acc& acc, double* lds) {
   const double* X = wmat(ms, sh);
   const long ld = ms.ld;
   const int K = (ms.nt - i) * MK_NB;
   const int kvalid = ns - i * MK_NB;
   acc_zero(acc);
+  // DIAG (i == j): both operands are the panel W(i:, i) -- loaded once
   if (kvalid > 0)
-    gemm_128<false, false>(X + i * MK_NB + (long)i * MK_NB * ld, ld, X + i * MK_NB + (long)j * MK_NB * ld, ld, K,
-                           kvalid, acc, lds);
+    gemm_128<false, false, false, false, DIAG>(X + i * MK_NB + (long)i * MK_NB * ld, ld,
+                                               X + i * MK_NB + (long)j * MK_NB * ld, ld, K, kvalid, acc, lds);
 }
 
 __global__ __launch_bounds__(256, 2) void k_lauum(MatSet ms, const int* __restrict__ n_s, const int* __restrict__ list,
@@ -433,7 +436,7 @@ __global__ __launch_bounds__(256, 2) void k_lauum(MatSet ms, const int* __restri
   const int j = t - i * (i + 1) / 2;
   const int sh = list[e];
   Acc acc;
-  wtw_tile(ms, sh, n_s[sh / ms.q], i, j, acc, lds);
+  wtw_tile<false>(ms, sh, n_s[sh / ms.q], i, j, acc, lds);
   const long ld = ms.ld;
   double* Q = ms.Q + (long)sh * mat_elems(ms);
   double* Ct = (i != j) ? Q + j * MK_NB + (long)i * MK_NB * ld : nullptr;
@@ -447,7 +450,7 @@ __global__ __launch_bounds__(256, 2) void k_qblocks(MatSet ms, const int* __rest
   if (!xcd_map(*count, ms.nt, &e, &i)) return;
   const int sh = list[e];
   Acc acc;
-  wtw_tile(ms, sh, n_s[sh / ms.q], i, i, acc, lds);
+  wtw_tile<true>(ms, sh, n_s[sh / ms.q], i, i, acc, lds);
   store_tile(ms.QB + ((long)sh * ms.nt + i) * MK_NB * MK_NB, MK_NB, acc);
 }
 

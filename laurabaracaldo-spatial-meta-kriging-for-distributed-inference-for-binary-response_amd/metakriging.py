@@ -9,6 +9,8 @@
 import numpy as np
 
 from .glm import glm_binomial
+from .post import combine_median
+from .post import posterior_summary as _post_summary
 from .session import SamplerConfig, Session, combine
 
 PROBS200 = None
@@ -54,11 +56,11 @@ def default_config(q, p, beta_starting, beta_tuning, cov_model="exponential", n_
                          batch_length=batch_length, accept_rate=0.43, seed=seed, **kw)
 
 
-def start_values(y, x, weight, q):
-    """MK.R:53-55 on the full data: beta.starting and the diagonal of t(chol(vcov))."""
+def start_values(y, x, weight, q, device=0):
+    """MK.R:53-55 on the full data, once, on device: beta.starting and t(chol(vcov))."""
     n_tot = len(y)
     wt = np.broadcast_to(np.asarray(weight, float), (n_tot,))
-    coef, vcov, bt = glm_binomial(y, x, wt)
+    coef, vcov, bt = glm_binomial(y, x, wt, device=device)
     return coef, bt
 
 
@@ -91,42 +93,22 @@ def partitioned_spMvGLM(i, y, x, weight, n, q, n_part, coords_test, x_test, inde
                     device=device, cov_model=cov_model, n_batch=n_batch, batch_length=batch_length, seed=seed)[0]
 
 
-def combine_results(obj, device=0):
-    """MK.R:123-133: result (200 x P) and result2 (200 x q n_test)."""
-    result = combine([o["parameters"] for o in obj], device=device)
-    result2 = combine([o["w.predict"] for o in obj], device=device) if "w.predict" in obj[0] else None
+def combine_results(obj, device=0, method="mean"):
+    """MK.R:123-133: result (200 x P) and result2 (200 x q n_test).  method="median" is the
+    Weiszfeld geometric-median extension (the reference averages)."""
+    if method == "mean":
+        comb = lambda grids: combine(grids, device=device)             # noqa: E731
+    elif method == "median":
+        comb = lambda grids: combine_median(grids, device=device)[0]   # noqa: E731
+    else:
+        raise ValueError(f"error: unknown combine method '{method}'")
+    result = comb([o["parameters"] for o in obj])
+    result2 = comb([o["w.predict"] for o in obj]) if "w.predict" in obj[0] else None
     return result, result2
 
 
-def r_approx(xg, y, xout):
-    """stats::approx linear interpolation (MK.R:142), vectorised over columns of y."""
-    xg = np.asarray(xg, float)
-    idx = np.searchsorted(xg, xout, side="right") - 1
-    idx = np.clip(idx, 0, len(xg) - 2)
-    x0, x1 = xg[idx], xg[idx + 1]
-    y0, y1 = y[idx], y[idx + 1]
-    frac = ((xout - x0) / (x1 - x0))[:, None]
-    out = y0 + (y1 - y0) * frac
-    exact0 = (xout == x0)
-    exact1 = (xout == x1)
-    out[exact0] = y0[exact0]
-    out[exact1] = y1[exact1]
-    return out
-
-
-def posterior_summary(result, result2, x_test, q, samplesize=1000, seed=20250114):
-    """MK.R:136-165: interpolate both combined grids to Xout (996 levels), draw one shared
-    resample index vector (comonotone draws, MK.R:141), p(y=1) = logistic(x.test B + w),
-    and the median / 2.5% / 97.5% summaries."""
-    rng = np.random.default_rng(seed)
-    idx = rng.integers(0, len(XOUT996), size=samplesize)
-    inter = r_approx(PROBS200, result, XOUT996)
-    inter2 = r_approx(PROBS200, result2, XOUT996)
-    sample_par = inter[idx]
-    sample_w = inter2[idx]
-    p = np.asarray(x_test).shape[1]
-    eta = sample_par[:, :p] @ np.asarray(x_test, float).T + sample_w
-    p_sample = 1.0 / (1.0 + np.exp(-eta))
-    probs = np.array([0.5, 0.025, 0.975])
-    return dict(SamplePar=sample_par, Samplew=sample_w, p_sample=p_sample,
-                w_quant=np.quantile(sample_w, probs, axis=0), param_quant=np.quantile(sample_par, probs, axis=0))
+def posterior_summary(result, result2, x_test, q=None, samplesize=1000, seed=20250114, device=0):
+    """MK.R:136-165 on device: interpolate both combined grids to Xout (996 levels), one shared
+    resample index vector (comonotone draws, MK.R:141), p(y=1) = logistic(x.test B + w) and the
+    median / 2.5% / 97.5% summaries (post.posterior_summary)."""
+    return _post_summary(result, result2, x_test, samplesize=samplesize, seed=seed, device=device)

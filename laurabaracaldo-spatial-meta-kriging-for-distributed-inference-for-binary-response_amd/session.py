@@ -14,7 +14,7 @@ from ._lib import Config, Outputs, Problem, check, dptr, iptr
 COV_MODELS = {"exponential": _lib.MK_COV_EXPONENTIAL, "matern": _lib.MK_COV_MATERN}
 
 # kernel-stat ids (mk_api.hip)
-KS_CHOL_UPDATE, KS_CHOL_DIAG, KS_CHOL_TRSM, KS_SWEEP, KS_LAUUM, KS_ITER = range(6)
+KS_CHOL_UPDATE, KS_CHOL_DIAG, KS_CHOL_TRSM, KS_SWEEP, KS_LAUUM, KS_ITER, KS_INV = range(7)
 
 
 def _f64(a):
@@ -27,7 +27,7 @@ class SamplerConfig:
     def __init__(self, q, p, beta_starting, beta_tuning, cov_model="exponential", n_batch=100, batch_length=50,
                  accept_rate=0.43, burn_in=None, phi_starting=None, phi_tuning=None, phi_unif=None,
                  A_starting=None, A_tuning=None, w_starting=0.0, w_tuning=0.5, nu_starting=None, nu_tuning=None,
-                 nu_unif=None, K_IW_df=None, K_IW_S=None, seed=20250114):
+                 nu_unif=None, K_IW_df=None, K_IW_S=None, seed=20250114, n_streams=0):
         if cov_model not in COV_MODELS:
             raise ValueError(f"error: specified cov.model '{cov_model}' is not a valid option")
         self.q, self.p = int(q), int(p)
@@ -69,6 +69,7 @@ class SamplerConfig:
         self.K_IW_df = float(q if K_IW_df is None else K_IW_df)
         self.K_IW_S = _f64(np.diag(np.full(q, 0.1)) if K_IW_S is None else K_IW_S).reshape(q, q)
         self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        self.n_streams = int(n_streams)     # device execution only (0 = library default); no effect on results
 
     @property
     def n_theta(self):
@@ -108,6 +109,7 @@ class SamplerConfig:
         c.record_samples = 1
         c.record_w = 1 if record_w else 0
         c.device = int(device)
+        c.n_streams = self.n_streams
         return c, keep
 
 

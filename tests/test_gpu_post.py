@@ -1,0 +1,100 @@
+"""Device post-processing, median combine, glm start values and stream grouping, through
+the C ABI, against the CPU oracle.
+
+* posterior_summary (MK.R:136-165): resample index and interpolated draws bit-exact;
+  p(y=1) within 1e-14 relative (device vs libm exp); summaries of identical draws bit-exact.
+* combine_median (Weiszfeld, extension): within 1e-9 of oracle/post.py (reduction order differs).
+* glm start values (MK.R:53-55): coefficients 1e-10, vcov 1e-8 relative to the QR-based oracle.
+* n_streams: the chains are independent of how subsets are grouped onto streams (bit-exact)."""
+import numpy as np
+import pytest
+
+from oracle import post, rstats
+
+pytestmark = pytest.mark.gpu
+
+
+def _grids(K, L=200, C=5, seed=0):
+    rng = np.random.default_rng(seed)
+    return np.stack([np.sort(rng.normal(loc=rng.normal(), size=(L, C)), axis=0) for _ in range(K)])
+
+
+@pytest.mark.parametrize("C,p,S", [(7, 2, 1000), (1, 4, 17), (300, 6, 2048)])
+def test_posterior_summary_matches_oracle(mk, C, p, S):
+    P = max(4, p + 2)
+    g = _grids(1, C=P + C, seed=C)[0]
+    res, res2 = g[:, :P], g[:, P:P + C]
+    x_test = np.random.default_rng(1).normal(size=(C, p))
+    dev = mk.posterior_summary(res, res2, x_test, samplesize=S, seed=11)
+    ref = post.posterior_summary(res, res2, x_test, samplesize=S, seed=11)
+    assert np.array_equal(dev["index"], ref["index"])
+    assert np.array_equal(dev["SamplePar"], ref["SamplePar"])
+    assert np.array_equal(dev["Samplew"], ref["Samplew"])
+    np.testing.assert_allclose(dev["p_sample"], ref["p_sample"], rtol=1e-14, atol=0)
+    assert np.array_equal(dev["w_quant"], ref["w_quant"])
+    assert np.array_equal(dev["param_quant"], ref["param_quant"])
+    np.testing.assert_allclose(dev["p_quant"], ref["p_quant"], rtol=1e-14, atol=0)
+
+
+def test_posterior_summary_parameters_only(mk):
+    res = _grids(1, C=3, seed=9)[0]
+    dev = mk.posterior_summary(res, None, None, samplesize=500, seed=2)
+    ref = post.posterior_summary(res, np.zeros((200, 1)), np.zeros((1, 0)), samplesize=500, seed=2)
+    assert np.array_equal(dev["SamplePar"], ref["SamplePar"])
+    assert np.array_equal(dev["param_quant"], ref["param_quant"])
+
+
+@pytest.mark.parametrize("K,L,C", [(9, 200, 11), (1, 200, 3), (2, 200, 4), (250, 200, 33), (5, 256, 2), (3, 17, 5)])
+def test_combine_median_matches_oracle(mk, K, L, C):
+    g = _grids(K, L=L, C=C, seed=K + C)
+    if K > 3:
+        g[0] += 20.0                               # an outlying subset
+    med, it = mk.combine_median(list(g))
+    ref, rit = post.weiszfeld_median(g)
+    np.testing.assert_allclose(med, ref, rtol=0, atol=1e-9 * (1 + np.abs(ref).max()))
+    assert np.all(np.abs(it - rit) <= 1)
+
+
+def test_combine_median_rejects_bad_levels(mk):
+    with pytest.raises(mk.MkError):
+        mk.combine_median(list(_grids(3, L=300, C=2)))
+
+
+@pytest.mark.parametrize("q,n", [(1, 20000), (2, 6000)])
+def test_glm_start_values_match_oracle(mk, q, n):
+    d = mk.synthetic.generate(n, q=q, n_test=0, seed=8)
+    coef, vcov, bt = mk.glm_binomial(d["y"], d["x"], np.ones(n * q))
+    rc, rv = rstats.glm_binomial(d["y"], d["x"], np.ones(n * q))
+    np.testing.assert_allclose(coef, rc, rtol=1e-10)
+    np.testing.assert_allclose(vcov, rv, rtol=1e-8)
+    np.testing.assert_allclose(bt @ bt.T, vcov, rtol=1e-12)        # t(chol(vcov)) is lower
+
+
+def test_glm_binomial_trials(mk):
+    """weights > 1: glm((y/weight) ~ x - 1, weights = weight) on counts."""
+    rng = np.random.default_rng(3)
+    n = 4000
+    x = np.column_stack([np.ones(n), rng.normal(size=n)])
+    wt = rng.integers(1, 6, size=n).astype(float)
+    y = rng.binomial(wt.astype(int), 1 / (1 + np.exp(-(0.3 - 0.8 * x[:, 1])))).astype(float)
+    coef, vcov, _ = mk.glm_binomial(y, x, wt)
+    rc, rv = rstats.glm_binomial(y / wt, x, wt)
+    np.testing.assert_allclose(coef, rc, rtol=1e-10)
+    np.testing.assert_allclose(vcov, rv, rtol=1e-8)
+
+
+def test_stream_grouping_does_not_change_the_chains(mk):
+    d = mk.synthetic.generate(5 * 90, q=1, n_test=6, seed=21)
+    subs = [dict(coords=d["coords"][i * 90:(i + 1) * 90], y=d["y"][i * 90:(i + 1) * 90], weights=np.ones(90),
+                 x=d["x"][i * 90:(i + 1) * 90]) for i in range(5)]
+    outs = []
+    for ns in (1, 2, 3, 5):
+        cfg = mk.SamplerConfig(1, 2, [0, 0], [0.05, 0.05], n_batch=2, batch_length=5, burn_in=6, seed=4, n_streams=ns)
+        with mk.Session(subs, cfg, coords_test=d["coords_test"]) as ses:
+            ses.run(cfg.n_samples)
+            outs.append(ses.outputs(samples=True, w_pred_samples=True))
+    for o in outs[1:]:
+        for s in range(5):
+            assert np.array_equal(o["samples"][s], outs[0]["samples"][s])
+            assert np.array_equal(o["w_pred_samples"][s], outs[0]["w_pred_samples"][s])
+            assert np.array_equal(o["w_predict"][s], outs[0]["w_predict"][s])

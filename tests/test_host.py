@@ -69,15 +69,6 @@ def test_subset_data_location_major(mk):
         np.testing.assert_array_equal(sub["coords"][k], d["coords"][i])
 
 
-def test_glm_start_values_match_oracle(mk):
-    d = mk.synthetic.generate(2500, q=2, n_test=0, seed=8)
-    coef, vcov, bt = mk.glm.glm_binomial(d["y"], d["x"], np.ones(5000))
-    rc, rv = rstats.glm_binomial(d["y"], d["x"], np.ones(5000))
-    np.testing.assert_allclose(coef, rc, rtol=1e-10)
-    np.testing.assert_allclose(vcov, rv, rtol=1e-8)
-    np.testing.assert_allclose(bt @ bt.T, vcov, rtol=1e-12)        # t(chol(vcov)) is lower
-
-
 def test_sampler_config_mirrors_reference_defaults(mk):
     cfg = mk.SamplerConfig(2, 4, np.zeros(4), np.eye(4) * 0.3)
     assert cfg.n_samples == 5000 and cfg.burn_in == 3750 and cfg.kept == 1251        # MK.R:57-59, 85
@@ -107,14 +98,31 @@ def test_spmvglm_argument_errors(mk):
         mk.spMvGLM(f, d["coords"], np.ones((10, 1)), family="poisson", **ok)
 
 
-def test_posterior_summary_shapes(mk):
+def test_sampler_config_n_streams_reaches_the_abi(mk):
+    cfg = mk.SamplerConfig(1, 2, [0, 0], [0.1, 0.1], n_streams=3)
+    c, _ = cfg.to_c()
+    assert c.n_streams == 3
+    assert mk.SamplerConfig(1, 2, [0, 0], [0.1, 0.1]).to_c()[0].n_streams == 0   # library default
+
+
+def test_device_only_entry_points_fail_loudly_without_gpu(mk):
+    """The post-processing, median combine and glm run only through libmk (no CPU fallback)."""
+    lib = mk.load()
+    if lib.mk_device_count() > 0:
+        pytest.skip("GPU present")
     rng = np.random.default_rng(0)
-    result = np.sort(rng.normal(size=(200, 4)), axis=0)
-    result2 = np.sort(rng.normal(size=(200, 7)), axis=0)
-    x_test = np.column_stack([np.ones(7), rng.normal(size=7)])
-    out = mk.posterior_summary(result, result2, np.hstack([x_test, np.zeros((7, 2))]), 1)
-    assert out["p_sample"].shape == (1000, 7)
-    assert out["w_quant"].shape == (3, 7) and out["param_quant"].shape == (3, 4)
-    # the interpolation the reference applies (MK.R:142) vs the oracle's approx
-    np.testing.assert_allclose(mk.metakriging.r_approx(rstats.PROBS200, result, rstats.XOUT996),
-                               rstats.r_approx(rstats.PROBS200, result, rstats.XOUT996), rtol=1e-14)
+    grids = [np.sort(rng.normal(size=(200, 3)), axis=0) for _ in range(4)]
+    with pytest.raises(mk.MkError):
+        mk.combine_median(grids)
+    with pytest.raises(mk.MkError):
+        mk.posterior_summary(grids[0], grids[1], np.ones((3, 2)))
+    with pytest.raises(mk.MkError):
+        mk.glm_binomial(np.ones(10), np.ones((10, 1)), np.ones(10))
+
+
+def test_summary_struct_matches_header(mk):
+    binding = __import__(mk.__name__ + "._lib", fromlist=["x"])
+    src = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    body = re.search(r"typedef struct mk_summary \{(.*?)\} mk_summary;", src, flags=re.S).group(1)
+    fields = re.findall(r"\b([A-Za-z_][A-Za-z0-9_]*)\s*;", body)
+    assert fields == [f[0] for f in binding.Summary._fields_]
