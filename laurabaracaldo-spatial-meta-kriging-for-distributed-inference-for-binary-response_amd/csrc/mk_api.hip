@@ -199,8 +199,8 @@ static void drain_timers(mk_session* s) {
 static inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
 
 // ------------------------------------------------------------------ Cholesky of all candidates of outcome h
-// gen: candidate tiles generated from coordinates (session); otherwise preloaded (test entry).
-static void launch_cholesky(mk_session* s, Group& g, int h, int which, int iter, bool gen) {
+// Candidate tiles are in the free slot (k_cov_candidate, or k_load_plain for the test entry).
+static void launch_cholesky(mk_session* s, Group& g, int h) {
   const int nt = s->nt, S = g.S;
   const size_t diag_lds = (size_t)(MK_NB * MK_NB + 2 * MK_NB + 4 * 256) * sizeof(double);
   // valid extent (excludes padding) for the algorithmic flop count
@@ -213,8 +213,7 @@ static void launch_cholesky(mk_session* s, Group& g, int h, int which, int iter,
       const double kk = std::fmin((double)k * MK_NB, nv);
       const double fl = 2.0 * rows * cols * kk * S;
       timed(s, g.stream, KS_CHOL_UPDATE, fl, [&] {
-        hipLaunchKernelGGL(k_chol_update, dim3(xcd_grid_h(S, nt - k)), dim3(256), 0, g.stream, g.md, g.ms, S, h, k,
-                           which, iter, (int)gen);
+        hipLaunchKernelGGL(k_chol_update, dim3(xcd_grid_h(S, nt - k)), dim3(256), 0, g.stream, g.ms, S, h, k);
       });
     }
     timed(s, g.stream, KS_CHOL_DIAG, 0.0, [&] {
@@ -282,7 +281,7 @@ static void run_iteration(mk_session* s, Group& g, int it) {
   for (int which = 0; which < nkinds; ++which)
     for (int h = 0; h < q; ++h) {
       hipLaunchKernelGGL(k_cov_candidate, dim3(xcd_grid_h(S, ntri_tiles)), dim3(256), 0, st, md, g.ms, h, which, it);
-      launch_cholesky(s, g, h, which, it, false);
+      launch_cholesky(s, g, h);
       hipLaunchKernelGGL(k_theta_mh, dim3((S + 63) / 64), dim3(64), 0, st, md, g.ms, h, which, it);
     }
   hipLaunchKernelGGL(k_dirty_list, dim3(1), dim3(256), 0, st, md, (int)(it == md.kept0), g.d_list, g.d_count,
@@ -578,7 +577,7 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
   const int ntri_tiles = nt * (nt + 1) / 2;
   for (int h = 0; h < q; ++h) {
     hipLaunchKernelGGL(k_cov_candidate, dim3(xcd_grid_h(S, ntri_tiles)), dim3(256), 0, s->stream, md, ms, h, 2, 0);
-    launch_cholesky(s, a, h, 2, 0, false);
+    launch_cholesky(s, a, h);
     hipLaunchKernelGGL(k_theta_init, dim3((S + 63) / 64), dim3(64), 0, s->stream, md, ms, h);
   }
   hipLaunchKernelGGL(k_dirty_list, dim3(1), dim3(256), 0, s->stream, md, 0, a.d_list, a.d_count, a.d_plist, a.d_pcount);
@@ -1015,7 +1014,7 @@ extern "C" int mk_cholesky_batched(const double* A, int32_t S, int32_t n, double
                           (MK_NB * MK_NB + 2 * MK_NB + 4 * 256) * 8) != hipSuccess)
     return fail(set_err(MK_E_HIP, "lds attribute"));
   hipLaunchKernelGGL(k_load_plain, dim3(2048), dim3(256), 0, s->stream, ms, dA, n, S);
-  launch_cholesky(s, a, 0, 2, 0, false);
+  launch_cholesky(s, a, 0);
   std::vector<double> part((size_t)S * nt);
   std::vector<int> info(S);
   if (hipStreamSynchronize(s->stream) != hipSuccess) return fail(set_err(MK_E_HIP, "cholesky run"));

@@ -86,8 +86,17 @@ __device__ inline void store_chunk(double* lds, const d2 (&r)[GB_PER]) {
   }
 }
 
-template <bool NEG = false, int SA = GB_SM, int SB = GB_SM>
-__device__ inline void mma_chunk(const double* As, const double* Bs, Acc& acc) {
+// Structural zeros (wave-uniform skips; the skipped MFMAs would add exact zeros or feed
+// outputs nobody reads, so results are unchanged and the SIMD's matrix pipe goes to the
+// co-resident wave instead):
+//   SKIP_UPPER  output tile on the diagonal of a symmetric update: 16-blocks above the
+//               diagonal (column block > row block) are never read   (flag = tile is diagonal)
+//   SKIP_TRI_B  op(B) lower-triangular in (n, k) over one 128-deep K: chunk c only touches
+//               output column blocks >= c                             (flag = chunk index c)
+enum { SKIP_NONE = 0, SKIP_UPPER = 1, SKIP_TRI_B = 2 };
+
+template <bool NEG = false, int SA = GB_SM, int SB = GB_SM, int SKIP = SKIP_NONE>
+__device__ inline void mma_chunk(const double* As, const double* Bs, Acc& acc, int flag = 0) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int wm = w & 1, wn = w >> 1;
   const int li = lane & 15, lk = lane >> 4;
@@ -103,8 +112,11 @@ __device__ inline void mma_chunk(const double* As, const double* Bs, Acc& acc) {
 #pragma unroll
     for (int bm = 0; bm < 4; ++bm)
 #pragma unroll
-      for (int bn = 0; bn < 4; ++bn)
+      for (int bn = 0; bn < 4; ++bn) {
+        if (SKIP == SKIP_UPPER && flag && wn * 4 + bn > wm * 4 + bm) continue;
+        if (SKIP == SKIP_TRI_B && flag > wn * 4 + bn) continue;
         acc.v[bm][bn] = __builtin_amdgcn_mfma_f64_16x16x4f64(xb[bn], ya[bm], acc.v[bm][bn], 0, 0, 0);
+      }
   }
 }
 
@@ -113,9 +125,10 @@ __device__ inline void mma_chunk(const double* As, const double* Bs, Acc& acc) {
 // (triangular operands) then stream the same chunks at the same time, so an XCD's L2
 // serves the shared panels once.  SAME: op(B) = op(A)^T read from the same memory (A'A
 // products): one load and one LDS image serve both fragments.
-template <bool A_MU, bool B_NU, bool NEG = false, bool REV = false, bool SAME = false>
+// SKIP (see mma_chunk): SKIP_UPPER with diag_tile != 0; SKIP_TRI_B for K = 128.
+template <bool A_MU, bool B_NU, bool NEG = false, bool REV = false, bool SAME = false, int SKIP = SKIP_NONE>
 __device__ inline void gemm_128(const double* __restrict__ A, long sA, const double* __restrict__ B, long sB,
-                                int K, int kvalid_total, Acc& acc, double* lds) {
+                                int K, int kvalid_total, Acc& acc, double* lds, int diag_tile = 0) {
   double* As = lds;
   double* Bs = SAME ? lds : lds + GB_K * GB_SMT;
   d2 ra[GB_PER], rb[GB_PER];
@@ -133,7 +146,8 @@ __device__ inline void gemm_128(const double* __restrict__ A, long sA, const dou
       load_chunk<A_MU>(A, sA, k1, kvalid_total - k1, ra);
       if (!SAME) load_chunk<B_NU>(B, sB, k1, kvalid_total - k1, rb);
     }
-    mma_chunk<NEG, sm_of<A_MU>(), sm_of<B_NU>()>(As, Bs, acc);
+    mma_chunk<NEG, sm_of<A_MU>(), sm_of<B_NU>(), SKIP>(As, Bs, acc,
+                                                       SKIP == SKIP_TRI_B ? (REV ? K - GB_K - kc : kc) / GB_K : diag_tile);
   }
 }
 

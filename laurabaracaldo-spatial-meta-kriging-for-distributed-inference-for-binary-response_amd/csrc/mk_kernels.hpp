@@ -6,7 +6,7 @@ namespace mk {
 inline int xcd_grid_h(int S, int T) { return 8 * ((S + 7) / 8) * T; }
 // mk_linalg.hip
 __global__ void k_cov_candidate(Model md, MatSet ms, int h, int which, int iter);
-__global__ void k_chol_update(Model md, MatSet ms, int S, int h, int k, int which, int iter, int gen);
+__global__ void k_chol_update(MatSet ms, int S, int h, int k);
 __global__ void k_chol_trsm(MatSet ms, int S, int h, int k);
 __global__ void k_chol_diag(MatSet ms, const int* n_s, int h, int k, double* ld_part, double* quad_c, int* info);
 __global__ void k_inv_copydiag(MatSet ms, const int* list, const int* count);

@@ -103,9 +103,10 @@ __global__ __launch_bounds__(256) void k_cov_candidate(Model md, MatSet ms, int 
 // Plain matrix (no border) loaded by the host for the standalone Cholesky test path.
 
 // ---------------------------------------------------------------- Cholesky
-// gen: C(i,k) is generated from coordinates (first touch of the tile); otherwise read.
-__global__ __launch_bounds__(256, 2) void k_chol_update(Model md, MatSet ms, int S, int h, int k, int which, int iter,
-                                                       int gen) {
+// (Generating C(i,k) from coordinates at its first touch inside this kernel was measured
+// slower on cfg3 and its code path made the kernel spill 80 VGPRs: candidates come from
+// k_cov_candidate.)
+__global__ __launch_bounds__(256, 2) void k_chol_update(MatSet ms, int S, int h, int k) {
   __shared__ __attribute__((aligned(16))) double lds[GB_LDS_DOUBLES];
   const int ntk = ms.nt - k;
   int s, t;
@@ -116,17 +117,7 @@ __global__ __launch_bounds__(256, 2) void k_chol_update(Model md, MatSet ms, int
   const long ld = ms.ld;
   double* C = M + i * MK_NB + (long)k * MK_NB * ld;
   Acc acc;
-  if (gen) {
-    const CandGen g = make_gen(md, s, h, which, iter);
-#pragma unroll
-    for (int bm = 0; bm < 4; ++bm)
-#pragma unroll
-      for (int bn = 0; bn < 4; ++bn)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc.v[bm][bn][r] = g(i * MK_NB + acc_row(bm), k * MK_NB + acc_col(bn, r));
-  } else {
-    acc_load(acc, C, ld);
-  }
+  acc_load(acc, C, ld);
   gemm_128<true, true, true>(M + i * MK_NB, ld, M + k * MK_NB, ld, k * MK_NB, k * MK_NB, acc, lds);
   store_tile(C, ld, acc);
 }
@@ -145,7 +136,8 @@ __global__ __launch_bounds__(256, 2) void k_chol_trsm(MatSet ms, int S, int h, i
   double* C = M + i * MK_NB + (long)k * MK_NB * ld;
   Acc acc;
   acc_zero(acc);
-  gemm_128<true, true>(C, ld, W, MK_NB, MK_NB, MK_NB, acc, lds);
+  // Winv_k lower triangular: (C Winv^T)(m, n) = sum_{j <= n} C(m, j) Winv(n, j)
+  gemm_128<true, true, false, false, false, SKIP_TRI_B>(C, ld, W, MK_NB, MK_NB, MK_NB, acc, lds);
   store_tile(C, ld, acc);
 }
 
