@@ -2,10 +2,11 @@
 
 Subsets are independent during the fit and kriging (MK.R:108: foreach over subsets),
 so every rank runs its contiguous block of subsets with no traffic.  The one exchange
-is the combine (MK.R:119-133): an all-gather of the per-subset 200-level grids in
-global subset order, after which every rank sums them in the reference's sequential
-order -- the multi-GPU result is bit-identical to the single-GPU one.  The same
-all-gathered grids feed the Weiszfeld / barycenter extensions.
+is the combine (MK.R:119-133), column-sharded: an all-to-all hands every rank all K
+subsets' grids for its block of columns, the rank combines them in global subset order
+(the reference's sequential mean -- bit-identical to one GPU -- or the Weiszfeld median,
+SURVEY.md 8f row 2) and the combined blocks are all-gathered.  allgather_grids keeps the
+plain all-gather of whole grids for small problems.
 """
 import numpy as np
 
@@ -35,13 +36,82 @@ def allgather_grids(local, K, dist, device=None):
     return full.cpu().numpy()
 
 
-def meta_fit_distributed(y, x, weight, coords, q, index_part, coords_test, cfg, dist, device=0):
-    """Fit this rank's shard of subsets on its GPU, all-gather the grids, combine (on device).
+def col_blocks(C, world):
+    """Contiguous column blocks of ceil(C/world) columns -> [(a, b)] per rank."""
+    per = (C + world - 1) // world
+    return [(min(C, r * per), min(C, (r + 1) * per)) for r in range(world)]
+
+
+def _exchange(send, recv, dist):
+    """recv[src] <- what rank src put in its send[me]: point-to-point pairs (RCCL and gloo)."""
+    world, rank = dist.get_world_size(), dist.get_rank()
+    recv[rank].copy_(send[rank])
+    ops = []
+    for r in range(world):
+        if r != rank:
+            ops.append(dist.P2POp(dist.isend, send[r], r))
+            ops.append(dist.P2POp(dist.irecv, recv[r], r))
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+
+
+def combine_sharded(local, K, dist, method="mean", device=None, gpu=0, combine_fn=None):
+    """Column-sharded combine of K subset grids held by contiguous subset blocks of the ranks.
+
+    local: (n_local, L, C) grids of this rank's subsets (shard_range order).  One all-to-all
+    exchange gives rank r every subset's grid for its column block; it combines them in global
+    subset order on its GPU -- "mean" is MK.R:123-133 in the reference's summation order (so the
+    result is bit-identical to one GPU), "median" the Weiszfeld extension (per column, so also
+    independent of the sharding) -- and the combined blocks are all-gathered.  Per-rank memory
+    is K x L x C / world, where a full all-gather needs K x L x C (400 GB at cfg5's 1M sites).
+    combine_fn(list of L x c grids) -> L x c overrides the device combine (CPU tests)."""
+    import torch
+    from .post import combine_median
+    from .session import combine
+    world, rank = dist.get_world_size(), dist.get_rank()
+    local = np.asarray(local, dtype=np.float64)
+    L, C = local.shape[1], local.shape[2]
+    per_k = (K + world - 1) // world
+    blocks = col_blocks(C, world)
+    cmax = max(1, max(b - a for a, b in blocks))
+    dev = torch.device("cpu") if device is None else torch.device(device)
+    send = torch.zeros((world, per_k, L, cmax), dtype=torch.float64)
+    for r, (a, b) in enumerate(blocks):
+        if b > a and local.shape[0]:
+            send[r, :local.shape[0], :, :b - a] = torch.from_numpy(np.ascontiguousarray(local[:, :, a:b]))
+    send = send.to(dev)
+    recv = torch.empty_like(send)
+    _exchange(send, recv, dist)
+    a, b = blocks[rank]
+    mine = recv.cpu().numpy()
+    grids = []
+    for src in range(world):                       # global subset order
+        lo, hi = shard_range(K, world, src)
+        grids += [mine[src, i, :, :b - a] for i in range(hi - lo)]
+    if combine_fn is None:
+        if method == "mean":
+            combine_fn = lambda g: combine(g, device=gpu)                 # noqa: E731
+        elif method == "median":
+            combine_fn = lambda g: combine_median(g, device=gpu)[0]       # noqa: E731
+        else:
+            raise ValueError(f"error: unknown combine method '{method}'")
+    buf = torch.zeros((L, cmax), dtype=torch.float64)
+    if b > a:
+        buf[:, :b - a] = torch.from_numpy(np.ascontiguousarray(combine_fn(grids)))
+    buf = buf.to(dev)
+    outs = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(outs, buf)
+    return np.concatenate([outs[r].cpu().numpy()[:, :blocks[r][1] - blocks[r][0]] for r in range(world)], axis=1)
+
+
+def meta_fit_distributed(y, x, weight, coords, q, index_part, coords_test, cfg, dist, device=0, method="mean"):
+    """Fit this rank's shard of subsets on its GPU, then the one exchange: the column-sharded
+    combine (MK.R:119-133; method="median" for the Weiszfeld extension).
 
     Returns (obj_local, result, result2): the local `obj` entries (MK.R:108) and the
     combined grids (MK.R:127, MK.R:133), identical on every rank."""
     from .metakriging import meta_fit
-    from .session import combine
     import torch
     K = len(index_part)
     lo, hi = shard_range(K, dist.get_world_size(), dist.get_rank())
@@ -50,12 +120,10 @@ def meta_fit_distributed(y, x, weight, coords, q, index_part, coords_test, cfg, 
     dev = torch.device("cuda", device) if dist.get_backend() == "nccl" else None
     P = cfg.P
     par = np.stack([o["parameters"] for o in obj]) if obj else np.zeros((0, 200, P))
-    allpar = allgather_grids(par, K, dist, dev)
-    result = combine(list(allpar), device=device)
+    result = combine_sharded(par, K, dist, method=method, device=dev, gpu=device)
     result2 = None
     if coords_test is not None:
         C = q * np.asarray(coords_test).shape[0]
         wp = np.stack([o["w.predict"] for o in obj]) if obj else np.zeros((0, 200, C))
-        allw = allgather_grids(wp, K, dist, dev)
-        result2 = combine(list(allw), device=device)
+        result2 = combine_sharded(wp, K, dist, method=method, device=dev, gpu=device)
     return obj, result, result2
