@@ -1,0 +1,82 @@
+#!/usr/bin/env python3
+"""Kriging throughput at BASELINE.json configs[4] scale: spPredict of 1,000,000 held-out sites
+(n = 500k, K = 250 subsets of 2,000, exponential, q = 1), run through the tiled path
+(predict_tile): the kept chain states are recorded during the fit and the kriging replays them
+over test-site tiles, so 1M x kept draws per subset never coexist in HBM.
+
+A full cfg5 run (250 subsets x 1M sites x 1,251 kept samples) is ~10^17 flops; this script times a
+bounded sample -- `--subsets` subsets, `--kept` kept samples, all 1M sites -- and reports the
+measured rates plus the extrapolation to the full configuration.  Unit of work: one kriging draw
+(subset, test site, kept sample).  Algorithmic flops: per (subset, distinct (phi, nu) run) the
+triangular X = W P^T costs n_s^2 * n_test (W lower-triangular n_s x n_s); the per-run Cholesky +
+inverse (2 n_s^3 / 3) and the draws (2 n_s per draw) are counted too.
+
+  python bench_kriging.py [--subsets 8] [--n-test 1000000] [--kept 6] [--tile 65536]
+"""
+import argparse
+import importlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+PKG = "laurabaracaldo-spatial-meta-kriging-for-distributed-inference-for-binary-response_amd"
+FP64_PEAK_TFLOPS = 78.6
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--subsets", type=int, default=8)
+    ap.add_argument("--n-sub", type=int, default=2000)
+    ap.add_argument("--n-test", type=int, default=1_000_000)
+    ap.add_argument("--kept", type=int, default=6)
+    ap.add_argument("--burn", type=int, default=14)
+    ap.add_argument("--tile", type=int, default=65536)
+    a = ap.parse_args()
+    mk = importlib.import_module(PKG)
+    S, ns = a.subsets, a.n_sub
+    d = mk.synthetic.generate(S * ns, q=1, n_test=a.n_test, seed=20250114)
+    beta0, bt = mk.start_values(d["y"], d["x"], 1.0, 1)
+    n_samples = a.burn + a.kept
+    cfg = mk.SamplerConfig(1, 2, beta0, bt, n_batch=1, batch_length=n_samples, burn_in=a.burn + 1, seed=20250114,
+                           predict_tile=a.tile)
+    subs = [dict(coords=d["coords"][i * ns:(i + 1) * ns], y=d["y"][i * ns:(i + 1) * ns], weights=np.ones(ns),
+                 x=d["x"][i * ns:(i + 1) * ns]) for i in range(S)]
+    with mk.Session(subs, cfg, coords_test=d["coords_test"]) as ses:
+        t0 = time.perf_counter()
+        ses.run(n_samples)
+        t1 = time.perf_counter()
+        out = ses.outputs(quantiles=False, samples=True, w_predict_sum=True)
+        t2 = time.perf_counter()
+    kept_phi = np.stack([smp[a.burn:, 3] for smp in out["samples"]])          # phi column of p.beta.theta.samples
+    runs = int(sum(1 + np.count_nonzero(np.diff(r)) for r in kept_phi))
+    pred_s = t2 - t1
+    flops = runs * (ns * ns * a.n_test + 2.0 * ns ** 3 / 3.0 * ((a.n_test + a.tile - 1) // a.tile)) \
+        + 2.0 * ns * S * a.n_test * a.kept
+    draws = S * a.n_test * a.kept
+    # extrapolation: cfg5 = 250 subsets x 1M sites x 1251 kept; runs scale with the kept acceptance of phi
+    run_frac = runs / (S * a.kept)
+    cfg5_flops = 250 * 1251 * run_frac * ns * ns * 1_000_000
+    rate_tf = flops / pred_s / 1e12
+    res = {
+        "metric": "kriging draws/s (tiled spPredict, configs[4] scale)",
+        "value": draws / pred_s, "unit": "draws/s", "n_gpus": 1, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": f"configs[4] sample: {S} subsets of {ns}, {a.n_test} test sites, {a.kept} kept samples, "
+                               f"tile {a.tile}", "subsets": S, "n_test": a.n_test, "kept": a.kept, "tile": a.tile},
+        "fit_seconds": t1 - t0, "predict_seconds": pred_s, "phi_runs": runs,
+        "roofline": {"bound": "mfma", "achieved": rate_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": rate_tf / FP64_PEAK_TFLOPS},
+        "cfg5_extrapolation": {"flops": cfg5_flops, "seconds_1gpu": cfg5_flops / (rate_tf * 1e12),
+                               "seconds_8gpu": cfg5_flops / (rate_tf * 1e12) / 8,
+                               "assumes": f"phi runs per kept sample {run_frac:.3f} as measured here"},
+        "w_predict_sum_finite": bool(np.isfinite(out["w_predict_sum"]).all()),
+    }
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -75,6 +75,11 @@ typedef struct mk_config {
   int32_t device;               /* HIP device ordinal                                    */
   int32_t n_streams;            /* subset groups run on this many HIP streams (0: default 1);
                                    results do not depend on it                          */
+  int32_t predict_tile;         /* 0 (or >= n_test): spPredict fused into the kept iterations.
+                                   Else the kept chain states are recorded and the kriging
+                                   runs after the fit over tiles of this many test sites, so
+                                   (q*n_test) x kept draws per subset never coexist (cfg5:
+                                   1M sites); results are identical either way            */
 } mk_config;
 
 /* Caller-allocated outputs; any pointer may be NULL to skip it.
@@ -87,6 +92,9 @@ typedef struct mk_outputs {
   double* w_pred_samples; /* [n_subsets] x ((q*n_test) x kept): m.s.pred$p.w.predictive.samples */
   double* acceptance;   /* [n_subsets] x (n_batch x (p + n_theta + 1)): per-batch accept rates,
                            last column = mean over the latent w                                  */
+  double* w_predict_sum; /* 200 x (q*n_test): w_predict summed over this call's subsets in subset
+                           order -- this shard's term of the combine (MK.R:129-132) without the
+                           per-subset grids on the host                                          */
 } mk_outputs;
 
 typedef struct mk_session mk_session;

@@ -47,12 +47,12 @@ class Config(ctypes.Structure):
                 ("phi_unif_a", _dp), ("phi_unif_b", _dp), ("nu_unif_a", _dp), ("nu_unif_b", _dp),
                 ("K_IW_df", ctypes.c_double), ("K_IW_S", _dp), ("seed", ctypes.c_uint64),
                 ("record_samples", ctypes.c_int32), ("record_w", ctypes.c_int32), ("device", ctypes.c_int32),
-                ("n_streams", ctypes.c_int32)]
+                ("n_streams", ctypes.c_int32), ("predict_tile", ctypes.c_int32)]
 
 
 class Outputs(ctypes.Structure):
     _fields_ = [("parameters", _dp), ("w_predict", _dp), ("samples", _dp), ("w_samples", _dp),
-                ("w_pred_samples", _dp), ("acceptance", _dp)]
+                ("w_pred_samples", _dp), ("acceptance", _dp), ("w_predict_sum", _dp)]
 
 
 class Summary(ctypes.Structure):

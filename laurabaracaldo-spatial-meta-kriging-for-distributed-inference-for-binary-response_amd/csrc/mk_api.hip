@@ -108,6 +108,9 @@ Model model_view(const Model& m, int s0, int S) {
   if (m.PT) v.PT = m.PT + s * q * np * m.n_test_pad;
   if (m.XK) v.XK = m.XK + s * q * np * m.n_test_pad;
   v.w_pred = m.w_pred + s * m.n_kept * q * (long)std::max(m.n_test, 1);
+  if (m.kz) v.kz = m.kz + s * q * np;
+  if (m.kth) v.kth = m.kth + s * m.n_theta;
+  if (m.kA) v.kA = m.kA + s * q * q;
   return v;
 }
 
@@ -134,6 +137,11 @@ struct mk_session {
   int iter = 0;
   bool matern = false, record_samples = true, record_w = false;
   Group all;                      // the whole shard on `stream`
+  bool tiled = false;             // kriging after the fit over test-site tiles (predict_tile)
+  int pred_tile = 0, n_test_all = 0, n_test_pad_all = 0;
+  double* d_ct_all = nullptr;     // all test sites [2][n_test_pad_all] (tiled mode)
+  int* d_slist = nullptr;         // tiled replay: per-outcome subset lists [q][S] + counts [q]
+  int* d_scount = nullptr;
   std::vector<Group> groups;      // the run-time split, one stream each
   double* d_probs = nullptr;
   std::vector<int> n_part;
@@ -200,7 +208,7 @@ static inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
 
 // ------------------------------------------------------------------ Cholesky of all candidates of outcome h
 // Candidate tiles are in the free slot (k_cov_candidate, or k_load_plain for the test entry).
-static void launch_cholesky(mk_session* s, Group& g, int h) {
+static void launch_cholesky(mk_session* s, Group& g, int h, const int* slist = nullptr, const int* scount = nullptr) {
   const int nt = s->nt, S = g.S;
   const size_t diag_lds = (size_t)(MK_NB * MK_NB + 2 * MK_NB + 4 * 256) * sizeof(double);
   // valid extent (excludes padding) for the algorithmic flop count
@@ -213,18 +221,20 @@ static void launch_cholesky(mk_session* s, Group& g, int h) {
       const double kk = std::fmin((double)k * MK_NB, nv);
       const double fl = 2.0 * rows * cols * kk * S;
       timed(s, g.stream, KS_CHOL_UPDATE, fl, [&] {
-        hipLaunchKernelGGL(k_chol_update, dim3(xcd_grid_h(S, nt - k)), dim3(256), 0, g.stream, g.ms, S, h, k);
+        hipLaunchKernelGGL(k_chol_update, dim3(xcd_grid_h(S, nt - k)), dim3(256), 0, g.stream, g.ms, S, h, k, slist,
+                           scount);
       });
     }
     timed(s, g.stream, KS_CHOL_DIAG, 0.0, [&] {
       hipLaunchKernelGGL(k_chol_diag, dim3(S), dim3(256), diag_lds, g.stream, g.ms, g.md.n_s, h, k, g.md.ld_part,
-                         g.md.quad_c, g.md.info);
+                         g.md.quad_c, g.md.info, slist, scount);
     });
     if (k < nt - 1) {
       const double rows = std::fmax(0.0, nv - (k + 1) * MK_NB);
       const double fl = 2.0 * rows * MK_NB * MK_NB * S;
       timed(s, g.stream, KS_CHOL_TRSM, fl, [&] {
-        hipLaunchKernelGGL(k_chol_trsm, dim3(xcd_grid_h(S, nt - k - 1)), dim3(256), 0, g.stream, g.ms, S, h, k);
+        hipLaunchKernelGGL(k_chol_trsm, dim3(xcd_grid_h(S, nt - k - 1)), dim3(256), 0, g.stream, g.ms, S, h, k, slist,
+                           scount);
       });
     }
   }
@@ -280,22 +290,24 @@ static void run_iteration(mk_session* s, Group& g, int it) {
   const int ntri_tiles = s->nt * (s->nt + 1) / 2;
   for (int which = 0; which < nkinds; ++which)
     for (int h = 0; h < q; ++h) {
-      hipLaunchKernelGGL(k_cov_candidate, dim3(xcd_grid_h(S, ntri_tiles)), dim3(256), 0, st, md, g.ms, h, which, it);
+      hipLaunchKernelGGL(k_cov_candidate, dim3(xcd_grid_h(S, ntri_tiles)), dim3(256), 0, st, md, g.ms, h, which, it,
+                         nullptr, nullptr);
       launch_cholesky(s, g, h);
       hipLaunchKernelGGL(k_theta_mh, dim3((S + 63) / 64), dim3(64), 0, st, md, g.ms, h, which, it);
     }
   hipLaunchKernelGGL(k_dirty_list, dim3(1), dim3(256), 0, st, md, (int)(it == md.kept0), g.d_list, g.d_count,
                      g.d_plist, g.d_pcount);
   launch_inverse(s, g);
-  if (kept) launch_pred_refresh(s, g);
+  if (kept && !s->tiled) launch_pred_refresh(s, g);
   const size_t sw_lds = (size_t)q * (64 * 64 + 2 * 64) * sizeof(double);
   timed(s, st, KS_SWEEP, 0.0, [&] { hipLaunchKernelGGL(k_sweep, dim3(S), dim3(512), sw_lds, st, md, g.ms, it); });
   if (s->record_samples) hipLaunchKernelGGL(k_record, dim3((S + 63) / 64), dim3(64), 0, st, md, it);
   if (s->record_w) hipLaunchKernelGGL(k_record_w, dim3((md.Np + 255) / 256, S), dim3(256), 0, st, md, it);
-  if (kept && md.n_test > 0) {
+  if (kept && md.n_test > 0 && !s->tiled) {
     const int per = (md.n_test + 3) / 4;
     hipLaunchKernelGGL(k_pred_draw, dim3(S * per), dim3(256), 0, st, md, it, it - md.kept0);
   }
+  if (kept && s->tiled) hipLaunchKernelGGL(k_record_kept, dim3(S), dim3(256), 0, st, md, it - md.kept0);
   if ((it + 1) % md.batch_length == 0) hipLaunchKernelGGL(k_adapt, dim3(S), dim3(256), 0, st, md, it / md.batch_length);
 }
 
@@ -312,6 +324,7 @@ static int check_cfg(const mk_problem* pr, const mk_config* c) {
   if (c->burn_in < 1 || c->burn_in > n_samples) return set_err(MK_E_ARG, "burn_in must be in [1, n.samples]");
   if (n_samples - c->burn_in + 1 > 2048) return set_err(MK_E_ARG, "at most 2048 kept samples supported");
   if (c->n_streams < 0 || c->n_streams > 8) return set_err(MK_E_ARG, "n_streams must be in [0, 8]");
+  if (c->predict_tile < 0) return set_err(MK_E_ARG, "predict_tile must be >= 0");
   if (!c->beta_starting || !c->beta_tuning || !c->phi_starting || !c->phi_tuning || !c->A_starting || !c->A_tuning ||
       !c->phi_unif_a || !c->phi_unif_b || !c->K_IW_S)
     return set_err(MK_E_ARG, "null starting/tuning/prior array");
@@ -398,7 +411,12 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
   const int n_samples = c->n_batch * c->batch_length;
   const int kept0 = c->burn_in - 1;
   const int n_kept = n_samples - kept0;
-  const int n_test = pr->n_test;
+  // tiled kriging: device kriging buffers hold one tile of test sites; all sites stay in HBM
+  s->tiled = c->predict_tile > 0 && c->predict_tile < pr->n_test;
+  s->n_test_all = pr->n_test;
+  s->n_test_pad_all = round_up(std::max(pr->n_test, 1), 256);
+  s->pred_tile = s->tiled ? c->predict_tile : pr->n_test;
+  const int n_test = s->pred_tile;
   const int n_test_pad = round_up(std::max(n_test, 1), 256);
 
   Model& md = s->md;
@@ -409,6 +427,8 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
   md.kept0 = kept0; md.n_kept = n_kept;
   md.n_test = n_test; md.n_test_pad = n_test_pad; md.ntt = n_test_pad / MK_NB;
   md.subset_base = pr->subset_base;
+  md.S_all = S;
+  md.t_off = 0;
   md.seed = c->seed;
   md.accept_rate = c->accept_rate;
   md.P = P;
@@ -426,7 +446,8 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
   int* d_ns; double *d_coords, *d_y, *d_wt, *d_X, *d_ct;
   if ((rc = s->alloc(&d_ns, S)) || (rc = s->alloc(&d_coords, (size_t)S * 2 * n_pad)) ||
       (rc = s->alloc(&d_y, (size_t)S * Np)) || (rc = s->alloc(&d_wt, (size_t)S * Np)) ||
-      (rc = s->alloc(&d_X, (size_t)S * p * Np)) || (rc = s->alloc(&d_ct, (size_t)2 * n_test_pad)))
+      (rc = s->alloc(&d_X, (size_t)S * p * Np)) || (rc = s->alloc(&d_ct, (size_t)2 * n_test_pad)) ||
+      (rc = s->alloc(&s->d_ct_all, (size_t)2 * s->n_test_pad_all)))
     return fail(rc);
   md.n_s = d_ns; md.coords = d_coords; md.y = d_y; md.wt = d_wt; md.X = d_X; md.coords_test = d_ct;
   if ((rc = s->alloc(&md.beta, (size_t)S * p)) || (rc = s->alloc(&md.theta, (size_t)S * n_theta)) ||
@@ -443,6 +464,11 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
       (rc = s->alloc(&md.acc_hist, (size_t)S * c->n_batch * (o_w + 1))))
     return fail(rc);
   if (s->record_w && (rc = s->alloc(&md.w_samples, (size_t)S * n_samples * Np))) return fail(rc);
+  if (s->tiled && ((rc = s->alloc(&md.kz, (size_t)n_kept * S * q * n_pad)) ||
+                   (rc = s->alloc(&md.kth, (size_t)n_kept * S * n_theta)) ||
+                   (rc = s->alloc(&md.kA, (size_t)n_kept * S * q * q)) ||
+                   (rc = s->alloc(&s->d_slist, (size_t)q * S)) || (rc = s->alloc(&s->d_scount, (size_t)q))))
+    return fail(rc);
   if ((rc = s->alloc(&md.s_pred, (size_t)S * q * n_test_pad)) ||
       (rc = s->alloc(&md.s_part, (size_t)S * q * nt * n_test_pad)) ||
       (n_test > 0 && (rc = s->alloc(&md.PT, (size_t)S * q * n_pad * n_test_pad))) ||
@@ -483,17 +509,20 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
       off_site += ns;
     }
   }
-  std::vector<double> hct((size_t)2 * n_test_pad, 0.0);
-  for (int t = 0; t < n_test; ++t) {
+  const int npa = s->n_test_pad_all, nta = s->n_test_all;
+  std::vector<double> hct((size_t)2 * npa, 0.0);
+  for (int t = 0; t < nta; ++t) {
     hct[t] = pr->coords_test[t];
-    hct[n_test_pad + t] = pr->coords_test[n_test + t];
+    hct[npa + t] = pr->coords_test[nta + t];
   }
   HIPCHK(hipMemcpy(d_ns, pr->n_part, S * sizeof(int), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(d_coords, hc.data(), hc.size() * 8, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(d_y, hy.data(), hy.size() * 8, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(d_wt, hw.data(), hw.size() * 8, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(d_X, hX.data(), hX.size() * 8, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(d_ct, hct.data(), hct.size() * 8, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(s->d_ct_all, hct.data(), hct.size() * 8, hipMemcpyHostToDevice));
+  // fused kriging reads every site from d_ct ([2][n_test_pad]); tiled mode fills it per tile
+  if (!s->tiled) HIPCHK(hipMemcpy(d_ct, hct.data(), hct.size() * 8, hipMemcpyHostToDevice));
 
   // ---------------- starting values (identical for every subset, MK.R:54-62)
   std::vector<double> hb((size_t)S * p), hth((size_t)S * n_theta), hwv((size_t)S * Np, 0.0),
@@ -576,7 +605,8 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
   hipLaunchKernelGGL(k_init_state, dim3(S), dim3(256), 0, s->stream, md);
   const int ntri_tiles = nt * (nt + 1) / 2;
   for (int h = 0; h < q; ++h) {
-    hipLaunchKernelGGL(k_cov_candidate, dim3(xcd_grid_h(S, ntri_tiles)), dim3(256), 0, s->stream, md, ms, h, 2, 0);
+    hipLaunchKernelGGL(k_cov_candidate, dim3(xcd_grid_h(S, ntri_tiles)), dim3(256), 0, s->stream, md, ms, h, 2, 0,
+                       nullptr, nullptr);
     launch_cholesky(s, a, h);
     hipLaunchKernelGGL(k_theta_init, dim3((S + 63) / 64), dim3(64), 0, s->stream, md, ms, h);
   }
@@ -626,6 +656,76 @@ extern "C" int mk_session_kernel_stats(const mk_session* s, int32_t which, int64
   return 0;
 }
 
+// spPredict after the fit (MK.R:87-89) over test-site tiles: replays the kriging of every kept
+// iteration from the recorded chain states (z, theta, A).  A factor is recomputed only where
+// (phi, nu) changed since the previous kept sample, with the same kernels and inputs as in the
+// fit (rows < n_s of a factor do not depend on its border row), so the draws, the quantiles and
+// their sum are bit-identical to the fused path.  Per tile the device holds q*T x kept draws
+// per subset instead of q*n_test x kept.
+static int predict_tiled(mk_session* s, mk_outputs* o) {
+  Model& md = s->md;
+  const int S = s->S, q = s->q, nt = s->nt, n_kept = md.n_kept;
+  const int T = s->pred_tile, T_pad = md.n_test_pad, n_test = s->n_test_all;
+  const long C = (long)q * n_test;
+  hipStream_t st = s->stream;
+  Group g = s->all;
+  const int ntri_tiles = nt * (nt + 1) / 2;
+  double *dq = nullptr, *dsum = nullptr;
+  int rc;
+  if ((rc = s->alloc(&dq, (size_t)S * q * T * MK_N_LEVELS)) || (rc = s->alloc(&dsum, (size_t)q * T * MK_N_LEVELS)))
+    return rc;
+  for (int t0 = 0; t0 < n_test; t0 += T) {
+    const int Tc = std::min(T, n_test - t0);
+    const int Ct = q * Tc;
+    HIPCHK(hipMemsetAsync((void*)md.coords_test, 0, (size_t)2 * T_pad * 8, st));
+    HIPCHK(hipMemcpyAsync((void*)md.coords_test, s->d_ct_all + t0, (size_t)Tc * 8, hipMemcpyDeviceToDevice, st));
+    HIPCHK(hipMemcpyAsync((void*)(md.coords_test + T_pad), s->d_ct_all + s->n_test_pad_all + t0, (size_t)Tc * 8,
+                          hipMemcpyDeviceToDevice, st));
+    Model mt = md;
+    mt.n_test = Tc;
+    mt.t_off = t0;
+    for (int k = 0; k < n_kept; ++k) {
+      mt.theta = md.kth + (long)k * S * md.n_theta;
+      mt.z = md.kz + (long)k * S * q * md.n_pad;
+      mt.A_full = md.kA + (long)k * S * q * q;
+      const double* prev = k ? md.kth + (long)(k - 1) * S * md.n_theta : nullptr;
+      hipLaunchKernelGGL(k_kept_dirty, dim3(1), dim3(256), 0, st, mt, prev, s->d_slist, s->d_scount, g.d_plist,
+                         g.d_pcount);
+      for (int h = 0; h < q; ++h) {
+        hipLaunchKernelGGL(k_cov_candidate, dim3(xcd_grid_h(S, ntri_tiles)), dim3(256), 0, st, mt, g.ms, h, 2, 0,
+                           s->d_slist + h * S, s->d_scount + h);
+        launch_cholesky(s, g, h, s->d_slist + h * S, s->d_scount + h);
+      }
+      hipLaunchKernelGGL(k_flip_pairs, dim3((S * q + 255) / 256), dim3(256), 0, st, g.ms, g.d_plist, g.d_pcount);
+      launch_trinv(s, g, S * q, g.d_plist, g.d_pcount);
+      g.md = mt;
+      launch_pred_refresh(s, g);
+      const int per = (Tc + 3) / 4;
+      hipLaunchKernelGGL(k_pred_draw, dim3(S * per), dim3(256), 0, st, mt, md.kept0 + k, k);
+      HIPCHK(hipGetLastError());
+    }
+    hipLaunchKernelGGL(k_quantiles, dim3(S * Ct), dim3(256), 0, st, md.w_pred, (long)n_kept * Ct, (long)Ct, n_kept, Ct,
+                       s->d_probs, MK_N_LEVELS, dq);
+    HIPCHK(hipGetLastError());
+    if (o->w_predict)   // per subset [C][200]: this tile's columns
+      HIPCHK(hipMemcpy2DAsync(o->w_predict + (size_t)t0 * q * MK_N_LEVELS, (size_t)C * MK_N_LEVELS * 8, dq,
+                              (size_t)Ct * MK_N_LEVELS * 8, (size_t)Ct * MK_N_LEVELS * 8, S, hipMemcpyDeviceToHost, st));
+    if (o->w_predict_sum) {
+      hipLaunchKernelGGL(k_combine, dim3((unsigned)(((long)Ct * MK_N_LEVELS + 255) / 256)), dim3(256), 0, st, dq, S,
+                         (long)Ct * MK_N_LEVELS, dsum, 0);
+      HIPCHK(hipMemcpyAsync(o->w_predict_sum + (size_t)t0 * q * MK_N_LEVELS, dsum, (size_t)Ct * MK_N_LEVELS * 8,
+                            hipMemcpyDeviceToHost, st));
+    }
+    if (o->w_pred_samples)   // per subset (C x kept) column-major
+      for (int i = 0; i < S; ++i)
+        HIPCHK(hipMemcpy2DAsync(o->w_pred_samples + (size_t)i * n_kept * C + (size_t)t0 * q, (size_t)C * 8,
+                                md.w_pred + (size_t)i * n_kept * Ct, (size_t)Ct * 8, (size_t)Ct * 8, n_kept,
+                                hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+  }
+  return 0;
+}
+
 extern "C" int mk_session_outputs(mk_session* s, mk_outputs* o) {
   if (!s || !o) return set_err(MK_E_ARG, "null session/outputs");
   HIPCHK(hipSetDevice(s->device));
@@ -645,7 +745,11 @@ extern "C" int mk_session_outputs(mk_session* s, mk_outputs* o) {
     // device layout [S][P][200] == R's 200 x P column-major per subset
     HIPCHK(hipMemcpyAsync(o->parameters, dq, (size_t)S * P * MK_N_LEVELS * 8, hipMemcpyDeviceToHost, s->stream));
   }
-  if (o->w_predict && n_test > 0) {
+  if (s->tiled && (o->w_predict || o->w_pred_samples || o->w_predict_sum)) {
+    HIPCHK(hipStreamSynchronize(s->stream));
+    int rc = predict_tiled(s, o);
+    if (rc) return rc;
+  } else if ((o->w_predict || o->w_predict_sum) && n_test > 0) {
     const int C = q * n_test;
     double* dq;
     int rc = s->alloc(&dq, (size_t)S * C * MK_N_LEVELS);
@@ -653,7 +757,15 @@ extern "C" int mk_session_outputs(mk_session* s, mk_outputs* o) {
     hipLaunchKernelGGL(k_quantiles, dim3(S * C), dim3(256), 0, s->stream, md.w_pred, (long)md.n_kept * C, (long)C,
                        md.n_kept, C, s->d_probs, MK_N_LEVELS, dq);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(o->w_predict, dq, (size_t)S * C * MK_N_LEVELS * 8, hipMemcpyDeviceToHost, s->stream));
+    if (o->w_predict)
+      HIPCHK(hipMemcpyAsync(o->w_predict, dq, (size_t)S * C * MK_N_LEVELS * 8, hipMemcpyDeviceToHost, s->stream));
+    if (o->w_predict_sum) {   // this shard's term of the combine: sequential sum over its subsets
+      double* dsum;
+      if ((rc = s->alloc(&dsum, (size_t)C * MK_N_LEVELS))) return rc;
+      hipLaunchKernelGGL(k_combine, dim3((unsigned)(((long)C * MK_N_LEVELS + 255) / 256)), dim3(256), 0, s->stream, dq,
+                         S, (long)C * MK_N_LEVELS, dsum, 0);
+      HIPCHK(hipMemcpyAsync(o->w_predict_sum, dsum, (size_t)C * MK_N_LEVELS * 8, hipMemcpyDeviceToHost, s->stream));
+    }
   }
   HIPCHK(hipStreamSynchronize(s->stream));
   const int it = s->iter;
@@ -680,7 +792,7 @@ extern "C" int mk_session_outputs(mk_session* s, mk_outputs* o) {
       off += (size_t)N * md.n_samples;
     }
   }
-  if (o->w_pred_samples && n_test > 0) {
+  if (o->w_pred_samples && n_test > 0 && !s->tiled) {
     const int C = q * n_test;
     std::vector<double> h((size_t)S * md.n_kept * C);
     HIPCHK(hipMemcpy(h.data(), md.w_pred, h.size() * 8, hipMemcpyDeviceToHost));
@@ -749,7 +861,7 @@ extern "C" int mk_combine(const double* grids, int32_t K, int64_t G, double* out
   double* dout = b.get<double>((size_t)G);
   if (!dg || !dout) return set_err(MK_E_NOMEM, "combine alloc");
   HIPCHK(hipMemcpy(dg, grids, (size_t)K * G * 8, hipMemcpyHostToDevice));
-  hipLaunchKernelGGL(k_combine, dim3((unsigned)((G + 255) / 256)), dim3(256), 0, 0, dg, K, (long)G, dout);
+  hipLaunchKernelGGL(k_combine, dim3((unsigned)((G + 255) / 256)), dim3(256), 0, 0, dg, K, (long)G, dout, 1);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpy(out, dout, (size_t)G * 8, hipMemcpyDeviceToHost));
   return 0;

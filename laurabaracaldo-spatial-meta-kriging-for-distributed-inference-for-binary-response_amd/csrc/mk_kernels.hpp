@@ -5,10 +5,11 @@
 namespace mk {
 inline int xcd_grid_h(int S, int T) { return 8 * ((S + 7) / 8) * T; }
 // mk_linalg.hip
-__global__ void k_cov_candidate(Model md, MatSet ms, int h, int which, int iter);
-__global__ void k_chol_update(MatSet ms, int S, int h, int k);
-__global__ void k_chol_trsm(MatSet ms, int S, int h, int k);
-__global__ void k_chol_diag(MatSet ms, const int* n_s, int h, int k, double* ld_part, double* quad_c, int* info);
+__global__ void k_cov_candidate(Model md, MatSet ms, int h, int which, int iter, const int* slist, const int* scount);
+__global__ void k_chol_update(MatSet ms, int S, int h, int k, const int* slist, const int* scount);
+__global__ void k_chol_trsm(MatSet ms, int S, int h, int k, const int* slist, const int* scount);
+__global__ void k_chol_diag(MatSet ms, const int* n_s, int h, int k, double* ld_part, double* quad_c, int* info,
+                            const int* slist, const int* scount);
 __global__ void k_inv_copydiag(MatSet ms, const int* list, const int* count);
 __global__ void k_inv_level(MatSet ms, const int* list, const int* count, int sz, int phase);
 __global__ void k_lauum(MatSet ms, const int* n_s, const int* list, const int* count);
@@ -30,7 +31,10 @@ __global__ void k_adapt(Model md, int b);
 __global__ void k_pred_draw(Model md, int iter, int kidx);
 __global__ void k_quantiles(const double* data, long subset_stride, long row_stride, int n_rows, int n_cols,
                             const double* probs, int n_probs, double* out);
-__global__ void k_combine(const double* grids, int K, long G, double* out);
+__global__ void k_combine(const double* grids, int K, long G, double* out, int mean);
+__global__ void k_record_kept(Model md, int kidx);
+__global__ void k_kept_dirty(Model md, const double* th_prev, int* slist, int* scount, int* plist, int* pcount);
+__global__ void k_flip_pairs(MatSet ms, const int* plist, const int* pcount);
 // mk_post.hip
 __global__ void k_weiszfeld(const double* grids, int K, int L, long C, int max_iter, double tol, double* out, int* iters);
 __global__ void k_post_index(uint64_t seed, int samplesize, int n_levels, int* idx);

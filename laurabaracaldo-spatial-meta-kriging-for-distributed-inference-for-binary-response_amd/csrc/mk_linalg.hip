@@ -82,10 +82,20 @@ __host__ inline int xcd_grid(int S, int T) { return 8 * ((S + 7) / 8) * T; }
 // Lower tiles (i >= j) of every candidate of outcome h (tiles with j < jmin are skipped).
 // Generating tiles inside k_chol_update at their first touch (gen = 1) was measured
 // slower on cfg3 (+3.5 ms of exp work at 2 waves/SIMD vs 1.7 ms for this pass).
-__global__ __launch_bounds__(256) void k_cov_candidate(Model md, MatSet ms, int h, int which, int iter) {
+// Optional subset list (tiled kriging refactors only the subsets whose (phi, nu) changed):
+// entry e -> subset slist[e] for e < *scount; slist == nullptr: every subset.
+__device__ inline bool pick_subset(const int* slist, const int* scount, int* s) {
+  if (!slist) return true;
+  if (*s >= *scount) return false;
+  *s = slist[*s];
+  return true;
+}
+
+__global__ __launch_bounds__(256) void k_cov_candidate(Model md, MatSet ms, int h, int which, int iter,
+                                                       const int* slist, const int* scount) {
   const int ntiles = ms.nt * (ms.nt + 1) / 2;
   int s, t;
-  if (!xcd_map(md.S, ntiles, &s, &t)) return;
+  if (!xcd_map(md.S, ntiles, &s, &t) || !pick_subset(slist, scount, &s)) return;
   int ti = 0;
   while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
   const int tj = t - ti * (ti + 1) / 2;
@@ -106,11 +116,12 @@ __global__ __launch_bounds__(256) void k_cov_candidate(Model md, MatSet ms, int 
 // (Generating C(i,k) from coordinates at its first touch inside this kernel was measured
 // slower on cfg3 and its code path made the kernel spill 80 VGPRs: candidates come from
 // k_cov_candidate.)
-__global__ __launch_bounds__(256, 2) void k_chol_update(MatSet ms, int S, int h, int k) {
+__global__ __launch_bounds__(256, 2) void k_chol_update(MatSet ms, int S, int h, int k, const int* slist,
+                                                       const int* scount) {
   __shared__ __attribute__((aligned(16))) double lds[GB_LDS_DOUBLES];
   const int ntk = ms.nt - k;
   int s, t;
-  if (!xcd_map(S, ntk, &s, &t)) return;
+  if (!xcd_map(S, ntk, &s, &t) || !pick_subset(slist, scount, &s)) return;
   const int i = k + t;
   const int sh = s * ms.q + h;
   double* M = mat_slot(ms, sh, 1 - ms.cur[sh]);
@@ -122,11 +133,12 @@ __global__ __launch_bounds__(256, 2) void k_chol_update(MatSet ms, int S, int h,
   store_tile(C, ld, acc);
 }
 
-__global__ __launch_bounds__(256, 2) void k_chol_trsm(MatSet ms, int S, int h, int k) {
+__global__ __launch_bounds__(256, 2) void k_chol_trsm(MatSet ms, int S, int h, int k, const int* slist,
+                                                     const int* scount) {
   __shared__ __attribute__((aligned(16))) double lds[GB_LDS_DOUBLES];
   const int ntk = ms.nt - k - 1;
   int s, t;
-  if (!xcd_map(S, ntk, &s, &t)) return;
+  if (!xcd_map(S, ntk, &s, &t) || !pick_subset(slist, scount, &s)) return;
   const int i = k + 1 + t;
   const int sh = s * ms.q + h;
   const int slot = 1 - ms.cur[sh];
@@ -296,14 +308,17 @@ __device__ void factor_invert_tile(double* T, double* dg, double* xd, double* Pb
 // (if inside the tile) is the bordered row: its pivot is -(u' R^-1 u) and it is not
 // factored (pivot set to 1).
 __global__ __launch_bounds__(256) void k_chol_diag(MatSet ms, const int* __restrict__ n_s, int h, int k,
-                                                   double* ld_part, double* quad_c, int* info) {
+                                                   double* ld_part, double* quad_c, int* info, const int* slist,
+                                                   const int* scount) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
   double* T = sm;                      // [128*128]
   double* dg = T + TLD * TLD;          // [128]
   double* xd = dg + MK_NB;             // [128]
   double* Pb = xd + MK_NB;             // [4][256]
   __shared__ int badf;
-  const int s = blockIdx.x, tid = threadIdx.x;
+  int s = blockIdx.x;
+  if (!pick_subset(slist, scount, &s)) return;
+  const int tid = threadIdx.x;
   const int sh = s * ms.q + h;
   const int slot = 1 - ms.cur[sh];
   double* M = mat_slot(ms, sh, slot);

@@ -480,7 +480,7 @@ __global__ __launch_bounds__(256) void k_pred_draw(Model md, int iter, int kidx)
   if (lane == 0) {
     const Key key = subset_key(md, s);
     double v[MK_QMAX];
-    for (int h = 0; h < q; ++h) v[h] = mean[h] + sd[h] * predict_normal(key, t * q + h, iter);
+    for (int h = 0; h < q; ++h) v[h] = mean[h] + sd[h] * predict_normal(key, (md.t_off + t) * q + h, iter);
     const double* A = md.A_full + (long)s * q * q;
     double* out = md.w_pred + ((long)s * md.n_kept + kidx) * q * md.n_test + (long)t * q;
     for (int a = 0; a < q; ++a) {
@@ -528,13 +528,81 @@ __global__ __launch_bounds__(256) void k_quantiles(const double* __restrict__ da
 }
 
 // ---------------------------------------------------------------- 9. combine (MK.R:123-133)
-// out = (((g_0 + g_1) + g_2) + ...) / K : the reference's sequential order.
-__global__ __launch_bounds__(256) void k_combine(const double* __restrict__ grids, int K, long G, double* __restrict__ out) {
+// out = (((g_0 + g_1) + g_2) + ...) / K : the reference's sequential order (mean = 0: the sum only,
+// one shard's term of the combine).
+__global__ __launch_bounds__(256) void k_combine(const double* __restrict__ grids, int K, long G, double* __restrict__ out,
+                                                 int mean) {
   const long e = (long)blockIdx.x * 256 + threadIdx.x;
   if (e >= G) return;
   double acc = grids[e];
   for (int k = 1; k < K; ++k) acc = acc + grids[(long)k * G + e];
-  out[e] = acc / K;
+  out[e] = mean ? acc / K : acc;
+}
+
+// ---------------------------------------------------------------- 10. tiled kriging support
+// Kept iteration kidx: record z, theta and A of every subset ([n_kept][S_all][...] records).
+__global__ __launch_bounds__(256) void k_record_kept(Model md, int kidx) {
+  const int s = blockIdx.x, q = md.q;
+  const long row = (long)kidx * md.S_all + s;
+  for (int i = threadIdx.x; i < q * md.n_pad; i += 256) md.kz[row * q * md.n_pad + i] = md.z[(long)s * q * md.n_pad + i];
+  if (threadIdx.x < md.n_theta) md.kth[row * md.n_theta + threadIdx.x] = md.theta[(long)s * md.n_theta + threadIdx.x];
+  if (threadIdx.x < q * q) md.kA[row * q * q + threadIdx.x] = md.A_full[(long)s * q * q + threadIdx.x];
+}
+
+// Replaying kept sample k (md.theta = its record): the (subset, outcome) pairs whose (phi_h, nu_h)
+// differ from sample k-1 (all of them when th_prev == nullptr).  Outputs, in subset order:
+// per outcome h the subset list slist[h*S .. ] / scount[h] (candidate + Cholesky launches), and
+// the pair list (s*q + h) plist / pcount (inverse + kriging refresh).  One 256-thread block.
+__global__ __launch_bounds__(256) void k_kept_dirty(Model md, const double* __restrict__ th_prev, int* slist,
+                                                    int* scount, int* plist, int* pcount) {
+  __shared__ int wc[4];
+  __shared__ int base, pbase;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int q = md.q, S = md.S;
+  if (threadIdx.x == 0) pbase = 0;
+  for (int h = 0; h < q; ++h) {
+    if (threadIdx.x == 0) base = 0;
+    __syncthreads();
+    for (int c0 = 0; c0 < S; c0 += 256) {
+      const int s = c0 + threadIdx.x;
+      int d = 0;
+      if (s < S) {
+        const double* th = md.theta + (long)s * md.n_theta;
+        if (!th_prev) {
+          d = 1;
+        } else {
+          const double* tp = th_prev + (long)s * md.n_theta;
+          d = th[md.ntri + h] != tp[md.ntri + h];
+          if (md.cov_model == MK_COV_MATERN) d |= th[md.ntri + q + h] != tp[md.ntri + q + h];
+        }
+      }
+      const unsigned long long bal = __ballot(d);
+      const int before = __popcll(bal & ((1ull << lane) - 1ull));
+      if (lane == 0) wc[wv] = __popcll(bal);
+      __syncthreads();
+      int off = 0;
+      for (int k = 0; k < wv; ++k) off += wc[k];
+      if (d) {
+        slist[h * S + base + off + before] = s;
+        plist[pbase + base + off + before] = s * q + h;
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) base += wc[0] + wc[1] + wc[2] + wc[3];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+      scount[h] = base;
+      pbase += base;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *pcount = pbase;
+}
+
+// The freshly factored candidates of the listed pairs become the current factors.
+__global__ __launch_bounds__(256) void k_flip_pairs(MatSet ms, const int* __restrict__ plist, const int* __restrict__ pcount) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e < *pcount) ms.cur[plist[e]] ^= 1;
 }
 
 }  // namespace mk

@@ -29,6 +29,8 @@ struct Model {
   int n_batch, batch_length, n_samples, kept0, n_kept;
   int n_test, n_test_pad, ntt;
   int subset_base;                        // global index of local subset 0
+  int S_all;                              // subsets of the whole shard (stride of the kept-state records)
+  int t_off;                              // global index of test site 0 (tiled kriging; 0 when fused)
   uint64_t seed;
   double accept_rate;
   double phi_a[MK_QMAX], phi_b[MK_QMAX], nu_a[MK_QMAX], nu_b[MK_QMAX];
@@ -72,7 +74,11 @@ struct Model {
   double* s_part;      // [S*q][nt][n_test_pad]
   double* PT;          // [S*q][n_pad][n_test_pad]
   double* XK;          // [S*q][n_test_pad][n_pad]  column t = W rho_t
-  double* w_pred;      // [S][n_kept][q*n_test]
+  double* w_pred;      // [S][n_kept][q*n_test]   (tiled kriging: q*tile)
+  // kept chain states for tiled kriging: [n_kept][S_all][...]
+  double* kz;          // z_h = W_h u_h   (q*n_pad)
+  double* kth;         // theta           (n_theta)
+  double* kA;          // A               (q*q)
   int P;               // reported columns
 };
 

@@ -27,7 +27,7 @@ class SamplerConfig:
     def __init__(self, q, p, beta_starting, beta_tuning, cov_model="exponential", n_batch=100, batch_length=50,
                  accept_rate=0.43, burn_in=None, phi_starting=None, phi_tuning=None, phi_unif=None,
                  A_starting=None, A_tuning=None, w_starting=0.0, w_tuning=0.5, nu_starting=None, nu_tuning=None,
-                 nu_unif=None, K_IW_df=None, K_IW_S=None, seed=20250114, n_streams=0):
+                 nu_unif=None, K_IW_df=None, K_IW_S=None, seed=20250114, n_streams=0, predict_tile=0):
         if cov_model not in COV_MODELS:
             raise ValueError(f"error: specified cov.model '{cov_model}' is not a valid option")
         self.q, self.p = int(q), int(p)
@@ -70,6 +70,7 @@ class SamplerConfig:
         self.K_IW_S = _f64(np.diag(np.full(q, 0.1)) if K_IW_S is None else K_IW_S).reshape(q, q)
         self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
         self.n_streams = int(n_streams)     # device execution only (0 = library default); no effect on results
+        self.predict_tile = int(predict_tile)   # 0: kriging fused into kept iterations; else test sites per pass
 
     @property
     def n_theta(self):
@@ -110,6 +111,7 @@ class SamplerConfig:
         c.record_w = 1 if record_w else 0
         c.device = int(device)
         c.n_streams = self.n_streams
+        c.predict_tile = self.predict_tile
         return c, keep
 
 
@@ -164,7 +166,8 @@ class Session:
         check(self._lib.mk_session_kernel_stats(self._h, which, ctypes.byref(n), ctypes.byref(ms), ctypes.byref(fl)))
         return dict(launches=n.value, ms=ms.value, flops=fl.value)
 
-    def outputs(self, quantiles=True, samples=False, w_samples=False, w_pred_samples=False, acceptance=False):
+    def outputs(self, quantiles=True, samples=False, w_samples=False, w_pred_samples=False, acceptance=False,
+                w_predict_sum=False):
         cfg = self.cfg
         S, P, q = self.S, cfg.P, cfg.q
         o = Outputs()
@@ -189,6 +192,9 @@ class Session:
             nrep = cfg.p + cfg.n_theta + 1
             res["acceptance"] = np.zeros((S, nrep, cfg.n_batch))
             o.acceptance = dptr(res["acceptance"])
+        if w_predict_sum and self.n_test:
+            res["w_predict_sum"] = np.zeros((q * self.n_test, _lib.N_LEVELS))
+            o.w_predict_sum = dptr(res["w_predict_sum"])
         check(self._lib.mk_session_outputs(self._h, ctypes.byref(o)))
         out = {}
         # device/R layout: per subset column-major (levels x cols) == row-major (cols, levels)
@@ -207,6 +213,8 @@ class Session:
             out["w_samples"] = ws
         if "w_pred_samples" in res:
             out["w_pred_samples"] = [res["w_pred_samples"][i].T.copy() for i in range(S)]  # (q n_test) x kept
+        if "w_predict_sum" in res:
+            out["w_predict_sum"] = res["w_predict_sum"].T.copy()                               # 200 x q*n_test
         if "acceptance" in res:
             out["acceptance"] = [res["acceptance"][i].T.copy() for i in range(S)]          # n_batch x nrep
         return out

@@ -69,3 +69,32 @@ def test_subset_streams_independent_of_sharding(mk):
         oneq = ses.outputs()
     assert np.array_equal(allq["parameters"][2], oneq["parameters"][0])
     assert np.array_equal(allq["w_predict"][2], oneq["w_predict"][0])
+
+
+@pytest.mark.parametrize("n,q,cov,tile", [(150, 1, 0, 5), (64, 2, 0, 7), (100, 1, 1, 4), (120, 1, 0, 1)])
+def test_tiled_kriging_is_bit_identical_to_fused(mk, n, q, cov, tile):
+    """spPredict replayed after the fit over test-site tiles (the cfg5 path: 1M sites) gives the
+    fused path's draws, quantile grids and their subset sum exactly."""
+    S, n_test = 3, 12
+    d = mk.synthetic.generate(n * S, q=q, n_test=n_test, seed=31 + q, cov_model=cov)
+    p = 2 * q
+    subs = [dict(coords=d["coords"][s * n:(s + 1) * n], y=d["y"][s * n * q:(s + 1) * n * q], weights=np.ones(n * q),
+                 x=d["x"][s * n * q:(s + 1) * n * q]) for s in range(S)]
+    outs = []
+    for pt in (0, tile):
+        cfg = mk.SamplerConfig(q, p, beta_starting=np.zeros(p), beta_tuning=np.full(p, 0.05),
+                               cov_model="matern" if cov else "exponential", n_batch=3, batch_length=4, burn_in=5,
+                               seed=12, predict_tile=pt)
+        with mk.Session(subs, cfg, coords_test=d["coords_test"], subset_base=4) as ses:
+            ses.run(cfg.n_samples)
+            outs.append(ses.outputs(samples=True, w_pred_samples=True, w_predict_sum=True))
+    fused, tiled = outs
+    for s in range(S):
+        assert np.array_equal(tiled["samples"][s], fused["samples"][s])
+        assert np.array_equal(tiled["w_pred_samples"][s], fused["w_pred_samples"][s])
+        assert np.array_equal(tiled["w_predict"][s], fused["w_predict"][s])
+    assert np.array_equal(tiled["w_predict_sum"], fused["w_predict_sum"])
+    seq = fused["w_predict"][0].copy()
+    for s in range(1, S):
+        seq = seq + fused["w_predict"][s]
+    assert np.array_equal(fused["w_predict_sum"], seq)
