@@ -210,7 +210,7 @@ static inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
 // Candidate tiles are in the free slot (k_cov_candidate, or k_load_plain for the test entry).
 static void launch_cholesky(mk_session* s, Group& g, int h, const int* slist = nullptr, const int* scount = nullptr) {
   const int nt = s->nt, S = g.S;
-  const size_t diag_lds = (size_t)(MK_NB * MK_NB + 2 * MK_NB + 4 * 256) * sizeof(double);
+  const size_t diag_lds = (size_t)MK_DIAG_LDS_BYTES;
   // valid extent (excludes padding) for the algorithmic flop count
   const double nv = (double)s->n_part[g.s0] + 1.0;
   for (int k = 0; k < nt; ++k) {
@@ -596,7 +596,7 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
     HIPCHK(hipMemcpy(s->d_probs, probs.data(), MK_N_LEVELS * 8, hipMemcpyHostToDevice));
   }
   HIPCHK(hipFuncSetAttribute((const void*)k_chol_diag, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (MK_NB * MK_NB + 2 * MK_NB + 4 * 256) * 8));
+                             MK_DIAG_LDS_BYTES));
   HIPCHK(hipFuncSetAttribute((const void*)k_sweep, hipFuncAttributeMaxDynamicSharedMemorySize,
                              q * (64 * 64 + 2 * 64) * 8));
 
@@ -1123,7 +1123,7 @@ extern "C" int mk_cholesky_batched(const double* A, int32_t S, int32_t n, double
       hipMemset(ms.cur, 0, S * 4) != hipSuccess || hipMemset(md.info, 0, S * 4) != hipSuccess)
     return fail(set_err(MK_E_HIP, "cholesky upload"));
   if (hipFuncSetAttribute((const void*)k_chol_diag, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (MK_NB * MK_NB + 2 * MK_NB + 4 * 256) * 8) != hipSuccess)
+                          MK_DIAG_LDS_BYTES) != hipSuccess)
     return fail(set_err(MK_E_HIP, "lds attribute"));
   hipLaunchKernelGGL(k_load_plain, dim3(2048), dim3(256), 0, s->stream, ms, dA, n, S);
   launch_cholesky(s, a, 0);

@@ -93,7 +93,8 @@ __device__ inline void store_chunk(double* lds, const d2 (&r)[GB_PER]) {
 //               diagonal (column block > row block) are never read   (flag = tile is diagonal)
 //   SKIP_TRI_B  op(B) lower-triangular in (n, k) over one 128-deep K: chunk c only touches
 //               output column blocks >= c                             (flag = chunk index c)
-enum { SKIP_NONE = 0, SKIP_UPPER = 1, SKIP_TRI_B = 2 };
+//   SKIP_WAVE   the calling wave's whole 64x64 quadrant is unused        (flag = skip this wave)
+enum { SKIP_NONE = 0, SKIP_UPPER = 1, SKIP_TRI_B = 2, SKIP_WAVE = 3 };
 
 template <bool NEG = false, int SA = GB_SM, int SB = GB_SM, int SKIP = SKIP_NONE>
 __device__ inline void mma_chunk(const double* As, const double* Bs, Acc& acc, int flag = 0) {
@@ -146,8 +147,12 @@ __device__ inline void gemm_128(const double* __restrict__ A, long sA, const dou
       load_chunk<A_MU>(A, sA, k1, kvalid_total - k1, ra);
       if (!SAME) load_chunk<B_NU>(B, sB, k1, kvalid_total - k1, rb);
     }
-    mma_chunk<NEG, sm_of<A_MU>(), sm_of<B_NU>(), SKIP>(As, Bs, acc,
-                                                       SKIP == SKIP_TRI_B ? (REV ? K - GB_K - kc : kc) / GB_K : diag_tile);
+    if (SKIP == SKIP_WAVE) {
+      if (!diag_tile) mma_chunk<NEG, sm_of<A_MU>(), sm_of<B_NU>()>(As, Bs, acc);
+    } else {
+      mma_chunk<NEG, sm_of<A_MU>(), sm_of<B_NU>(), SKIP>(As, Bs, acc,
+                                                         SKIP == SKIP_TRI_B ? (REV ? K - GB_K - kc : kc) / GB_K : diag_tile);
+    }
   }
 }
 

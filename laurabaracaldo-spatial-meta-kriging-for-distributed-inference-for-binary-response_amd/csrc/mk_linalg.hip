@@ -103,10 +103,16 @@ __global__ __launch_bounds__(256) void k_cov_candidate(Model md, MatSet ms, int 
   const CandGen g = make_gen(md, s, h, which, iter);
   double* M = mat_slot(ms, sh, 1 - ms.cur[sh]);
   const long ld = ms.ld;
-  const int R = ti * MK_NB + (threadIdx.x & 127);
-  for (int cc = threadIdx.x >> 7; cc < MK_NB; cc += 2) {
+  // two rows per lane, 16-byte stores; the upper half of a diagonal tile is never read (the
+  // factor kernels read lower tiles only) and is left unwritten
+  const int R = ti * MK_NB + (threadIdx.x & 63) * 2;
+  for (int cc = threadIdx.x >> 6; cc < MK_NB; cc += 4) {
     const int C = tj * MK_NB + cc;
-    M[R + (long)C * ld] = g(R, C);
+    if (ti == tj && R + 1 < C) continue;
+    d2 v;
+    v.x = g(R, C);
+    v.y = g(R + 1, C);
+    *reinterpret_cast<d2*>(M + R + (long)C * ld) = v;
   }
 }
 
@@ -129,6 +135,7 @@ __global__ __launch_bounds__(256, 2) void k_chol_update(MatSet ms, int S, int h,
   double* C = M + i * MK_NB + (long)k * MK_NB * ld;
   Acc acc;
   acc_load(acc, C, ld);
+  // (Skipping the diagonal tiles' unused upper quadrant -- per MFMA or per chunk -- measured slower.)
   gemm_128<true, true, true>(M + i * MK_NB, ld, M + k * MK_NB, ld, k * MK_NB, k * MK_NB, acc, lds);
   store_tile(C, ld, acc);
 }
@@ -160,7 +167,10 @@ __global__ __launch_bounds__(256, 2) void k_chol_trsm(MatSet ms, int S, int h, i
 // Inverse X = L^-1 by block rows: X_ij = -Dinv_i sum_k L_ik X_kj (MFMA, 16x16 blocks).
 // Storage: L in the lower triangle; X strictly-lower transposed into the upper triangle
 // (X[r][c] at T[c + r*128]); diag(L) in dg, diag(X) in xd.
-#define TLD 128
+// Odd LDS column stride: lanes walking a row (the transposed inverse, column-index accesses)
+// hit distinct banks instead of one (stride 128 doubles = 0 mod 64 banks).
+#define TLD MK_TLD
+#define SLD 17     // wave-private 16 x 16 staging, padded likewise
 
 __device__ inline double rlane(double v, int lane) {
   const long long b = __double_as_longlong(v);
@@ -284,14 +294,14 @@ __device__ void factor_invert_tile(double* T, double* dg, double* xd, double* Pb
       // S = sum_{K=Cb}^{i-1} L_iK X_K,Cb
       acc = mfma16(acc, 16 * (i - Cb), [&](int r, int m) { return T[(16 * i + r) + (16 * Cb + m) * TLD]; },
                    [&](int m, int c) { return xget(T, xd, 16 * Cb + m, 16 * Cb + c); });
-      double* S = Pb + wv * 256;       // wave-private 16x16 staging (column-major)
+      double* S = Pb + wv * 16 * SLD;  // wave-private 16x16 staging (column-major, stride SLD)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) S[((l >> 4) + 4 * r) + (l & 15) * 16] = acc[r];
+      for (int r = 0; r < 4; ++r) S[((l >> 4) + 4 * r) + (l & 15) * SLD] = acc[r];
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
       d4 out = {0.0, 0.0, 0.0, 0.0};
       out = mfma16(out, 16, [&](int r, int m) { return -xget(T, xd, 16 * i + r, 16 * i + m); },
-                   [&](int m, int c) { return S[m + c * 16]; });
+                   [&](int m, int c) { return S[m + c * SLD]; });
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int rr = 16 * i + (l >> 4) + 4 * r, cc = 16 * Cb + (l & 15);
@@ -312,9 +322,9 @@ __global__ __launch_bounds__(256) void k_chol_diag(MatSet ms, const int* __restr
                                                    const int* scount) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
   double* T = sm;                      // [128*128]
-  double* dg = T + TLD * TLD;          // [128]
+  double* dg = T + MK_NB * TLD;        // [128]
   double* xd = dg + MK_NB;             // [128]
-  double* Pb = xd + MK_NB;             // [4][256]
+  double* Pb = xd + MK_NB;             // [4][16 * SLD]
   __shared__ int badf;
   int s = blockIdx.x;
   if (!pick_subset(slist, scount, &s)) return;
