@@ -36,81 +36,107 @@ __host__ __device__ inline void temme_gammas(double mu, double* gam1, double* ga
   }
 }
 
-__host__ __device__ inline double bessel_k(double x, double nu) {
-  const double EPS = 1e-16;
-  const double PI = 3.141592653589793;
-  const int nl = (int)(nu + 0.5);
-  const double mu = nu - nl, mu2 = mu * mu;
-  const double xi = 1.0 / x, xi2 = 2.0 * xi;
-  double rkmu, rk1;
-  if (x < 2.0) {
-    const double x2 = 0.5 * x, pimu = PI * mu;
-    const double fact = (fabs(pimu) < EPS) ? 1.0 : pimu / sin(pimu);
-    double d = -log(x2);
-    double e = mu * d;
-    const double fact2 = (fabs(e) < EPS) ? 1.0 : sinh(e) / e;
-    double gam1, gam2, gampl, gammi;
-    temme_gammas(mu, &gam1, &gam2, &gampl, &gammi);
-    double ff = fact * (gam1 * cosh(e) + gam2 * fact2 * d);
-    double sum = ff;
-    e = exp(e);
-    double p = 0.5 * e / gampl, q = 0.5 / (e * gammi);
-    double c = 1.0;
-    d = x2 * x2;
-    double sum1 = p;
-    for (int i = 1; i <= 500; ++i) {
-      ff = (i * ff + p + q) / (i * (double)i - mu2);
-      c *= d / i;
-      p /= (i - mu);
-      q /= (i + mu);
-      const double del = c * ff;
-      sum += del;
-      sum1 += c * (p - i * ff);
-      if (fabs(del) < fabs(sum) * EPS) break;
-    }
-    rkmu = sum;
-    rk1 = sum1 * xi2;
-  } else {
-    double b = 2.0 * (1.0 + x), d = 1.0 / b, h = d, delh = d;
-    double q1 = 0.0, q2 = 1.0;
-    const double a1 = 0.25 - mu2;
-    double q = a1, c = a1, a = -a1;
-    double s = 1.0 + q * delh;
-    for (int i = 2; i <= 500; ++i) {
-      a -= 2 * (i - 1);
-      c = -a * c / i;
-      const double qnew = (q1 - b * q2) / a;
-      q1 = q2;
-      q2 = qnew;
-      q += c * qnew;
-      b += 2.0;
-      d = 1.0 / (b + a * d);
-      delh = (b * d - 1.0) * delh;
-      h += delh;
-      const double dels = q * delh;
-      s += dels;
-      if (fabs(dels / s) < EPS) break;
-    }
-    h = a1 * h;
-    rkmu = sqrt(PI / (2.0 * x)) * exp(-x) / s;
-    rk1 = rkmu * (mu + x + 0.5 - h) * xi;
-  }
-  for (int i = 1; i <= nl; ++i) {
-    const double t = (mu + i) * xi2 * rk1 + rkmu;
-    rkmu = rk1;
-    rk1 = t;
-  }
-  return rkmu;
-}
+// Correlation function of one (phi, nu): the nu-only pieces -- Matern's normaliser
+// 2^(nu-1) Gamma(nu), Temme's reciprocal gammas, pi mu / sin(pi mu), the CF2 constant and the
+// recurrence count -- are computed once per candidate (init), so an element costs only its
+// x-dependent series / continued fraction.  The arithmetic per element is the classic
+// bessik scheme, operation for operation.
+struct CorrFn {
+  int model;
+  double phi, nu;
+  int nl;
+  double mu, mu2, gam1, gam2, gampl, gammi, fact, a1, den;
 
-__host__ __device__ inline double matern_corr(double d, double phi, double nu) {
-  const double x = d * phi;
-  if (!(x > 0.0)) return 1.0;
-  return pow(x, nu) / (pow(2.0, nu - 1.0) * tgamma(nu)) * bessel_k(x, nu);
-}
+  __host__ __device__ void init(double phi_, double nu_, int model_) {
+    model = model_;
+    phi = phi_;
+    nu = nu_;
+    if (model != MK_COV_MATERN) return;
+    const double EPS = 1e-16, PI = 3.141592653589793;
+    nl = (int)(nu + 0.5);
+    mu = nu - nl;
+    mu2 = mu * mu;
+    const double pimu = PI * mu;
+    fact = (fabs(pimu) < EPS) ? 1.0 : pimu / sin(pimu);
+    temme_gammas(mu, &gam1, &gam2, &gampl, &gammi);
+    a1 = 0.25 - mu2;
+    den = pow(2.0, nu - 1.0) * tgamma(nu);
+  }
+
+  // K_nu(x), x > 0 (Temme series for x < 2, Steed's CF2 above, forward recurrence in nu).
+  __host__ __device__ double bessel_k(double x) const {
+    const double EPS = 1e-16, PI = 3.141592653589793;
+    const double xi = 1.0 / x, xi2 = 2.0 * xi;
+    double rkmu, rk1;
+    if (x < 2.0) {
+      const double x2 = 0.5 * x;
+      double d = -log(x2);
+      double e = mu * d;
+      const double fact2 = (fabs(e) < EPS) ? 1.0 : sinh(e) / e;
+      double ff = fact * (gam1 * cosh(e) + gam2 * fact2 * d);
+      double sum = ff;
+      e = exp(e);
+      double p = 0.5 * e / gampl, q = 0.5 / (e * gammi);
+      double c = 1.0;
+      d = x2 * x2;
+      double sum1 = p;
+      for (int i = 1; i <= 500; ++i) {
+        ff = (i * ff + p + q) / (i * (double)i - mu2);
+        c *= d / i;
+        p /= (i - mu);
+        q /= (i + mu);
+        const double del = c * ff;
+        sum += del;
+        sum1 += c * (p - i * ff);
+        if (fabs(del) < fabs(sum) * EPS) break;
+      }
+      rkmu = sum;
+      rk1 = sum1 * xi2;
+    } else {
+      double b = 2.0 * (1.0 + x), d = 1.0 / b, h = d, delh = d;
+      double q1 = 0.0, q2 = 1.0;
+      double q = a1, c = a1, a = -a1;
+      double s = 1.0 + q * delh;
+      for (int i = 2; i <= 500; ++i) {
+        a -= 2 * (i - 1);
+        c = -a * c / i;
+        const double qnew = (q1 - b * q2) / a;
+        q1 = q2;
+        q2 = qnew;
+        q += c * qnew;
+        b += 2.0;
+        d = 1.0 / (b + a * d);
+        delh = (b * d - 1.0) * delh;
+        h += delh;
+        const double dels = q * delh;
+        s += dels;
+        if (fabs(dels / s) < EPS) break;
+      }
+      h = a1 * h;
+      rkmu = sqrt(PI / (2.0 * x)) * exp(-x) / s;
+      rk1 = rkmu * (mu + x + 0.5 - h) * xi;
+    }
+    for (int i = 1; i <= nl; ++i) {
+      const double t = (mu + i) * xi2 * rk1 + rkmu;
+      rkmu = rk1;
+      rk1 = t;
+    }
+    return rkmu;
+  }
+
+  // rho(d): exponential exp(-phi d); Matern (phi d)^nu / (2^(nu-1) Gamma(nu)) K_nu(phi d), 1 at d = 0
+  __host__ __device__ double operator()(double d) const {
+    if (model == MK_COV_EXPONENTIAL) return exp(-phi * d);
+    const double x = d * phi;
+    if (!(x > 0.0)) return 1.0;
+    return pow(x, nu) / den * bessel_k(x);
+  }
+};
 
 __host__ __device__ inline double correlation(double d, double phi, double nu, int model) {
-  return (model == MK_COV_EXPONENTIAL) ? exp(-phi * d) : matern_corr(d, phi, nu);
+  CorrFn f;
+  f.init(phi, nu, model);
+  return f(d);
 }
 
 __host__ __device__ inline double dist2d(double x0, double y0, double x1, double y1) {

@@ -48,10 +48,10 @@ struct CandGen {
   const double* cx;
   const double* cy;
   const double* uh;
-  int ns, model;
-  double phi, nu;
+  int ns;
+  CorrFn rho;
   __device__ inline double operator()(int R, int C) const {
-    if (R < ns && C < ns) return (R == C) ? 1.0 : correlation(dist2d(cx[R], cy[R], cx[C], cy[C]), phi, nu, model);
+    if (R < ns && C < ns) return (R == C) ? 1.0 : rho(dist2d(cx[R], cy[R], cx[C], cy[C]));
     if (R == ns && C < ns) return uh[C];
     return (R == C && R != ns) ? 1.0 : 0.0;
   }
@@ -59,12 +59,13 @@ struct CandGen {
 
 __device__ inline CandGen make_gen(const Model& md, int s, int h, int which, int iter) {
   CandGen g;
-  candidate_theta(md, s, h, which, iter, &g.phi, &g.nu);
+  double phi, nu;
+  candidate_theta(md, s, h, which, iter, &phi, &nu);
+  g.rho.init(phi, nu, md.cov_model);
   g.cx = md.coords + (long)s * 2 * md.n_pad;
   g.cy = g.cx + md.n_pad;
   g.uh = md.u + ((long)s * md.q + h) * md.n_pad;
   g.ns = md.n_s[s];
-  g.model = md.cov_model;
   return g;
 }
 
@@ -525,13 +526,15 @@ __global__ __launch_bounds__(256) void k_pred_PT(Model md, const int* __restrict
   const int ns = md.n_s[s];
   double phi, nu;
   current_phi_nu(md, s, h, &phi, &nu);
+  CorrFn rho;
+  rho.init(phi, nu, md.cov_model);
   const double* cx = md.coords + (long)s * 2 * md.n_pad;
   const double ox = cx[k], oy = cx[md.n_pad + k];
   double* row = md.PT + ((long)sh * md.n_pad + k) * md.n_test_pad;
   for (int t = threadIdx.x; t < md.n_test_pad; t += 256) {
     double v = 0.0;
     if (k < ns && t < md.n_test)
-      v = correlation(dist2d(ox, oy, md.coords_test[t], md.coords_test[md.n_test_pad + t]), phi, nu, md.cov_model);
+      v = rho(dist2d(ox, oy, md.coords_test[t], md.coords_test[md.n_test_pad + t]));
     row[t] = v;
   }
 }

@@ -167,7 +167,9 @@ class Session:
         return dict(launches=n.value, ms=ms.value, flops=fl.value)
 
     def outputs(self, quantiles=True, samples=False, w_samples=False, w_pred_samples=False, acceptance=False,
-                w_predict_sum=False):
+                w_predict_sum=False, w_predict=True):
+        """quantiles: obj[[i]]$parameters (and $w.predict unless w_predict=False -- at 1M test sites the
+        per-subset grids are 1.6 GB each; w_predict_sum gives this shard's term of the combine)."""
         cfg = self.cfg
         S, P, q = self.S, cfg.P, cfg.q
         o = Outputs()
@@ -175,7 +177,7 @@ class Session:
         if quantiles:
             res["parameters"] = np.zeros((S, P, _lib.N_LEVELS))
             o.parameters = dptr(res["parameters"])
-            if self.n_test:
+            if self.n_test and w_predict:
                 res["w_predict"] = np.zeros((S, q * self.n_test, _lib.N_LEVELS))
                 o.w_predict = dptr(res["w_predict"])
         if samples:

@@ -1,0 +1,137 @@
+#!/usr/bin/env python3
+"""MetaKriging_BinaryResponse.R end to end on the MI355X path, one process per GPU.
+
+The reference script's flow with its drop-ins (MK.R line numbers):
+  data (the driver the reference lacks)   -> synthetic.generate
+  partition                      MK.R:15-41             -> metakriging.partition
+  glm start values               MK.R:53-55             -> glm_binomial (device, once)
+  foreach %dopar% worker         MK.R:100-114           -> Session: every subset of the shard at once
+     spMvGLM + spPredict + quantiles  MK.R:80-89
+  combine                        MK.R:119-133           -> combine / combine_median / column-sharded (N > 1)
+  resample + p(y=1) + summaries  MK.R:136-165           -> posterior_summary (device)
+
+Prints one JSON line with the wall-clock of every phase (rank 0).  Multi-GPU:
+  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 run_metakriging.py ...
+
+  python run_metakriging.py --config 3          # configs[2]: n=500k, K=250, exponential, q=1
+"""
+import argparse
+import importlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+PKG = "laurabaracaldo-spatial-meta-kriging-for-distributed-inference-for-binary-response_amd"
+
+# BASELINE.json configs (1-based as in SURVEY.md): n, K, cov, q, n_test, n_batch x batch_length
+CONFIGS = {
+    1: dict(n=2000, K=5, cov="exponential", q=1, n_test=1000, n_batch=20, batch_length=50),
+    2: dict(n=50000, K=50, cov="matern", q=1, n_test=1000, n_batch=100, batch_length=50),
+    3: dict(n=500000, K=250, cov="exponential", q=1, n_test=1000, n_batch=100, batch_length=50),
+    4: dict(n=100000, K=50, cov="exponential", q=3, n_test=1000, n_batch=100, batch_length=50),
+    5: dict(n=500000, K=250, cov="exponential", q=1, n_test=1000000, n_batch=100, batch_length=50,
+            predict_tile=65536),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", type=int, default=1, choices=sorted(CONFIGS))
+    ap.add_argument("--n", type=int)
+    ap.add_argument("--subsets", type=int)
+    ap.add_argument("--n-test", type=int)
+    ap.add_argument("--n-batch", type=int)
+    ap.add_argument("--batch-length", type=int)
+    ap.add_argument("--combine", default="mean", choices=["mean", "median"])
+    ap.add_argument("--predict-tile", type=int)
+    ap.add_argument("--seed", type=int, default=20250114)
+    a = ap.parse_args()
+    c = dict(CONFIGS[a.config])
+    for k_arg, k_cfg in [("n", "n"), ("subsets", "K"), ("n_test", "n_test"), ("n_batch", "n_batch"),
+                         ("batch_length", "batch_length"), ("predict_tile", "predict_tile")]:
+        v = getattr(a, k_arg)
+        if v is not None:
+            c[k_cfg] = v
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", rank=rank, world_size=world)
+    mk = importlib.import_module(PKG)
+    dmod = importlib.import_module(PKG + ".distributed")
+    t = {}
+    t0 = time.perf_counter()
+    q, n, K = c["q"], c["n"], c["K"]
+    d = mk.synthetic.generate(n, q=q, n_test=c["n_test"], cov_model=1 if c["cov"] == "matern" else 0, seed=a.seed)
+    t["data_s"] = time.perf_counter() - t0
+
+    t1 = time.perf_counter()
+    n_part, index_part = mk.partition(n, K, seed=a.seed)                       # MK.R:15-41
+    beta0, bt = mk.start_values(d["y"], d["x"], 1.0, q, device=local)         # MK.R:53-55
+    p = d["x"].shape[1]
+    cfg = mk.SamplerConfig(q, p, beta0, bt, cov_model=c["cov"], n_batch=c["n_batch"], batch_length=c["batch_length"],
+                           seed=a.seed, predict_tile=c.get("predict_tile", 0))
+    lo, hi = dmod.shard_range(K, world, rank)
+    subs = [mk.subset_data(d["y"], d["x"], 1.0, d["coords"], q, index_part[i]) for i in range(lo, hi)]
+    t["setup_s"] = time.perf_counter() - t1
+
+    t2 = time.perf_counter()
+    big = cfg.predict_tile > 0 and cfg.predict_tile < c["n_test"]
+    with mk.Session(subs, cfg, coords_test=d["coords_test"], subset_base=lo, device=local) as ses:   # MK.R:108
+        for b in range(cfg.n_batch):          # progress every n.report = 10 batches (MK.R:84)
+            ses.run(cfg.batch_length)
+            if rank == 0 and (b + 1) % 10 == 0:
+                print(f"batch {b + 1}/{cfg.n_batch}  {time.perf_counter() - t2:.1f}s", file=sys.stderr, flush=True)
+        t3 = time.perf_counter()
+        # 1M sites: per-subset parameter grids, w.predict only as this shard's partial sum
+        out = ses.outputs(quantiles=True, w_predict=not big, w_predict_sum=big)
+    t["fit_s"] = t3 - t2
+    t["predict_quantiles_s"] = time.perf_counter() - t3
+
+    t4 = time.perf_counter()
+    if world > 1 and not big:
+        import torch
+        dev = torch.device("cuda", local)
+        par = np.stack(out["parameters"])
+        result = dmod.combine_sharded(par, K, dist, method=a.combine, device=dev, gpu=local)   # MK.R:123-127
+        result2 = dmod.combine_sharded(np.stack(out["w_predict"]), K, dist, method=a.combine, device=dev, gpu=local)
+    elif not big:
+        obj = [{"parameters": out["parameters"][i], "w.predict": out["w_predict"][i]} for i in range(len(subs))]
+        result, result2 = mk.combine_results(obj, device=local, method=a.combine)             # MK.R:123-133
+    else:   # tiled kriging (cfg5), one process: the partial sum over all K subsets is the whole sum
+        result = mk.combine(out["parameters"], device=local)
+        result2 = out["w_predict_sum"] / K
+    t["combine_s"] = time.perf_counter() - t4
+
+    t5 = time.perf_counter()
+    summ = None
+    if result is not None:
+        summ = mk.posterior_summary(result, result2, d["x_test"], samplesize=1000, seed=a.seed, device=local)
+    t["post_s"] = time.perf_counter() - t5
+    t["end_to_end_s"] = time.perf_counter() - t1
+    if rank == 0:
+        rec = dict(config=a.config, workload=c, n_gpus=world, combine=a.combine, phases=t,
+                   subset_iters_per_s=K * cfg.n_samples / (t["fit_s"]) if world == 1 else None)
+        if summ is not None:
+            truth = np.concatenate([d["beta_true"], [1.0] if q == 1 else [], [6.0] if q == 1 else []])
+            rec["param_median"] = summ["param_quant"][0].tolist()
+            rec["param_95ci"] = [summ["param_quant"][1].tolist(), summ["param_quant"][2].tolist()]
+            wq = summ["w_quant"]
+            rec["w_test_coverage_95"] = float(np.mean((d["w_test_true"] >= wq[1]) & (d["w_test_true"] <= wq[2])))
+            rec["truth_beta_phi"] = truth.tolist()
+        print(json.dumps(rec), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
