@@ -93,9 +93,9 @@ Model model_view(const Model& m, int s0, int S) {
   v.A_full = m.A_full + s * q * q;
   v.Ainv = m.Ainv + s * q * q;
   v.dirty = m.dirty + s * q;
-  v.ld_part = m.ld_part + s * m.nt;
-  v.quad_c = m.quad_c + s;
-  v.info = m.info + s;
+  v.ld_part = m.ld_part + (long)s * m.q * m.nt;   // per (subset, outcome) pair
+  v.quad_c = m.quad_c + (long)s * m.q;
+  v.info = m.info + (long)s * m.q;
   v.sw_delta = m.sw_delta + s * Np;
   v.sw_dll = m.sw_dll + s * Np;
   v.sw_logu = m.sw_logu + s * Np;
@@ -208,8 +208,10 @@ static inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
 
 // ------------------------------------------------------------------ Cholesky of all candidates of outcome h
 // Candidate tiles are in the free slot (k_cov_candidate, or k_load_plain for the test entry).
-static void launch_cholesky(mk_session* s, Group& g, int h, const int* slist = nullptr, const int* scount = nullptr) {
-  const int nt = s->nt, S = g.S;
+// One launch per step covers outcomes h0 .. h0+hc-1 of every subset (hc = q in the sampler).
+static void launch_cholesky(mk_session* s, Group& g, int h0, int hc, const int* slist = nullptr,
+                            const int* scount = nullptr) {
+  const int nt = s->nt, S = g.S, E = S * hc;
   const size_t diag_lds = (size_t)MK_DIAG_LDS_BYTES;
   // valid extent (excludes padding) for the algorithmic flop count
   const double nv = (double)s->n_part[g.s0] + 1.0;
@@ -219,22 +221,22 @@ static void launch_cholesky(mk_session* s, Group& g, int h, const int* slist = n
       const double rows = std::fmax(0.0, nv - k * MK_NB);
       const double cols = std::fmin((double)MK_NB, std::fmax(0.0, nv - k * MK_NB));
       const double kk = std::fmin((double)k * MK_NB, nv);
-      const double fl = 2.0 * rows * cols * kk * S;
+      const double fl = 2.0 * rows * cols * kk * E;
       timed(s, g.stream, KS_CHOL_UPDATE, fl, [&] {
-        hipLaunchKernelGGL(k_chol_update, dim3(xcd_grid_h(S, nt - k)), dim3(256), 0, g.stream, g.ms, S, h, k, slist,
-                           scount);
+        hipLaunchKernelGGL(k_chol_update, dim3(xcd_grid_h(E, nt - k)), dim3(256), 0, g.stream, g.ms, S, h0, hc, k,
+                           slist, scount);
       });
     }
     timed(s, g.stream, KS_CHOL_DIAG, 0.0, [&] {
-      hipLaunchKernelGGL(k_chol_diag, dim3(S), dim3(256), diag_lds, g.stream, g.ms, g.md.n_s, h, k, g.md.ld_part,
+      hipLaunchKernelGGL(k_chol_diag, dim3(E), dim3(256), diag_lds, g.stream, g.ms, g.md.n_s, h0, hc, k, g.md.ld_part,
                          g.md.quad_c, g.md.info, slist, scount);
     });
     if (k < nt - 1) {
       const double rows = std::fmax(0.0, nv - (k + 1) * MK_NB);
-      const double fl = 2.0 * rows * MK_NB * MK_NB * S;
+      const double fl = 2.0 * rows * MK_NB * MK_NB * E;
       timed(s, g.stream, KS_CHOL_TRSM, fl, [&] {
-        hipLaunchKernelGGL(k_chol_trsm, dim3(xcd_grid_h(S, nt - k - 1)), dim3(256), 0, g.stream, g.ms, S, h, k, slist,
-                           scount);
+        hipLaunchKernelGGL(k_chol_trsm, dim3(xcd_grid_h(E, nt - k - 1)), dim3(256), 0, g.stream, g.ms, S, h0, hc, k,
+                           slist, scount);
       });
     }
   }
@@ -288,19 +290,19 @@ static void run_iteration(mk_session* s, Group& g, int it) {
   hipLaunchKernelGGL(k_Aphase, dim3(S), dim3(256), 0, st, md, it);
   const int nkinds = s->matern ? 2 : 1;
   const int ntri_tiles = s->nt * (s->nt + 1) / 2;
-  for (int which = 0; which < nkinds; ++which)
-    for (int h = 0; h < q; ++h) {
-      hipLaunchKernelGGL(k_cov_candidate, dim3(xcd_grid_h(S, ntri_tiles)), dim3(256), 0, st, md, g.ms, h, which, it,
-                         nullptr, nullptr);
-      launch_cholesky(s, g, h);
-      hipLaunchKernelGGL(k_theta_mh, dim3((S + 63) / 64), dim3(64), 0, st, md, g.ms, h, which, it);
-    }
+  // the q outcomes' (phi_h, nu_h) steps are independent given u: one batched pass per kind
+  for (int which = 0; which < nkinds; ++which) {
+    hipLaunchKernelGGL(k_cov_candidate, dim3(xcd_grid_h(S * q, ntri_tiles)), dim3(256), 0, st, md, g.ms, 0, q, which,
+                       it, nullptr, nullptr);
+    launch_cholesky(s, g, 0, q);
+    hipLaunchKernelGGL(k_theta_mh, dim3((S * q + 63) / 64), dim3(64), 0, st, md, g.ms, 0, q, which, it);
+  }
   hipLaunchKernelGGL(k_dirty_list, dim3(1), dim3(256), 0, st, md, (int)(it == md.kept0), g.d_list, g.d_count,
                      g.d_plist, g.d_pcount);
   launch_inverse(s, g);
   if (kept && !s->tiled) launch_pred_refresh(s, g);
   const size_t sw_lds = (size_t)q * (64 * 64 + 2 * 64) * sizeof(double);
-  timed(s, st, KS_SWEEP, 0.0, [&] { hipLaunchKernelGGL(k_sweep, dim3(S), dim3(512), sw_lds, st, md, g.ms, it); });
+  timed(s, st, KS_SWEEP, 0.0, [&] { hipLaunchKernelGGL(k_sweep, dim3(S), dim3(MK_SW_T), sw_lds, st, md, g.ms, it); });
   if (s->record_samples) hipLaunchKernelGGL(k_record, dim3((S + 63) / 64), dim3(64), 0, st, md, it);
   if (s->record_w) hipLaunchKernelGGL(k_record_w, dim3((md.Np + 255) / 256, S), dim3(256), 0, st, md, it);
   if (kept && md.n_test > 0 && !s->tiled) {
@@ -457,8 +459,8 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
       (rc = s->alloc(&md.Z, (size_t)S * q * q * n_pad)) || (rc = s->alloc(&md.logdetR, (size_t)S * q)) ||
       (rc = s->alloc(&md.quad, (size_t)S * q)) || (rc = s->alloc(&md.A_full, (size_t)S * q * q)) ||
       (rc = s->alloc(&md.Ainv, (size_t)S * q * q)) || (rc = s->alloc(&md.dirty, (size_t)S * q)) ||
-      (rc = s->alloc(&md.ld_part, (size_t)S * nt)) || (rc = s->alloc(&md.quad_c, (size_t)S)) ||
-      (rc = s->alloc(&md.info, (size_t)S)) || (rc = s->alloc(&md.sw_delta, (size_t)S * Np)) ||
+      (rc = s->alloc(&md.ld_part, (size_t)S * q * nt)) || (rc = s->alloc(&md.quad_c, (size_t)S * q)) ||
+      (rc = s->alloc(&md.info, (size_t)S * q)) || (rc = s->alloc(&md.sw_delta, (size_t)S * Np)) ||
       (rc = s->alloc(&md.sw_dll, (size_t)S * Np)) || (rc = s->alloc(&md.sw_logu, (size_t)S * Np)) ||
       (rc = s->alloc(&md.sw_acc, (size_t)S * Np)) || (rc = s->alloc(&md.samples, (size_t)S * n_samples * P)) ||
       (rc = s->alloc(&md.acc_hist, (size_t)S * c->n_batch * (o_w + 1))))
@@ -582,7 +584,7 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
   HIPCHK(hipMemcpy(md.Ainv, hAi.data(), hAi.size() * 8, hipMemcpyHostToDevice));
   HIPCHK(hipMemsetAsync(md.acc, 0, (size_t)S * n_mh_max * 8, s->stream));
   HIPCHK(hipMemsetAsync(md.dirty, 0, (size_t)S * q * 4, s->stream));
-  HIPCHK(hipMemsetAsync(md.info, 0, (size_t)S * 4, s->stream));
+  HIPCHK(hipMemsetAsync(md.info, 0, (size_t)S * q * 4, s->stream));
   HIPCHK(hipMemsetAsync(ms.cur, 0, (size_t)S * q * 4, s->stream));
   HIPCHK(hipMemsetAsync(md.u, 0, (size_t)S * q * n_pad * 8, s->stream));
   HIPCHK(hipMemsetAsync(md.z, 0, (size_t)S * q * n_pad * 8, s->stream));
@@ -604,12 +606,10 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
   Group& a = s->all;
   hipLaunchKernelGGL(k_init_state, dim3(S), dim3(256), 0, s->stream, md);
   const int ntri_tiles = nt * (nt + 1) / 2;
-  for (int h = 0; h < q; ++h) {
-    hipLaunchKernelGGL(k_cov_candidate, dim3(xcd_grid_h(S, ntri_tiles)), dim3(256), 0, s->stream, md, ms, h, 2, 0,
-                       nullptr, nullptr);
-    launch_cholesky(s, a, h);
-    hipLaunchKernelGGL(k_theta_init, dim3((S + 63) / 64), dim3(64), 0, s->stream, md, ms, h);
-  }
+  hipLaunchKernelGGL(k_cov_candidate, dim3(xcd_grid_h(S * q, ntri_tiles)), dim3(256), 0, s->stream, md, ms, 0, q, 2,
+                     0, nullptr, nullptr);
+  launch_cholesky(s, a, 0, q);
+  hipLaunchKernelGGL(k_theta_init, dim3((S * q + 63) / 64), dim3(64), 0, s->stream, md, ms, 0, q);
   hipLaunchKernelGGL(k_dirty_list, dim3(1), dim3(256), 0, s->stream, md, 0, a.d_list, a.d_count, a.d_plist, a.d_pcount);
   launch_inverse(s, a);
   HIPCHK(hipGetLastError());
@@ -692,9 +692,9 @@ static int predict_tiled(mk_session* s, mk_outputs* o) {
       hipLaunchKernelGGL(k_kept_dirty, dim3(1), dim3(256), 0, st, mt, prev, s->d_slist, s->d_scount, g.d_plist,
                          g.d_pcount);
       for (int h = 0; h < q; ++h) {
-        hipLaunchKernelGGL(k_cov_candidate, dim3(xcd_grid_h(S, ntri_tiles)), dim3(256), 0, st, mt, g.ms, h, 2, 0,
+        hipLaunchKernelGGL(k_cov_candidate, dim3(xcd_grid_h(S, ntri_tiles)), dim3(256), 0, st, mt, g.ms, h, 1, 2, 0,
                            s->d_slist + h * S, s->d_scount + h);
-        launch_cholesky(s, g, h, s->d_slist + h * S, s->d_scount + h);
+        launch_cholesky(s, g, h, 1, s->d_slist + h * S, s->d_scount + h);
       }
       hipLaunchKernelGGL(k_flip_pairs, dim3((S * q + 255) / 256), dim3(256), 0, st, g.ms, g.d_plist, g.d_pcount);
       launch_trinv(s, g, S * q, g.d_plist, g.d_pcount);
@@ -1126,7 +1126,7 @@ extern "C" int mk_cholesky_batched(const double* A, int32_t S, int32_t n, double
                           MK_DIAG_LDS_BYTES) != hipSuccess)
     return fail(set_err(MK_E_HIP, "lds attribute"));
   hipLaunchKernelGGL(k_load_plain, dim3(2048), dim3(256), 0, s->stream, ms, dA, n, S);
-  launch_cholesky(s, a, 0);
+  launch_cholesky(s, a, 0, 1);
   std::vector<double> part((size_t)S * nt);
   std::vector<int> info(S);
   if (hipStreamSynchronize(s->stream) != hipSuccess) return fail(set_err(MK_E_HIP, "cholesky run"));
@@ -1134,7 +1134,7 @@ extern "C" int mk_cholesky_batched(const double* A, int32_t S, int32_t n, double
     return fail(set_err(MK_E_HIP, "info download"));
   for (int i = 0; i < S; ++i)
     if (info[i]) return fail(set_err(MK_E_ARG, "matrix " + std::to_string(i) + " is not positive definite"));
-  hipLaunchKernelGGL(k_theta_init, dim3((S + 63) / 64), dim3(64), 0, s->stream, md, ms, 0);
+  hipLaunchKernelGGL(k_theta_init, dim3((S + 63) / 64), dim3(64), 0, s->stream, md, ms, 0, 1);
   double* dL = nullptr;
   if ((rc = s->alloc(&dL, (size_t)S * n * n))) return fail(rc);
   if (L_out) {

@@ -9,6 +9,7 @@
 #include <stdint.h>
 
 #define MK_NB 128          // Cholesky / GEMM tile edge (fp64)
+#define MK_SW_T 1024       // threads of the latent-w sweep workgroup (one per subset): loads in flight for the W panels
 #define MK_TLD 129         // LDS column stride of the diagonal-tile factor/inverse (k_chol_diag)
 // dynamic LDS of k_chol_diag: tile + diag(L) + diag(L^-1) + 4 wave-private 16 x 17 stagings
 #define MK_DIAG_LDS_BYTES ((MK_NB * MK_TLD + 2 * MK_NB + 4 * 16 * 17) * 8)

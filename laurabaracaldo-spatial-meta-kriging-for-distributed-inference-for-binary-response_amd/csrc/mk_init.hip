@@ -24,18 +24,19 @@ __global__ __launch_bounds__(256) void k_init_state(Model md) {
     }
 }
 
-// Accept the starting-value factorisation of outcome h unconditionally.
-__global__ __launch_bounds__(64) void k_theta_init(Model md, MatSet ms, int h) {
-  const int s = blockIdx.x * 64 + threadIdx.x;
-  if (s >= md.S) return;
+// Accept the starting-value factorisations of outcomes h0 .. h0+hc-1 unconditionally.
+__global__ __launch_bounds__(64) void k_theta_init(Model md, MatSet ms, int h0, int hc) {
+  const int e = blockIdx.x * 64 + threadIdx.x;
+  if (e >= md.S * hc) return;
+  const int s = e / hc, h = h0 + e % hc;
   const int sh = s * md.q + h;
   double ld = 0.0;
-  for (int k = 0; k < md.nt; ++k) ld += md.ld_part[(long)s * md.nt + k];
+  for (int k = 0; k < md.nt; ++k) ld += md.ld_part[(long)sh * md.nt + k];
   md.logdetR[sh] = ld;
-  md.quad[sh] = md.quad_c[s];
+  md.quad[sh] = md.quad_c[sh];
   ms.cur[sh] ^= 1;
   md.dirty[sh] = 1;
-  md.info[s] = 0;
+  md.info[sh] = 0;
 }
 
 // Copy S dense n x n matrices into the candidate slot, identity-padded, zero border row.

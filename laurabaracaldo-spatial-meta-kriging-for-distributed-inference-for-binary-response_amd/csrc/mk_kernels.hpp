@@ -5,10 +5,10 @@
 namespace mk {
 inline int xcd_grid_h(int S, int T) { return 8 * ((S + 7) / 8) * T; }
 // mk_linalg.hip
-__global__ void k_cov_candidate(Model md, MatSet ms, int h, int which, int iter, const int* slist, const int* scount);
-__global__ void k_chol_update(MatSet ms, int S, int h, int k, const int* slist, const int* scount);
-__global__ void k_chol_trsm(MatSet ms, int S, int h, int k, const int* slist, const int* scount);
-__global__ void k_chol_diag(MatSet ms, const int* n_s, int h, int k, double* ld_part, double* quad_c, int* info,
+__global__ void k_cov_candidate(Model md, MatSet ms, int h0, int hc, int which, int iter, const int* slist, const int* scount);
+__global__ void k_chol_update(MatSet ms, int S, int h0, int hc, int k, const int* slist, const int* scount);
+__global__ void k_chol_trsm(MatSet ms, int S, int h0, int hc, int k, const int* slist, const int* scount);
+__global__ void k_chol_diag(MatSet ms, const int* n_s, int h0, int hc, int k, double* ld_part, double* quad_c, int* info,
                             const int* slist, const int* scount);
 __global__ void k_inv_copydiag(MatSet ms, const int* list, const int* count);
 __global__ void k_inv_level(MatSet ms, const int* list, const int* count, int sz, int phase);
@@ -22,7 +22,7 @@ __global__ void k_pred_var_reduce(Model md, int nt, const int* list, const int* 
 // mk_mcmc.hip
 __global__ void k_beta(Model md, int iter);
 __global__ void k_Aphase(Model md, int iter);
-__global__ void k_theta_mh(Model md, MatSet ms, int h, int which, int iter);
+__global__ void k_theta_mh(Model md, MatSet ms, int h0, int hc, int which, int iter);
 __global__ void k_dirty_list(Model md, int force, int* list_inv, int* count_inv, int* list_pred, int* count_pred);
 __global__ void k_sweep(Model md, MatSet ms, int iter);
 __global__ void k_record(Model md, int iter);
@@ -46,7 +46,7 @@ __global__ void k_glm_pass(const double* yprop, const double* wt, const double* 
                            int mode, double* part);
 // mk_init.hip
 __global__ void k_init_state(Model md);
-__global__ void k_theta_init(Model md, MatSet ms, int h);
+__global__ void k_theta_init(Model md, MatSet ms, int h0, int hc);
 __global__ void k_load_plain(MatSet ms, const double* A, int n, int S);
 __global__ void k_corr_plain(const double* coords, int S, int n, const double* phi, const double* nu, int model,
                              double* out);

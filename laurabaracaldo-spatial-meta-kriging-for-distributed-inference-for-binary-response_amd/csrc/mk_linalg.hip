@@ -92,11 +92,20 @@ __device__ inline bool pick_subset(const int* slist, const int* scount, int* s) 
   return true;
 }
 
-__global__ __launch_bounds__(256) void k_cov_candidate(Model md, MatSet ms, int h, int which, int iter,
+// Entry e of a launch over hc outcomes h0 .. h0+hc-1 -> (subset, outcome).  The outcomes'
+// factorisations are independent (LMC: u_h has its own GP), so one launch carries all q of
+// them and the grid is q times fuller than an outcome-at-a-time schedule.
+__device__ inline bool pick_pair(const int* slist, const int* scount, int e, int h0, int hc, int* s, int* h) {
+  *s = e / hc;
+  *h = h0 + e % hc;
+  return pick_subset(slist, scount, s);
+}
+
+__global__ __launch_bounds__(256) void k_cov_candidate(Model md, MatSet ms, int h0, int hc, int which, int iter,
                                                        const int* slist, const int* scount) {
   const int ntiles = ms.nt * (ms.nt + 1) / 2;
-  int s, t;
-  if (!xcd_map(md.S, ntiles, &s, &t) || !pick_subset(slist, scount, &s)) return;
+  int e, t, s, h;
+  if (!xcd_map(md.S * hc, ntiles, &e, &t) || !pick_pair(slist, scount, e, h0, hc, &s, &h)) return;
   int ti = 0;
   while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
   const int tj = t - ti * (ti + 1) / 2;
@@ -123,12 +132,12 @@ __global__ __launch_bounds__(256) void k_cov_candidate(Model md, MatSet ms, int 
 // (Generating C(i,k) from coordinates at its first touch inside this kernel was measured
 // slower on cfg3 and its code path made the kernel spill 80 VGPRs: candidates come from
 // k_cov_candidate.)
-__global__ __launch_bounds__(256, 2) void k_chol_update(MatSet ms, int S, int h, int k, const int* slist,
+__global__ __launch_bounds__(256, 2) void k_chol_update(MatSet ms, int S, int h0, int hc, int k, const int* slist,
                                                        const int* scount) {
   __shared__ __attribute__((aligned(16))) double lds[GB_LDS_DOUBLES];
   const int ntk = ms.nt - k;
-  int s, t;
-  if (!xcd_map(S, ntk, &s, &t) || !pick_subset(slist, scount, &s)) return;
+  int e, t, s, h;
+  if (!xcd_map(S * hc, ntk, &e, &t) || !pick_pair(slist, scount, e, h0, hc, &s, &h)) return;
   const int i = k + t;
   const int sh = s * ms.q + h;
   double* M = mat_slot(ms, sh, 1 - ms.cur[sh]);
@@ -141,12 +150,12 @@ __global__ __launch_bounds__(256, 2) void k_chol_update(MatSet ms, int S, int h,
   store_tile(C, ld, acc);
 }
 
-__global__ __launch_bounds__(256, 2) void k_chol_trsm(MatSet ms, int S, int h, int k, const int* slist,
+__global__ __launch_bounds__(256, 2) void k_chol_trsm(MatSet ms, int S, int h0, int hc, int k, const int* slist,
                                                      const int* scount) {
   __shared__ __attribute__((aligned(16))) double lds[GB_LDS_DOUBLES];
   const int ntk = ms.nt - k - 1;
-  int s, t;
-  if (!xcd_map(S, ntk, &s, &t) || !pick_subset(slist, scount, &s)) return;
+  int e, t, s, h;
+  if (!xcd_map(S * hc, ntk, &e, &t) || !pick_pair(slist, scount, e, h0, hc, &s, &h)) return;
   const int i = k + 1 + t;
   const int sh = s * ms.q + h;
   const int slot = 1 - ms.cur[sh];
@@ -318,7 +327,7 @@ __device__ void factor_invert_tile(double* T, double* dg, double* xd, double* Pb
 // Factor + invert the 128x128 diagonal tile k of each candidate.  Row rb = n_s - 128k
 // (if inside the tile) is the bordered row: its pivot is -(u' R^-1 u) and it is not
 // factored (pivot set to 1).
-__global__ __launch_bounds__(256) void k_chol_diag(MatSet ms, const int* __restrict__ n_s, int h, int k,
+__global__ __launch_bounds__(256) void k_chol_diag(MatSet ms, const int* __restrict__ n_s, int h0, int hc, int k,
                                                    double* ld_part, double* quad_c, int* info, const int* slist,
                                                    const int* scount) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
@@ -327,8 +336,8 @@ __global__ __launch_bounds__(256) void k_chol_diag(MatSet ms, const int* __restr
   double* xd = dg + MK_NB;             // [128]
   double* Pb = xd + MK_NB;             // [4][16 * SLD]
   __shared__ int badf;
-  int s = blockIdx.x;
-  if (!pick_subset(slist, scount, &s)) return;
+  int s, h;
+  if (!pick_pair(slist, scount, blockIdx.x, h0, hc, &s, &h)) return;
   const int tid = threadIdx.x;
   const int sh = s * ms.q + h;
   const int slot = 1 - ms.cur[sh];
@@ -344,7 +353,7 @@ __global__ __launch_bounds__(256) void k_chol_diag(MatSet ms, const int* __restr
   if (tid == 0) badf = 0;
   __syncthreads();
   bool bad = false;
-  factor_invert_tile(T, dg, xd, Pb, ns - base, quad_c + s, &bad);
+  factor_invert_tile(T, dg, xd, Pb, ns - base, quad_c + sh, &bad);
   if (bad) badf = 1;
   __syncthreads();
   if (tid < 64) {
@@ -353,8 +362,8 @@ __global__ __launch_bounds__(256) void k_chol_diag(MatSet ms, const int* __restr
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     if (tid == 0) {
-      ld_part[(long)s * ms.nt + k] = v;
-      if (badf) info[s] = 1;
+      ld_part[(long)sh * ms.nt + k] = v;
+      if (badf) info[sh] = 1;
     }
   }
   double* W = winv_slot(ms, sh, slot, k);

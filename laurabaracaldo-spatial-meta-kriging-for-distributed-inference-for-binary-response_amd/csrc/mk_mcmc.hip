@@ -189,9 +189,10 @@ __global__ __launch_bounds__(256) void k_Aphase(Model md, int iter) {
 }
 
 // ---------------------------------------------------------------- 3. phi_h / nu_h decision
-__global__ __launch_bounds__(64) void k_theta_mh(Model md, MatSet ms, int h, int which, int iter) {
-  const int s = blockIdx.x * 64 + threadIdx.x;
-  if (s >= md.S) return;
+__global__ __launch_bounds__(64) void k_theta_mh(Model md, MatSet ms, int h0, int hc, int which, int iter) {
+  const int e = blockIdx.x * 64 + threadIdx.x;
+  if (e >= md.S * hc) return;
+  const int s = e / hc, h = h0 + e % hc;
   const Key key = subset_key(md, s);
   const int sh = s * md.q + h;
   double* th = md.theta + (long)s * md.n_theta;
@@ -204,11 +205,11 @@ __global__ __launch_bounds__(64) void k_theta_mh(Model md, MatSet ms, int h, int
   const double th_c = th[idx] + exp(md.tune[(long)s * md.n_mh_max + j_mh]) * z;
   const double v_c = logit_inv(th_c, a, b), v_cur = logit_inv(th[idx], a, b);
   double ldc = 0.0;
-  for (int k = 0; k < md.nt; ++k) ldc += md.ld_part[(long)s * md.nt + k];
-  const double qc = md.quad_c[s];
+  for (int k = 0; k < md.nt; ++k) ldc += md.ld_part[(long)sh * md.nt + k];
+  const double qc = md.quad_c[sh];
   const double ratio = -0.5 * (ldc - md.logdetR[sh]) - 0.5 * (qc - md.quad[sh]) + unif_jacobian(v_c, a, b) -
                        unif_jacobian(v_cur, a, b);
-  if (md.info[s] == 0 && lu <= ratio) {
+  if (md.info[sh] == 0 && lu <= ratio) {
     th[idx] = th_c;
     ms.cur[sh] ^= 1;
     md.logdetR[sh] = ldc;
@@ -216,7 +217,7 @@ __global__ __launch_bounds__(64) void k_theta_mh(Model md, MatSet ms, int h, int
     md.dirty[sh] = 1;
     md.acc[(long)s * md.n_mh_max + j_mh] += 1.0;
   }
-  md.info[s] = 0;
+  md.info[sh] = 0;
 }
 
 // Compact lists (deterministic order) of (subset, outcome) pairs: list_inv = pairs whose
@@ -260,7 +261,7 @@ __global__ __launch_bounds__(256) void k_dirty_list(Model md, int force, int* li
 // accepted moves forward (g_i += delta'_k Q_ik), then z += W[:,B] delta'_B (rows >= b0).
 // W panels are streamed twice per sweep (dots, update) -> n^2 doubles per subset per sweep.
 #define SW_B 64
-#define SW_T 512
+#define SW_T MK_SW_T
 __global__ __launch_bounds__(SW_T) void k_sweep(Model md, MatSet ms, int iter) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int q = md.q;

@@ -58,9 +58,9 @@ struct Model {
   double* Ainv;      // [S][q*q]
   int* dirty;        // [S*q]
   // candidate scratch
-  double* ld_part;   // [S][nt]     logdet partials of the candidate factor
-  double* quad_c;    // [S]
-  int* info;         // [S]
+  double* ld_part;   // [S*q][nt]   logdet partials of the candidate factor (per (subset, outcome) pair)
+  double* quad_c;    // [S*q]
+  int* info;         // [S*q]
   // sweep scratch
   double* sw_delta;  // [S][Np]
   double* sw_dll;    // [S][Np]
