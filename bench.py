@@ -101,7 +101,7 @@ def main():
     K, n, n_test = a.subsets, a.n, a.n_test
 
     cpu = None
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+    if rank == 0 and world == 1 and not a.no_cpu_baseline and a.cpu_iters > 0:
         workers = max(1, min(16, os.cpu_count() or 1))
         cpu = cpu_baseline(n // K, a.cpu_iters, workers)   # before any GPU initialisation (spawn pool)
 

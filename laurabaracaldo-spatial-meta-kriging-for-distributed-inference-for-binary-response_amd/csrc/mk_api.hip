@@ -223,7 +223,7 @@ static void launch_cholesky(mk_session* s, Group& g, int h0, int hc, const int* 
       const double kk = std::fmin((double)k * MK_NB, nv);
       const double fl = 2.0 * rows * cols * kk * E;
       timed(s, g.stream, KS_CHOL_UPDATE, fl, [&] {
-        hipLaunchKernelGGL(k_chol_update, dim3(xcd_grid_h(E, nt - k)), dim3(256), 0, g.stream, g.ms, S, h0, hc, k,
+        hipLaunchKernelGGL(k_chol_update, dim3(xcd_grid_h(E, nt - k)), dim3(256), MK_GD_LDS_BYTES, g.stream, g.ms, S, h0, hc, k,
                            slist, scount);
       });
     }
@@ -599,6 +599,7 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
   }
   HIPCHK(hipFuncSetAttribute((const void*)k_chol_diag, hipFuncAttributeMaxDynamicSharedMemorySize,
                              MK_DIAG_LDS_BYTES));
+  HIPCHK(hipFuncSetAttribute((const void*)k_chol_update, hipFuncAttributeMaxDynamicSharedMemorySize, MK_GD_LDS_BYTES));
   HIPCHK(hipFuncSetAttribute((const void*)k_sweep, hipFuncAttributeMaxDynamicSharedMemorySize,
                              q * (64 * 64 + 2 * 64) * 8));
 
@@ -1123,7 +1124,9 @@ extern "C" int mk_cholesky_batched(const double* A, int32_t S, int32_t n, double
       hipMemset(ms.cur, 0, S * 4) != hipSuccess || hipMemset(md.info, 0, S * 4) != hipSuccess)
     return fail(set_err(MK_E_HIP, "cholesky upload"));
   if (hipFuncSetAttribute((const void*)k_chol_diag, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          MK_DIAG_LDS_BYTES) != hipSuccess)
+                          MK_DIAG_LDS_BYTES) != hipSuccess ||
+      hipFuncSetAttribute((const void*)k_chol_update, hipFuncAttributeMaxDynamicSharedMemorySize, MK_GD_LDS_BYTES) !=
+          hipSuccess)
     return fail(set_err(MK_E_HIP, "lds attribute"));
   hipLaunchKernelGGL(k_load_plain, dim3(2048), dim3(256), 0, s->stream, ms, dA, n, S);
   launch_cholesky(s, a, 0, 1);

@@ -156,6 +156,43 @@ __device__ inline void gemm_128(const double* __restrict__ A, long sA, const dou
   }
 }
 
+// LDS-DMA variant for operands whose 128 m (n) values per k are contiguous (A_MU, B_NU) and
+// K fully valid: each k-row of a chunk is ONE global_load_lds_dwordx4 wave instruction
+// (64 lanes x 16 B = the 1 KiB row; rows padded to GB_SM, no instruction crosses a row), so
+// the chunk lands in LDS with no staging registers and no ds_write pass.  Two stages: chunk
+// c+1 streams in while chunk c is multiplied; one barrier per chunk (its vmcnt(0) retires
+// the DMA, and every wave has finished reading the stage the next DMA overwrites).
+constexpr int GD_STAGE = 2 * GB_K * GB_SM;                 // A + B images of one chunk
+constexpr int GD_LDS_BYTES = 2 * GD_STAGE * 8;             // two stages
+static_assert(GD_LDS_BYTES == MK_GD_LDS_BYTES, "mk_common.hpp LDS size");
+template <bool NEG = false>
+__device__ inline void gemm_128_dma(const double* __restrict__ A, long sA, const double* __restrict__ B, long sB,
+                                    int K, Acc& acc, double* lds) {
+  if (K <= 0) return;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  auto issue = [&](int k0, double* st) {
+#pragma unroll
+    for (int r = w; r < GB_K; r += 4) {
+      __builtin_amdgcn_global_load_lds((const void*)(A + (long)(k0 + r) * sA + 2 * lane), (void*)(st + r * GB_SM),
+                                       16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(B + (long)(k0 + r) * sB + 2 * lane),
+                                       (void*)(st + (GB_K + r) * GB_SM), 16, 0, 0);
+    }
+  };
+  issue(0, lds);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int cur = 0;
+  for (int kc = 0; kc < K; kc += GB_K) {
+    double* st = lds + cur * GD_STAGE;
+    if (kc + GB_K < K) issue(kc + GB_K, lds + (cur ^ 1) * GD_STAGE);
+    mma_chunk<NEG, GB_SM, GB_SM>(st, st + GB_K * GB_SM, acc);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    cur ^= 1;
+  }
+}
+
 // acc = C (column-major, ldc): preload for C -= A B^T updates (no read-modify-write epilogue).
 __device__ inline void acc_load(Acc& acc, const double* C, long ldc);
 

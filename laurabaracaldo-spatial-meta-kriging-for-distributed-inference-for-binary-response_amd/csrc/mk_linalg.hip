@@ -134,7 +134,7 @@ __global__ __launch_bounds__(256) void k_cov_candidate(Model md, MatSet ms, int 
 // k_cov_candidate.)
 __global__ __launch_bounds__(256, 2) void k_chol_update(MatSet ms, int S, int h0, int hc, int k, const int* slist,
                                                        const int* scount) {
-  __shared__ __attribute__((aligned(16))) double lds[GB_LDS_DOUBLES];
+  extern __shared__ __attribute__((aligned(16))) double lds[];   // GD_LDS_BYTES (two DMA stages)
   const int ntk = ms.nt - k;
   int e, t, s, h;
   if (!xcd_map(S * hc, ntk, &e, &t) || !pick_pair(slist, scount, e, h0, hc, &s, &h)) return;
@@ -146,7 +146,7 @@ __global__ __launch_bounds__(256, 2) void k_chol_update(MatSet ms, int S, int h0
   Acc acc;
   acc_load(acc, C, ld);
   // (Skipping the diagonal tiles' unused upper quadrant -- per MFMA or per chunk -- measured slower.)
-  gemm_128<true, true, true>(M + i * MK_NB, ld, M + k * MK_NB, ld, k * MK_NB, k * MK_NB, acc, lds);
+  gemm_128_dma<true>(M + i * MK_NB, ld, M + k * MK_NB, ld, k * MK_NB, acc, lds);
   store_tile(C, ld, acc);
 }
 
