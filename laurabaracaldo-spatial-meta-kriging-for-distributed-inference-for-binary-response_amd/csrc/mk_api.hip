@@ -235,7 +235,7 @@ static void launch_cholesky(mk_session* s, Group& g, int h0, int hc, const int* 
       const double rows = std::fmax(0.0, nv - (k + 1) * MK_NB);
       const double fl = 2.0 * rows * MK_NB * MK_NB * E;
       timed(s, g.stream, KS_CHOL_TRSM, fl, [&] {
-        hipLaunchKernelGGL(k_chol_trsm, dim3(xcd_grid_h(E, nt - k - 1)), dim3(256), 0, g.stream, g.ms, S, h0, hc, k,
+        hipLaunchKernelGGL(k_chol_trsm, dim3(xcd_grid_h(E, nt - k - 1)), dim3(256), MK_GD_LDS_BYTES, g.stream, g.ms, S, h0, hc, k,
                            slist, scount);
       });
     }
@@ -274,7 +274,7 @@ static void launch_pred_refresh(mk_session* s, Group& g) {
   if (md.n_test <= 0) return;
   const int nt = s->nt, max_entries = g.S * s->q;
   hipLaunchKernelGGL(k_pred_PT, dim3(max_entries * md.n_pad), dim3(256), 0, g.stream, md, g.d_plist, g.d_pcount);
-  hipLaunchKernelGGL(k_pred_var, dim3(xcd_grid_h(max_entries, nt * md.ntt)), dim3(256), 0, g.stream, md, g.ms,
+  hipLaunchKernelGGL(k_pred_var, dim3(xcd_grid_h(max_entries, nt * md.ntt)), dim3(256), MK_GD_LDS_BYTES, g.stream, md, g.ms,
                      g.d_plist, g.d_pcount);
   hipLaunchKernelGGL(k_pred_var_reduce, dim3(max_entries * (md.n_test_pad / 256)), dim3(256), 0, g.stream, md, nt,
                      g.d_plist, g.d_pcount);
@@ -599,7 +599,8 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
   }
   HIPCHK(hipFuncSetAttribute((const void*)k_chol_diag, hipFuncAttributeMaxDynamicSharedMemorySize,
                              MK_DIAG_LDS_BYTES));
-  HIPCHK(hipFuncSetAttribute((const void*)k_chol_update, hipFuncAttributeMaxDynamicSharedMemorySize, MK_GD_LDS_BYTES));
+  for (const void* kfn : {(const void*)k_chol_update, (const void*)k_chol_trsm, (const void*)k_pred_var})
+    HIPCHK(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, MK_GD_LDS_BYTES));
   HIPCHK(hipFuncSetAttribute((const void*)k_sweep, hipFuncAttributeMaxDynamicSharedMemorySize,
                              q * (64 * 64 + 2 * 64) * 8));
 
@@ -1126,6 +1127,8 @@ extern "C" int mk_cholesky_batched(const double* A, int32_t S, int32_t n, double
   if (hipFuncSetAttribute((const void*)k_chol_diag, hipFuncAttributeMaxDynamicSharedMemorySize,
                           MK_DIAG_LDS_BYTES) != hipSuccess ||
       hipFuncSetAttribute((const void*)k_chol_update, hipFuncAttributeMaxDynamicSharedMemorySize, MK_GD_LDS_BYTES) !=
+          hipSuccess ||
+      hipFuncSetAttribute((const void*)k_chol_trsm, hipFuncAttributeMaxDynamicSharedMemorySize, MK_GD_LDS_BYTES) !=
           hipSuccess)
     return fail(set_err(MK_E_HIP, "lds attribute"));
   hipLaunchKernelGGL(k_load_plain, dim3(2048), dim3(256), 0, s->stream, ms, dA, n, S);

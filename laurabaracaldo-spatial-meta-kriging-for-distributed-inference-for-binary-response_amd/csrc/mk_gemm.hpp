@@ -165,7 +165,7 @@ __device__ inline void gemm_128(const double* __restrict__ A, long sA, const dou
 constexpr int GD_STAGE = 2 * GB_K * GB_SM;                 // A + B images of one chunk
 constexpr int GD_LDS_BYTES = 2 * GD_STAGE * 8;             // two stages
 static_assert(GD_LDS_BYTES == MK_GD_LDS_BYTES, "mk_common.hpp LDS size");
-template <bool NEG = false>
+template <bool NEG = false, int SKIP = SKIP_NONE>
 __device__ inline void gemm_128_dma(const double* __restrict__ A, long sA, const double* __restrict__ B, long sB,
                                     int K, Acc& acc, double* lds) {
   if (K <= 0) return;
@@ -186,7 +186,7 @@ __device__ inline void gemm_128_dma(const double* __restrict__ A, long sA, const
   for (int kc = 0; kc < K; kc += GB_K) {
     double* st = lds + cur * GD_STAGE;
     if (kc + GB_K < K) issue(kc + GB_K, lds + (cur ^ 1) * GD_STAGE);
-    mma_chunk<NEG, GB_SM, GB_SM>(st, st + GB_K * GB_SM, acc);
+    mma_chunk<NEG, GB_SM, GB_SM, SKIP>(st, st + GB_K * GB_SM, acc, SKIP == SKIP_TRI_B ? kc / GB_K : 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     cur ^= 1;

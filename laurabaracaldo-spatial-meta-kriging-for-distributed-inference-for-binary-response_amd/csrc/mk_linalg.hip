@@ -152,7 +152,7 @@ __global__ __launch_bounds__(256, 2) void k_chol_update(MatSet ms, int S, int h0
 
 __global__ __launch_bounds__(256, 2) void k_chol_trsm(MatSet ms, int S, int h0, int hc, int k, const int* slist,
                                                      const int* scount) {
-  __shared__ __attribute__((aligned(16))) double lds[GB_LDS_DOUBLES];
+  extern __shared__ __attribute__((aligned(16))) double lds[];   // MK_GD_LDS_BYTES
   const int ntk = ms.nt - k - 1;
   int e, t, s, h;
   if (!xcd_map(S * hc, ntk, &e, &t) || !pick_pair(slist, scount, e, h0, hc, &s, &h)) return;
@@ -166,7 +166,7 @@ __global__ __launch_bounds__(256, 2) void k_chol_trsm(MatSet ms, int S, int h0, 
   Acc acc;
   acc_zero(acc);
   // Winv_k lower triangular: (C Winv^T)(m, n) = sum_{j <= n} C(m, j) Winv(n, j)
-  gemm_128<true, true, false, false, false, SKIP_TRI_B>(C, ld, W, MK_NB, MK_NB, MK_NB, acc, lds);
+  gemm_128_dma<false, SKIP_TRI_B>(C, ld, W, MK_NB, MK_NB, acc, lds);
   store_tile(C, ld, acc);
 }
 
@@ -552,7 +552,7 @@ __global__ __launch_bounds__(256) void k_pred_PT(Model md, const int* __restrict
 // partial column sums of squares over valid rows -> s_part[sh][i][t].
 __global__ __launch_bounds__(256, 2) void k_pred_var(Model md, MatSet ms, const int* __restrict__ list,
                                                   const int* __restrict__ count) {
-  __shared__ __attribute__((aligned(16))) double lds[GB_LDS_DOUBLES];
+  extern __shared__ __attribute__((aligned(16))) double lds[];   // MK_GD_LDS_BYTES
   __shared__ double red[2][MK_NB];
   const int per = ms.nt * md.ntt;
   int e, t_;
@@ -567,7 +567,7 @@ __global__ __launch_bounds__(256, 2) void k_pred_var(Model md, MatSet ms, const 
   Acc acc;
   acc_zero(acc);
   const int K = (i + 1) * MK_NB;   // W lower-triangular
-  gemm_128<true, true>(Wm + i * MK_NB, ld, PT, md.n_test_pad, K, K, acc, lds);
+  gemm_128_dma(Wm + i * MK_NB, ld, PT, md.n_test_pad, K, acc, lds);
   double* XK = md.XK + (long)sh * md.n_test_pad * md.n_pad + (long)tb * MK_NB * md.n_pad + i * MK_NB;
   store_tile(XK, md.n_pad, acc);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w & 1;
