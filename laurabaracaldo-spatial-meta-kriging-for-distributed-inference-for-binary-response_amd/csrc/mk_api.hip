@@ -206,6 +206,15 @@ static void drain_timers(mk_session* s) {
 
 static inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
 
+// Every tile-GEMM kernel takes MK_GD_LDS_BYTES (> 64 KiB) of dynamic LDS: two DMA stages.
+static bool set_gemm_lds() {
+  for (const void* kfn : {(const void*)k_chol_update, (const void*)k_chol_trsm, (const void*)k_inv_level,
+                          (const void*)k_qblocks, (const void*)k_lauum, (const void*)k_pred_var})
+    if (hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, MK_GD_LDS_BYTES) != hipSuccess)
+      return false;
+  return true;
+}
+
 // ------------------------------------------------------------------ Cholesky of all candidates of outcome h
 // Candidate tiles are in the free slot (k_cov_candidate, or k_load_plain for the test entry).
 // One launch per step covers outcomes h0 .. h0+hc-1 of every subset (hc = q in the sampler).
@@ -250,7 +259,8 @@ static void launch_trinv(mk_session* s, Group& g, int max_entries, const int* li
     const int npairs = (nt + 2 * sz - 1) / (2 * sz);
     for (int phase = 0; phase < 2; ++phase)
       timed(s, g.stream, KS_INV, 0.0, [&] {
-        hipLaunchKernelGGL(k_inv_level, dim3(xcd_grid_h(max_entries, npairs * sz * sz)), dim3(256), 0, g.stream, g.ms,
+        hipLaunchKernelGGL(k_inv_level, dim3(xcd_grid_h(max_entries, npairs * sz * sz)), dim3(256), MK_GD_LDS_BYTES,
+                           g.stream, g.ms,
                            list, count, sz, phase);
       });
   }
@@ -261,7 +271,7 @@ static void launch_inverse(mk_session* s, Group& g) {
   const int nt = s->nt, max_entries = g.S * s->q;
   launch_trinv(s, g, max_entries, g.d_list, g.d_count);
   timed(s, g.stream, KS_LAUUM, 0.0, [&] {
-    hipLaunchKernelGGL(k_qblocks, dim3(xcd_grid_h(max_entries, nt)), dim3(256), 0, g.stream, g.ms, g.md.n_s, g.d_list,
+    hipLaunchKernelGGL(k_qblocks, dim3(xcd_grid_h(max_entries, nt)), dim3(256), MK_GD_LDS_BYTES, g.stream, g.ms, g.md.n_s, g.d_list,
                        g.d_count);
   });
   hipLaunchKernelGGL(k_take_border, dim3(max_entries * ((s->n_pad + 255) / 256)), dim3(256), 0, g.stream, g.md, g.ms,
@@ -599,8 +609,7 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
   }
   HIPCHK(hipFuncSetAttribute((const void*)k_chol_diag, hipFuncAttributeMaxDynamicSharedMemorySize,
                              MK_DIAG_LDS_BYTES));
-  for (const void* kfn : {(const void*)k_chol_update, (const void*)k_chol_trsm, (const void*)k_pred_var})
-    HIPCHK(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, MK_GD_LDS_BYTES));
+  if (!set_gemm_lds()) return fail(set_err(MK_E_HIP, "gemm lds attribute"));
   HIPCHK(hipFuncSetAttribute((const void*)k_sweep, hipFuncAttributeMaxDynamicSharedMemorySize,
                              q * (64 * 64 + 2 * 64) * 8));
 
@@ -1125,11 +1134,7 @@ extern "C" int mk_cholesky_batched(const double* A, int32_t S, int32_t n, double
       hipMemset(ms.cur, 0, S * 4) != hipSuccess || hipMemset(md.info, 0, S * 4) != hipSuccess)
     return fail(set_err(MK_E_HIP, "cholesky upload"));
   if (hipFuncSetAttribute((const void*)k_chol_diag, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          MK_DIAG_LDS_BYTES) != hipSuccess ||
-      hipFuncSetAttribute((const void*)k_chol_update, hipFuncAttributeMaxDynamicSharedMemorySize, MK_GD_LDS_BYTES) !=
-          hipSuccess ||
-      hipFuncSetAttribute((const void*)k_chol_trsm, hipFuncAttributeMaxDynamicSharedMemorySize, MK_GD_LDS_BYTES) !=
-          hipSuccess)
+                          MK_DIAG_LDS_BYTES) != hipSuccess || !set_gemm_lds())
     return fail(set_err(MK_E_HIP, "lds attribute"));
   hipLaunchKernelGGL(k_load_plain, dim3(2048), dim3(256), 0, s->stream, ms, dA, n, S);
   launch_cholesky(s, a, 0, 1);
@@ -1162,7 +1167,7 @@ extern "C" int mk_cholesky_batched(const double* A, int32_t S, int32_t n, double
                        a.d_count);
     const int ntiles = nt * (nt + 1) / 2;
     launch_trinv(s, a, S, a.d_list, a.d_count);
-    hipLaunchKernelGGL(k_lauum, dim3(S * ntiles), dim3(256), 0, s->stream, ms, md.n_s, a.d_list, a.d_count);
+    hipLaunchKernelGGL(k_lauum, dim3(S * ntiles), dim3(256), MK_GD_LDS_BYTES, s->stream, ms, md.n_s, a.d_list, a.d_count);
     hipLaunchKernelGGL(k_extract_L, dim3(2048), dim3(256), 0, s->stream, ms, n, S, dL, 1);
     if (hipMemcpyAsync(inv_out, dL, (size_t)S * n * n * 8, hipMemcpyDeviceToHost, s->stream) != hipSuccess)
       return fail(set_err(MK_E_HIP, "inverse download"));

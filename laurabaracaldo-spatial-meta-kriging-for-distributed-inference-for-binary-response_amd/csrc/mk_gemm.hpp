@@ -2,17 +2,24 @@
 //
 // One 256-thread workgroup (4 waves, 2x2) owns one 128x128 output tile; each
 // wave owns a 64x64 quadrant = 4x4 MFMA blocks (64 fp64 accumulators/lane).
-// K is streamed in chunks of 16 through LDS ([k][m] images, row stride 144
-// doubles so the two 16-lane halves of a ds_read_b64 group land on disjoint
-// banks), register-prefetching chunk c+1 while chunk c is multiplied.  Kernels
-// built on it stay within 256 registers (__launch_bounds__(256, 2)) so two
-// workgroups share a CU and one's HBM stalls hide behind the other's MFMAs
-// (measured on the cfg3 Cholesky update: 35.8 -> 56.2 TFLOP/s).
+// K is streamed in chunks of 16 straight from HBM into LDS by global_load_lds
+// (LDS-DMA: no staging registers, no ds_write pass), two stages deep: chunk c+1
+// streams in while chunk c is multiplied, one barrier per chunk.  Kernels built on
+// it stay within 256 registers (__launch_bounds__(256, 2)) and 2 x 72 KiB of LDS,
+// so two workgroups share a CU and one's waits hide behind the other's MFMAs.
 //
 // Operands are described by strides so that every product the Cholesky /
 // inverse / kriging code needs (NT, NN, TN) is the same kernel body:
 //   op(A)(m,k) = A[m + k*sA]  (A_MU)   or  A[m*sA + k]  (!A_MU)
 //   op(B)(k,n) = B[k*sB + n]  (B_NU)   or  B[k + n*sB]  (!B_NU)
+// LDS images (a DMA wave instruction writes 64 lanes x 16 B = 1 KiB lane-linearly):
+//   m-contiguous: [k][m], k-row stride GB_SM = 144 doubles; one instruction per k-row
+//     (rows may be padded because no instruction crosses a row).  Stride 144 puts the
+//     two 16-lane halves of a ds_read_b64 group on disjoint banks.
+//   k-contiguous: [m][16], the 8 k-pairs of row m XOR-swizzled by (m >> 1) & 7.  One
+//     instruction fills 8 rows (lane L: row L>>3, slot L&7 holds pair (L&7)^swz); the
+//     swizzle is applied to the SOURCE address, so the image stays lane-linear while a
+//     fragment read (16 m x 2 k per half-wave) touches 64 distinct banks.
 // The MFMA is issued with (B-fragment, A-fragment) so the accumulator holds
 // C^T: lane l, register r of block (bm,bn) is C[m = 16bm + (l&15)][n = 16bn +
 // (l>>4) + 4r] -- consecutive lanes walk consecutive rows of a column-major C
@@ -25,17 +32,13 @@ namespace mk {
 typedef double d4 __attribute__((ext_vector_type(4)));
 typedef double d2 __attribute__((ext_vector_type(2)));
 
-#ifndef MK_GB_K
-#define MK_GB_K 16
-#endif
-constexpr int GB_K = MK_GB_K;  // K chunk
-constexpr int GB_SM = 144;     // LDS row stride (doubles) for m-contiguous operands
-// k-contiguous operands are transposed while stored to LDS; an odd stride spreads
-// the 8 k values a 16-lane ds_write group stores for one m over distinct banks.
-constexpr int GB_SMT = 145;
-template <bool MU> constexpr int sm_of() { return MU ? GB_SM : GB_SMT; }
-constexpr int GB_LDS_DOUBLES = 2 * GB_K * GB_SMT;
-constexpr int GB_PER = GB_K / 4;   // d2 loads per thread per operand per chunk
+constexpr int GB_K = 16;                      // K chunk (the k-contiguous image assumes 8 pairs per row)
+constexpr int GB_SM = 144;                    // k-row stride of an m-contiguous image (doubles)
+constexpr int GB_IMG = GB_K * GB_SM;          // one operand image slot (a k-contiguous image uses 128*16)
+constexpr int GB_STAGE = 2 * GB_IMG;          // A + B
+constexpr int GB_LDS_BYTES = 2 * GB_STAGE * 8;  // two stages
+static_assert(GB_LDS_BYTES == MK_GD_LDS_BYTES, "mk_common.hpp LDS size");
+static_assert(128 * GB_K <= GB_IMG, "k-contiguous image fits its slot");
 
 struct Acc {
   d4 v[4][4];
@@ -48,42 +51,31 @@ __device__ inline void acc_zero(Acc& a) {
     for (int j = 0; j < 4; ++j) a.v[i][j] = (d4){0.0, 0.0, 0.0, 0.0};
 }
 
-// Load one 128 x 16 chunk of op(X) into registers (8 doubles per thread).
-// `kvalid`: elements with chunk-relative k >= kvalid are zero (K masking).
+__device__ inline int ku_swz(int m) { return (m >> 1) & 7; }
+
+// DMA one 128 x 16 chunk of op(X) (k = k0 .. k0+15) into an LDS image: 4 instructions per wave.
 template <bool MU>
-__device__ inline void load_chunk(const double* __restrict__ X, long s, int k0, int kvalid, d2 (&r)[GB_PER]) {
-  const int t = threadIdx.x;
+__device__ inline void dma_chunk(const double* __restrict__ X, long s, int k0, double* img) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
-  for (int i = 0; i < GB_PER; ++i) {
-    const int e = t + 256 * i;
+  for (int j = 0; j < 4; ++j) {
     if (MU) {
-      const int k = e >> 6, m = (e & 63) * 2;
-      r[i] = (k < kvalid) ? *reinterpret_cast<const d2*>(X + m + (long)(k0 + k) * s) : (d2){0.0, 0.0};
+      const int r = w + 4 * j;
+      __builtin_amdgcn_global_load_lds((const void*)(X + (long)(k0 + r) * s + 2 * lane), (void*)(img + r * GB_SM), 16,
+                                       0, 0);
     } else {
-      const int k = (e % (GB_K / 2)) * 2, m = e / (GB_K / 2);
-      d2 v = *reinterpret_cast<const d2*>(X + (long)m * s + k0 + k);
-      if (k >= kvalid) v.x = 0.0;
-      if (k + 1 >= kvalid) v.y = 0.0;
-      r[i] = v;
+      const int m8 = (w + 4 * j) * 8;
+      const int m = m8 + (lane >> 3);
+      const int pr = (lane & 7) ^ ku_swz(m);
+      __builtin_amdgcn_global_load_lds((const void*)(X + (long)m * s + k0 + 2 * pr), (void*)(img + m8 * GB_K), 16, 0,
+                                       0);
     }
   }
 }
 
 template <bool MU>
-__device__ inline void store_chunk(double* lds, const d2 (&r)[GB_PER]) {
-  const int t = threadIdx.x;
-#pragma unroll
-  for (int i = 0; i < GB_PER; ++i) {
-    const int e = t + 256 * i;
-    if (MU) {
-      const int k = e >> 6, m = (e & 63) * 2;
-      *reinterpret_cast<d2*>(lds + k * GB_SM + m) = r[i];
-    } else {
-      const int k = (e % (GB_K / 2)) * 2, m = e / (GB_K / 2);
-      lds[k * GB_SMT + m] = r[i].x;
-      lds[(k + 1) * GB_SMT + m] = r[i].y;
-    }
-  }
+__device__ inline double frag(const double* img, int m, int k) {
+  return MU ? img[k * GB_SM + m] : img[m * GB_K + 2 * ((k >> 1) ^ ku_swz(m)) + (k & 1)];
 }
 
 // Structural zeros (wave-uniform skips; the skipped MFMAs would add exact zeros or feed
@@ -93,22 +85,24 @@ __device__ inline void store_chunk(double* lds, const d2 (&r)[GB_PER]) {
 //               diagonal (column block > row block) are never read   (flag = tile is diagonal)
 //   SKIP_TRI_B  op(B) lower-triangular in (n, k) over one 128-deep K: chunk c only touches
 //               output column blocks >= c                             (flag = chunk index c)
-//   SKIP_WAVE   the calling wave's whole 64x64 quadrant is unused        (flag = skip this wave)
-enum { SKIP_NONE = 0, SKIP_UPPER = 1, SKIP_TRI_B = 2, SKIP_WAVE = 3 };
+enum { SKIP_NONE = 0, SKIP_UPPER = 1, SKIP_TRI_B = 2 };
 
-template <bool NEG = false, int SA = GB_SM, int SB = GB_SM, int SKIP = SKIP_NONE>
-__device__ inline void mma_chunk(const double* As, const double* Bs, Acc& acc, int flag = 0) {
+// MASK: fragments with chunk-relative k >= kvalid read as zero.
+template <bool NEG, bool A_MU, bool B_NU, int SKIP, bool MASK>
+__device__ inline void mma_chunk(const double* As, const double* Bs, Acc& acc, int flag, int kvalid) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int wm = w & 1, wn = w >> 1;
   const int li = lane & 15, lk = lane >> 4;
 #pragma unroll
   for (int ks = 0; ks < GB_K / 4; ++ks) {
+    const int k = ks * 4 + lk;
+    const bool live = !MASK || k < kvalid;
     double ya[4], xb[4];
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
-      const double av = As[(ks * 4 + lk) * SA + wm * 64 + b * 16 + li];
+      const double av = live ? frag<A_MU>(As, wm * 64 + b * 16 + li, k) : 0.0;
       ya[b] = NEG ? -av : av;
-      xb[b] = Bs[(ks * 4 + lk) * SB + wn * 64 + b * 16 + li];
+      xb[b] = live ? frag<B_NU>(Bs, wn * 64 + b * 16 + li, k) : 0.0;
     }
 #pragma unroll
     for (int bm = 0; bm < 4; ++bm)
@@ -121,80 +115,40 @@ __device__ inline void mma_chunk(const double* As, const double* Bs, Acc& acc, i
   }
 }
 
-// acc += (NEG ? -1 : 1) op(A)[128 x K] * op(B)[K x 128], K % GB_K == 0; k >= kvalid_total zeroed.
+// acc += (NEG ? -1 : 1) op(A)[128 x K] * op(B)[K x 128], K % GB_K == 0 (MASK: k >= kvalid_total
+// read as zero; the chunk's memory must still be addressable).
 // REV: K chunks in descending order -- tiles of one launch whose K ranges share their END
 // (triangular operands) then stream the same chunks at the same time, so an XCD's L2
 // serves the shared panels once.  SAME: op(B) = op(A)^T read from the same memory (A'A
-// products): one load and one LDS image serve both fragments.
+// products): one DMA and one LDS image serve both fragments.
 // SKIP (see mma_chunk): SKIP_UPPER with diag_tile != 0; SKIP_TRI_B for K = 128.
-template <bool A_MU, bool B_NU, bool NEG = false, bool REV = false, bool SAME = false, int SKIP = SKIP_NONE>
+// lds: GB_LDS_BYTES of dynamic LDS.  Ends with a barrier (the caller may reuse the LDS).
+template <bool A_MU, bool B_NU, bool NEG = false, bool REV = false, bool SAME = false, int SKIP = SKIP_NONE,
+          bool MASK = false>
 __device__ inline void gemm_128(const double* __restrict__ A, long sA, const double* __restrict__ B, long sB,
                                 int K, int kvalid_total, Acc& acc, double* lds, int diag_tile = 0) {
-  double* As = lds;
-  double* Bs = SAME ? lds : lds + GB_K * GB_SMT;
-  d2 ra[GB_PER], rb[GB_PER];
   if (K <= 0) return;
-  const int k_first = REV ? K - GB_K : 0;
-  load_chunk<A_MU>(A, sA, k_first, kvalid_total - k_first, ra);
-  if (!SAME) load_chunk<B_NU>(B, sB, k_first, kvalid_total - k_first, rb);
-  for (int kc = 0; kc < K; kc += GB_K) {
-    __syncthreads();
-    store_chunk<A_MU>(As, ra);
-    if (!SAME) store_chunk<B_NU>(Bs, rb);
-    __syncthreads();
-    if (kc + GB_K < K) {
-      const int k1 = REV ? K - 2 * GB_K - kc : kc + GB_K;
-      load_chunk<A_MU>(A, sA, k1, kvalid_total - k1, ra);
-      if (!SAME) load_chunk<B_NU>(B, sB, k1, kvalid_total - k1, rb);
-    }
-    if (SKIP == SKIP_WAVE) {
-      if (!diag_tile) mma_chunk<NEG, sm_of<A_MU>(), sm_of<B_NU>()>(As, Bs, acc);
-    } else {
-      mma_chunk<NEG, sm_of<A_MU>(), sm_of<B_NU>(), SKIP>(As, Bs, acc,
-                                                         SKIP == SKIP_TRI_B ? (REV ? K - GB_K - kc : kc) / GB_K : diag_tile);
-    }
-  }
-}
-
-// LDS-DMA variant for operands whose 128 m (n) values per k are contiguous (A_MU, B_NU) and
-// K fully valid: each k-row of a chunk is ONE global_load_lds_dwordx4 wave instruction
-// (64 lanes x 16 B = the 1 KiB row; rows padded to GB_SM, no instruction crosses a row), so
-// the chunk lands in LDS with no staging registers and no ds_write pass.  Two stages: chunk
-// c+1 streams in while chunk c is multiplied; one barrier per chunk (its vmcnt(0) retires
-// the DMA, and every wave has finished reading the stage the next DMA overwrites).
-constexpr int GD_STAGE = 2 * GB_K * GB_SM;                 // A + B images of one chunk
-constexpr int GD_LDS_BYTES = 2 * GD_STAGE * 8;             // two stages
-static_assert(GD_LDS_BYTES == MK_GD_LDS_BYTES, "mk_common.hpp LDS size");
-template <bool NEG = false, int SKIP = SKIP_NONE>
-__device__ inline void gemm_128_dma(const double* __restrict__ A, long sA, const double* __restrict__ B, long sB,
-                                    int K, Acc& acc, double* lds) {
-  if (K <= 0) return;
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  auto issue = [&](int k0, double* st) {
-#pragma unroll
-    for (int r = w; r < GB_K; r += 4) {
-      __builtin_amdgcn_global_load_lds((const void*)(A + (long)(k0 + r) * sA + 2 * lane), (void*)(st + r * GB_SM),
-                                       16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(B + (long)(k0 + r) * sB + 2 * lane),
-                                       (void*)(st + (GB_K + r) * GB_SM), 16, 0, 0);
-    }
+  const int nch = K / GB_K;
+  auto k_of = [&](int c) { return REV ? K - GB_K * (c + 1) : GB_K * c; };
+  auto issue = [&](int c) {
+    double* st = lds + (c & 1) * GB_STAGE;
+    dma_chunk<A_MU>(A, sA, k_of(c), st);
+    if (!SAME) dma_chunk<B_NU>(B, sB, k_of(c), st + GB_IMG);
   };
-  issue(0, lds);
+  issue(0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  int cur = 0;
-  for (int kc = 0; kc < K; kc += GB_K) {
-    double* st = lds + cur * GD_STAGE;
-    if (kc + GB_K < K) issue(kc + GB_K, lds + (cur ^ 1) * GD_STAGE);
-    mma_chunk<NEG, GB_SM, GB_SM, SKIP>(st, st + GB_K * GB_SM, acc, SKIP == SKIP_TRI_B ? kc / GB_K : 0);
+  for (int c = 0; c < nch; ++c) {
+    const double* st = lds + (c & 1) * GB_STAGE;
+    // the stage chunk c+1 overwrites was last read in iteration c-1, which every wave has left
+    if (c + 1 < nch) issue(c + 1);
+    const int k0 = k_of(c);
+    mma_chunk<NEG, A_MU, B_NU, SKIP, MASK>(st, SAME ? st : st + GB_IMG, acc,
+                                           SKIP == SKIP_TRI_B ? k0 / GB_K : diag_tile, kvalid_total - k0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    cur ^= 1;
   }
 }
-
-// acc = C (column-major, ldc): preload for C -= A B^T updates (no read-modify-write epilogue).
-__device__ inline void acc_load(Acc& acc, const double* C, long ldc);
 
 // Element coordinates of accumulator (bm,bn,r) for this lane.
 __device__ inline int acc_row(int bm) {
@@ -206,6 +160,7 @@ __device__ inline int acc_col(int bn, int r) {
   return wn * 64 + bn * 16 + (lane >> 4) + 4 * r;
 }
 
+// acc = C (column-major, ldc): preload for C -= A B^T updates (no read-modify-write epilogue).
 __device__ inline void acc_load(Acc& acc, const double* C, long ldc) {
 #pragma unroll
   for (int bm = 0; bm < 4; ++bm)

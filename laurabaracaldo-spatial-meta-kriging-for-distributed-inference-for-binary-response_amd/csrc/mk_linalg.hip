@@ -146,7 +146,7 @@ __global__ __launch_bounds__(256, 2) void k_chol_update(MatSet ms, int S, int h0
   Acc acc;
   acc_load(acc, C, ld);
   // (Skipping the diagonal tiles' unused upper quadrant -- per MFMA or per chunk -- measured slower.)
-  gemm_128_dma<true>(M + i * MK_NB, ld, M + k * MK_NB, ld, k * MK_NB, acc, lds);
+  gemm_128<true, true, true>(M + i * MK_NB, ld, M + k * MK_NB, ld, k * MK_NB, k * MK_NB, acc, lds);
   store_tile(C, ld, acc);
 }
 
@@ -166,7 +166,7 @@ __global__ __launch_bounds__(256, 2) void k_chol_trsm(MatSet ms, int S, int h0, 
   Acc acc;
   acc_zero(acc);
   // Winv_k lower triangular: (C Winv^T)(m, n) = sum_{j <= n} C(m, j) Winv(n, j)
-  gemm_128_dma<false, SKIP_TRI_B>(C, ld, W, MK_NB, MK_NB, acc, lds);
+  gemm_128<true, true, false, false, false, SKIP_TRI_B>(C, ld, W, MK_NB, MK_NB, MK_NB, acc, lds);
   store_tile(C, ld, acc);
 }
 
@@ -404,7 +404,7 @@ __global__ __launch_bounds__(256) void k_inv_copydiag(MatSet ms, const int* __re
 // with W_TT, W_BB complete from the lower levels.  Triangularity bounds every K range.
 __global__ __launch_bounds__(256, 2) void k_inv_level(MatSet ms, const int* __restrict__ list,
                                                       const int* __restrict__ count, int sz, int phase) {
-  __shared__ __attribute__((aligned(16))) double lds[GB_LDS_DOUBLES];
+  extern __shared__ __attribute__((aligned(16))) double lds[];   // MK_GD_LDS_BYTES
   const int npairs = (ms.nt + 2 * sz - 1) / (2 * sz);
   const int per = npairs * sz * sz;
   int e, t;
@@ -447,13 +447,13 @@ __device__ inline void wtw_tile(const MatSet& ms, int sh, int ns, int i, int j, 
   acc_zero(acc);
   // DIAG (i == j): both operands are the panel W(i:, i) -- loaded once
   if (kvalid > 0)
-    gemm_128<false, false, false, false, DIAG>(X + i * MK_NB + (long)i * MK_NB * ld, ld,
+    gemm_128<false, false, false, false, DIAG, SKIP_NONE, true>(X + i * MK_NB + (long)i * MK_NB * ld, ld,
                                                X + i * MK_NB + (long)j * MK_NB * ld, ld, K, kvalid, acc, lds);
 }
 
 __global__ __launch_bounds__(256, 2) void k_lauum(MatSet ms, const int* __restrict__ n_s, const int* __restrict__ list,
                                                const int* __restrict__ count) {
-  __shared__ __attribute__((aligned(16))) double lds[GB_LDS_DOUBLES];
+  extern __shared__ __attribute__((aligned(16))) double lds[];   // MK_GD_LDS_BYTES
   const int ntiles = ms.nt * (ms.nt + 1) / 2;
   const int e = blockIdx.x / ntiles;
   if (e >= *count) return;
@@ -472,7 +472,7 @@ __global__ __launch_bounds__(256, 2) void k_lauum(MatSet ms, const int* __restri
 
 __global__ __launch_bounds__(256, 2) void k_qblocks(MatSet ms, const int* __restrict__ n_s, const int* __restrict__ list,
                                                  const int* __restrict__ count) {
-  __shared__ __attribute__((aligned(16))) double lds[GB_LDS_DOUBLES];
+  extern __shared__ __attribute__((aligned(16))) double lds[];   // MK_GD_LDS_BYTES
   int e, i;
   if (!xcd_map(*count, ms.nt, &e, &i)) return;
   const int sh = list[e];
@@ -567,7 +567,7 @@ __global__ __launch_bounds__(256, 2) void k_pred_var(Model md, MatSet ms, const 
   Acc acc;
   acc_zero(acc);
   const int K = (i + 1) * MK_NB;   // W lower-triangular
-  gemm_128_dma(Wm + i * MK_NB, ld, PT, md.n_test_pad, K, acc, lds);
+  gemm_128<true, true>(Wm + i * MK_NB, ld, PT, md.n_test_pad, K, K, acc, lds);
   double* XK = md.XK + (long)sh * md.n_test_pad * md.n_pad + (long)tb * MK_NB * md.n_pad + i * MK_NB;
   store_tile(XK, md.n_pad, acc);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w & 1;
