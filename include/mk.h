@@ -153,6 +153,16 @@ int mk_glm_binomial(const double* y, const double* weights, const double* x, int
                     double epsilon, int32_t maxit, double* coef, double* vcov, int32_t* iters,
                     int32_t device);
 
+/* ---- partition (MK.R:15-41) with R's own RNG stream, host side ----
+ * After `set.seed(seed)` under R >= 3.6.0 defaults (Mersenne-Twister, Rejection sampling),
+ * the reference's loop `index.part[[i]] <- sample(a, n.part[i]); a <- setdiff(a, ...)`.
+ * n_part: [n_core] out (MK.R:17-18); index_out: [n] out, subset i's 1-based indices at offset
+ * n_part[0] + ... + n_part[i-1], in R's draw order.  Replaces nothing on the R side (R keeps
+ * its own partition); it lets a non-R host fit exactly the subsets an R session fits. */
+int mk_partition_r(int32_t n, int32_t n_core, int32_t seed, int32_t* n_part, int32_t* index_out);
+/* sample.int(n, size) (without replacement, 1-based) right after set.seed(seed). */
+int mk_r_sample(int32_t seed, int32_t n, int32_t size, int32_t* out);
+
 /* ---- exposed kernels for parity tests ---- */
 /* R_k = correlation(coords_k) (n x n column-major) for S point sets of n sites. */
 int mk_correlation_batched(const double* coords, int32_t S, int32_t n, const double* phi, const double* nu,

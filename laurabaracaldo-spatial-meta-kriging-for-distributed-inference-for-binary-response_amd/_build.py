@@ -6,7 +6,7 @@ import sys
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_PATH = os.path.join(PKG_DIR, "libmk.so")
-SOURCES = ["mk_linalg.hip", "mk_mcmc.hip", "mk_init.hip", "mk_post.hip", "mk_api.hip"]
+SOURCES = ["mk_linalg.hip", "mk_mcmc.hip", "mk_init.hip", "mk_post.hip", "mk_api.hip", "mk_rsample.cpp"]
 HEADERS = ["mk_common.hpp", "mk_types.hpp", "mk_gemm.hpp", "mk_corr.hpp", "mk_kernels.hpp"]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wno-unused-value",
          "-Wno-unused-result"]
@@ -28,7 +28,7 @@ def build(force=False, verbose=False):
     objs = []
     procs = []
     for src in SOURCES:
-        obj = os.path.join(CSRC, src.replace(".hip", ".o"))
+        obj = os.path.join(CSRC, os.path.splitext(src)[0] + ".o")
         cmd = [hipcc] + FLAGS + ["-c", os.path.join(CSRC, src), "-o", obj]
         procs.append((cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
         objs.append(obj)

@@ -81,6 +81,8 @@ EXPORTS = {
     "mk_correlation_batched": (ctypes.c_int, [_dp, ctypes.c_int32, ctypes.c_int32, _dp, _dp, ctypes.c_int32, _dp,
                                               ctypes.c_int32]),
     "mk_cholesky_batched": (ctypes.c_int, [_dp, ctypes.c_int32, ctypes.c_int32, _dp, _dp, _dp, ctypes.c_int32]),
+    "mk_partition_r": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _ip, _ip]),
+    "mk_r_sample": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _ip]),
     "mk_last_error": (ctypes.c_char_p, []),
     "mk_device_count": (ctypes.c_int, []),
 }

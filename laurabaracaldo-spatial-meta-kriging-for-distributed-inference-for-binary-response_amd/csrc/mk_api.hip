@@ -34,6 +34,9 @@ static int set_err(int code, const std::string& msg) {
   } while (0)
 
 extern "C" const char* mk_last_error(void) { return g_err.c_str(); }
+namespace mk {
+int host_error(int code, const char* msg) { return set_err(code, msg); }   // for host-only sources
+}
 
 extern "C" int mk_device_count(void) {
   int n = 0;

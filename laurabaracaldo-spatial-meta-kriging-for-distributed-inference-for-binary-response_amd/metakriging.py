@@ -1,6 +1,7 @@
 """Meta-kriging workflow around the device path (MetaKriging_BinaryResponse.R).
 
-  partition            MK.R:15-41   random split into n.core subsets (last takes the remainder)
+  partition            MK.R:15-41   random split into n.core subsets (last takes the remainder);
+                                    method="R" replays R's own sample()/setdiff stream
   partitioned_spMvGLM  MK.R:46-96   one subset: glm start values -> spMvGLM -> spPredict -> quantiles
   meta_fit             MK.R:100-114 every subset of a shard at once on one GPU (replaces foreach %dopar%)
   combine              MK.R:119-133 mean of the subsets' 200-quantile grids (device kernel)
@@ -8,6 +9,7 @@
 """
 import numpy as np
 
+from ._lib import _ip, check, load
 from .glm import glm_binomial
 from .post import combine_median
 from .post import posterior_summary as _post_summary
@@ -26,11 +28,24 @@ PROBS200 = r_seq(0.005, 1.0, 0.005)     # MK.R:88
 XOUT996 = r_seq(0.005, 1.0, 0.001)      # MK.R:140
 
 
-def partition(n, n_core, seed=20250114):
+def partition(n, n_core, seed=20250114, method="permutation"):
     """MK.R:15-41: n.part = c(rep(floor(n/K), K-1), remainder); random indices without replacement.
 
-    Returns (n_part, index_part) with 0-based index arrays.  R's sample() stream is
-    not reproduced (documented; a seeded permutation gives the same distribution)."""
+    Returns (n_part, index_part) with 0-based index arrays.
+    method="R": the index sets R itself draws after `set.seed(seed)` (R >= 3.6 defaults:
+    Mersenne-Twister + rejection sampling), via libmk's mk_partition_r -- the reference's
+    sample()/setdiff loop (MK.R:29-41), in R's draw order.
+    method="permutation": a seeded NumPy permutation split (same distribution, not R's stream)."""
+    if method == "R":
+        lib = load()
+        n_part = np.empty(n_core, dtype=np.int32)
+        idx = np.empty(n, dtype=np.int32)
+        check(lib.mk_partition_r(int(n), int(n_core), int(seed),
+                                 n_part.ctypes.data_as(_ip), idx.ctypes.data_as(_ip)))
+        offs = np.concatenate([[0], np.cumsum(n_part)])
+        return n_part, [idx[offs[i]:offs[i + 1]].astype(np.int64) - 1 for i in range(n_core)]
+    if method != "permutation":
+        raise ValueError(f"error: unknown partition method '{method}'")
     per = n // n_core
     n_part = [per] * (n_core - 1) + [n - per * (n_core - 1)]
     perm = np.random.default_rng(seed).permutation(n)

@@ -104,8 +104,14 @@ def partition(n, n_core, seed):
     a = np.arange(1, n + 1, dtype=np.int64)
     index_part = []
     for m in n_part:
-        # sample(a, m): a[sample.int(length(a), m)] (length(a) > 1 here)
-        idx = a[np.asarray(rng.sample_int(len(a), m), dtype=np.int64) - 1]
+        if len(a) == 1 and a[0] >= 1:
+            # sample(x, size) with one number x >= 1 is sample.int(x, size) (R's quirk)
+            idx = np.asarray(rng.sample_int(int(a[0]), m), dtype=np.int64)
+        else:
+            # sample(a, m): a[sample.int(length(a), m)]
+            if m > len(a):
+                raise ValueError("cannot take a sample larger than the population when 'replace = FALSE'")
+            idx = a[np.asarray(rng.sample_int(len(a), m), dtype=np.int64) - 1]
         index_part.append(idx)
         a = a[~np.isin(a, idx)]            # setdiff(a, idx): a's order, idx removed
     return n_part, index_part

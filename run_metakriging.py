@@ -50,6 +50,8 @@ def main():
     ap.add_argument("--combine", default="mean", choices=["mean", "median"])
     ap.add_argument("--predict-tile", type=int)
     ap.add_argument("--seed", type=int, default=20250114)
+    ap.add_argument("--partition", default="R", choices=["R", "permutation"],
+                    help="R: the subsets R draws after set.seed(seed) (mk_partition_r)")
     a = ap.parse_args()
     c = dict(CONFIGS[a.config])
     for k_arg, k_cfg in [("n", "n"), ("subsets", "K"), ("n_test", "n_test"), ("n_batch", "n_batch"),
@@ -75,7 +77,7 @@ def main():
     t["data_s"] = time.perf_counter() - t0
 
     t1 = time.perf_counter()
-    n_part, index_part = mk.partition(n, K, seed=a.seed)                       # MK.R:15-41
+    n_part, index_part = mk.partition(n, K, seed=a.seed, method=a.partition)                     # MK.R:15-41
     beta0, bt = mk.start_values(d["y"], d["x"], 1.0, q, device=local)         # MK.R:53-55
     p = d["x"].shape[1]
     cfg = mk.SamplerConfig(q, p, beta0, bt, cov_model=c["cov"], n_batch=c["n_batch"], batch_length=c["batch_length"],
