@@ -305,7 +305,7 @@ static void run_iteration(mk_session* s, Group& g, int it) {
   const int ntri_tiles = s->nt * (s->nt + 1) / 2;
   // the q outcomes' (phi_h, nu_h) steps are independent given u: one batched pass per kind
   for (int which = 0; which < nkinds; ++which) {
-    hipLaunchKernelGGL(k_cov_candidate, dim3(xcd_grid_h(S * q, ntri_tiles)), dim3(256), 0, st, md, g.ms, 0, q, which,
+    hipLaunchKernelGGL(cov_candidate_kernel(md.cov_model), dim3(xcd_grid_h(S * q, ntri_tiles)), dim3(256), 0, st, md, g.ms, 0, q, which,
                        it, nullptr, nullptr);
     launch_cholesky(s, g, 0, q);
     hipLaunchKernelGGL(k_theta_mh, dim3((S * q + 63) / 64), dim3(64), 0, st, md, g.ms, 0, q, which, it);
@@ -620,7 +620,7 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
   Group& a = s->all;
   hipLaunchKernelGGL(k_init_state, dim3(S), dim3(256), 0, s->stream, md);
   const int ntri_tiles = nt * (nt + 1) / 2;
-  hipLaunchKernelGGL(k_cov_candidate, dim3(xcd_grid_h(S * q, ntri_tiles)), dim3(256), 0, s->stream, md, ms, 0, q, 2,
+  hipLaunchKernelGGL(cov_candidate_kernel(md.cov_model), dim3(xcd_grid_h(S * q, ntri_tiles)), dim3(256), 0, s->stream, md, ms, 0, q, 2,
                      0, nullptr, nullptr);
   launch_cholesky(s, a, 0, q);
   hipLaunchKernelGGL(k_theta_init, dim3((S * q + 63) / 64), dim3(64), 0, s->stream, md, ms, 0, q);
@@ -706,7 +706,7 @@ static int predict_tiled(mk_session* s, mk_outputs* o) {
       hipLaunchKernelGGL(k_kept_dirty, dim3(1), dim3(256), 0, st, mt, prev, s->d_slist, s->d_scount, g.d_plist,
                          g.d_pcount);
       for (int h = 0; h < q; ++h) {
-        hipLaunchKernelGGL(k_cov_candidate, dim3(xcd_grid_h(S, ntri_tiles)), dim3(256), 0, st, mt, g.ms, h, 1, 2, 0,
+        hipLaunchKernelGGL(cov_candidate_kernel(mt.cov_model), dim3(xcd_grid_h(S, ntri_tiles)), dim3(256), 0, st, mt, g.ms, h, 1, 2, 0,
                            s->d_slist + h * S, s->d_scount + h);
         launch_cholesky(s, g, h, 1, s->d_slist + h * S, s->d_scount + h);
       }

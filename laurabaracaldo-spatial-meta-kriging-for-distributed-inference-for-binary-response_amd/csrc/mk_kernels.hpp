@@ -5,7 +5,13 @@
 namespace mk {
 inline int xcd_grid_h(int S, int T) { return 8 * ((S + 7) / 8) * T; }
 // mk_linalg.hip
+template <int MODEL>
 __global__ void k_cov_candidate(Model md, MatSet ms, int h0, int hc, int which, int iter, const int* slist, const int* scount);
+// the candidate kernel specialised for the session's covariance model
+typedef void (*CovCandidateKernel)(Model, MatSet, int, int, int, int, const int*, const int*);
+inline CovCandidateKernel cov_candidate_kernel(int model) {
+  return model == MK_COV_EXPONENTIAL ? k_cov_candidate<MK_COV_EXPONENTIAL> : k_cov_candidate<MK_COV_MATERN>;
+}
 __global__ void k_chol_update(MatSet ms, int S, int h0, int hc, int k, const int* slist, const int* scount);
 __global__ void k_chol_trsm(MatSet ms, int S, int h0, int hc, int k, const int* slist, const int* scount);
 __global__ void k_chol_diag(MatSet ms, const int* n_s, int h0, int hc, int k, double* ld_part, double* quad_c, int* info,

@@ -101,6 +101,20 @@ __device__ inline bool pick_pair(const int* slist, const int* scount, int e, int
   return pick_subset(slist, scount, s);
 }
 
+// MODEL = MK_COV_EXPONENTIAL: exp(-phi d) inline (the same expression CorrFn evaluates, so
+// bit-identical), without the Matern/Bessel code and its registers in the kernel.
+template <int MODEL>
+__device__ inline double cand_value(const CandGen& g, int R, int C) {
+  if (R < g.ns && C < g.ns) {
+    if (R == C) return 1.0;
+    const double d = dist2d(g.cx[R], g.cy[R], g.cx[C], g.cy[C]);
+    return (MODEL == MK_COV_EXPONENTIAL) ? exp(-g.rho.phi * d) : g.rho(d);
+  }
+  if (R == g.ns && C < g.ns) return g.uh[C];
+  return (R == C && R != g.ns) ? 1.0 : 0.0;
+}
+
+template <int MODEL>
 __global__ __launch_bounds__(256) void k_cov_candidate(Model md, MatSet ms, int h0, int hc, int which, int iter,
                                                        const int* slist, const int* scount) {
   const int ntiles = ms.nt * (ms.nt + 1) / 2;
@@ -120,11 +134,13 @@ __global__ __launch_bounds__(256) void k_cov_candidate(Model md, MatSet ms, int 
     const int C = tj * MK_NB + cc;
     if (ti == tj && R + 1 < C) continue;
     d2 v;
-    v.x = g(R, C);
-    v.y = g(R + 1, C);
+    v.x = cand_value<MODEL>(g, R, C);
+    v.y = cand_value<MODEL>(g, R + 1, C);
     *reinterpret_cast<d2*>(M + R + (long)C * ld) = v;
   }
 }
+template __global__ void k_cov_candidate<MK_COV_EXPONENTIAL>(Model, MatSet, int, int, int, int, const int*, const int*);
+template __global__ void k_cov_candidate<MK_COV_MATERN>(Model, MatSet, int, int, int, int, const int*, const int*);
 
 // Plain matrix (no border) loaded by the host for the standalone Cholesky test path.
 
@@ -346,9 +362,22 @@ __global__ __launch_bounds__(256) void k_chol_diag(MatSet ms, const int* __restr
   const int base = k * MK_NB;
   const int ns = n_s[s];
   double* Mt = M + base + (long)base * ld;
-  for (int e = tid; e < MK_NB * MK_NB; e += 256) {
-    const int r = e & 127, c = e >> 7;
-    T[r + c * TLD] = (r >= c) ? Mt[r + (long)c * ld] : 0.0;
+  // Unconditional 16-byte loads, 8 in flight per thread, then the upper triangle is zeroed in
+  // LDS (a masked load per element compiled to one dependent round trip each: 64 per thread).
+  for (int e0 = 0; e0 < MK_NB * MK_NB; e0 += 256 * 2 * 8) {
+    d2 v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int e = e0 + 2 * (tid + 256 * j);
+      v[j] = *reinterpret_cast<const d2*>(Mt + (e & 127) + (long)(e >> 7) * ld);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int e = e0 + 2 * (tid + 256 * j);
+      const int r = e & 127, c = e >> 7;
+      T[r + c * TLD] = (r >= c) ? v[j].x : 0.0;
+      T[r + 1 + c * TLD] = (r + 1 >= c) ? v[j].y : 0.0;
+    }
   }
   if (tid == 0) badf = 0;
   __syncthreads();

@@ -329,7 +329,8 @@ __global__ __launch_bounds__(SW_T) void k_sweep(Model md, MatSet ms, int iter) {
       const double* QBt = ms.QB + (((long)s * q + h) * ms.nt + tile) * MK_NB * MK_NB;
       for (int e = tid; e < SW_B * SW_B; e += SW_T) {
         const int r = e & (SW_B - 1), c = e / SW_B;
-        Qb[h * SW_B * SW_B + e] = (r < nb && c < nb) ? QBt[(off + r) + (off + c) * MK_NB] : 0.0;
+        const double v = QBt[(off + r) + (off + c) * MK_NB];   // in the tile: off + 63 < 128
+        Qb[h * SW_B * SW_B + e] = (r < nb && c < nb) ? v : 0.0;  // (a masked load would serialise)
       }
       if (tid < SW_B) dacc[h * SW_B + tid] = 0.0;
       const double* Wb = ms.W + ((long)s * q + h) * (ld * ld) + (long)b0 * ld;

@@ -29,7 +29,7 @@ __global__ void k_fill(double* p, long n) {
 template <bool BNU>
 __global__ __launch_bounds__(256, 2) void k_probe(const double* A, const double* B, double* C, int K, long strideA,
                                                long strideB, int lda) {
-  __shared__ __attribute__((aligned(16))) double lds[GB_LDS_DOUBLES];
+  extern __shared__ __attribute__((aligned(16))) double lds[];   // GB_LDS_BYTES
   const double* a = A + blockIdx.x * strideA;
   const double* b = B + blockIdx.x * strideB;
   Acc acc;
@@ -45,6 +45,19 @@ int main() {
   hipEventCreate(&e0);
   hipEventCreate(&e1);
   const int iters = 4000;
+  // 1) raw MFMA rate: 16 independent accumulators per wave, 1 or 2 waves per SIMD
+  for (int wps : {1, 2}) {
+    const int grid = 256 * wps;
+    hipLaunchKernelGGL(k_mfma_peak, dim3(grid), dim3(256), 0, 0, out, iters);
+    hipEventRecord(e0);
+    for (int r = 0; r < 5; ++r) hipLaunchKernelGGL(k_mfma_peak, dim3(grid), dim3(256), 0, 0, out, iters);
+    hipEventRecord(e1);
+    hipEventSynchronize(e1);
+    float ms;
+    hipEventElapsedTime(&ms, e0, e1);
+    const double fl = 5.0 * grid * 4.0 * 64 * 16.0 * iters * 2048 / 64;   // 2048 flops per wave-MFMA
+    printf("raw v_mfma_f64_16x16x4: %d wave(s)/SIMD  %.2f TFLOP/s  (%.3f ms/launch)\n", wps, fl / ms / 1e9, ms / 5);
+  }
   // GEMM probe: ntile tiles of 128x128, K deep.  distinct: every tile streams its own
   // 128 x K A panel from HBM (B shared, L2); shared: both operands shared (L2 resident).
   for (int bnu : {1, 0})
@@ -63,9 +76,11 @@ int main() {
       }
       const long sA = shared ? 0 : (long)128 * K;
       auto kern = bnu ? k_probe<true> : k_probe<false>;
-      hipLaunchKernelGGL(kern, dim3(ntile), dim3(256), 0, 0, A, B, C, K, sA, 0L, 128);
+      hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, GB_LDS_BYTES);
+      hipLaunchKernelGGL(kern, dim3(ntile), dim3(256), GB_LDS_BYTES, 0, A, B, C, K, sA, 0L, 128);
       hipEventRecord(e0);
-      for (int r = 0; r < 3; ++r) hipLaunchKernelGGL(kern, dim3(ntile), dim3(256), 0, 0, A, B, C, K, sA, 0L, 128);
+      for (int r = 0; r < 3; ++r)
+        hipLaunchKernelGGL(kern, dim3(ntile), dim3(256), GB_LDS_BYTES, 0, A, B, C, K, sA, 0L, 128);
       hipEventRecord(e1);
       hipEventSynchronize(e1);
       float ms;
