@@ -28,7 +28,7 @@ def test_correlation_matches_oracle(mk, model, nu):
         assert np.max(np.abs(R[s] - ref)) <= REL * np.max(np.abs(ref))
 
 
-@pytest.mark.parametrize("n", [1, 5, 127, 128, 200, 255, 256, 400, 700])
+@pytest.mark.parametrize("n", [1, 5, 127, 128, 200, 255, 256, 400, 700, 2000, 2047, 2048, 2049])
 def test_cholesky_logdet_inverse(mk, n):
     S = 3
     c = _coords(S, n, n)

@@ -12,18 +12,21 @@ pytestmark = pytest.mark.gpu
 TOL = 1e-8
 
 
-def _run_both(mk, n, q, cov, n_test=12, n_batch=3, batch_length=4, burn_in=7, seed=9, subset_base=0, S=2):
-    d = mk.synthetic.generate(n * S, q=q, n_test=n_test, seed=seed + q, cov_model=cov)
+def _run_both(mk, n, q, cov, n_test=12, n_batch=3, batch_length=4, burn_in=7, seed=9, subset_base=0, S=2,
+              sizes=None):
+    sizes = list(sizes) if sizes is not None else [n] * S
+    off = np.concatenate([[0], np.cumsum(sizes)])
+    d = mk.synthetic.generate(int(off[-1]), q=q, n_test=n_test, seed=seed + q, cov_model=cov)
     p = 2 * q
     kw = dict(n_batch=n_batch, batch_length=batch_length, burn_in=burn_in, seed=seed)
     cfg = mk.SamplerConfig(q, p, beta_starting=np.zeros(p), beta_tuning=np.full(p, 0.05),
                            cov_model="matern" if cov else "exponential", **kw)
     ocfg = om.Config(q, p, beta_starting=np.zeros(p), beta_tuning=np.full(p, 0.05), cov_model=cov, **kw)
     subs = []
-    for s in range(S):
-        sl = slice(s * n, (s + 1) * n)
-        rows = slice(s * n * q, (s + 1) * n * q)
-        subs.append(dict(coords=d["coords"][sl], y=d["y"][rows], weights=np.ones(n * q), x=d["x"][rows]))
+    for s, m in enumerate(sizes):
+        sl = slice(off[s], off[s] + m)
+        rows = slice(off[s] * q, (off[s] + m) * q)
+        subs.append(dict(coords=d["coords"][sl], y=d["y"][rows], weights=np.ones(m * q), x=d["x"][rows]))
     with mk.Session(subs, cfg, coords_test=d["coords_test"], subset_base=subset_base, record_w=True) as ses:
         ses.run(cfg.n_samples)
         dev = ses.outputs(samples=True, w_samples=True, w_pred_samples=True, acceptance=True)
@@ -32,9 +35,7 @@ def _run_both(mk, n, q, cov, n_test=12, n_batch=3, batch_length=4, burn_in=7, se
     return dev, refs
 
 
-@pytest.mark.parametrize("n,q,cov", [(150, 1, 0), (300, 1, 0), (64, 2, 0), (100, 1, 1), (40, 3, 0)])
-def test_replay_matches_oracle(mk, n, q, cov):
-    dev, refs = _run_both(mk, n, q, cov)
+def _check(dev, refs):
     for s, ref in enumerate(refs):
         np.testing.assert_allclose(dev["samples"][s], ref["samples"], rtol=0, atol=TOL)
         np.testing.assert_allclose(dev["w_samples"][s].T, ref["w_samples"], rtol=0, atol=TOL)
@@ -42,9 +43,29 @@ def test_replay_matches_oracle(mk, n, q, cov):
         np.testing.assert_allclose(dev["parameters"][s], ref["param_q"], rtol=0, atol=TOL)
         np.testing.assert_allclose(dev["w_predict"][s], ref["w_q"], rtol=0, atol=TOL)
         # accept rates of beta / A / phi per batch
-        nrep = ref["accept"].shape[1]
         o_w = dev["acceptance"][s].shape[1] - 1
         np.testing.assert_allclose(dev["acceptance"][s][:, :o_w], ref["accept"][:, :o_w], atol=1e-12)
+
+
+@pytest.mark.parametrize("n,q,cov", [(150, 1, 0), (300, 1, 0), (64, 2, 0), (100, 1, 1), (40, 3, 0)])
+def test_replay_matches_oracle(mk, n, q, cov):
+    dev, refs = _run_both(mk, n, q, cov)
+    _check(dev, refs)
+
+
+@pytest.mark.parametrize("sizes,q", [([150, 163, 127], 1), ([128, 129], 1), ([64, 71], 2)])
+def test_replay_ragged_subsets(mk, sizes, q):
+    """Subsets of different sizes in one session (the reference's last subset takes the
+    remainder, MK.R:18); sizes straddle the 128-tile boundary with the bordered row."""
+    dev, refs = _run_both(mk, None, q, 0, sizes=sizes)
+    _check(dev, refs)
+
+
+def test_replay_cfg3_subset_size(mk):
+    """A configs[2] subset (n_s = 2000, 16 tiles of 128 with the bordered row in the last):
+    a short chain replayed against the oracle."""
+    dev, refs = _run_both(mk, 2000, 1, 0, n_test=40, n_batch=2, batch_length=2, burn_in=3, S=1)
+    _check(dev, refs)
 
 
 def test_quantiles_bit_exact_on_device_samples(mk):
