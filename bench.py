@@ -1,14 +1,16 @@
 #!/usr/bin/env python3
 """Benchmark: MCMC subset-iterations/s (all subsets, whole node) on BASELINE.json's
 headline configuration -- n=500,000 binary sites split into K=250 subsets of 2,000,
-exponential covariance, q=1, 1,000 kriging sites (configs[2]).
+exponential covariance, q=1, 1,000 kriging sites (configs[2]), on each GPU.
 
 A step = one spMvGLM amcmc iteration of EVERY subset (beta, A, phi MH with a fresh
 2000x2000 Cholesky per subset, inverse where phi moved, single-site w sweep) plus,
 on kept iterations, the fused spPredict kriging draw.  The timed window follows the
 reference schedule (MK.R:57-59, 85): 3 burn-in iterations per kept one.  Subsets are
-sharded over ranks (contiguous blocks, strong scaling: K=250 fixed); no data-path
-collective.  roofline.traffic is the PMC-measured HBM traffic of the same kernel from
+independent, so the default is weak scaling: every rank fits a configs[2]-sized shard
+(250 subsets of 2,000 sites; rank r's sites drawn with seed 20250114 + r, global subset
+indices 250r ...), i.e. a node job of n = N x 500k, K = N x 250; no data-path collective.
+--scaling strong splits the one K=250 job over the ranks instead (contiguous blocks).  roofline.traffic is the PMC-measured HBM traffic of the same kernel from
 profiles/ (rocprofv3 --pmc passes of this command, gfx950 FETCH_SIZE x2 correction).
 
   python bench.py --gpus N --steps K --warmup W
@@ -40,6 +42,8 @@ def parse():
     ap.add_argument("--n-test", type=int, default=1000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-iters", type=int, default=40)
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
+                    help="weak: K subsets per rank (node job N*K); strong: one K-subset job split over ranks")
     ap.add_argument("--streams", type=int, default=0, help="HIP streams per GPU for subset groups (0: library default)")
     return ap.parse_args()
 
@@ -113,12 +117,17 @@ def main():
         dist.init_process_group("nccl", rank=rank, world_size=world)
 
     mk = importlib.import_module(PKG)
-    d = mk.synthetic.generate(n, q=1, n_test=n_test, seed=20250114)
-    n_part, idx = mk.partition(n, K, seed=20250114)
+    weak = a.scaling == "weak"
+    dseed = 20250114 + (rank if weak else 0)      # weak: each rank's 500k sites are its own draw
+    d = mk.synthetic.generate(n, q=1, n_test=n_test, seed=dseed)
+    n_part, idx = mk.partition(n, K, seed=dseed)
     beta0, bt = mk.start_values(d["y"], d["x"], 1.0, 1)
     dmod = importlib.import_module(PKG + ".distributed")
-    lo, hi = dmod.shard_range(K, world, rank)
-    per = (K + world - 1) // world
+    if weak:
+        lo, hi, base, per = 0, K, rank * K, K     # global subset indices rank*K ... (distinct Philox streams)
+    else:
+        lo, hi = dmod.shard_range(K, world, rank)
+        base, per = lo, (K + world - 1) // world
     W = max(1, a.warmup)
     # amcmc batches of 50 as MK.R:57-58; the timed window holds burn-in and kept (kriging)
     # iterations in the reference's 3:1 ratio (burn.in = 0.75 n.samples, MK.R:85)
@@ -128,7 +137,7 @@ def main():
     cfg = mk.SamplerConfig(1, 2, beta0, bt, n_batch=n_batch, batch_length=50, burn_in=burn_in, seed=20250114,
                            n_streams=a.streams)
     subs = [mk.subset_data(d["y"], d["x"], 1.0, d["coords"], 1, idx[i]) for i in range(lo, hi)]
-    ses = mk.Session(subs, cfg, coords_test=d["coords_test"], subset_base=lo, device=local if world > 1 else 0)
+    ses = mk.Session(subs, cfg, coords_test=d["coords_test"], subset_base=base, device=local if world > 1 else 0)
     ses.run(W)                                    # warmup
     ses.profile(True)
 
@@ -158,7 +167,8 @@ def main():
         if dist is not None:
             dist.destroy_process_group()
         return
-    value = K * a.steps / elapsed
+    K_job = K * world if weak else K
+    value = K_job * a.steps / elapsed
     avg_ms = st["ms"] / max(1, st["launches"])
     achieved = st["flops"] / (st["ms"] * 1e-3) / 1e12 if st["ms"] > 0 else 0.0
     out = {
@@ -170,14 +180,16 @@ def main():
         "warmup": W,
         "ms_per_step": elapsed / a.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "strong",
+        "scaling": a.scaling,
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (seeded binary GP field, RFF, SURVEY.md 8d generator)",
-        "config": {"workload": f"configs[2]: n={n}, K={K} subsets of {n // K}, exponential, q=1, "
+        "config": {"workload": (f"configs[2] per GPU (node job n={n * world}, K={K_job})" if weak else
+                                f"configs[2] split over {world} GPU(s)") +
+                               f": n={n}, K={K} subsets of {n // K}, exponential, q=1, "
                                f"n_test={n_test}, amcmc batches of 50, timed window {n_burn_timed} burn-in + "
                                f"{a.steps - n_burn_timed} kept (fused kriging) iterations",
-                   "subsets_per_gpu": per, "streams_per_gpu": a.streams or 1,
+                   "subsets_per_gpu": per, "total_subsets": K_job, "streams_per_gpu": a.streams or 1,
                    "parallelism": f"subset-sharded x{world}"},
         "roofline": {"bound": "mfma", "kernel": "k_chol_update (left-looking Cholesky panel GEMM, fp64 MFMA)",
                      "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",

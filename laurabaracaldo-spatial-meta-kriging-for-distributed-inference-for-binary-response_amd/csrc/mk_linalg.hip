@@ -187,16 +187,20 @@ __global__ __launch_bounds__(256, 2) void k_chol_trsm(MatSet ms, int S, int h0, 
 }
 
 // ---------------------------------------------------------------- diagonal tile: factor + invert in LDS
-// 128x128 tile T (column-major, ld 128) in LDS, 256 threads.  Blocked by 16:
-//   F1 (wave 0)  factor the 16x16 pivot block and invert it in registers (readlane only);
-//   F2 (MFMA)    panel below: P = C Dinv^T;   F3 (MFMA) trailing update T -= P P^T.
-// Inverse X = L^-1 by block rows: X_ij = -Dinv_i sum_k L_ik X_kj (MFMA, 16x16 blocks).
-// Storage: L in the lower triangle; X strictly-lower transposed into the upper triangle
-// (X[r][c] at T[c + r*128]); diag(L) in dg, diag(X) in xd.
+// 128x128 tile T (column-major, stride TLD) in LDS, 256 threads, blocked by 16 (see
+// factor_invert_tile): F1 factor + invert of the 16x16 pivot in one wave's registers, F2 panel
+// P = C Dinv^T, F3 trailing update T -= P P^T, inverse block rows X_pc = -Dinv_p sum L_pK X_Kc
+// (MFMA 16x16x4 on LDS operands).
 // Odd LDS column stride: lanes walking a row (the transposed inverse, column-index accesses)
 // hit distinct banks instead of one (stride 128 doubles = 0 mod 64 banks).
 #define TLD MK_TLD
-#define SLD 17     // wave-private 16 x 16 staging, padded likewise
+#define SLD 17
+#ifdef MK_DIAG_TIMING   // development probe only (tools/diag_probe.hip): shader-clock stamps per phase
+__device__ long long* mk_diag_ts;
+#define MK_TSTAMP(i) do { if (threadIdx.x == 0) mk_diag_ts[blockIdx.x * 64 + (i)] = clock64(); } while (0)
+#else
+#define MK_TSTAMP(i) do { } while (0)
+#endif     // wave-private 16 x 16 staging, padded likewise
 
 __device__ inline double rlane(double v, int lane) {
   const long long b = __double_as_longlong(v);
@@ -205,139 +209,197 @@ __device__ inline double rlane(double v, int lane) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
-// D(16x16) += sum_k A(i,k) B(k,j); lane l, reg r holds D[(l>>4) + 4r][l&15].
+// D(16x16) += sum_k A(i,k) B(k,j); lane l, reg r holds D[(l>>4) + 4r][l&15].  K is a
+// multiple of 16: the operands of four MFMAs are loaded together (LDS latency paid once per 4).
 template <class FA, class FB>
 __device__ inline d4 mfma16(d4 acc, int K, FA fa, FB fb) {
   const int l = threadIdx.x & 63;
-  for (int k0 = 0; k0 < K; k0 += 4) {
-    const double a = fa(l & 15, k0 + (l >> 4));
-    const double b = fb(k0 + (l >> 4), l & 15);
-    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+  for (int k0 = 0; k0 < K; k0 += 16) {
+    double a[4], b[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      a[u] = fa(l & 15, k0 + 4 * u + (l >> 4));
+      b[u] = fb(k0 + 4 * u + (l >> 4), l & 15);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u], b[u], acc, 0, 0, 0);
   }
   return acc;
 }
 
-// X[r][c] (r >= c) of the inverse as stored during/after the inverse phase.
-__device__ inline double xget(const double* T, const double* xd, int r, int c) {
-  return (r > c) ? T[c + r * TLD] : ((r == c) ? xd[r] : 0.0);
+// Value of lane n of this lane's 16-lane DPP row (row_newbcast:n, one v_mov_b64_dpp).
+template <int N>
+__device__ inline double bcast16_t(double v) { return __builtin_amdgcn_update_dpp(v, v, 0x150 + N, 0xf, 0xf, false); }
+__device__ __forceinline__ double bcast16(double v, int n) {
+  switch (n) {
+    case 0: return bcast16_t<0>(v);   case 1: return bcast16_t<1>(v);   case 2: return bcast16_t<2>(v);
+    case 3: return bcast16_t<3>(v);   case 4: return bcast16_t<4>(v);   case 5: return bcast16_t<5>(v);
+    case 6: return bcast16_t<6>(v);   case 7: return bcast16_t<7>(v);   case 8: return bcast16_t<8>(v);
+    case 9: return bcast16_t<9>(v);   case 10: return bcast16_t<10>(v); case 11: return bcast16_t<11>(v);
+    case 12: return bcast16_t<12>(v); case 13: return bcast16_t<13>(v); case 14: return bcast16_t<14>(v);
+    default: return bcast16_t<15>(v);
+  }
 }
 
-__device__ void factor_invert_tile(double* T, double* dg, double* xd, double* Pb, int rb, double* quad_out,
+// d = sqrt(a) and inv = 1/d from the hardware rsq estimate: two Newton steps on 1/sqrt(a), a
+// residual-corrected square root and one Newton step on the reciprocal (both within 1 ulp).
+__device__ inline void rsqrt_sqrt(double a, double* d, double* inv) {
+  double y = __builtin_amdgcn_rsq(a);
+  double e = fma(-a * y, y, 1.0);
+  y = fma(0.5 * y, e, y);
+  e = fma(-a * y, y, 1.0);
+  y = fma(0.5 * y, e, y);
+  const double d0 = a * y;
+  const double r = fma(-d0, d0, a);
+  const double dd = fma(r, 0.5 * y, d0);
+  *d = dd;
+  *inv = fma(y, fma(-dd, y, 1.0), y);
+}
+
+// X[r][c] of the inverse: stored transposed in the upper triangle, diagonal included
+// (T[r + r*TLD] holds X[r][r] once its pivot block is done); zero above the diagonal.  The
+// load is unconditional (always in bounds) and the mask a select: no per-element branch.
+__device__ inline double xget(const double* T, int r, int c) {
+  const double v = T[c + r * TLD];
+  return (r >= c) ? v : 0.0;
+}
+
+// Pivot block p: factor the 16x16 block in registers of one wave and invert it (F1).
+// Lane l holds row (l & 15); lanes 16..63 mirror lanes 0..15 (same instructions, results
+// unused).  Column values are broadcast by 64-bit DPP row_newbcast (no SGPR round trips);
+// upper-triangle entries are updated unconditionally and never read.
+__device__ inline void factor_pivot(double* T, double* dg, double* xd, int b, int rb, double* quad_out, bool& bad) {
+  const int l = threadIdx.x & 63, lr = l & 15;
+  double row[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) row[c] = T[(b + lr) + (b + c) * TLD];
+  double myinv = 0.0;   // 1 / L(lr, lr)
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const double a = bcast16(row[j], j);
+    double d, inv;
+    if (b + j == rb) {
+      d = 1.0;
+      inv = 1.0;
+      if (l == 0) *quad_out = -a;
+    } else {
+      bad |= !(a > 0.0);
+      rsqrt_sqrt(a, &d, &inv);
+    }
+    if (lr == j) myinv = inv;
+    row[j] = (lr == j) ? d : row[j] * inv;
+#pragma unroll
+    for (int c = j + 1; c < 16; ++c) row[c] = fma(-row[j], bcast16(row[j], c), row[c]);
+  }
+  // inverse of the pivot block, row lr of Dinv in xr: with the row-scaled factor
+  // Ls(l, m) = L(l, m) / L(l, l),  X(l, c) = [l == c] / L(l, l) - sum_{c <= m < l} Ls(l, m) X(m, c)
+  double xr[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) xr[c] = (c == lr) ? myinv : 0.0;
+#pragma unroll
+  for (int m = 0; m < 15; ++m) {
+    const double cf = (lr > m) ? row[m] * myinv : 0.0;
+#pragma unroll
+    for (int c = 0; c <= m; ++c) xr[c] = fma(-cf, bcast16(xr[c], m), xr[c]);
+  }
+  if (l < 16) {
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      if (c < l) {
+        T[(b + l) + (b + c) * TLD] = row[c];
+        T[(b + c) + (b + l) * TLD] = xr[c];     // Dinv strictly lower, transposed
+      }
+    }
+    dg[b + l] = row[l];
+    xd[b + l] = xr[l];
+    T[(b + l) + (b + l) * TLD] = xr[l];   // X diagonal in place (the L diagonal lives in dg)
+  }
+}
+
+// F3 block (RR, CC) of the trailing update after pivot column block pc: T_RC -= P_R P_C^T.
+__device__ inline void trailing_block(double* T, int pc, int RR, int CC) {
+  const int l = threadIdx.x & 63, bc = 16 * pc;
+  d4 acc;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) acc[r] = T[(16 * RR + (l >> 4) + 4 * r) + (16 * CC + (l & 15)) * TLD];
+  acc = mfma16(acc, 16, [&](int i, int k) { return -T[(16 * RR + i) + (bc + k) * TLD]; },
+               [&](int k, int j) { return T[(16 * CC + j) + (bc + k) * TLD]; });
+#pragma unroll
+  for (int r = 0; r < 4; ++r) T[(16 * RR + (l >> 4) + 4 * r) + (16 * CC + (l & 15)) * TLD] = acc[r];
+}
+
+// Blocked by 16, two barriers per pivot step p, the inverse X = L^-1 computed by block rows
+// alongside the factorisation (block row p of X needs L(p, <p) and X(<p, <p) only):
+//   phase 1  wave 0: trailing block (p, p) of step p-1, then F1 (factor + invert the pivot);
+//            waves 1-3: the other trailing blocks of step p-1, and S_pc = sum_{c<=K<p} L_pK X_Kc
+//            for every c < p (staged in LDS);
+//   phase 2  F2: panel P_R = C_R Dinv_p^T (R > p), and X_pc = -Dinv_p S_pc (c < p).
+// Storage: L in the lower triangle; X strictly-lower transposed into the upper triangle
+// (X[r][c] at T[c + r*TLD]); diag(L) in dg, diag(X) in xd; S stagings in Sb (7 x 16 x SLD).
+__device__ void factor_invert_tile(double* T, double* dg, double* xd, double* Sb, int rb, double* quad_out,
                                    bool* bad_out) {
   const int tid = threadIdx.x, l = tid & 63, wv = tid >> 6;
   bool bad = false;
-  // ================= factorisation
   for (int p = 0; p < 8; ++p) {
-    const int b = 16 * p;
+    // ---- phase 1
+    const int nb = 8 - p;                       // trailing blocks of step p-1: rows/cols p..7
+    const int ntrail = (p > 0) ? nb * (nb + 1) / 2 : 0;
     if (wv == 0) {
-      double row[16];
+      if (p > 0) {
+        trailing_block(T, p - 1, p, p);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+      }
+      factor_pivot(T, dg, xd, 16 * p, rb, quad_out, bad);
+    } else {
+      // tasks: S_pc (c < p, longest first), then trailing blocks t = 1 .. ntrail-1
+      for (int t = wv - 1; t < p + ntrail - 1; t += 3) {
+        if (t < p) {
+          const int Cb = t;
+          d4 acc = {0.0, 0.0, 0.0, 0.0};
+          acc = mfma16(acc, 16 * (p - Cb), [&](int r, int m) { return T[(16 * p + r) + (16 * Cb + m) * TLD]; },
+                       [&](int m, int c) { return xget(T, 16 * Cb + m, 16 * Cb + c); });
+          double* S = Sb + Cb * 16 * SLD;
 #pragma unroll
-      for (int c = 0; c < 16; ++c) row[c] = (l < 16 && c <= l) ? T[(b + l) + (b + c) * TLD] : 0.0;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const double a = rlane(row[j], j);
-        double d;
-        if (b + j == rb) {
-          d = 1.0;
-          if (l == 0) *quad_out = -a;
+          for (int r = 0; r < 4; ++r) S[((l >> 4) + 4 * r) + (l & 15) * SLD] = acc[r];
         } else {
-          d = sqrt(a);
-          bad |= !(a > 0.0);
+          const int u = t - p + 1;              // trailing block index (0 = (p, p), done by wave 0)
+          int R = 0;
+          while ((R + 1) * (R + 2) / 2 <= u) ++R;
+          const int C = u - R * (R + 1) / 2;
+          trailing_block(T, p - 1, p + R, p + C);
         }
-        const double inv = 1.0 / d;
-        row[j] = (l == j) ? d : ((l > j) ? row[j] * inv : row[j]);
-#pragma unroll
-        for (int c = j + 1; c < 16; ++c) {
-          const double lc = rlane(row[j], c);
-          if (l >= c) row[c] -= row[j] * lc;
-        }
-      }
-      // inverse of the pivot block, row l of Dinv in xr
-      double xr[16];
-#pragma unroll
-      for (int c = 0; c < 16; ++c) xr[c] = (c == l) ? 1.0 : 0.0;
-#pragma unroll
-      for (int m = 0; m < 16; ++m) {
-        const double dm = rlane(row[m], m);
-        const double idm = 1.0 / dm;
-        if (l == m) {
-#pragma unroll
-          for (int c = 0; c <= m; ++c) xr[c] *= idm;
-        }
-#pragma unroll
-        for (int c = 0; c <= m; ++c) {
-          const double xmc = rlane(xr[c], m);
-          if (l > m) xr[c] -= row[m] * xmc;
-        }
-      }
-      if (l < 16) {
-#pragma unroll
-        for (int c = 0; c < 16; ++c) {
-          if (c < l) {
-            T[(b + l) + (b + c) * TLD] = row[c];
-            T[(b + c) + (b + l) * TLD] = xr[c];     // Dinv strictly lower, transposed
-          }
-        }
-        dg[b + l] = row[l];
-        xd[b + l] = xr[l];
       }
     }
     __syncthreads();
-    // ---- F2: panel rows below: P_R = C_R Dinv^T (in place), one 16-row block per wave round-robin
-    for (int R = p + 1 + wv; R < 8; R += 4) {
-      d4 acc = {0.0, 0.0, 0.0, 0.0};
-      acc = mfma16(acc, 16, [&](int i, int k) { return T[(16 * R + i) + (b + k) * TLD]; },
-                   [&](int k, int j) { return xget(T, xd, b + j, b + k); });
+    MK_TSTAMP(1 + 3 * p);
+    // ---- phase 2: F2 panel blocks R = p+1..7, inverse blocks X_pc, c = 0..p-1
+    const int b = 16 * p;
+    for (int t = wv; t < 7; t += 4) {
+      if (t < 7 - p) {
+        const int R = p + 1 + t;
+        d4 acc = {0.0, 0.0, 0.0, 0.0};
+        acc = mfma16(acc, 16, [&](int i, int k) { return T[(16 * R + i) + (b + k) * TLD]; },
+                     [&](int k, int j) { return xget(T, b + j, b + k); });
 #pragma unroll
-      for (int r = 0; r < 4; ++r) T[(16 * R + (l >> 4) + 4 * r) + (b + (l & 15)) * TLD] = acc[r];
-    }
-    __syncthreads();
-    // ---- F3: trailing blocks (R, C), p < C <= R: T_RC -= P_R P_C^T
-    {
-      const int nb = 7 - p;
-      const int nblk = nb * (nb + 1) / 2;
-      for (int t = wv; t < nblk; t += 4) {
-        int R = 0;
-        while ((R + 1) * (R + 2) / 2 <= t) ++R;
-        const int C = t - R * (R + 1) / 2;
-        const int RR = p + 1 + R, CC = p + 1 + C;
-        d4 acc;
+        for (int r = 0; r < 4; ++r) T[(16 * R + (l >> 4) + 4 * r) + (b + (l & 15)) * TLD] = acc[r];
+      } else {
+        const int Cb = t - (7 - p);
+        const double* S = Sb + Cb * 16 * SLD;
+        d4 out = {0.0, 0.0, 0.0, 0.0};
+        out = mfma16(out, 16, [&](int r, int m) { return -xget(T, b + r, b + m); },
+                     [&](int m, int c) { return S[m + c * SLD]; });
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[r] = T[(16 * RR + (l >> 4) + 4 * r) + (16 * CC + (l & 15)) * TLD];
-        acc = mfma16(acc, 16, [&](int i, int k) { return -T[(16 * RR + i) + (b + k) * TLD]; },
-                     [&](int k, int j) { return T[(16 * CC + j) + (b + k) * TLD]; });
-#pragma unroll
-        for (int r = 0; r < 4; ++r) T[(16 * RR + (l >> 4) + 4 * r) + (16 * CC + (l & 15)) * TLD] = acc[r];
+        for (int r = 0; r < 4; ++r) {
+          const int rr = b + (l >> 4) + 4 * r, cc = 16 * Cb + (l & 15);
+          T[cc + rr * TLD] = out[r];
+        }
       }
     }
     __syncthreads();
+    MK_TSTAMP(2 + 3 * p);
   }
   if (l == 0 && wv == 0) *bad_out = bad;
-  // ================= inverse X = L^-1 (diagonal blocks = Dinv already in place)
-  for (int i = 1; i < 8; ++i) {
-    for (int Cb = wv; Cb < i; Cb += 4) {
-      d4 acc = {0.0, 0.0, 0.0, 0.0};
-      // S = sum_{K=Cb}^{i-1} L_iK X_K,Cb
-      acc = mfma16(acc, 16 * (i - Cb), [&](int r, int m) { return T[(16 * i + r) + (16 * Cb + m) * TLD]; },
-                   [&](int m, int c) { return xget(T, xd, 16 * Cb + m, 16 * Cb + c); });
-      double* S = Pb + wv * 16 * SLD;  // wave-private 16x16 staging (column-major, stride SLD)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) S[((l >> 4) + 4 * r) + (l & 15) * SLD] = acc[r];
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      d4 out = {0.0, 0.0, 0.0, 0.0};
-      out = mfma16(out, 16, [&](int r, int m) { return -xget(T, xd, 16 * i + r, 16 * i + m); },
-                   [&](int m, int c) { return S[m + c * SLD]; });
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int rr = 16 * i + (l >> 4) + 4 * r, cc = 16 * Cb + (l & 15);
-        T[cc + rr * TLD] = out[r];
-      }
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-    }
-    __syncthreads();
-  }
 }
 
 // Factor + invert the 128x128 diagonal tile k of each candidate.  Row rb = n_s - 128k
@@ -350,10 +412,11 @@ __global__ __launch_bounds__(256) void k_chol_diag(MatSet ms, const int* __restr
   double* T = sm;                      // [128*128]
   double* dg = T + MK_NB * TLD;        // [128]
   double* xd = dg + MK_NB;             // [128]
-  double* Pb = xd + MK_NB;             // [4][16 * SLD]
+  double* Sb = xd + MK_NB;             // [7][16 * SLD]
   __shared__ int badf;
   int s, h;
   if (!pick_pair(slist, scount, blockIdx.x, h0, hc, &s, &h)) return;
+  MK_TSTAMP(0);
   const int tid = threadIdx.x;
   const int sh = s * ms.q + h;
   const int slot = 1 - ms.cur[sh];
@@ -381,8 +444,9 @@ __global__ __launch_bounds__(256) void k_chol_diag(MatSet ms, const int* __restr
   }
   if (tid == 0) badf = 0;
   __syncthreads();
+  MK_TSTAMP(40);
   bool bad = false;
-  factor_invert_tile(T, dg, xd, Pb, ns - base, quad_c + sh, &bad);
+  factor_invert_tile(T, dg, xd, Sb, ns - base, quad_c + sh, &bad);
   if (bad) badf = 1;
   __syncthreads();
   if (tid < 64) {
@@ -395,6 +459,7 @@ __global__ __launch_bounds__(256) void k_chol_diag(MatSet ms, const int* __restr
       if (badf) info[sh] = 1;
     }
   }
+  MK_TSTAMP(41);
   double* W = winv_slot(ms, sh, slot, k);
   for (int e = tid; e < MK_NB * MK_NB; e += 256) {
     const int r = e & 127, c = e >> 7;
@@ -408,6 +473,7 @@ __global__ __launch_bounds__(256) void k_chol_diag(MatSet ms, const int* __restr
       W[r + c * MK_NB] = 0.0;
     }
   }
+  MK_TSTAMP(42);
 }
 
 // ---------------------------------------------------------------- inverse (W = L^-1, persistent)
