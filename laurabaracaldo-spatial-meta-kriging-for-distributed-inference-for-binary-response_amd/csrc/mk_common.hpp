@@ -24,6 +24,8 @@
 
 namespace mk {
 
+typedef double d2 __attribute__((ext_vector_type(2)));   // 16-byte fp64 pair loads/stores
+
 struct Key { uint32_t k0, k1; };
 
 __host__ __device__ inline Key make_key(uint64_t seed, uint32_t subset) {

@@ -262,6 +262,13 @@ __global__ __launch_bounds__(256) void k_dirty_list(Model md, int force, int* li
 // W panels are streamed twice per sweep (dots, update) -> n^2 doubles per subset per sweep.
 #define SW_B 64
 #define SW_T MK_SW_T
+// Lane i's value (i wave-uniform) as a scalar: two v_readlane_b32.
+__device__ inline double rlane_u(double v, int i) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), i);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), i);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
 __global__ __launch_bounds__(SW_T) void k_sweep(Model md, MatSet ms, int iter) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int q = md.q;
@@ -301,22 +308,30 @@ __global__ __launch_bounds__(SW_T) void k_sweep(Model md, MatSet ms, int iter) {
   for (int b0 = 0; b0 < ns + SW_B; b0 += SW_B) {
     const int nb = min(SW_B, ns - b0);
     // ---- (a) z += W[:, prev block] delta'_prev   (rows >= p0)
+    // Thread t owns the row pair p0 + 2t, p0 + 2t + 1 (16-byte loads; p0 is even, ld even) and
+    // issues the 16 column loads of a group before using them: unconditional loads (clamped
+    // column; W is finite everywhere), the short-block tail masked by a zero coefficient.
     if (pnb > 0 && any_acc) {
       for (int h = 0; h < q; ++h) {
-        const double* Wp = ms.W + ((long)s * q + h) * (ld * ld) + (long)p0 * ld;
-        const double* da = dacc + h * SW_B;
-        double* zh = z + (long)h * md.n_pad;
-        for (int r = p0 + tid; r < ns; r += SW_T) {
-          double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
-          int k = 0;
-          for (; k + 4 <= pnb; k += 4) {
-            v0 += Wp[r + (long)k * ld] * da[k];
-            v1 += Wp[r + (long)(k + 1) * ld] * da[k + 1];
-            v2 += Wp[r + (long)(k + 2) * ld] * da[k + 2];
-            v3 += Wp[r + (long)(k + 3) * ld] * da[k + 3];
+        for (int r = p0 + 2 * tid; r < ns; r += 2 * SW_T) {
+          const double* Wp = ms.W + ((long)s * q + h) * (ld * ld) + (long)p0 * ld + r;
+          const double* da = dacc + h * SW_B;
+          double* zh = z + (long)h * md.n_pad;
+          d2 v = {0.0, 0.0};
+          for (int k0 = 0; k0 < pnb; k0 += 16) {
+            d2 wv2[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u)
+              wv2[u] = *reinterpret_cast<const d2*>(Wp + (long)min(k0 + u, pnb - 1) * ld);
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+              const double c = (k0 + u < pnb) ? da[k0 + u] : 0.0;
+              v.x = fma(wv2[u].x, c, v.x);
+              v.y = fma(wv2[u].y, c, v.y);
+            }
           }
-          for (; k < pnb; ++k) v0 += Wp[r + (long)k * ld] * da[k];
-          zh[r] += (v0 + v1) + (v2 + v3);
+          zh[r] += v.x;
+          if (r + 1 < ns) zh[r + 1] += v.y;
         }
       }
     }
@@ -335,42 +350,70 @@ __global__ __launch_bounds__(SW_T) void k_sweep(Model md, MatSet ms, int iter) {
       if (tid < SW_B) dacc[h * SW_B + tid] = 0.0;
       const double* Wb = ms.W + ((long)s * q + h) * (ld * ld) + (long)b0 * ld;
       const double* zh = z + (long)h * md.n_pad;
+      // one wave per column; lane l reads rows b0 + 2l + 128j (16-byte loads, 8 in flight,
+      // clamped inside the padded column and masked by a select)
+      const int nj = (ns - b0 + 127) / 128;
       for (int i = wv; i < nb; i += SW_T / 64) {
         const double* col = Wb + (long)i * ld;
-        double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-        int r = b0 + lane;
-        for (; r + 192 < ns; r += 256) {
-          a0 += col[r] * zh[r];
-          a1 += col[r + 64] * zh[r + 64];
-          a2 += col[r + 128] * zh[r + 128];
-          a3 += col[r + 192] * zh[r + 192];
+        double a0 = 0.0, a1 = 0.0;
+        for (int j0 = 0; j0 < nj; j0 += 8) {
+          d2 wv2[8], zv2[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const int rc = min(b0 + 2 * lane + 128 * (j0 + u), md.n_pad - 2);
+            wv2[u] = *reinterpret_cast<const d2*>(col + rc);
+            zv2[u] = *reinterpret_cast<const d2*>(zh + rc);
+          }
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const int rr = b0 + 2 * lane + 128 * (j0 + u);
+            a0 = (rr < ns) ? fma(wv2[u].x, zv2[u].x, a0) : a0;
+            a1 = (rr + 1 < ns) ? fma(wv2[u].y, zv2[u].y, a1) : a1;
+          }
         }
-        for (; r < ns; r += 64) a0 += col[r] * zh[r];
-        double acc = (a0 + a1) + (a2 + a3);
+        double acc = a0 + a1;
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
         if (lane == 0) gb[h * SW_B + i] = acc;
       }
     }
     __syncthreads();
-    // ---- (c) sequential Metropolis steps of the block (wave 0)
+    // ---- (c) sequential Metropolis steps of the block (wave 0).  Lane i preloads site b0+i's
+    // proposal, likelihood difference, accept draw and Q diagonal; each step reads them (and
+    // the carried g) by readlane with the uniform step index: no memory round trip per step.
     if (wv == 0) {
-      double gl[MK_QMAX];
-      for (int h = 0; h < q; ++h) gl[h] = (lane < nb) ? gb[h * SW_B + lane] : 0.0;
+      // (register arrays indexed by compile-time constants only: loops over MK_QMAX, q-guarded)
+      double gl[MK_QMAX], qd[MK_QMAX], dlr[MK_QMAX], dllr[MK_QMAX], lgr[MK_QMAX];
+      const int ls = (lane < nb) ? lane : 0;
+#pragma unroll
+      for (int h = 0; h < MK_QMAX; ++h) {
+        gl[h] = (h < q && lane < nb) ? gb[h * SW_B + lane] : 0.0;
+        qd[h] = (h < q) ? Qb[h * SW_B * SW_B + ls * SW_B + ls] : 0.0;
+        const int k = (b0 + ls) * q + h;
+        dlr[h] = (h < q) ? dl[k] : 0.0;
+        dllr[h] = (h < q) ? dll[k] : 0.0;
+        lgr[h] = (h < q) ? lgu[k] : 0.0;
+      }
       int anyl = 0;
       for (int i = 0; i < nb; ++i) {
-        for (int a = 0; a < q; ++a) {
+#pragma unroll
+        for (int a = 0; a < MK_QMAX; ++a) {
+          if (a >= q) break;
           const int k = (b0 + i) * q + a;
-          const double d = dl[k];
+          const double d = rlane_u(dlr[a], i);
           double c = 0.0, dd = 0.0;
-          for (int h = 0; h < q; ++h) {
+#pragma unroll
+          for (int h = 0; h < MK_QMAX; ++h) {
+            if (h >= q) break;
             const double aih = Ai[h + a * q];
-            c += aih * __shfl(gl[h], i, 64);
-            dd += (aih * aih) * Qb[h * SW_B * SW_B + i * SW_B + i];
+            c += aih * rlane_u(gl[h], i);
+            dd += (aih * aih) * rlane_u(qd[h], i);
           }
-          const double ratio = dll[k] - (d * c + 0.5 * d * d * dd);
-          if (lgu[k] <= ratio) {
-            for (int h = 0; h < q; ++h) {
+          const double ratio = rlane_u(dllr[a], i) - (d * c + 0.5 * d * d * dd);
+          if (rlane_u(lgr[a], i) <= ratio) {
+#pragma unroll
+            for (int h = 0; h < MK_QMAX; ++h) {
+              if (h >= q) break;
               const double coef = d * Ai[h + a * q];
               gl[h] = gl[h] + coef * Qb[h * SW_B * SW_B + i * SW_B + lane];
               if (lane == 0) dacc[h * SW_B + i] += coef;
