@@ -68,6 +68,13 @@ def test_replay_cfg3_subset_size(mk):
     _check(dev, refs)
 
 
+def test_replay_subset_beyond_2048_sites(mk):
+    """n_s = 2200 (18 tiles): the sweep's row-pair pass wraps (more rows than 2 x its 1024
+    threads) and the diagonal-tile kernel runs past 16 pivots; replayed against the oracle."""
+    dev, refs = _run_both(mk, 2200, 1, 0, n_test=16, n_batch=2, batch_length=2, burn_in=3, S=1)
+    _check(dev, refs)
+
+
 def test_quantiles_bit_exact_on_device_samples(mk):
     dev, _ = _run_both(mk, 130, 1, 0, n_batch=4, batch_length=5, burn_in=3)
     for s in range(len(dev["samples"])):
