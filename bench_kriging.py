@@ -11,7 +11,7 @@ measured rates plus the extrapolation to the full configuration.  Unit of work: 
 triangular X = W P^T costs n_s^2 * n_test (W lower-triangular n_s x n_s); the per-run Cholesky +
 inverse (2 n_s^3 / 3) and the draws (2 n_s per draw) are counted too.
 
-  python bench_kriging.py [--subsets 8] [--n-test 1000000] [--kept 6] [--tile 65536]
+  python bench_kriging.py [--subsets 32] [--n-test 1000000] [--kept 6] [--tile 65536]
 """
 import argparse
 import importlib
@@ -30,7 +30,7 @@ FP64_PEAK_TFLOPS = 78.6
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--subsets", type=int, default=8)
+    ap.add_argument("--subsets", type=int, default=32)   # the per-GPU share of K = 250 on 8 GPUs
     ap.add_argument("--n-sub", type=int, default=2000)
     ap.add_argument("--n-test", type=int, default=1_000_000)
     ap.add_argument("--kept", type=int, default=6)

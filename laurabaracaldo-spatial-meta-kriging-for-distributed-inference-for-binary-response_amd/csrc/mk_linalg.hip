@@ -69,14 +69,22 @@ __device__ inline CandGen make_gen(const Model& md, int s, int h, int which, int
   return g;
 }
 
-// XCD-aware block -> (subset, tile) map: subsets s with s % 8 == x are served by blocks
-// b with b % 8 == x (blocks are dealt round-robin over the 8 XCDs), so a subset's tiles
-// share one L2 and its shared panel is fetched once.  Speed only; any placement is correct.
+// XCD-aware block -> (entry, tile) map.  Blocks are dealt round-robin over the 8 XCDs
+// (block b runs on XCD b % 8); the S*T work items are cut into 8 contiguous chunks and XCD x
+// takes chunk x in order, so the tiles of one entry (subset) run on one XCD and share its L2
+// (its shared panel is fetched once), and every XCD gets an equal share however few entries
+// are active (a short list of changed subsets no longer leaves XCDs idle).  S is the number of
+// ACTIVE entries; the grid (xcd_grid of the maximum) covers any S up to that maximum.  Speed
+// only; any placement is correct.
 __device__ inline bool xcd_map(int S, int T, int* s, int* t) {
+  const int W = S * T, C = (W + 7) >> 3;
   const int x = blockIdx.x & 7, j = blockIdx.x >> 3;
-  *s = x + 8 * (j / T);
-  *t = j % T;
-  return *s < S;
+  if (j >= C) return false;
+  const int w = x * C + j;
+  if (w >= W) return false;
+  *s = w / T;
+  *t = w % T;
+  return true;
 }
 __host__ inline int xcd_grid(int S, int T) { return 8 * ((S + 7) / 8) * T; }
 
@@ -85,6 +93,10 @@ __host__ inline int xcd_grid(int S, int T) { return 8 * ((S + 7) / 8) * T; }
 // slower on cfg3 (+3.5 ms of exp work at 2 waves/SIMD vs 1.7 ms for this pass).
 // Optional subset list (tiled kriging refactors only the subsets whose (phi, nu) changed):
 // entry e -> subset slist[e] for e < *scount; slist == nullptr: every subset.
+// Number of active (subset, outcome) entries of a launch over hc outcomes (list-aware).
+__device__ inline int active_pairs(const int* slist, const int* scount, int S, int hc) {
+  return (slist ? *scount : S) * hc;
+}
 __device__ inline bool pick_subset(const int* slist, const int* scount, int* s) {
   if (!slist) return true;
   if (*s >= *scount) return false;
@@ -119,7 +131,7 @@ __global__ __launch_bounds__(256) void k_cov_candidate(Model md, MatSet ms, int 
                                                        const int* slist, const int* scount) {
   const int ntiles = ms.nt * (ms.nt + 1) / 2;
   int e, t, s, h;
-  if (!xcd_map(md.S * hc, ntiles, &e, &t) || !pick_pair(slist, scount, e, h0, hc, &s, &h)) return;
+  if (!xcd_map(active_pairs(slist, scount, md.S, hc), ntiles, &e, &t) || !pick_pair(slist, scount, e, h0, hc, &s, &h)) return;
   int ti = 0;
   while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
   const int tj = t - ti * (ti + 1) / 2;
@@ -153,7 +165,7 @@ __global__ __launch_bounds__(256, 2) void k_chol_update(MatSet ms, int S, int h0
   extern __shared__ __attribute__((aligned(16))) double lds[];   // GD_LDS_BYTES (two DMA stages)
   const int ntk = ms.nt - k;
   int e, t, s, h;
-  if (!xcd_map(S * hc, ntk, &e, &t) || !pick_pair(slist, scount, e, h0, hc, &s, &h)) return;
+  if (!xcd_map(active_pairs(slist, scount, S, hc), ntk, &e, &t) || !pick_pair(slist, scount, e, h0, hc, &s, &h)) return;
   const int i = k + t;
   const int sh = s * ms.q + h;
   double* M = mat_slot(ms, sh, 1 - ms.cur[sh]);
@@ -171,7 +183,7 @@ __global__ __launch_bounds__(256, 2) void k_chol_trsm(MatSet ms, int S, int h0, 
   extern __shared__ __attribute__((aligned(16))) double lds[];   // MK_GD_LDS_BYTES
   const int ntk = ms.nt - k - 1;
   int e, t, s, h;
-  if (!xcd_map(S * hc, ntk, &e, &t) || !pick_pair(slist, scount, e, h0, hc, &s, &h)) return;
+  if (!xcd_map(active_pairs(slist, scount, S, hc), ntk, &e, &t) || !pick_pair(slist, scount, e, h0, hc, &s, &h)) return;
   const int i = k + 1 + t;
   const int sh = s * ms.q + h;
   const int slot = 1 - ms.cur[sh];
