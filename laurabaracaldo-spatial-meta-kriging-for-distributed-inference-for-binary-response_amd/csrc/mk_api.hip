@@ -1097,7 +1097,7 @@ extern "C" int mk_correlation_batched(const double* coords, int32_t S, int32_t n
   HIPCHK(hipMemcpy(dc, coords, (size_t)S * 2 * n * 8, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(dphi, phi, (size_t)S * 8, hipMemcpyHostToDevice));
   if (nu) HIPCHK(hipMemcpy(dnu, nu, (size_t)S * 8, hipMemcpyHostToDevice));
-  hipLaunchKernelGGL(k_corr_plain, dim3(2048), dim3(256), 0, 0, dc, S, n, dphi, dnu, cov_model, dr);
+  hipLaunchKernelGGL(k_corr_plain, dim3(64, S), dim3(256), 0, 0, dc, S, n, dphi, dnu, cov_model, dr);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpy(R_out, dr, (size_t)S * n * n * 8, hipMemcpyDeviceToHost));
   return 0;

@@ -13,6 +13,7 @@ namespace mk {
 
 #define MK_COV_EXPONENTIAL 0
 #define MK_COV_MATERN 1
+#define MK_BK_NTAB 64   // terms of the reciprocal tables (CorrFn::fill_tables)
 
 __host__ __device__ inline void temme_gammas(double mu, double* gam1, double* gam2, double* gampl, double* gammi) {
   // 1/Gamma(1+z) = sum_k a_k z^(k-1)  (A&S 6.1.34)
@@ -46,11 +47,17 @@ struct CorrFn {
   double phi, nu;
   int nl;
   double mu, mu2, gam1, gam2, gampl, gammi, fact, a1, den;
+  // Optional reciprocal tables of the candidate's mu (LDS, filled by fill_tables): the series
+  // and CF2 divisions by i - mu, i + mu, i^2 - mu^2, i and a_i = -a1 - i(i-1) become
+  // multiplications for i < MK_BK_NTAB (a division costs ~10 dependent fp64 ops; these loops
+  // dominate the Matern candidate kernel).  nullptr: divide (host, parity entry points).
+  const double* tab;
 
   __host__ __device__ void init(double phi_, double nu_, int model_) {
     model = model_;
     phi = phi_;
     nu = nu_;
+    tab = nullptr;
     if (model != MK_COV_MATERN) return;
     const double EPS = 1e-16, PI = 3.141592653589793;
     nl = (int)(nu + 0.5);
@@ -61,6 +68,18 @@ struct CorrFn {
     temme_gammas(mu, &gam1, &gam2, &gampl, &gammi);
     a1 = 0.25 - mu2;
     den = pow(2.0, nu - 1.0) * tgamma(nu);
+  }
+
+  // tab[j * MK_BK_NTAB + i]: j = 0 1/(i-mu), 1 1/(i+mu), 2 1/(i^2-mu^2), 3 1/i, 4 1/a_i
+  __host__ __device__ void fill_tables(double* t, int tid, int nthreads) const {
+    for (int i = tid; i < MK_BK_NTAB; i += nthreads) {
+      const double di = (double)i;
+      t[i] = 1.0 / (di - mu);
+      t[MK_BK_NTAB + i] = 1.0 / (di + mu);
+      t[2 * MK_BK_NTAB + i] = 1.0 / (di * di - mu2);
+      t[3 * MK_BK_NTAB + i] = (i > 0) ? 1.0 / di : 0.0;
+      t[4 * MK_BK_NTAB + i] = 1.0 / (-a1 - di * (di - 1.0));
+    }
   }
 
   // K_nu(x), x > 0 (Temme series for x < 2, Steed's CF2 above, forward recurrence in nu).
@@ -80,7 +99,21 @@ struct CorrFn {
       double c = 1.0;
       d = x2 * x2;
       double sum1 = p;
-      for (int i = 1; i <= 500; ++i) {
+      int i = 1;
+      bool done = false;
+      if (tab) {
+        for (; i < MK_BK_NTAB; ++i) {
+          ff = (i * ff + p + q) * tab[2 * MK_BK_NTAB + i];
+          c *= d * tab[3 * MK_BK_NTAB + i];
+          p *= tab[i];
+          q *= tab[MK_BK_NTAB + i];
+          const double del = c * ff;
+          sum += del;
+          sum1 += c * (p - i * ff);
+          if (fabs(del) < fabs(sum) * EPS) { done = true; break; }
+        }
+      }
+      for (; !done && i <= 500; ++i) {
         ff = (i * ff + p + q) / (i * (double)i - mu2);
         c *= d / i;
         p /= (i - mu);
@@ -97,7 +130,26 @@ struct CorrFn {
       double q1 = 0.0, q2 = 1.0;
       double q = a1, c = a1, a = -a1;
       double s = 1.0 + q * delh;
-      for (int i = 2; i <= 500; ++i) {
+      int i = 2;
+      bool done = false;
+      if (tab) {
+        for (; i < MK_BK_NTAB; ++i) {
+          a -= 2 * (i - 1);
+          c = -a * c * tab[3 * MK_BK_NTAB + i];
+          const double qnew = (q1 - b * q2) * tab[4 * MK_BK_NTAB + i];
+          q1 = q2;
+          q2 = qnew;
+          q += c * qnew;
+          b += 2.0;
+          d = 1.0 / (b + a * d);
+          delh = (b * d - 1.0) * delh;
+          h += delh;
+          const double dels = q * delh;
+          s += dels;
+          if (fabs(dels) < fabs(s) * EPS) { done = true; break; }
+        }
+      }
+      for (; !done && i <= 500; ++i) {
         a -= 2 * (i - 1);
         c = -a * c / i;
         const double qnew = (q1 - b * q2) / a;

@@ -136,7 +136,13 @@ __global__ __launch_bounds__(256) void k_cov_candidate(Model md, MatSet ms, int 
   while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
   const int tj = t - ti * (ti + 1) / 2;
   const int sh = s * md.q + h;
-  const CandGen g = make_gen(md, s, h, which, iter);
+  CandGen g = make_gen(md, s, h, which, iter);
+  if (MODEL == MK_COV_MATERN) {
+    __shared__ double btab[5 * MK_BK_NTAB];
+    g.rho.fill_tables(btab, threadIdx.x, 256);
+    __syncthreads();
+    g.rho.tab = btab;
+  }
   double* M = mat_slot(ms, sh, 1 - ms.cur[sh]);
   const long ld = ms.ld;
   // two rows per lane, 16-byte stores; the upper half of a diagonal tile is never read (the
@@ -644,6 +650,12 @@ __global__ __launch_bounds__(256) void k_pred_PT(Model md, const int* __restrict
   current_phi_nu(md, s, h, &phi, &nu);
   CorrFn rho;
   rho.init(phi, nu, md.cov_model);
+  __shared__ double btab[5 * MK_BK_NTAB];
+  if (md.cov_model == MK_COV_MATERN) {
+    rho.fill_tables(btab, threadIdx.x, 256);
+    __syncthreads();
+    rho.tab = btab;
+  }
   const double* cx = md.coords + (long)s * 2 * md.n_pad;
   const double ox = cx[k], oy = cx[md.n_pad + k];
   double* row = md.PT + ((long)sh * md.n_pad + k) * md.n_test_pad;
