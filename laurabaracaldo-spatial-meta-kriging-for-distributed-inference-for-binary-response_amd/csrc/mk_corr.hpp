@@ -15,7 +15,17 @@ namespace mk {
 #define MK_COV_MATERN 1
 #define MK_BK_NTAB 64   // terms of the reciprocal tables (CorrFn::fill_tables)
 
-__host__ __device__ inline void temme_gammas(double mu, double* gam1, double* gam2, double* gampl, double* gammi) {
+// 1/y from the hardware reciprocal estimate and two Newton steps (within an ulp of 1.0/y;
+// ~5 dependent fp64 ops instead of the IEEE division sequence).
+__device__ inline double rcp_nr(double y) {
+  double r = __builtin_amdgcn_rcp(y);
+  double e = fma(-y, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-y, r, 1.0);
+  return fma(r, e, r);
+}
+
+__device__ inline void temme_gammas(double mu, double* gam1, double* gam2, double* gampl, double* gammi) {
   // 1/Gamma(1+z) = sum_k a_k z^(k-1)  (A&S 6.1.34)
   const double a[15] = {1.0, 0.5772156649015329, -0.6558780715202538, -0.0420026350340952,
                         0.1665386113822915, -0.0421977345555443, -0.0096219715278770, 0.0072189432466630,
@@ -53,7 +63,7 @@ struct CorrFn {
   // dominate the Matern candidate kernel).  nullptr: divide (host, parity entry points).
   const double* tab;
 
-  __host__ __device__ void init(double phi_, double nu_, int model_) {
+  __device__ void init(double phi_, double nu_, int model_) {
     model = model_;
     phi = phi_;
     nu = nu_;
@@ -71,7 +81,7 @@ struct CorrFn {
   }
 
   // tab[j * MK_BK_NTAB + i]: j = 0 1/(i-mu), 1 1/(i+mu), 2 1/(i^2-mu^2), 3 1/i, 4 1/a_i
-  __host__ __device__ void fill_tables(double* t, int tid, int nthreads) const {
+  __device__ void fill_tables(double* t, int tid, int nthreads) const {
     for (int i = tid; i < MK_BK_NTAB; i += nthreads) {
       const double di = (double)i;
       t[i] = 1.0 / (di - mu);
@@ -83,19 +93,20 @@ struct CorrFn {
   }
 
   // K_nu(x), x > 0 (Temme series for x < 2, Steed's CF2 above, forward recurrence in nu).
-  __host__ __device__ double bessel_k(double x) const {
-    const double EPS = 1e-16, PI = 3.141592653589793;
+  // lx = log(x).  sinh, cosh and exp of e = mu log(2/x) come from one expm1.
+  __device__ double bessel_k(double x, double lx) const {
+    const double EPS = 1e-16, PI = 3.141592653589793, LN2 = 0.6931471805599453;
     const double xi = 1.0 / x, xi2 = 2.0 * xi;
     double rkmu, rk1;
     if (x < 2.0) {
       const double x2 = 0.5 * x;
-      double d = -log(x2);
-      double e = mu * d;
-      const double fact2 = (fabs(e) < EPS) ? 1.0 : sinh(e) / e;
-      double ff = fact * (gam1 * cosh(e) + gam2 * fact2 * d);
+      double d = LN2 - lx;
+      const double e = mu * d;
+      const double em1 = expm1(e), E = em1 + 1.0, iE = 1.0 / E;
+      const double fact2 = (fabs(e) < EPS) ? 1.0 : 0.5 * em1 * (1.0 + iE) / e;   // sinh(e) / e
+      double ff = fact * (gam1 * (0.5 * (E + iE)) + gam2 * fact2 * d);
       double sum = ff;
-      e = exp(e);
-      double p = 0.5 * e / gampl, q = 0.5 / (e * gammi);
+      double p = 0.5 * E / gampl, q = 0.5 * iE / gammi;
       double c = 1.0;
       d = x2 * x2;
       double sum1 = p;
@@ -141,7 +152,7 @@ struct CorrFn {
           q2 = qnew;
           q += c * qnew;
           b += 2.0;
-          d = 1.0 / (b + a * d);
+          d = rcp_nr(b + a * d);
           delh = (b * d - 1.0) * delh;
           h += delh;
           const double dels = q * delh;
@@ -177,21 +188,22 @@ struct CorrFn {
   }
 
   // rho(d): exponential exp(-phi d); Matern (phi d)^nu / (2^(nu-1) Gamma(nu)) K_nu(phi d), 1 at d = 0
-  __host__ __device__ double operator()(double d) const {
+  __device__ double operator()(double d) const {
     if (model == MK_COV_EXPONENTIAL) return exp(-phi * d);
     const double x = d * phi;
     if (!(x > 0.0)) return 1.0;
-    return pow(x, nu) / den * bessel_k(x);
+    const double lx = log(x);
+    return exp(nu * lx) / den * bessel_k(x, lx);
   }
 };
 
-__host__ __device__ inline double correlation(double d, double phi, double nu, int model) {
+__device__ inline double correlation(double d, double phi, double nu, int model) {
   CorrFn f;
   f.init(phi, nu, model);
   return f(d);
 }
 
-__host__ __device__ inline double dist2d(double x0, double y0, double x1, double y1) {
+__device__ inline double dist2d(double x0, double y0, double x1, double y1) {
   const double dx = x0 - x1, dy = y0 - y1;
   return sqrt(dx * dx + dy * dy);
 }
