@@ -109,9 +109,12 @@ int32_t mk_session_iteration(const mk_session* s);
 /* Quantile summaries + optional sample copies (requires all iterations done
  * for parameters / w_predict). */
 int mk_session_outputs(mk_session* s, mk_outputs* out);
-/* Per-kernel timing (HIP events on the session stream) for the MFMA-bound
- * Cholesky panel update: launches, total ms, algorithmic flops.  Enabled by
- * mk_session_profile(s, 1) before mk_session_run. */
+/* Per-kernel timing (HIP events on the session stream): launches, total ms and
+ * algorithmic flops per kernel kind (0 Cholesky panel update, 1 diagonal tile,
+ * 2 panel trsm, 3 latent sweep, 4 R^-1 diagonal tiles, 5 whole iterations, 6
+ * inverse levels).  mk_session_profile(s, enable) before mk_session_run:
+ * enable 0 = off, 1 = every kind, otherwise a mask with bit (1 + kind) per kind
+ * bracketed (e.g. 2 << 0 = the panel update only; fewer events, less overhead). */
 int mk_session_profile(mk_session* s, int32_t enable);
 int mk_session_kernel_stats(const mk_session* s, int32_t which, int64_t* launches, double* total_ms, double* flops);
 void mk_session_destroy(mk_session* s);

@@ -150,6 +150,7 @@ struct mk_session {
   std::vector<int> n_part;
   std::vector<void*> allocs;
   bool prof = false;
+  uint32_t prof_kinds = ~0u;   // kernel kinds bracketed by events while prof (bit per KS_ kind)
   std::vector<Timed> pending;
   Stat stats[NKSTAT];
 
@@ -182,7 +183,7 @@ static hipEvent_t ev_new() {
 // Launch helper that optionally brackets a kernel with events on its stream.
 template <typename F>
 static void timed(mk_session* s, hipStream_t st, int which, double flops, F&& launch) {
-  if (!s->prof) {
+  if (!s->prof || !((s->prof_kinds >> which) & 1u)) {
     launch();
     return;
   }
@@ -658,6 +659,7 @@ extern "C" int32_t mk_session_iteration(const mk_session* s) { return s ? s->ite
 extern "C" int mk_session_profile(mk_session* s, int32_t enable) {
   if (!s) return set_err(MK_E_ARG, "null session");
   s->prof = enable != 0;
+  s->prof_kinds = (enable == 1) ? ~0u : ((uint32_t)enable >> 1);
   return 0;
 }
 

@@ -156,8 +156,18 @@ class Session:
     def iteration(self):
         return self._lib.mk_session_iteration(self._h)
 
-    def profile(self, on=True):
-        check(self._lib.mk_session_profile(self._h, 1 if on else 0))
+    def profile(self, on=True, kinds=None):
+        """Per-kernel HIP-event timing from the next run on: every kind, or only `kinds`
+        (KS_* constants; fewer events in the stream)."""
+        if not on:
+            v = 0
+        elif kinds is None:
+            v = 1
+        else:
+            v = 0
+            for k in kinds:
+                v |= 2 << int(k)
+        check(self._lib.mk_session_profile(self._h, v))
 
     def kernel_stats(self, which):
         n = ctypes.c_int64()
