@@ -126,6 +126,72 @@ __device__ inline double cand_value(const CandGen& g, int R, int C) {
   return (R == C && R != g.ns) ? 1.0 : 0.0;
 }
 
+// Matern candidate tile.  K_nu costs a Temme series (x < 2) or Steed's CF2 (x >= 2) of
+// data-dependent length; with lanes mapped to rows, nearly every wave holds both kinds and
+// pays for both.  Per 32-column chunk the elements are binned by branch (wave ballots + one
+// LDS atomic per wave and bin: order within a bin is arbitrary, every element's value is
+// not) and evaluated bin by bin, so waves run one branch; results go through LDS and leave
+// as the same 16-byte row-pair stores as the exponential path.
+#define MK_MT_COLS 32
+__device__ inline void matern_tile(const CandGen& g, double* M, long ld, int ti, int tj, double* buf,
+                                   unsigned short* idx, int* cnt) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  constexpr int CH = MK_NB * MK_MT_COLS;   // elements per chunk
+  for (int c0 = 0; c0 < MK_NB; c0 += MK_MT_COLS) {
+    if (tid < 2) cnt[tid] = 0;
+    __syncthreads();
+    for (int j = 0; j < CH / 256; ++j) {
+      const int e = tid + 256 * j;
+      const int r = e & (MK_NB - 1), cc = e >> 7;
+      const int R = ti * MK_NB + r, C = tj * MK_NB + c0 + cc;
+      const bool skip = (ti == tj) && ((R & ~1) + 1 < C);      // pair never stored (upper half)
+      int kind = 0;
+      double v = 0.0;
+      if (!skip) {
+        if (R < g.ns && C < g.ns && R != C) {
+          v = dist2d(g.cx[R], g.cy[R], g.cx[C], g.cy[C]);     // distance; rho applied below
+          const double x = v * g.rho.phi;
+          kind = (x > 0.0 && x < 2.0) ? 1 : 2;                // x == 0 goes with CF2's bin (rho = 1)
+        } else {
+          v = cand_value<MK_COV_MATERN>(g, R, C);             // diagonal, border row, padding
+        }
+      }
+      buf[e] = v;
+#pragma unroll
+      for (int b = 1; b <= 2; ++b) {
+        const unsigned long long m = __ballot(kind == b);
+        if (m) {
+          const int leader = __ffsll((long long)m) - 1;
+          int base = 0;
+          if (lane == leader) base = atomicAdd(&cnt[b - 1], __popcll(m));
+          base = __shfl(base, leader, 64);
+          if (kind == b) {
+            const int pos = base + __popcll(m & ((1ull << lane) - 1ull));
+            idx[(b == 1) ? pos : CH - 1 - pos] = (unsigned short)e;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    const int n1 = cnt[0], n = cnt[0] + cnt[1];
+    for (int p = tid; p < n; p += 256) {
+      const int e = (p < n1) ? idx[p] : idx[CH - 1 - (p - n1)];
+      buf[e] = g.rho(buf[e]);
+    }
+    __syncthreads();
+    const int r2 = 2 * lane;
+    for (int cc = tid >> 6; cc < MK_MT_COLS; cc += 4) {
+      const int R = ti * MK_NB + r2, C = tj * MK_NB + c0 + cc;
+      if (ti == tj && R + 1 < C) continue;
+      d2 v;
+      v.x = buf[cc * MK_NB + r2];
+      v.y = buf[cc * MK_NB + r2 + 1];
+      *reinterpret_cast<d2*>(M + R + (long)C * ld) = v;
+    }
+    __syncthreads();
+  }
+}
+
 template <int MODEL>
 __global__ __launch_bounds__(256) void k_cov_candidate(Model md, MatSet ms, int h0, int hc, int which, int iter,
                                                        const int* slist, const int* scount) {
@@ -137,14 +203,19 @@ __global__ __launch_bounds__(256) void k_cov_candidate(Model md, MatSet ms, int 
   const int tj = t - ti * (ti + 1) / 2;
   const int sh = s * md.q + h;
   CandGen g = make_gen(md, s, h, which, iter);
+  double* M = mat_slot(ms, sh, 1 - ms.cur[sh]);
+  const long ld = ms.ld;
   if (MODEL == MK_COV_MATERN) {
     __shared__ double btab[5 * MK_BK_NTAB];
+    __shared__ double buf[MK_NB * MK_MT_COLS];
+    __shared__ unsigned short idx[MK_NB * MK_MT_COLS];
+    __shared__ int cnt[2];
     g.rho.fill_tables(btab, threadIdx.x, 256);
     __syncthreads();
     g.rho.tab = btab;
+    matern_tile(g, M, ld, ti, tj, buf, idx, cnt);
+    return;
   }
-  double* M = mat_slot(ms, sh, 1 - ms.cur[sh]);
-  const long ld = ms.ld;
   // two rows per lane, 16-byte stores; the upper half of a diagonal tile is never read (the
   // factor kernels read lower tiles only) and is left unwritten
   const int R = ti * MK_NB + (threadIdx.x & 63) * 2;
