@@ -126,56 +126,82 @@ __device__ inline double cand_value(const CandGen& g, int R, int C) {
   return (R == C && R != g.ns) ? 1.0 : 0.0;
 }
 
-// Matern candidate tile.  K_nu costs a Temme series (x < 2) or Steed's CF2 (x >= 2) of
-// data-dependent length; with lanes mapped to rows, nearly every wave holds both kinds and
-// pays for both.  Per 32-column chunk the elements are binned by branch (wave ballots + one
-// LDS atomic per wave and bin: order within a bin is arbitrary, every element's value is
-// not) and evaluated bin by bin, so waves run one branch; results go through LDS and leave
-// as the same 16-byte row-pair stores as the exponential path.
+// Matern candidate tile.  K_nu costs a Temme series (x < 2) or Steed's CF2 (x >= 2) whose
+// length depends on x; with lanes mapped to rows nearly every wave holds both branches and a
+// spread of x, and pays for both branches at their longest.  Per 32-column chunk the elements
+// are binned by x (branch and convergence length: bins of MK_MT_EDGES), counted and placed with
+// wave ballots + one LDS atomic per wave and bin (order within a bin is arbitrary, every
+// element's value is not), and evaluated bin after bin, so a wave runs one branch over similar
+// lengths; results go through LDS and leave as the exponential path's 16-byte row-pair stores.
 #define MK_MT_COLS 32
+#define MK_MT_NBIN 10
+__device__ inline int matern_bin(double x) {
+  // 1..4: series (x < 2), 5..10: CF2
+  return (x < 1.0) ? ((x < 0.5) ? 1 : 2) : (x < 2.0) ? ((x < 1.5) ? 3 : 4)
+       : (x < 3.0) ? ((x < 2.5) ? 5 : 6) : (x < 5.0) ? ((x < 4.0) ? 7 : 8) : ((x < 7.0) ? 9 : 10);
+}
 __device__ inline void matern_tile(const CandGen& g, double* M, long ld, int ti, int tj, double* buf,
-                                   unsigned short* idx, int* cnt) {
+                                   unsigned short* idx, unsigned char* binb, int* cnt) {
   const int tid = threadIdx.x, lane = tid & 63;
   constexpr int CH = MK_NB * MK_MT_COLS;   // elements per chunk
+  constexpr int NJ = CH / 256;
+  int* cur = cnt + MK_MT_NBIN + 1;         // placement cursors
   for (int c0 = 0; c0 < MK_NB; c0 += MK_MT_COLS) {
-    if (tid < 2) cnt[tid] = 0;
+    if (tid <= MK_MT_NBIN) cnt[tid] = 0;
     __syncthreads();
-    for (int j = 0; j < CH / 256; ++j) {
+#pragma unroll 1
+    for (int j = 0; j < NJ; ++j) {
       const int e = tid + 256 * j;
       const int r = e & (MK_NB - 1), cc = e >> 7;
       const int R = ti * MK_NB + r, C = tj * MK_NB + c0 + cc;
       const bool skip = (ti == tj) && ((R & ~1) + 1 < C);      // pair never stored (upper half)
-      int kind = 0;
+      int bin = 0;
       double v = 0.0;
       if (!skip) {
         if (R < g.ns && C < g.ns && R != C) {
           v = dist2d(g.cx[R], g.cy[R], g.cx[C], g.cy[C]);     // distance; rho applied below
-          const double x = v * g.rho.phi;
-          kind = (x > 0.0 && x < 2.0) ? 1 : 2;                // x == 0 goes with CF2's bin (rho = 1)
+          bin = matern_bin(v * g.rho.phi);
         } else {
           v = cand_value<MK_COV_MATERN>(g, R, C);             // diagonal, border row, padding
         }
       }
       buf[e] = v;
+      binb[e] = (unsigned char)bin;
 #pragma unroll
-      for (int b = 1; b <= 2; ++b) {
-        const unsigned long long m = __ballot(kind == b);
+      for (int bb = 1; bb <= MK_MT_NBIN; ++bb) {
+        const unsigned long long m = __ballot(bin == bb);
+        if (m && lane == __ffsll((long long)m) - 1) atomicAdd(&cnt[bb], __popcll(m));
+      }
+    }
+    __syncthreads();
+    if (tid == 0) {                           // bin offsets (exclusive scan), cursors
+      int o = 0;
+      for (int bb = 1; bb <= MK_MT_NBIN; ++bb) {
+        cur[bb] = o;
+        o += cnt[bb];
+      }
+      cnt[0] = o;                             // total
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (int j = 0; j < NJ; ++j) {
+      const int e = tid + 256 * j, bin = binb[e];
+#pragma unroll
+      for (int bb = 1; bb <= MK_MT_NBIN; ++bb) {
+        const unsigned long long m = __ballot(bin == bb);
         if (m) {
           const int leader = __ffsll((long long)m) - 1;
           int base = 0;
-          if (lane == leader) base = atomicAdd(&cnt[b - 1], __popcll(m));
+          if (lane == leader) base = atomicAdd(&cur[bb], __popcll(m));
           base = __shfl(base, leader, 64);
-          if (kind == b) {
-            const int pos = base + __popcll(m & ((1ull << lane) - 1ull));
-            idx[(b == 1) ? pos : CH - 1 - pos] = (unsigned short)e;
-          }
+          if (bin == bb) idx[base + __popcll(m & ((1ull << lane) - 1ull))] = (unsigned short)e;
         }
       }
     }
     __syncthreads();
-    const int n1 = cnt[0], n = cnt[0] + cnt[1];
+    const int n = cnt[0];
     for (int p = tid; p < n; p += 256) {
-      const int e = (p < n1) ? idx[p] : idx[CH - 1 - (p - n1)];
+      const int e = idx[p];
       buf[e] = g.rho(buf[e]);
     }
     __syncthreads();
@@ -209,11 +235,12 @@ __global__ __launch_bounds__(256) void k_cov_candidate(Model md, MatSet ms, int 
     __shared__ double btab[5 * MK_BK_NTAB];
     __shared__ double buf[MK_NB * MK_MT_COLS];
     __shared__ unsigned short idx[MK_NB * MK_MT_COLS];
-    __shared__ int cnt[2];
+    __shared__ int cnt[2 * (MK_MT_NBIN + 1)];
+    __shared__ unsigned char binb[MK_NB * MK_MT_COLS];
     g.rho.fill_tables(btab, threadIdx.x, 256);
     __syncthreads();
     g.rho.tab = btab;
-    matern_tile(g, M, ld, ti, tj, buf, idx, cnt);
+    matern_tile(g, M, ld, ti, tj, buf, idx, binb, cnt);
     return;
   }
   // two rows per lane, 16-byte stores; the upper half of a diagonal tile is never read (the
