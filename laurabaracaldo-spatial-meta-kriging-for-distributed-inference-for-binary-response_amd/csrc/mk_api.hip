@@ -700,6 +700,8 @@ static int predict_tiled(mk_session* s, mk_outputs* o) {
     Model mt = md;
     mt.n_test = Tc;
     mt.t_off = t0;
+    mt.ntt = (Tc + MK_NB - 1) / MK_NB;   // a short last tile: only its valid 128-site column blocks
+                                          // (strides stay those of the full tile, n_test_pad)
     for (int k = 0; k < n_kept; ++k) {
       mt.theta = md.kth + (long)k * S * md.n_theta;
       mt.z = md.kz + (long)k * S * q * md.n_pad;

@@ -757,7 +757,8 @@ __global__ __launch_bounds__(256) void k_pred_PT(Model md, const int* __restrict
   const double* cx = md.coords + (long)s * 2 * md.n_pad;
   const double ox = cx[k], oy = cx[md.n_pad + k];
   double* row = md.PT + ((long)sh * md.n_pad + k) * md.n_test_pad;
-  for (int t = threadIdx.x; t < md.n_test_pad; t += 256) {
+  const int tlim = md.ntt * MK_NB;   // the column blocks k_pred_var reads (all of n_test_pad when fused)
+  for (int t = threadIdx.x; t < tlim; t += 256) {
     double v = 0.0;
     if (k < ns && t < md.n_test)
       v = rho(dist2d(ox, oy, md.coords_test[t], md.coords_test[md.n_test_pad + t]));
