@@ -708,24 +708,55 @@ __global__ __launch_bounds__(256) void k_take_border(Model md, MatSet ms, const 
 }
 
 // Z_{h,c} = W_h u_c for every subset, outcome h and c (q > 1, start of the A phase).
+// Thread = row r of W_h (coalesced column walks); the q vectors u_c are staged in LDS per
+// 512-column chunk (one broadcast read per column instead of q global loads), the column loop
+// is unrolled by 8 with its loads issued together, and the q accumulators are indexed at
+// compile time (loops over MK_QMAX, q-guarded: no scratch).
+#define MK_ZCH 512
 __global__ __launch_bounds__(256) void k_trmv_Z(Model md, MatSet ms) {
+  __shared__ double us[MK_QMAX][MK_ZCH];
   const int per = (md.n_pad + 255) / 256;
   const int sh = blockIdx.x / per;
   const int s = sh / md.q, h = sh % md.q;
   const int ns = md.n_s[s];
-  const int r = (blockIdx.x % per) * 256 + threadIdx.x;
-  if (r >= md.n_pad) return;
-  const double* Wm = wmat(ms, sh);
+  const int r0 = (blockIdx.x % per) * 256, r = r0 + threadIdx.x;
+  const double* Wm = wmat(ms, sh) + r;
   const long ld = ms.ld;
   const int q = md.q;
+  const double* u = md.u + (long)s * q * md.n_pad;
   double acc[MK_QMAX] = {0.0, 0.0, 0.0, 0.0};
-  const int jmax = min(r + 1, ns);
-  for (int j = 0; j < jmax; ++j) {
-    const double wv = Wm[r + (long)j * ld];
-    for (int c = 0; c < q; ++c) acc[c] += wv * md.u[((long)s * q + c) * md.n_pad + j];
+  const int jmax = (r < md.n_pad) ? min(r + 1, ns) : 0;            // this row's columns
+  const int jblk = min(min(r0 + 256, md.n_pad), ns);              // the block's widest row
+  for (int j0 = 0; j0 < jblk; j0 += MK_ZCH) {
+    __syncthreads();
+    for (int t = threadIdx.x; t < q * MK_ZCH; t += 256) {
+      const int c = t / MK_ZCH, jj = t % MK_ZCH;
+      us[c][jj] = (j0 + jj < ns) ? u[(long)c * md.n_pad + j0 + jj] : 0.0;
+    }
+    __syncthreads();
+    const int jend = min(MK_ZCH, jmax - j0);   // <= 0: nothing left for this row
+    int jj = 0;
+    for (; jj + 8 <= jend; jj += 8) {
+      double wv[8];
+#pragma unroll
+      for (int v = 0; v < 8; ++v) wv[v] = Wm[(long)(j0 + jj + v) * ld];
+#pragma unroll
+      for (int v = 0; v < 8; ++v)
+#pragma unroll
+        for (int c = 0; c < MK_QMAX; ++c)
+          if (c < q) acc[c] += wv[v] * us[c][jj + v];
+    }
+    for (; jj < jend; ++jj) {
+      const double wv = Wm[(long)(j0 + jj) * ld];
+#pragma unroll
+      for (int c = 0; c < MK_QMAX; ++c)
+        if (c < q) acc[c] += wv * us[c][jj];
+    }
   }
-  for (int c = 0; c < q; ++c)
-    md.Z[(((long)s * q + h) * q + c) * md.n_pad + r] = (r < ns) ? acc[c] : 0.0;
+  if (r >= md.n_pad) return;
+#pragma unroll
+  for (int c = 0; c < MK_QMAX; ++c)
+    if (c < q) md.Z[(((long)s * q + h) * q + c) * md.n_pad + r] = (r < ns) ? acc[c] : 0.0;
 }
 
 // ---------------------------------------------------------------- kriging (kept iterations)
