@@ -17,6 +17,7 @@ def _run_both(mk, n, q, cov, n_test=12, n_batch=3, batch_length=4, burn_in=7, se
     sizes = list(sizes) if sizes is not None else [n] * S
     off = np.concatenate([[0], np.cumsum(sizes)])
     d = mk.synthetic.generate(int(off[-1]), q=q, n_test=n_test, seed=seed + q, cov_model=cov)
+    ct = d["coords_test"] if n_test else None
     p = 2 * q
     kw = dict(n_batch=n_batch, batch_length=batch_length, burn_in=burn_in, seed=seed)
     cfg = mk.SamplerConfig(q, p, beta_starting=np.zeros(p), beta_tuning=np.full(p, 0.05),
@@ -27,11 +28,11 @@ def _run_both(mk, n, q, cov, n_test=12, n_batch=3, batch_length=4, burn_in=7, se
         sl = slice(off[s], off[s] + m)
         rows = slice(off[s] * q, (off[s] + m) * q)
         subs.append(dict(coords=d["coords"][sl], y=d["y"][rows], weights=np.ones(m * q), x=d["x"][rows]))
-    with mk.Session(subs, cfg, coords_test=d["coords_test"], subset_base=subset_base, record_w=True) as ses:
+    with mk.Session(subs, cfg, coords_test=ct, subset_base=subset_base, record_w=True) as ses:
         ses.run(cfg.n_samples)
         dev = ses.outputs(samples=True, w_samples=True, w_pred_samples=True, acceptance=True)
     refs = [om.fit_subset(sb["coords"], sb["y"], sb["weights"], sb["x"], ocfg, subset=subset_base + s,
-                          coords_test=d["coords_test"], record_w=True) for s, sb in enumerate(subs)]
+                          coords_test=ct, record_w=True) for s, sb in enumerate(subs)]
     return dev, refs
 
 
@@ -39,9 +40,12 @@ def _check(dev, refs):
     for s, ref in enumerate(refs):
         np.testing.assert_allclose(dev["samples"][s], ref["samples"], rtol=0, atol=TOL)
         np.testing.assert_allclose(dev["w_samples"][s].T, ref["w_samples"], rtol=0, atol=TOL)
-        np.testing.assert_allclose(dev["w_pred_samples"][s].T, ref["w_pred"], rtol=0, atol=TOL)
         np.testing.assert_allclose(dev["parameters"][s], ref["param_q"], rtol=0, atol=TOL)
-        np.testing.assert_allclose(dev["w_predict"][s], ref["w_q"], rtol=0, atol=TOL)
+        if "w_q" in ref:
+            np.testing.assert_allclose(dev["w_pred_samples"][s].T, ref["w_pred"], rtol=0, atol=TOL)
+            np.testing.assert_allclose(dev["w_predict"][s], ref["w_q"], rtol=0, atol=TOL)
+        else:
+            assert "w_predict" not in dev and "w_pred_samples" not in dev
         # accept rates of beta / A / phi per batch
         o_w = dev["acceptance"][s].shape[1] - 1
         np.testing.assert_allclose(dev["acceptance"][s][:, :o_w], ref["accept"][:, :o_w], atol=1e-12)
@@ -58,6 +62,22 @@ def test_replay_ragged_subsets(mk, sizes, q):
     """Subsets of different sizes in one session (the reference's last subset takes the
     remainder, MK.R:18); sizes straddle the 128-tile boundary with the bordered row."""
     dev, refs = _run_both(mk, None, q, 0, sizes=sizes)
+    _check(dev, refs)
+
+
+@pytest.mark.parametrize("sizes,q,cov", [([1, 2, 3], 1, 0), ([1, 2], 2, 0), ([1, 3], 1, 1)])
+def test_replay_tiny_subsets(mk, sizes, q, cov):
+    """Subsets of one to three sites (the remainder subset of MK.R:18 can be that small): the
+    bordered row sits in the first tile next to the identity padding."""
+    dev, refs = _run_both(mk, None, q, cov, sizes=sizes, n_test=5)
+    _check(dev, refs)
+
+
+@pytest.mark.parametrize("q", [1, 2])
+def test_replay_without_test_sites(mk, q):
+    """No kriging sites (coords.test empty): the fit alone replays the oracle and no
+    w.predict output is produced."""
+    dev, refs = _run_both(mk, None, q, 0, sizes=[70, 45], n_test=0)
     _check(dev, refs)
 
 
