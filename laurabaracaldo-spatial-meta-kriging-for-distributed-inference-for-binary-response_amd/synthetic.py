@@ -16,10 +16,12 @@ i*q + a); x (n*q, p) block-diagonal; coords (n, 2).  Test sites: coords_test
 """
 import numpy as np
 
-TRUE_BETA = {1: [1.0, -1.0], 2: [1.0, -1.0, -1.0, 1.0], 3: [1.0, -1.0, -1.0, 1.0, 0.5, -0.5]}
+TRUE_BETA = {1: [1.0, -1.0], 2: [1.0, -1.0, -1.0, 1.0], 3: [1.0, -1.0, -1.0, 1.0, 0.5, -0.5],
+             4: [1.0, -1.0, -1.0, 1.0, 0.5, -0.5, -0.5, 0.5]}   # q = 4: the library's maximum (MK_QMAX)
 TRUE_A = {1: [[1.0]],
           2: [[1.0, 0.0], [-0.5, 1.0]],
-          3: [[1.0, 0.0, 0.0], [-0.5, 1.0, 0.0], [0.25, 0.3, 0.8]]}
+          3: [[1.0, 0.0, 0.0], [-0.5, 1.0, 0.0], [0.25, 0.3, 0.8]],
+          4: [[1.0, 0.0, 0.0, 0.0], [-0.5, 1.0, 0.0, 0.0], [0.25, 0.3, 0.8, 0.0], [0.1, -0.2, 0.3, 0.7]]}
 
 
 def block_design(xcov, q):

@@ -51,7 +51,7 @@ def _check(dev, refs):
         np.testing.assert_allclose(dev["acceptance"][s][:, :o_w], ref["accept"][:, :o_w], atol=1e-12)
 
 
-@pytest.mark.parametrize("n,q,cov", [(150, 1, 0), (300, 1, 0), (64, 2, 0), (100, 1, 1), (40, 3, 0)])
+@pytest.mark.parametrize("n,q,cov", [(150, 1, 0), (300, 1, 0), (64, 2, 0), (100, 1, 1), (40, 3, 0), (48, 2, 1), (30, 4, 0)])
 def test_replay_matches_oracle(mk, n, q, cov):
     dev, refs = _run_both(mk, n, q, cov)
     _check(dev, refs)
