@@ -623,7 +623,9 @@ __global__ __launch_bounds__(256, 2) void k_inv_level(MatSet ms, const int* __re
   const int p = t / (sz * sz);
   t %= sz * sz;
   const int T0 = 2 * p * sz, B0 = T0 + sz;
-  const int i = B0 + t / sz, j = T0 + t % sz;
+  // consecutive work items share the operand whose K range is the same for all of them:
+  // phase 0 a column j (W_TT(j:B0, j)), phase 1 a row i (W_BB(i, B0:i+1))
+  const int i = B0 + (phase == 0 ? t % sz : t / sz), j = T0 + (phase == 0 ? t / sz : t % sz);
   if (i >= ms.nt) return;
   const int sh = list[e];
   const int cur = ms.cur[sh];
