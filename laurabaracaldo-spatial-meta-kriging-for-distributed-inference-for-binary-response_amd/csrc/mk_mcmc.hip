@@ -509,14 +509,26 @@ __global__ __launch_bounds__(256) void k_pred_draw(Model md, int iter, int kidx)
     const long sh = (long)s * q + h;
     const double* xk = md.XK + (sh * md.n_test_pad + t) * md.n_pad;
     const double* zh = md.z + sh * md.n_pad;
-    double a0 = 0.0, a1 = 0.0;
-    int i = lane;
-    for (; i + 64 < ns; i += 128) {
-      a0 += xk[i] * zh[i];
-      a1 += xk[i + 64] * zh[i + 64];
+    // 16-byte row pairs, 4 pairs per lane in flight (unconditional loads clamped inside the
+    // n_pad rows, rows >= n_s masked by selects); fixed summation order
+    const int np2 = md.n_pad >> 1;
+    double a[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int base = 0; base < ns; base += 512) {
+      d2 xv[4], zv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int pr = min((base >> 1) + u * 64 + lane, np2 - 1);
+        xv[u] = *reinterpret_cast<const d2*>(xk + 2 * pr);
+        zv[u] = *reinterpret_cast<const d2*>(zh + 2 * pr);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int r = base + 2 * (u * 64 + lane);
+        a[u] += (r < ns) ? xv[u].x * zv[u].x : 0.0;
+        a[u] += (r + 1 < ns) ? xv[u].y * zv[u].y : 0.0;
+      }
     }
-    for (; i < ns; i += 64) a0 += xk[i] * zh[i];
-    double acc = a0 + a1;
+    double acc = (a[0] + a[1]) + (a[2] + a[3]);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
     mean[h] = acc;
