@@ -287,7 +287,7 @@ static void launch_pred_refresh(mk_session* s, Group& g) {
   Model& md = g.md;
   if (md.n_test <= 0) return;
   const int nt = s->nt, max_entries = g.S * s->q;
-  hipLaunchKernelGGL(k_pred_PT, dim3(max_entries * md.n_pad), dim3(256), 0, g.stream, md, g.d_plist, g.d_pcount);
+  hipLaunchKernelGGL(pred_PT_kernel(md.cov_model), dim3(max_entries * md.n_pad), dim3(256), 0, g.stream, md, g.d_plist, g.d_pcount);
   hipLaunchKernelGGL(k_pred_var, dim3(xcd_grid_h(max_entries, nt * md.ntt)), dim3(256), MK_GD_LDS_BYTES, g.stream, md, g.ms,
                      g.d_plist, g.d_pcount);
   hipLaunchKernelGGL(k_pred_var_reduce, dim3(max_entries * (md.n_test_pad / 256)), dim3(256), 0, g.stream, md, nt,

@@ -22,7 +22,12 @@ __global__ void k_lauum(MatSet ms, const int* n_s, const int* list, const int* c
 __global__ void k_qblocks(MatSet ms, const int* n_s, const int* list, const int* count);
 __global__ void k_take_border(Model md, MatSet ms, const int* list, const int* count);
 __global__ void k_trmv_Z(Model md, MatSet ms);
+template <int MODEL>
 __global__ void k_pred_PT(Model md, const int* list, const int* count);
+typedef void (*PredPTKernel)(Model, const int*, const int*);
+inline PredPTKernel pred_PT_kernel(int model) {
+  return model == MK_COV_EXPONENTIAL ? k_pred_PT<MK_COV_EXPONENTIAL> : k_pred_PT<MK_COV_MATERN>;
+}
 __global__ void k_pred_var(Model md, MatSet ms, const int* list, const int* count);
 __global__ void k_pred_var_reduce(Model md, int nt, const int* list, const int* count);
 // mk_mcmc.hip

@@ -769,6 +769,8 @@ __device__ inline void current_phi_nu(const Model& md, int s, int h, double* phi
 }
 
 // P^T[k][t] = rho(|obs_k - test_t|) for the listed pairs (zero outside the valid block).
+// MODEL = MK_COV_EXPONENTIAL: exp(-phi d) inline, as in cand_value (bit-identical to CorrFn).
+template <int MODEL>
 __global__ __launch_bounds__(256) void k_pred_PT(Model md, const int* __restrict__ list, const int* __restrict__ count) {
   const int per = md.n_pad;   // one block per observation row
   const int e = blockIdx.x / per;
@@ -782,7 +784,7 @@ __global__ __launch_bounds__(256) void k_pred_PT(Model md, const int* __restrict
   CorrFn rho;
   rho.init(phi, nu, md.cov_model);
   __shared__ double btab[5 * MK_BK_NTAB];
-  if (md.cov_model == MK_COV_MATERN) {
+  if (MODEL == MK_COV_MATERN) {
     rho.fill_tables(btab, threadIdx.x, 256);
     __syncthreads();
     rho.tab = btab;
@@ -793,11 +795,15 @@ __global__ __launch_bounds__(256) void k_pred_PT(Model md, const int* __restrict
   const int tlim = md.ntt * MK_NB;   // the column blocks k_pred_var reads (all of n_test_pad when fused)
   for (int t = threadIdx.x; t < tlim; t += 256) {
     double v = 0.0;
-    if (k < ns && t < md.n_test)
-      v = rho(dist2d(ox, oy, md.coords_test[t], md.coords_test[md.n_test_pad + t]));
+    if (k < ns && t < md.n_test) {
+      const double d = dist2d(ox, oy, md.coords_test[t], md.coords_test[md.n_test_pad + t]);
+      v = (MODEL == MK_COV_EXPONENTIAL) ? exp(-rho.phi * d) : rho(d);
+    }
     row[t] = v;
   }
 }
+template __global__ void k_pred_PT<MK_COV_EXPONENTIAL>(Model, const int*, const int*);
+template __global__ void k_pred_PT<MK_COV_MATERN>(Model, const int*, const int*);
 
 // X = W P^T (row tile i, test tile tb), stored column-major by test site (XK[t][row]);
 // partial column sums of squares over valid rows -> s_part[sh][i][t].
