@@ -167,7 +167,9 @@ int mk_partition_r(int32_t n, int32_t n_core, int32_t seed, int32_t* n_part, int
 int mk_r_sample(int32_t seed, int32_t n, int32_t size, int32_t* out);
 
 /* ---- exposed kernels for parity tests ---- */
-/* R_k = correlation(coords_k) (n x n column-major) for S point sets of n sites. */
+/* R_k = correlation(coords_k) (n x n column-major) for S point sets of n sites, computed by
+ * the sampler's own candidate kernel (k_cov_candidate: exponential, or Matern with the binned
+ * Temme/CF2 Bessel-K evaluation) -- the covariance-assembly arithmetic the chains use. */
 int mk_correlation_batched(const double* coords, int32_t S, int32_t n, const double* phi, const double* nu,
                            int32_t cov_model, double* R_out, int32_t device);
 /* Cholesky (lower) + log-determinant (+ optional inverse) of S SPD n x n matrices. */

@@ -1091,17 +1091,60 @@ extern "C" int mk_glm_binomial(const double* y, const double* weights, const dou
 extern "C" int mk_correlation_batched(const double* coords, int32_t S, int32_t n, const double* phi, const double* nu,
                                       int32_t cov_model, double* R_out, int32_t device) {
   if (!coords || !phi || !R_out || S < 1 || n < 1) return set_err(MK_E_ARG, "bad correlation arguments");
+  if (cov_model != MK_COV_EXPONENTIAL && cov_model != MK_COV_MATERN) return set_err(MK_E_ARG, "bad cov_model");
+  if (cov_model == MK_COV_MATERN && !nu) return set_err(MK_E_ARG, "matern needs nu");
+  for (int s = 0; s < S; ++s)
+    if (!(phi[s] > 0.0) || (nu && cov_model == MK_COV_MATERN && !(nu[s] > 0.0)))
+      return set_err(MK_E_ARG, "phi and nu must be > 0");
   HIPCHK(hipSetDevice(device));
+  // The sampler's own candidate kernel (k_cov_candidate, which = 2: the current theta) on a
+  // one-outcome model per point set: theta = 0 with Unif(0, 2 phi) / Unif(0, 2 nu) supports gives
+  // exactly phi and nu (logitInv(0, 0, b) = b - b/2).  The border row is u = 0.
+  const int n_pad = round_up(n + 1, MK_NB), nt = n_pad / MK_NB;
+  const bool matern = cov_model == MK_COV_MATERN;
+  const int n_theta = matern ? 3 : 2;
   DevBufs b;
-  double* dc = b.get<double>((size_t)S * 2 * n);
-  double* dphi = b.get<double>(S);
+  double* dc = b.get<double>((size_t)S * 2 * n_pad);
+  double* dth = b.get<double>((size_t)S * n_theta);
+  double* du = b.get<double>((size_t)S * n_pad);
+  int* dns = b.get<int>(S);
+  int* dcur = b.get<int>(S);
+  double* dL = b.get<double>((size_t)S * 2 * n_pad * n_pad);
   double* dr = b.get<double>((size_t)S * n * n);
-  double* dnu = nu ? b.get<double>(S) : nullptr;
-  if (!dc || !dphi || !dr || (nu && !dnu)) return set_err(MK_E_NOMEM, "correlation alloc");
-  HIPCHK(hipMemcpy(dc, coords, (size_t)S * 2 * n * 8, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(dphi, phi, (size_t)S * 8, hipMemcpyHostToDevice));
-  if (nu) HIPCHK(hipMemcpy(dnu, nu, (size_t)S * 8, hipMemcpyHostToDevice));
-  hipLaunchKernelGGL(k_corr_plain, dim3(64, S), dim3(256), 0, 0, dc, S, n, dphi, dnu, cov_model, dr);
+  if (!dc || !dth || !du || !dns || !dcur || !dL || !dr) return set_err(MK_E_NOMEM, "correlation alloc");
+  std::vector<double> hc((size_t)S * 2 * n_pad, 0.0);
+  for (int s = 0; s < S; ++s)
+    for (int r = 0; r < n; ++r) {
+      hc[(size_t)s * 2 * n_pad + r] = coords[(size_t)s * 2 * n + r];
+      hc[(size_t)s * 2 * n_pad + n_pad + r] = coords[(size_t)s * 2 * n + n + r];
+    }
+  std::vector<int> hn(S, n);
+  HIPCHK(hipMemcpy(dc, hc.data(), hc.size() * 8, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dns, hn.data(), (size_t)S * 4, hipMemcpyHostToDevice));
+  HIPCHK(hipMemset(dth, 0, (size_t)S * n_theta * 8));
+  HIPCHK(hipMemset(du, 0, (size_t)S * n_pad * 8));
+  HIPCHK(hipMemset(dcur, 0, (size_t)S * 4));
+  MatSet ms{};
+  ms.L = dL; ms.cur = dcur; ms.ld = n_pad; ms.nt = nt; ms.q = 1;
+  const int ntri_tiles = nt * (nt + 1) / 2;
+  for (int s = 0; s < S; ++s) {
+    Model md{};
+    md.S = 1; md.q = 1; md.p = 0; md.n_pad = n_pad; md.Np = n_pad; md.nt = nt; md.ntri = 1; md.n_theta = n_theta;
+    md.cov_model = cov_model;
+    md.o_A = 0; md.o_phi = 1; md.o_nu = 2; md.o_w = n_theta; md.n_mh_max = n_theta;
+    md.phi_a[0] = 0.0; md.phi_b[0] = 2.0 * phi[s];
+    md.nu_a[0] = 0.0; md.nu_b[0] = matern ? 2.0 * nu[s] : 1.0;
+    md.n_s = dns + s;
+    md.coords = dc + (size_t)s * 2 * n_pad;
+    md.theta = dth + (size_t)s * n_theta;
+    md.u = du + (size_t)s * n_pad;
+    MatSet mv = ms;
+    mv.L = dL + (size_t)s * 2 * n_pad * n_pad;
+    mv.cur = dcur + s;
+    hipLaunchKernelGGL(cov_candidate_kernel(cov_model), dim3(xcd_grid_h(1, ntri_tiles)), dim3(256), 0, 0, md, mv, 0, 1,
+                       2, 0, nullptr, nullptr);
+  }
+  hipLaunchKernelGGL(k_extract_candidate, dim3(2048), dim3(256), 0, 0, ms, n, S, dr);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpy(R_out, dr, (size_t)S * n * n * 8, hipMemcpyDeviceToHost));
   return 0;

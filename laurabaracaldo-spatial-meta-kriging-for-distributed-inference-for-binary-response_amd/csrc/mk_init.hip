@@ -53,24 +53,17 @@ __global__ __launch_bounds__(256) void k_load_plain(MatSet ms, const double* A, 
   }
 }
 
-__global__ __launch_bounds__(256) void k_corr_plain(const double* coords, int S, int n, const double* phi,
-                                                    const double* nu, int model, double* out) {
-  // block (x, s): subset s, elements strided over the x blocks; the product kernels' CorrFn
-  // (Matern reciprocal tables in LDS included) so the parity test covers their arithmetic
-  const int s = blockIdx.y;
-  CorrFn rho;
-  rho.init(phi[s], nu ? nu[s] : 0.0, model);
-  __shared__ double btab[5 * MK_BK_NTAB];
-  if (model == MK_COV_MATERN) {
-    rho.fill_tables(btab, threadIdx.x, 256);
-    __syncthreads();
-    rho.tab = btab;
-  }
-  const long nn = (long)n * n;
-  const double* cs = coords + (long)s * 2 * n;
-  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < nn; e += (long)gridDim.x * 256) {
-    const int r = (int)(e % n), c = (int)(e / n);
-    out[(long)s * nn + e] = (r == c) ? 1.0 : rho(dist2d(cs[r], cs[n + r], cs[c], cs[n + c]));
+// Dense symmetric n x n image of the candidate slot's lower tiles (k_cov_candidate output: the
+// upper half of its diagonal tiles is never written), for the correlation parity entry point.
+__global__ __launch_bounds__(256) void k_extract_candidate(MatSet ms, int n, int S, double* out) {
+  const long tot = (long)S * n * n;
+  const long ld = ms.ld;
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < tot; e += (long)gridDim.x * 256) {
+    const int s = (int)(e / ((long)n * n));
+    const long rem = e % ((long)n * n);
+    const int r = (int)(rem % n), c = (int)(rem / n);
+    const double* M = mat_slot(ms, s, 1 - ms.cur[s]);
+    out[e] = (r >= c) ? M[r + (long)c * ld] : M[c + (long)r * ld];
   }
 }
 

@@ -59,7 +59,6 @@ __global__ void k_glm_pass(const double* yprop, const double* wt, const double* 
 __global__ void k_init_state(Model md);
 __global__ void k_theta_init(Model md, MatSet ms, int h0, int hc);
 __global__ void k_load_plain(MatSet ms, const double* A, int n, int S);
-__global__ void k_corr_plain(const double* coords, int S, int n, const double* phi, const double* nu, int model,
-                             double* out);
+__global__ void k_extract_candidate(MatSet ms, int n, int S, double* out);
 __global__ void k_extract_L(MatSet ms, int n, int S, double* L, int inv_slot_mode);
 }  // namespace mk

@@ -28,6 +28,28 @@ def test_correlation_matches_oracle(mk, model, nu):
         assert np.max(np.abs(R[s] - ref)) <= REL * np.max(np.abs(ref))
 
 
+@pytest.mark.parametrize("nu", [0.21, 0.5, 1.3, 1.9])
+def test_candidate_matern_cfg2_geometry_vs_scipy(mk, nu):
+    """configs[1] geometry (n_s = 1000, 8 tiles of 128): the sampler's binned Matern candidate
+    kernel (k_cov_candidate<MK_COV_MATERN>, series / CF2 branches and x-range bins) against
+    scipy.special.kv element by element, 1e-10 relative.  phi spans the
+    prior support (4, 12) so x = phi d covers both Bessel branches and every bin."""
+    import scipy.special as ssp
+    n = 1000
+    phi = np.array([4.0 + 1e-9, 7.3, 12.0 - 1e-9])
+    c = _coords(len(phi), n, 17)
+    R = mk.correlation_batched(c, phi, nu=np.full(len(phi), nu), cov_model="matern")
+    for s in range(len(phi)):
+        x = phi[s] * om.distance_matrix(c[s], c[s])
+        ref = np.ones_like(x)
+        m = x > 0
+        ref[m] = np.power(x[m], nu) / (2.0 ** (nu - 1.0) * ssp.gamma(nu)) * ssp.kv(nu, x[m])
+        np.fill_diagonal(ref, 1.0)
+        err = np.abs(R[s] - ref)
+        assert np.max(err / np.maximum(np.abs(ref), 1e-300)) <= REL, (s, np.max(err))
+        assert np.array_equal(R[s], R[s].T)
+
+
 @pytest.mark.parametrize("n", [1, 5, 127, 128, 200, 255, 256, 400, 700, 2000, 2047, 2048, 2049])
 def test_cholesky_logdet_inverse(mk, n):
     S = 3

@@ -88,6 +88,33 @@ def test_replay_cfg3_subset_size(mk):
     _check(dev, refs)
 
 
+def test_replay_cfg2_matern_geometry(mk):
+    """configs[1] geometry: Matern, q = 1, n_s = 1000 (50,000 sites / 50 subsets; 8 tiles of 128
+    with the bordered row in the last).  Every phi and nu candidate goes through the binned
+    Bessel candidate kernel; 6 iterations with accepted and rejected phi / nu steps
+    (MK.R:80-84 with cov.model = "matern")."""
+    dev, refs = _run_both(mk, 1000, 1, 1, n_test=40, n_batch=2, batch_length=3, burn_in=4, S=1)
+    acc = refs[0]["accept"]
+    assert 0 < acc[:, 4].sum() < 2 and 0 < acc[:, 3].sum() < 2     # nu, phi: some accepted, some not
+    _check(dev, refs)
+
+
+def test_replay_cfg4_lmc_geometry(mk):
+    """configs[3] geometry: q = 3 LMC, n_s = 2000 (100,000 sites / 50 subsets), N = 6000: multi-tile
+    factors for each outcome (16 tiles), k_trmv_Z staging four 512-column chunks, 64-site sweep
+    blocks with three outcomes per site, kriging of 3 x 40 test outcomes (MK.R:80 formula list)."""
+    dev, refs = _run_both(mk, 2000, 3, 0, n_test=40, n_batch=2, batch_length=3, burn_in=4, S=1)
+    _check(dev, refs)
+
+
+def test_replay_lmc_ragged_multi_tile(mk):
+    """q = 2 and q = 3 LMC with several multi-tile subsets of different sizes in one session
+    (ragged across the 128 and 512 boundaries)."""
+    for q, sizes in ((2, [700, 513]), (3, [600, 129])):
+        dev, refs = _run_both(mk, None, q, 0, sizes=sizes, n_test=24, n_batch=2, batch_length=2, burn_in=3)
+        _check(dev, refs)
+
+
 def test_replay_subset_beyond_2048_sites(mk):
     """n_s = 2200 (18 tiles): the sweep's row-pair pass wraps (more rows than 2 x its 1024
     threads) and the diagonal-tile kernel runs past 16 pivots; replayed against the oracle."""
