@@ -1,17 +1,22 @@
 #!/usr/bin/env python3
 """Benchmark: MCMC subset-iterations/s (all subsets, whole node) on BASELINE.json's
 headline configuration -- n=500,000 binary sites split into K=250 subsets of 2,000,
-exponential covariance, q=1, 1,000 kriging sites (configs[2]), on each GPU.
+exponential covariance, q=1, 1,000 kriging sites (configs[2]).
 
 A step = one spMvGLM amcmc iteration of EVERY subset (beta, A, phi MH with a fresh
 2000x2000 Cholesky per subset, inverse where phi moved, single-site w sweep) plus,
 on kept iterations, the fused spPredict kriging draw.  The timed window follows the
-reference schedule (MK.R:57-59, 85): 3 burn-in iterations per kept one.  Subsets are
-independent, so the default is weak scaling: every rank fits a configs[2]-sized shard
-(250 subsets of 2,000 sites; rank r's sites drawn with seed 20250114 + r, global subset
-indices 250r ...), i.e. a node job of n = N x 500k, K = N x 250; no data-path collective.
---scaling strong splits the one K=250 job over the ranks instead (contiguous blocks).  roofline.traffic is the PMC-measured HBM traffic of the same kernel from
-profiles/ (rocprofv3 --pmc passes of this command, gfx950 FETCH_SIZE x2 correction).
+reference schedule (MK.R:57-59, 85): 3 burn-in iterations per kept one.
+
+Multi-GPU (torch.distributed.run, one rank per GPU): by default the ONE configs[2] job is
+split over the ranks (strong scaling, balanced contiguous subset blocks: 250 over 8 GPUs is
+31-32 subsets each) -- the job BASELINE's metric is quoted on.  --scaling weak is opt-in:
+every rank then fits its own configs[2]-sized shard (a node job of n = N x 500k, K = N x 250)
+and the metric / config strings say so.  No data-path collective either way (the subsets are
+independent until the combine, which run_metakriging.py measures).
+
+roofline.traffic is the PMC-measured HBM traffic of the same kernel from profiles/
+(rocprofv3 --pmc passes of this command, gfx950 FETCH_SIZE x2 correction).
 
   python bench.py --gpus N --steps K --warmup W
 """
@@ -44,8 +49,9 @@ def parse():
     ap.add_argument("--cpu-iters", type=int, default=40)
     ap.add_argument("--no-kernel-events", action="store_true",
                     help="diagnostic: no per-kernel HIP events in the timed region (roofline fields then null)")
-    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
-                    help="weak: K subsets per rank (node job N*K); strong: one K-subset job split over ranks")
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="strong",
+                    help="strong (default): the one K-subset job split over the ranks; weak: K subsets per rank "
+                         "(node job N*K)")
     ap.add_argument("--streams", type=int, default=0, help="HIP streams per GPU for subset groups (0: library default)")
     return ap.parse_args()
 
@@ -89,6 +95,31 @@ def cpu_baseline(n_s, iters, workers):
                        f"thread per core; wall {wall:.1f}s incl. start-up")
 
 
+def host_cores():
+    """Cores this process may use: the affinity mask, capped by the job's CPU share when the
+    launcher states one (OMP_NUM_THREADS: 16 per GPU on the MI355X pool, whose nproc shows the
+    whole machine).  Returns the count used plus nproc, the affinity size and the CPU model."""
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = nproc
+    usable, note = aff, "all cores in the affinity mask"
+    share = os.environ.get("OMP_NUM_THREADS")
+    if share and share.isdigit() and 0 < int(share) < aff:
+        usable, note = int(share), f"the job's CPU share (OMP_NUM_THREADS={share}) of {aff} cores in the affinity mask"
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return dict(usable=max(1, usable), nproc=nproc, affinity=aff, model=model, note=note)
+
+
 def _pmc_traffic():
     """HBM bytes per k_chol_update launch from the committed rocprofv3 --pmc passes (or None)."""
     path = os.path.join(ROOT, "profiles", "pmc_chol_update.json")
@@ -108,8 +139,10 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline and a.cpu_iters > 0:
-        workers = max(1, min(16, os.cpu_count() or 1))
-        cpu = cpu_baseline(n // K, a.cpu_iters, workers)   # before any GPU initialisation (spawn pool)
+        host = host_cores()
+        cpu = cpu_baseline(n // K, a.cpu_iters, host["usable"])   # before any GPU initialisation (spawn pool)
+        cpu.update(host_nproc=host["nproc"], host_affinity=host["affinity"], cpu_model=host["model"],
+                   cores_note=host["note"])
 
     dist = None
     if world > 1:
@@ -123,13 +156,13 @@ def main():
     dseed = 20250114 + (rank if weak else 0)      # weak: each rank's 500k sites are its own draw
     d = mk.synthetic.generate(n, q=1, n_test=n_test, seed=dseed)
     n_part, idx = mk.partition(n, K, seed=dseed)
-    beta0, bt = mk.start_values(d["y"], d["x"], 1.0, 1)
+    beta0, bt = mk.start_values(d["y"], d["x"], 1.0, 1, device=local if world > 1 else 0)
     dmod = importlib.import_module(PKG + ".distributed")
     if weak:
         lo, hi, base, per = 0, K, rank * K, K     # global subset indices rank*K ... (distinct Philox streams)
     else:
         lo, hi = dmod.shard_range(K, world, rank)
-        base, per = lo, (K + world - 1) // world
+        base, per = lo, dmod.shard_capacity(K, world)
     W = max(1, a.warmup)
     # amcmc batches of 50 as MK.R:57-58; the timed window holds burn-in and kept (kriging)
     # iterations in the reference's 3:1 ratio (burn.in = 0.75 n.samples, MK.R:85)
@@ -179,8 +212,11 @@ def main():
     value = K_job * a.steps / elapsed
     avg_ms = st["ms"] / max(1, st["launches"])
     achieved = st["flops"] / (st["ms"] * 1e-3) / 1e12 if st["ms"] > 0 else 0.0
+    metric = "MCMC iters/sec (all subsets, whole node) + end-to-end wall-clock, n=500k K=250"
+    if weak and world > 1:   # a different (N x larger) job: not the headline metric
+        metric = f"MCMC iters/sec (all subsets, whole node), weak scaling: n={n * world // 1000}k K={K_job}"
     out = {
-        "metric": "MCMC iters/sec (all subsets, whole node) + end-to-end wall-clock, n=500k K=250",
+        "metric": metric,
         "value": value,
         "unit": "subset-iters/s",
         "n_gpus": world,

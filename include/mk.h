@@ -26,6 +26,8 @@ extern "C" {
 
 #define MK_COV_EXPONENTIAL 0
 #define MK_COV_MATERN 1
+#define MK_LINK_LOGIT 0    /* spMvGLM's binomial family (MK.R:80-84), logistic p(y=1) (MK.R:160) */
+#define MK_LINK_PROBIT 1   /* north-star extension: Phi link (no reference parity target)        */
 #define MK_N_LEVELS 200    /* quantile(x, probs = seq(0.005, 1, 0.005)), MK.R:88 */
 
 /* Subset data.  Replaces the globals Y*.part / X*.part / coords.part the
@@ -80,6 +82,7 @@ typedef struct mk_config {
                                    runs after the fit over tiles of this many test sites, so
                                    (q*n_test) x kept draws per subset never coexist (cfg5:
                                    1M sites); results are identical either way            */
+  int32_t link;                 /* MK_LINK_LOGIT (the reference) or MK_LINK_PROBIT              */
 } mk_config;
 
 /* Caller-allocated outputs; any pointer may be NULL to skip it.
@@ -118,6 +121,8 @@ int mk_session_outputs(mk_session* s, mk_outputs* out);
 int mk_session_profile(mk_session* s, int32_t enable);
 int mk_session_kernel_stats(const mk_session* s, int32_t which, int64_t* launches, double* total_ms, double* flops);
 void mk_session_destroy(mk_session* s);
+/* Sessions alive in this process (a failed mk_session_create leaves none behind). */
+int32_t mk_session_count(void);
 
 /* One-shot convenience: create, run n_batch*batch_length iterations, outputs, destroy. */
 int mk_fit_predict_batched(const mk_problem* prob, const mk_config* cfg, mk_outputs* out);
@@ -125,12 +130,23 @@ int mk_fit_predict_batched(const mk_problem* prob, const mk_config* cfg, mk_outp
 /* ---- combine (MK.R:123-133): out = (grid_1 + ... + grid_K) / K, sequential order ---- */
 int mk_combine(const double* grids, int32_t K, int64_t grid_len, double* out, int32_t device);
 
+/* The sum only (no 1/K): one shard's term of the combine, or the rank-ordered sum of shard terms. */
+int mk_combine_sum(const double* grids, int32_t K, int64_t grid_len, double* out, int32_t device);
+/* Device-resident form for the multi-GPU combine (grids already in HBM, e.g. RCCL receive
+ * buffers): d_out[e] = sum_k d_grids[k*grid_len + e] in k order, divided by K when mean != 0.
+ * stream: a hipStream_t (NULL = the legacy default stream); returns after the kernel is queued. */
+int mk_combine_device(const double* d_grids, int32_t K, int64_t grid_len, double* d_out, int32_t mean,
+                      int32_t device, void* stream);
+
 /* ---- combine extension (north star; not in the reference, which averages at MK.R:123-133):
  * per column, the Weiszfeld geometric median of the K subset quantile functions in the
  * Wasserstein-2 metric, started from the mean.  grids: K x (n_levels x n_cols) column-major;
  * out: n_levels x n_cols; iters (optional): [n_cols] iterations used.  n_levels <= 256. ---- */
 int mk_combine_median(const double* grids, int32_t K, int32_t n_levels, int64_t n_cols, int32_t max_iter,
                       double tol, double* out, int32_t* iters, int32_t device);
+/* Device-resident form (grids, out, iters in HBM; stream as in mk_combine_device). */
+int mk_combine_median_device(const double* d_grids, int32_t K, int32_t n_levels, int64_t n_cols, int32_t max_iter,
+                             double tol, double* d_out, int32_t* d_iters, int32_t device, void* stream);
 
 /* ---- post-combine steps (MK.R:136-165) ---- */
 typedef struct mk_summary {
@@ -147,6 +163,13 @@ typedef struct mk_summary {
 int mk_posterior_summary(const double* result, int32_t P, const double* result2, int64_t C,
                          const double* x_test, int32_t p, int32_t samplesize, uint64_t seed,
                          mk_summary* out, int32_t device);
+/* As mk_posterior_summary, plus: index (optional, [samplesize], 1-based) is sampleparIndex drawn
+ * by the caller -- the R glue passes R's own sample(seq(1, length(Xout), 1), samplesize,
+ * replace=TRUE) (MK.R:141), so the draws follow R's RNG stream; NULL draws it from Philox(seed).
+ * link: MK_LINK_LOGIT (MK.R:160) or MK_LINK_PROBIT for p.sample. */
+int mk_posterior_summary_ex(const double* result, int32_t P, const double* result2, int64_t C,
+                            const double* x_test, int32_t p, int32_t samplesize, uint64_t seed,
+                            const int32_t* index, int32_t link, mk_summary* out, int32_t device);
 
 /* ---- glm start values (MK.R:53-55), once on the full data: binomial-logit IRLS with
  * glm.fit's rules (mustart init, |dev - devold|/(|dev| + 0.1) < epsilon, maxit).
@@ -155,6 +178,11 @@ int mk_posterior_summary(const double* result, int32_t P, const double* result2,
 int mk_glm_binomial(const double* y, const double* weights, const double* x, int64_t n, int32_t p,
                     double epsilon, int32_t maxit, double* coef, double* vcov, int32_t* iters,
                     int32_t device);
+/* binomial(link = "probit") too: R's make.link("probit") (eta clamped to +-qnorm(eps) in linkinv,
+ * mu.eta = max(dnorm(eta), eps), linkfun = qnorm). link = MK_LINK_LOGIT is mk_glm_binomial. */
+int mk_glm_binomial_link(const double* y, const double* weights, const double* x, int64_t n, int32_t p,
+                         int32_t link, double epsilon, int32_t maxit, double* coef, double* vcov,
+                         int32_t* iters, int32_t device);
 
 /* ---- partition (MK.R:15-41) with R's own RNG stream, host side ----
  * After `set.seed(seed)` under R >= 3.6.0 defaults (Mersenne-Twister, Rejection sampling),
@@ -165,6 +193,9 @@ int mk_glm_binomial(const double* y, const double* weights, const double* x, int
 int mk_partition_r(int32_t n, int32_t n_core, int32_t seed, int32_t* n_part, int32_t* index_out);
 /* sample.int(n, size) (without replacement, 1-based) right after set.seed(seed). */
 int mk_r_sample(int32_t seed, int32_t n, int32_t size, int32_t* out);
+/* sample.int(n, size, replace = TRUE) right after set.seed(seed): MK.R:141's sampleparIndex
+ * (n = length(Xout) = 996) as an R session that set the seed just before would draw it. */
+int mk_r_sample_replace(int32_t seed, int32_t n, int32_t size, int32_t* out);
 
 /* ---- exposed kernels for parity tests ---- */
 /* R_k = correlation(coords_k) (n x n column-major) for S point sets of n sites, computed by
@@ -178,6 +209,8 @@ int mk_cholesky_batched(const double* A, int32_t S, int32_t n, double* L_out, do
 
 const char* mk_last_error(void);
 int mk_device_count(void);
+/* Free and total HBM of a device (hipMemGetInfo), e.g. to size shards or check for leaks. */
+int mk_device_memory(int32_t device, int64_t* free_bytes, int64_t* total_bytes);
 
 #ifdef __cplusplus
 }

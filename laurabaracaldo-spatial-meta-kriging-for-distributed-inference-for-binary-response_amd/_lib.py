@@ -18,6 +18,8 @@ MK_E_NOMEM = -3
 MK_E_NODEV = -4
 MK_COV_EXPONENTIAL = 0
 MK_COV_MATERN = 1
+MK_LINK_LOGIT = 0
+MK_LINK_PROBIT = 1
 N_LEVELS = 200
 
 _dp = ctypes.POINTER(ctypes.c_double)
@@ -47,7 +49,7 @@ class Config(ctypes.Structure):
                 ("phi_unif_a", _dp), ("phi_unif_b", _dp), ("nu_unif_a", _dp), ("nu_unif_b", _dp),
                 ("K_IW_df", ctypes.c_double), ("K_IW_S", _dp), ("seed", ctypes.c_uint64),
                 ("record_samples", ctypes.c_int32), ("record_w", ctypes.c_int32), ("device", ctypes.c_int32),
-                ("n_streams", ctypes.c_int32), ("predict_tile", ctypes.c_int32)]
+                ("n_streams", ctypes.c_int32), ("predict_tile", ctypes.c_int32), ("link", ctypes.c_int32)]
 
 
 class Outputs(ctypes.Structure):
@@ -69,13 +71,25 @@ EXPORTS = {
     "mk_session_kernel_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64),
                                                _dp, _dp]),
     "mk_session_destroy": (None, [ctypes.c_void_p]),
+    "mk_session_count": (ctypes.c_int32, []),
     "mk_fit_predict_batched": (ctypes.c_int, [ctypes.POINTER(Problem), ctypes.POINTER(Config), ctypes.POINTER(Outputs)]),
     "mk_combine": (ctypes.c_int, [_dp, ctypes.c_int32, ctypes.c_int64, _dp, ctypes.c_int32]),
+    "mk_combine_sum": (ctypes.c_int, [_dp, ctypes.c_int32, ctypes.c_int64, _dp, ctypes.c_int32]),
+    "mk_combine_median_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int64,
+                                                ctypes.c_int32, ctypes.c_double, ctypes.c_void_p, ctypes.c_void_p,
+                                                ctypes.c_int32, ctypes.c_void_p]),
+    "mk_combine_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_void_p,
+                                         ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p]),
     "mk_combine_median": (ctypes.c_int, [_dp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32,
                                          ctypes.c_double, _dp, _ip, ctypes.c_int32]),
     "mk_posterior_summary": (ctypes.c_int, [_dp, ctypes.c_int32, _dp, ctypes.c_int64, _dp, ctypes.c_int32,
                                             ctypes.c_int32, ctypes.c_uint64, ctypes.POINTER(Summary),
                                             ctypes.c_int32]),
+    "mk_posterior_summary_ex": (ctypes.c_int, [_dp, ctypes.c_int32, _dp, ctypes.c_int64, _dp, ctypes.c_int32,
+                                               ctypes.c_int32, ctypes.c_uint64, _ip, ctypes.c_int32,
+                                               ctypes.POINTER(Summary), ctypes.c_int32]),
+    "mk_glm_binomial_link": (ctypes.c_int, [_dp, _dp, _dp, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
+                                            ctypes.c_double, ctypes.c_int32, _dp, _dp, _ip, ctypes.c_int32]),
     "mk_glm_binomial": (ctypes.c_int, [_dp, _dp, _dp, ctypes.c_int64, ctypes.c_int32, ctypes.c_double,
                                        ctypes.c_int32, _dp, _dp, _ip, ctypes.c_int32]),
     "mk_correlation_batched": (ctypes.c_int, [_dp, ctypes.c_int32, ctypes.c_int32, _dp, _dp, ctypes.c_int32, _dp,
@@ -83,8 +97,10 @@ EXPORTS = {
     "mk_cholesky_batched": (ctypes.c_int, [_dp, ctypes.c_int32, ctypes.c_int32, _dp, _dp, _dp, ctypes.c_int32]),
     "mk_partition_r": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _ip, _ip]),
     "mk_r_sample": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _ip]),
+    "mk_r_sample_replace": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _ip]),
     "mk_last_error": (ctypes.c_char_p, []),
     "mk_device_count": (ctypes.c_int, []),
+    "mk_device_memory": (ctypes.c_int, [ctypes.c_int32, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
 }
 
 _LIB = None

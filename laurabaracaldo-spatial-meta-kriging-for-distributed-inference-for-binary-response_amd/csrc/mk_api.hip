@@ -9,10 +9,12 @@
 // is a pointer view into the shard's arrays (every array is [subset][...]); the chains do
 // not depend on the grouping (RNG streams are keyed by global subset index).
 #include <hip/hip_runtime.h>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <vector>
 #include "../../include/mk.h"
@@ -42,6 +44,15 @@ extern "C" int mk_device_count(void) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
   return n;
+}
+
+extern "C" int mk_device_memory(int32_t device, int64_t* free_bytes, int64_t* total_bytes) {
+  HIPCHK(hipSetDevice(device));
+  size_t f = 0, t = 0;
+  HIPCHK(hipMemGetInfo(&f, &t));
+  if (free_bytes) *free_bytes = (int64_t)f;
+  if (total_bytes) *total_bytes = (int64_t)t;
+  return 0;
 }
 
 namespace {
@@ -131,7 +142,10 @@ MatSet matset_view(const MatSet& m, int s0) {
 
 }  // namespace
 
+static std::atomic<int> g_live_sessions{0};
+
 struct mk_session {
+  mk_session() { g_live_sessions.fetch_add(1); }
   int device = 0;
   hipStream_t stream = nullptr;   // set-up, outputs and the one-group paths
   Model md{};
@@ -159,12 +173,16 @@ struct mk_session {
     void* ptr = nullptr;
     if (n == 0) n = 1;
     hipError_t e = hipMalloc(&ptr, n * sizeof(T));
-    if (e != hipSuccess) return set_err(MK_E_NOMEM, std::string("hipMalloc ") + std::to_string(n * sizeof(T)) + " B");
+    if (e != hipSuccess) {
+      (void)hipGetLastError();   // the failed malloc is sticky in hipGetLastError: clear it for later calls
+      return set_err(MK_E_NOMEM, std::string("hipMalloc ") + std::to_string(n * sizeof(T)) + " B");
+    }
     allocs.push_back(ptr);
     *p_ = (T*)ptr;
     return 0;
   }
   ~mk_session() {
+    g_live_sessions.fetch_sub(1);
     if (device >= 0) hipSetDevice(device);
     for (auto& t : pending) { hipEventDestroy(t.a); hipEventDestroy(t.b); }
     for (auto& g : groups)
@@ -226,16 +244,29 @@ static void launch_cholesky(mk_session* s, Group& g, int h0, int hc, const int* 
                             const int* scount = nullptr) {
   const int nt = s->nt, S = g.S, E = S * hc;
   const size_t diag_lds = (size_t)MK_DIAG_LDS_BYTES;
-  // valid extent (excludes padding) for the algorithmic flop count
-  const double nv = (double)s->n_part[g.s0] + 1.0;
+  // Algorithmic flops of a launch: every (subset, outcome) factor counted over its own valid
+  // extent n_s + 1 (the bordered row; padding excluded), so ragged subsets (MK.R:18: the last
+  // takes the remainder) are priced exactly.  With a subset list (tiled kriging replay) the
+  // active subsets live on the device: the count is then an upper bound (every subset).
+  auto panel_flops = [&](int k, bool trsm) {
+    double fl = 0.0;
+    for (int i = g.s0; i < g.s0 + S; ++i) {
+      const double nv = (double)s->n_part[i] + 1.0;
+      if (trsm) {
+        fl += 2.0 * std::fmax(0.0, nv - (k + 1) * MK_NB) * MK_NB * MK_NB;
+      } else {
+        const double rows = std::fmax(0.0, nv - k * MK_NB);
+        const double cols = std::fmin((double)MK_NB, rows);
+        const double kk = std::fmin((double)k * MK_NB, nv);
+        fl += 2.0 * rows * cols * kk;
+      }
+    }
+    return fl * hc;
+  };
   for (int k = 0; k < nt; ++k) {
     if (k > 0) {
-      // algorithmic flops: rows below panel start x panel cols x K, clipped to the valid extent
-      const double rows = std::fmax(0.0, nv - k * MK_NB);
-      const double cols = std::fmin((double)MK_NB, std::fmax(0.0, nv - k * MK_NB));
-      const double kk = std::fmin((double)k * MK_NB, nv);
-      const double fl = 2.0 * rows * cols * kk * E;
-      timed(s, g.stream, KS_CHOL_UPDATE, fl, [&] {
+      // rows below the panel start x panel columns x K, per factor
+      timed(s, g.stream, KS_CHOL_UPDATE, panel_flops(k, false), [&] {
         hipLaunchKernelGGL(k_chol_update, dim3(xcd_grid_h(E, nt - k)), dim3(256), MK_GD_LDS_BYTES, g.stream, g.ms, S, h0, hc, k,
                            slist, scount);
       });
@@ -245,9 +276,7 @@ static void launch_cholesky(mk_session* s, Group& g, int h0, int hc, const int* 
                          g.md.quad_c, g.md.info, slist, scount);
     });
     if (k < nt - 1) {
-      const double rows = std::fmax(0.0, nv - (k + 1) * MK_NB);
-      const double fl = 2.0 * rows * MK_NB * MK_NB * E;
-      timed(s, g.stream, KS_CHOL_TRSM, fl, [&] {
+      timed(s, g.stream, KS_CHOL_TRSM, panel_flops(k, true), [&] {
         hipLaunchKernelGGL(k_chol_trsm, dim3(xcd_grid_h(E, nt - k - 1)), dim3(256), MK_GD_LDS_BYTES, g.stream, g.ms, S, h0, hc, k,
                            slist, scount);
       });
@@ -341,6 +370,7 @@ static int check_cfg(const mk_problem* pr, const mk_config* c) {
   if (n_samples - c->burn_in + 1 > 2048) return set_err(MK_E_ARG, "at most 2048 kept samples supported");
   if (c->n_streams < 0 || c->n_streams > 8) return set_err(MK_E_ARG, "n_streams must be in [0, 8]");
   if (c->predict_tile < 0) return set_err(MK_E_ARG, "predict_tile must be >= 0");
+  if (c->link != MK_LINK_LOGIT && c->link != MK_LINK_PROBIT) return set_err(MK_E_ARG, "link must be logit or probit");
   if (!c->beta_starting || !c->beta_tuning || !c->phi_starting || !c->phi_tuning || !c->A_starting || !c->A_tuning ||
       !c->phi_unif_a || !c->phi_unif_b || !c->K_IW_S)
     return set_err(MK_E_ARG, "null starting/tuning/prior array");
@@ -403,10 +433,12 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return set_err(MK_E_NODEV, "no HIP device");
   if (c->device < 0 || c->device >= ndev) return set_err(MK_E_ARG, "bad device ordinal");
   HIPCHK(hipSetDevice(c->device));
-  mk_session* s = new mk_session();
+  // the guard owns the session until it is handed out: every early return (allocation failure,
+  // HIPCHK, argument error) frees the session and every device buffer allocated so far
+  std::unique_ptr<mk_session> hold(new mk_session());
+  mk_session* s = hold.get();
   s->device = c->device;
-  auto fail = [&](int code) { delete s; return code; };
-  if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) return fail(set_err(MK_E_HIP, "stream"));
+  if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) return set_err(MK_E_HIP, "stream");
 
   const int S = pr->n_subsets, q = pr->q, p = pr->p;
   s->S = S; s->q = q; s->p = p;
@@ -438,6 +470,7 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
   Model& md = s->md;
   md.S = S; md.q = q; md.p = p; md.n_pad = n_pad; md.Np = Np; md.nt = nt; md.ntri = ntri; md.n_theta = n_theta;
   md.cov_model = c->cov_model;
+  md.link = c->link;
   md.o_A = p; md.o_phi = p + ntri; md.o_nu = p + ntri + q; md.o_w = o_w; md.n_mh_max = n_mh_max;
   md.n_batch = c->n_batch; md.batch_length = c->batch_length; md.n_samples = n_samples;
   md.kept0 = kept0; md.n_kept = n_kept;
@@ -464,7 +497,7 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
       (rc = s->alloc(&d_y, (size_t)S * Np)) || (rc = s->alloc(&d_wt, (size_t)S * Np)) ||
       (rc = s->alloc(&d_X, (size_t)S * p * Np)) || (rc = s->alloc(&d_ct, (size_t)2 * n_test_pad)) ||
       (rc = s->alloc(&s->d_ct_all, (size_t)2 * s->n_test_pad_all)))
-    return fail(rc);
+    return rc;
   md.n_s = d_ns; md.coords = d_coords; md.y = d_y; md.wt = d_wt; md.X = d_X; md.coords_test = d_ct;
   if ((rc = s->alloc(&md.beta, (size_t)S * p)) || (rc = s->alloc(&md.theta, (size_t)S * n_theta)) ||
       (rc = s->alloc(&md.w, (size_t)S * Np)) || (rc = s->alloc(&md.eta, (size_t)S * Np)) ||
@@ -478,19 +511,19 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
       (rc = s->alloc(&md.sw_dll, (size_t)S * Np)) || (rc = s->alloc(&md.sw_logu, (size_t)S * Np)) ||
       (rc = s->alloc(&md.sw_acc, (size_t)S * Np)) || (rc = s->alloc(&md.samples, (size_t)S * n_samples * P)) ||
       (rc = s->alloc(&md.acc_hist, (size_t)S * c->n_batch * (o_w + 1))))
-    return fail(rc);
-  if (s->record_w && (rc = s->alloc(&md.w_samples, (size_t)S * n_samples * Np))) return fail(rc);
+    return rc;
+  if (s->record_w && (rc = s->alloc(&md.w_samples, (size_t)S * n_samples * Np))) return rc;
   if (s->tiled && ((rc = s->alloc(&md.kz, (size_t)n_kept * S * q * n_pad)) ||
                    (rc = s->alloc(&md.kth, (size_t)n_kept * S * n_theta)) ||
                    (rc = s->alloc(&md.kA, (size_t)n_kept * S * q * q)) ||
                    (rc = s->alloc(&s->d_slist, (size_t)q * S)) || (rc = s->alloc(&s->d_scount, (size_t)q))))
-    return fail(rc);
+    return rc;
   if ((rc = s->alloc(&md.s_pred, (size_t)S * q * n_test_pad)) ||
       (rc = s->alloc(&md.s_part, (size_t)S * q * nt * n_test_pad)) ||
       (n_test > 0 && (rc = s->alloc(&md.PT, (size_t)S * q * n_pad * n_test_pad))) ||
       (n_test > 0 && (rc = s->alloc(&md.XK, (size_t)S * q * n_pad * n_test_pad))) ||
       (rc = s->alloc(&md.w_pred, (size_t)S * n_kept * q * std::max(n_test, 1))))
-    return fail(rc);
+    return rc;
   MatSet& ms = s->ms;
   ms.ld = n_pad; ms.nt = nt; ms.q = q;
   if ((rc = s->alloc(&ms.L, (size_t)S * q * 2 * n_pad * n_pad)) ||
@@ -498,8 +531,8 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
       (rc = s->alloc(&ms.W, (size_t)S * q * n_pad * n_pad)) ||
       (rc = s->alloc(&ms.QB, (size_t)S * q * nt * MK_NB * MK_NB)) || (rc = s->alloc(&ms.cur, (size_t)S * q)) ||
       (rc = s->alloc(&s->d_probs, MK_N_LEVELS)))
-    return fail(rc);
-  if ((rc = setup_groups(s, c->n_streams > 0 ? c->n_streams : 1))) return fail(rc);
+    return rc;
+  if ((rc = setup_groups(s, c->n_streams > 0 ? c->n_streams : 1))) return rc;
 
   // ---------------- host staging (R layout -> padded device layout)
   std::vector<double> hc((size_t)S * 2 * n_pad, 0.0), hy((size_t)S * Np, 0.0), hw((size_t)S * Np, 0.0),
@@ -549,7 +582,7 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
     for (int j = 0; j < q; ++j)
       for (int i = j; i < q; ++i, ++k) {
         const double a = c->A_starting[k];
-        if (i == j && !(a > 0.0)) { delete s; return set_err(MK_E_ARG, "A starting diagonal must be > 0"); }
+        if (i == j && !(a > 0.0)) { return set_err(MK_E_ARG, "A starting diagonal must be > 0"); }
         th0[k] = (i == j) ? std::log(a) : a;
         A0[i + j * q] = a;
       }
@@ -558,7 +591,7 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
       th0[ntri + h] = std::log((ph - md.phi_a[h]) / (md.phi_b[h] - ph));
       if (s->matern) {
         const double nv = c->nu_starting[h];
-        if (!(md.nu_a[h] < nv && nv < md.nu_b[h])) { delete s; return set_err(MK_E_ARG, "nu starting value outside nu.Unif support"); }
+        if (!(md.nu_a[h] < nv && nv < md.nu_b[h])) { return set_err(MK_E_ARG, "nu starting value outside nu.Unif support"); }
         th0[ntri + q + h] = std::log((nv - md.nu_a[h]) / (md.nu_b[h] - nv));
       }
     }
@@ -570,7 +603,7 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
         Ai0[r + cc * q] = sum / A0[r + r * q];
       }
     for (int j = 0; j < p; ++j) {
-      if (!(c->beta_tuning[j] > 0.0)) { delete s; return set_err(MK_E_ARG, "beta tuning must be > 0"); }
+      if (!(c->beta_tuning[j] > 0.0)) { return set_err(MK_E_ARG, "beta tuning must be > 0"); }
       tune0[j] = std::log(std::sqrt(c->beta_tuning[j]));
     }
     for (int k2 = 0; k2 < ntri; ++k2) tune0[p + k2] = std::log(std::sqrt(c->A_tuning[k2]));
@@ -613,7 +646,7 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
   }
   HIPCHK(hipFuncSetAttribute((const void*)k_chol_diag, hipFuncAttributeMaxDynamicSharedMemorySize,
                              MK_DIAG_LDS_BYTES));
-  if (!set_gemm_lds()) return fail(set_err(MK_E_HIP, "gemm lds attribute"));
+  if (!set_gemm_lds()) return set_err(MK_E_HIP, "gemm lds attribute");
   HIPCHK(hipFuncSetAttribute((const void*)k_sweep, hipFuncAttributeMaxDynamicSharedMemorySize,
                              q * (64 * 64 + 2 * 64) * 8));
 
@@ -631,7 +664,7 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
   HIPCHK(hipStreamSynchronize(s->stream));
   drain_timers(s);
   for (auto& st : s->stats) st = Stat();
-  *out = s;
+  *out = hold.release();
   return 0;
 }
 
@@ -672,6 +705,27 @@ extern "C" int mk_session_kernel_stats(const mk_session* s, int32_t which, int64
   return 0;
 }
 
+// ------------------------------------------------------------------ scoped device scratch (freed on every return path)
+namespace {
+struct DevBufs {
+  std::vector<void*> p;
+  ~DevBufs() {
+    for (void* x : p) hipFree(x);
+  }
+  template <typename T>
+  T* get(size_t n) {
+    void* x = nullptr;
+    if (hipMalloc(&x, std::max<size_t>(n, 1) * sizeof(T)) != hipSuccess) {
+      (void)hipGetLastError();   // not sticky for the caller's later launch checks
+      return nullptr;
+    }
+    p.push_back(x);
+    return (T*)x;
+  }
+};
+
+}  // namespace
+
 // spPredict after the fit (MK.R:87-89) over test-site tiles: replays the kriging of every kept
 // iteration from the recorded chain states (z, theta, A).  A factor is recomputed only where
 // (phi, nu) changed since the previous kept sample, with the same kernels and inputs as in the
@@ -686,10 +740,10 @@ static int predict_tiled(mk_session* s, mk_outputs* o) {
   hipStream_t st = s->stream;
   Group g = s->all;
   const int ntri_tiles = nt * (nt + 1) / 2;
-  double *dq = nullptr, *dsum = nullptr;
-  int rc;
-  if ((rc = s->alloc(&dq, (size_t)S * q * T * MK_N_LEVELS)) || (rc = s->alloc(&dsum, (size_t)q * T * MK_N_LEVELS)))
-    return rc;
+  DevBufs scratch;
+  double* dq = scratch.get<double>((size_t)S * q * T * MK_N_LEVELS);
+  double* dsum = scratch.get<double>((size_t)q * T * MK_N_LEVELS);
+  if (!dq || !dsum) return set_err(MK_E_NOMEM, "tiled kriging scratch");
   for (int t0 = 0; t0 < n_test; t0 += T) {
     const int Tc = std::min(T, n_test - t0);
     const int Ct = q * Tc;
@@ -753,10 +807,10 @@ extern "C" int mk_session_outputs(mk_session* s, mk_outputs* o) {
   const bool done = s->iter >= md.n_samples;
   if ((o->parameters || o->w_predict || o->w_pred_samples) && !done)
     return set_err(MK_E_ARG, "quantile/predictive outputs need all n.samples iterations");
+  DevBufs scratch;
   if (o->parameters) {
-    double* dq;
-    int rc = s->alloc(&dq, (size_t)S * P * MK_N_LEVELS);
-    if (rc) return rc;
+    double* dq = scratch.get<double>((size_t)S * P * MK_N_LEVELS);
+    if (!dq) return set_err(MK_E_NOMEM, "quantile scratch");
     hipLaunchKernelGGL(k_quantiles, dim3(S * P), dim3(256), 0, s->stream, md.samples + (long)md.kept0 * P,
                        (long)md.n_samples * P, (long)P, md.n_kept, P, s->d_probs, MK_N_LEVELS, dq);
     HIPCHK(hipGetLastError());
@@ -769,17 +823,16 @@ extern "C" int mk_session_outputs(mk_session* s, mk_outputs* o) {
     if (rc) return rc;
   } else if ((o->w_predict || o->w_predict_sum) && n_test > 0) {
     const int C = q * n_test;
-    double* dq;
-    int rc = s->alloc(&dq, (size_t)S * C * MK_N_LEVELS);
-    if (rc) return rc;
+    double* dq = scratch.get<double>((size_t)S * C * MK_N_LEVELS);
+    if (!dq) return set_err(MK_E_NOMEM, "quantile scratch");
     hipLaunchKernelGGL(k_quantiles, dim3(S * C), dim3(256), 0, s->stream, md.w_pred, (long)md.n_kept * C, (long)C,
                        md.n_kept, C, s->d_probs, MK_N_LEVELS, dq);
     HIPCHK(hipGetLastError());
     if (o->w_predict)
       HIPCHK(hipMemcpyAsync(o->w_predict, dq, (size_t)S * C * MK_N_LEVELS * 8, hipMemcpyDeviceToHost, s->stream));
     if (o->w_predict_sum) {   // this shard's term of the combine: sequential sum over its subsets
-      double* dsum;
-      if ((rc = s->alloc(&dsum, (size_t)C * MK_N_LEVELS))) return rc;
+      double* dsum = scratch.get<double>((size_t)C * MK_N_LEVELS);
+      if (!dsum) return set_err(MK_E_NOMEM, "combine scratch");
       hipLaunchKernelGGL(k_combine, dim3((unsigned)(((long)C * MK_N_LEVELS + 255) / 256)), dim3(256), 0, s->stream, dq,
                          S, (long)C * MK_N_LEVELS, dsum, 0);
       HIPCHK(hipMemcpyAsync(o->w_predict_sum, dsum, (size_t)C * MK_N_LEVELS * 8, hipMemcpyDeviceToHost, s->stream));
@@ -835,6 +888,8 @@ extern "C" int mk_session_outputs(mk_session* s, mk_outputs* o) {
 
 extern "C" void mk_session_destroy(mk_session* s) { delete s; }
 
+extern "C" int32_t mk_session_count(void) { return g_live_sessions.load(); }
+
 extern "C" int mk_fit_predict_batched(const mk_problem* pr, const mk_config* c, mk_outputs* o) {
   mk_session* s = nullptr;
   int rc = mk_session_create(pr, c, &s);
@@ -845,22 +900,7 @@ extern "C" int mk_fit_predict_batched(const mk_problem* pr, const mk_config* c, 
   return rc;
 }
 
-// ------------------------------------------------------------------ device scratch for the one-shot entry points
 namespace {
-struct DevBufs {
-  std::vector<void*> p;
-  ~DevBufs() {
-    for (void* x : p) hipFree(x);
-  }
-  template <typename T>
-  T* get(size_t n) {
-    void* x = nullptr;
-    if (hipMalloc(&x, std::max<size_t>(n, 1) * sizeof(T)) != hipSuccess) return nullptr;
-    p.push_back(x);
-    return (T*)x;
-  }
-};
-
 // R's seq.default(from, to, by) for by > 0: from + (0:n)*by, n = as.integer(del/by + 1e-10), pmin(x, to).
 std::vector<double> r_seq(double from, double to, double by) {
   const int n = (int)((to - from) / by + 1e-10);
@@ -871,7 +911,7 @@ std::vector<double> r_seq(double from, double to, double by) {
 }  // namespace
 
 // ------------------------------------------------------------------ combine
-extern "C" int mk_combine(const double* grids, int32_t K, int64_t G, double* out, int32_t device) {
+static int combine_host(const double* grids, int32_t K, int64_t G, double* out, int mean, int32_t device) {
   if (!grids || !out || K < 1 || G < 1) return set_err(MK_E_ARG, "bad combine arguments");
   HIPCHK(hipSetDevice(device));
   DevBufs b;
@@ -879,9 +919,27 @@ extern "C" int mk_combine(const double* grids, int32_t K, int64_t G, double* out
   double* dout = b.get<double>((size_t)G);
   if (!dg || !dout) return set_err(MK_E_NOMEM, "combine alloc");
   HIPCHK(hipMemcpy(dg, grids, (size_t)K * G * 8, hipMemcpyHostToDevice));
-  hipLaunchKernelGGL(k_combine, dim3((unsigned)((G + 255) / 256)), dim3(256), 0, 0, dg, K, (long)G, dout, 1);
+  hipLaunchKernelGGL(k_combine, dim3((unsigned)((G + 255) / 256)), dim3(256), 0, 0, dg, K, (long)G, dout, mean);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpy(out, dout, (size_t)G * 8, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+extern "C" int mk_combine(const double* grids, int32_t K, int64_t G, double* out, int32_t device) {
+  return combine_host(grids, K, G, out, 1, device);
+}
+
+extern "C" int mk_combine_sum(const double* grids, int32_t K, int64_t G, double* out, int32_t device) {
+  return combine_host(grids, K, G, out, 0, device);
+}
+
+extern "C" int mk_combine_device(const double* d_grids, int32_t K, int64_t G, double* d_out, int32_t mean,
+                                 int32_t device, void* stream) {
+  if (!d_grids || !d_out || K < 1 || G < 1) return set_err(MK_E_ARG, "bad combine arguments");
+  HIPCHK(hipSetDevice(device));
+  hipLaunchKernelGGL(k_combine, dim3((unsigned)((G + 255) / 256)), dim3(256), 0, (hipStream_t)stream, d_grids, K, (long)G,
+                     d_out, mean ? 1 : 0);
+  HIPCHK(hipGetLastError());
   return 0;
 }
 
@@ -906,12 +964,24 @@ extern "C" int mk_combine_median(const double* grids, int32_t K, int32_t L, int6
 }
 
 // ------------------------------------------------------------------ post-combine steps (MK.R:136-165)
-extern "C" int mk_posterior_summary(const double* result, int32_t P, const double* result2, int64_t C,
-                                    const double* x_test, int32_t p, int32_t S, uint64_t seed, mk_summary* o,
-                                    int32_t device) {
+extern "C" int mk_combine_median_device(const double* d_grids, int32_t K, int32_t L, int64_t C, int32_t max_iter,
+                                        double tol, double* d_out, int32_t* d_iters, int32_t device, void* stream) {
+  if (!d_grids || !d_out || K < 1 || L < 1 || L > 256 || C < 1 || max_iter < 1 || !(tol >= 0.0))
+    return set_err(MK_E_ARG, "bad combine_median arguments (1 <= n_levels <= 256, max_iter >= 1, tol >= 0)");
+  HIPCHK(hipSetDevice(device));
+  hipLaunchKernelGGL(k_weiszfeld, dim3((unsigned)((C + 3) / 4)), dim3(256), 0, (hipStream_t)stream, d_grids, K, L, (long)C,
+                     max_iter, tol, d_out, d_iters);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+extern "C" int mk_posterior_summary_ex(const double* result, int32_t P, const double* result2, int64_t C,
+                                       const double* x_test, int32_t p, int32_t S, uint64_t seed,
+                                       const int32_t* index, int32_t link, mk_summary* o, int32_t device) {
   if (!result || !o || P < 1 || C < 0 || p < 0 || p > P || S < 1 || S > 2048)
     return set_err(MK_E_ARG, "bad posterior_summary arguments (P >= 1, 0 <= p <= P, 1 <= samplesize <= 2048)");
   if (C > 0 && (!result2 || (p > 0 && !x_test))) return set_err(MK_E_ARG, "result2 / x_test missing");
+  if (link != MK_LINK_LOGIT && link != MK_LINK_PROBIT) return set_err(MK_E_ARG, "link must be logit or probit");
   HIPCHK(hipSetDevice(device));
   const int L = MK_N_LEVELS;
   const std::vector<double> xg = r_seq(0.005, 1.0, 0.005);   // allquant levels (MK.R:88)
@@ -962,14 +1032,23 @@ extern "C" int mk_posterior_summary(const double* result, int32_t P, const doubl
   HIPCHK(hipMemcpy(d_mode, mode.data(), NL * 4, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(d_t, tt.data(), NL * 8, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(d_pr, probs3, 3 * 8, hipMemcpyHostToDevice));
-  hipLaunchKernelGGL(k_post_index, dim3((S + 255) / 256), dim3(256), 0, st, seed, S, NL, d_idx);
+  if (index) {   // sampleparIndex drawn by the caller (R: sample(seq(1, length(Xout), 1), ...)), 1-based
+    std::vector<int> hidx(S);
+    for (int j = 0; j < S; ++j) {
+      if (index[j] < 1 || index[j] > NL) return set_err(MK_E_ARG, "index entries must be in 1..length(Xout)");
+      hidx[j] = index[j] - 1;
+    }
+    HIPCHK(hipMemcpy(d_idx, hidx.data(), (size_t)S * 4, hipMemcpyHostToDevice));
+  } else {
+    hipLaunchKernelGGL(k_post_index, dim3((S + 255) / 256), dim3(256), 0, st, seed, S, NL, d_idx);
+  }
   hipLaunchKernelGGL(k_post_interp, dim3((unsigned)(((long)S * P + 255) / 256)), dim3(256), 0, st, d_res, L, (long)P,
                      d_idx, S, d_lo, d_hi, d_mode, d_t, d_spar);
   if (C > 0) {
     const unsigned nb = (unsigned)(((long)S * C + 255) / 256);
     hipLaunchKernelGGL(k_post_interp, dim3(nb), dim3(256), 0, st, d_res2, L, (long)C, d_idx, S, d_lo, d_hi, d_mode, d_t,
                        d_sw);
-    hipLaunchKernelGGL(k_post_prob, dim3(nb), dim3(256), 0, st, d_spar, S, d_xt, (long)C, p, d_sw, d_p);
+    hipLaunchKernelGGL(k_post_prob, dim3(nb), dim3(256), 0, st, d_spar, S, d_xt, (long)C, p, d_sw, link, d_p);
   }
   HIPCHK(hipGetLastError());
   if (o->index) HIPCHK(hipMemcpy(o->index, d_idx, (size_t)S * 4, hipMemcpyDeviceToHost));
@@ -988,6 +1067,12 @@ extern "C" int mk_posterior_summary(const double* result, int32_t P, const doubl
   if (C > 0 && o->w_quant && (rc = quant(d_sw, C, o->w_quant))) return rc;
   if (C > 0 && o->p_quant && (rc = quant(d_p, C, o->p_quant))) return rc;
   return 0;
+}
+
+extern "C" int mk_posterior_summary(const double* result, int32_t P, const double* result2, int64_t C,
+                                    const double* x_test, int32_t p, int32_t S, uint64_t seed, mk_summary* o,
+                                    int32_t device) {
+  return mk_posterior_summary_ex(result, P, result2, C, x_test, p, S, seed, nullptr, MK_LINK_LOGIT, o, device);
 }
 
 // ------------------------------------------------------------------ glm start values (MK.R:53-55)
@@ -1022,11 +1107,12 @@ static void chol_solve_small(const std::vector<double>& Lc, int p, const double*
   }
 }
 
-extern "C" int mk_glm_binomial(const double* y, const double* weights, const double* x, int64_t n, int32_t p,
-                               double epsilon, int32_t maxit, double* coef, double* vcov, int32_t* iters,
-                               int32_t device) {
+extern "C" int mk_glm_binomial_link(const double* y, const double* weights, const double* x, int64_t n, int32_t p,
+                                    int32_t link, double epsilon, int32_t maxit, double* coef, double* vcov,
+                                    int32_t* iters, int32_t device) {
   if (!y || !weights || !x || !coef || n < 1 || p < 1 || p > 8 || maxit < 1)
     return set_err(MK_E_ARG, "bad glm arguments (n >= 1, 1 <= p <= 8, maxit >= 1)");
+  if (link != MK_LINK_LOGIT && link != MK_LINK_PROBIT) return set_err(MK_E_ARG, "link must be logit or probit");
   HIPCHK(hipSetDevice(device));
   std::vector<double> yp((size_t)n);
   for (int64_t i = 0; i < n; ++i) yp[i] = y[i] / weights[i];     // glm((y/weight) ~ x - 1, ...)  MK.R:53
@@ -1046,7 +1132,7 @@ extern "C" int mk_glm_binomial(const double* y, const double* weights, const dou
   double dev = 0.0;
   auto pass = [&](int mode) -> int {
     if (mode == 1) HIPCHK(hipMemcpy(d_c, c.data(), (size_t)p * 8, hipMemcpyHostToDevice));
-    hipLaunchKernelGGL(k_glm_pass, dim3(nblk), dim3(256), 0, 0, d_y, d_w, d_x, (long)n, p, d_c, mode, d_part);
+    hipLaunchKernelGGL(k_glm_pass, dim3(nblk), dim3(256), 0, 0, d_y, d_w, d_x, (long)n, p, d_c, mode, link, d_part);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpy(part.data(), d_part, part.size() * 8, hipMemcpyDeviceToHost));
     std::vector<double> tot(NP, 0.0);
@@ -1085,6 +1171,12 @@ extern "C" int mk_glm_binomial(const double* y, const double* weights, const dou
   }
   if (iters) *iters = it;
   return 0;
+}
+
+extern "C" int mk_glm_binomial(const double* y, const double* weights, const double* x, int64_t n, int32_t p,
+                               double epsilon, int32_t maxit, double* coef, double* vcov, int32_t* iters,
+                               int32_t device) {
+  return mk_glm_binomial_link(y, weights, x, n, p, MK_LINK_LOGIT, epsilon, maxit, coef, vcov, iters, device);
 }
 
 // ------------------------------------------------------------------ parity-test entry points

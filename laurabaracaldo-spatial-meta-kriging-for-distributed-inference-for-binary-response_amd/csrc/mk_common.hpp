@@ -20,6 +20,11 @@
 #define MK_TAG_RESAMPLE 3u
 
 #define MK_TWO_PI 6.283185307179586
+#define MK_SQRT1_2 0.7071067811865476
+// binomial links: logit is the reference's (spMvGLM's binomial family, MK.R:80-84, 160);
+// probit is the north-star extension ("logit/probit latent-GP"), no reference parity target
+#define MK_LINK_LOGIT 0
+#define MK_LINK_PROBIT 1
 #define MK_TWO_M52 2.220446049250313e-16   // 2^-52
 
 namespace mk {
@@ -72,7 +77,18 @@ __device__ inline double predict_normal(Key key, uint32_t idx, uint32_t s) {
 }
 
 __device__ inline double softplus(double x) { return fmax(x, 0.0) + log1p(exp(-fabs(x))); }
-__device__ inline double loglik_term(double y, double wt, double eta) { return y * eta - wt * softplus(eta); }
+// Phi(x) and log Phi(x): erfc for x >= 0 (log1p keeps the digits near 1), the scaled erfcx
+// below 0 (no underflow: log Phi(-40) is finite).  oracle/spmvglm.py log_ndtr states the same.
+__device__ inline double norm_cdf(double x) { return 0.5 * erfc(-x * MK_SQRT1_2); }
+__device__ inline double log_norm_cdf(double x) {
+  return (x >= 0.0) ? log1p(-0.5 * erfc(x * MK_SQRT1_2)) : log(0.5 * erfcx(-x * MK_SQRT1_2)) - 0.5 * x * x;
+}
+// Binomial log-likelihood of y successes in wt trials at linear predictor eta (constants dropped):
+// logit  y eta - wt log(1 + e^eta);  probit  y log Phi(eta) + (wt - y) log Phi(-eta).
+__device__ inline double loglik_term(double y, double wt, double eta, int link) {
+  if (link == MK_LINK_PROBIT) return y * log_norm_cdf(eta) + (wt - y) * log_norm_cdf(-eta);
+  return y * eta - wt * softplus(eta);
+}
 
 // spBayes util logitInv(z, a, b) = b - (b-a)/(1+exp(z))
 __device__ __host__ inline double logit_inv(double z, double a, double b) { return b - (b - a) / (1.0 + exp(z)); }

@@ -52,9 +52,9 @@ __global__ void k_post_index(uint64_t seed, int samplesize, int n_levels, int* i
 __global__ void k_post_interp(const double* grid, int L, long C, const int* idx, int S, const int* lo, const int* hi,
                               const int* mode, const double* t, double* out);
 __global__ void k_post_prob(const double* sample_par, int S, const double* x_test, long C, int p, const double* sample_w,
-                            double* pout);
+                            int link, double* pout);
 __global__ void k_glm_pass(const double* yprop, const double* wt, const double* X, long n, int p, const double* coef,
-                           int mode, double* part);
+                           int mode, int link, double* part);
 // mk_init.hip
 __global__ void k_init_state(Model md);
 __global__ void k_theta_init(Model md, MatSet ms, int h0, int hc);

@@ -69,7 +69,7 @@ __global__ __launch_bounds__(256) void k_beta(Model md, int iter) {
     double loc = 0.0;
     for (int k = tid; k < Ns; k += 256) {
       const double e0 = eta[k];
-      loc += loglik_term(y[k], wt[k], e0 + delta * xj[k]) - loglik_term(y[k], wt[k], e0);
+      loc += loglik_term(y[k], wt[k], e0 + delta * xj[k], md.link) - loglik_term(y[k], wt[k], e0, md.link);
     }
     const double tot = block_sum<256>(loc, red);
     if (lu <= tot) {
@@ -298,7 +298,7 @@ __global__ __launch_bounds__(SW_T) void k_sweep(Model md, MatSet ms, int iter) {
     const double zz = proposal_normal(key, j, iter);
     const double d = exp(tune[k]) * zz;
     dl[k] = d;
-    dll[k] = loglik_term(y[k], wt[k], eta[k] + d) - loglik_term(y[k], wt[k], eta[k]);
+    dll[k] = loglik_term(y[k], wt[k], eta[k] + d, md.link) - loglik_term(y[k], wt[k], eta[k], md.link);
     lgu[k] = accept_log_uniform(key, j, iter);
     sacc[k] = 0;
   }

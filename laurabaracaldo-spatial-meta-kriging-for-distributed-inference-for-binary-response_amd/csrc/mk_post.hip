@@ -130,27 +130,36 @@ __global__ __launch_bounds__(256) void k_post_interp(const double* __restrict__ 
 
 // p.sample[j, c] = 1 / (1 + exp(-(x.test[c, ] %*% SamplePar[j, 1:p] + Samplew[j, c])))  (MK.R:156-161),
 // x.test %*% B.s summed in column order.  All matrices column-major (R).
+// link = MK_LINK_PROBIT (north-star extension; the reference is logit): Phi(eta) = erfc(-eta/sqrt 2)/2.
 __global__ __launch_bounds__(256) void k_post_prob(const double* __restrict__ sample_par, int S,
                                                    const double* __restrict__ x_test, long C, int p,
-                                                   const double* __restrict__ sample_w, double* __restrict__ pout) {
+                                                   const double* __restrict__ sample_w, int link,
+                                                   double* __restrict__ pout) {
   const long e = (long)blockIdx.x * 256 + threadIdx.x;
   if (e >= (long)S * C) return;
   const int j = (int)(e % S);
   const long c = e / S;
   double xb = 0.0;
   for (int m = 0; m < p; ++m) xb = xb + x_test[c + (long)m * C] * sample_par[j + (long)m * S];
-  pout[e] = 1.0 / (1.0 + exp(-(xb + sample_w[e])));
+  const double eta = xb + sample_w[e];
+  pout[e] = (link == MK_LINK_PROBIT) ? norm_cdf(eta) : 1.0 / (1.0 + exp(-eta));
 }
 
-// ---------------------------------------------------------------- glm.fit IRLS pass (binomial, logit)
-// R's family.c logit link with its eta thresholds (binomial()$linkinv / $mu.eta).
+// ---------------------------------------------------------------- glm.fit IRLS pass (binomial)
+// logit: R's family.c logit link with its eta thresholds (binomial()$linkinv / $mu.eta);
+// probit: make.link("probit") -- linkinv = pnorm(eta clamped to +-(-qnorm(eps))),
+// mu.eta = max(dnorm(eta), eps), linkfun = qnorm.
 #define GLM_THRESH 30.0
 #define GLM_EPS 2.220446049250313e-16
-__device__ inline double glm_linkinv(double eta) {
+#define GLM_PROBIT_THRESH 8.125890664701906   // -qnorm(.Machine$double.eps)
+#define GLM_INV_SQRT_2PI 0.3989422804014327
+__device__ inline double glm_linkinv(double eta, int link) {
+  if (link == MK_LINK_PROBIT) return norm_cdf(fmin(fmax(eta, -GLM_PROBIT_THRESH), GLM_PROBIT_THRESH));
   const double tmp = (eta < -GLM_THRESH) ? GLM_EPS : ((eta > GLM_THRESH) ? 1.0 / GLM_EPS : exp(eta));
   return tmp / (1.0 + tmp);
 }
-__device__ inline double glm_mu_eta(double eta) {
+__device__ inline double glm_mu_eta(double eta, int link) {
+  if (link == MK_LINK_PROBIT) return fmax(GLM_INV_SQRT_2PI * exp(-0.5 * eta * eta), GLM_EPS);
   const double opexp = 1.0 + exp(eta);
   return (eta > GLM_THRESH || eta < -GLM_THRESH) ? GLM_EPS : exp(eta) / (opexp * opexp);
 }
@@ -162,7 +171,7 @@ __device__ inline double y_log_y(double y, double mu) { return (y != 0.0) ? y * 
 #define GLM_PMAX 8
 __global__ __launch_bounds__(256) void k_glm_pass(const double* __restrict__ yprop, const double* __restrict__ wt,
                                                   const double* __restrict__ X, long n, int p,
-                                                  const double* __restrict__ coef, int mode,
+                                                  const double* __restrict__ coef, int mode, int link,
                                                   double* __restrict__ part) {
   __shared__ double red[8];
   const int np_tri = p * (p + 1) / 2;
@@ -174,15 +183,15 @@ __global__ __launch_bounds__(256) void k_glm_pass(const double* __restrict__ ypr
     double eta, mu;
     if (mode == 0) {
       mu = (w * y + 0.5) / (w + 1.0);
-      eta = log(mu / (1.0 - mu));
+      eta = (link == MK_LINK_PROBIT) ? normcdfinv(mu) : log(mu / (1.0 - mu));
     } else {
       eta = 0.0;
       for (int j = 0; j < p; ++j) eta += X[r + (long)j * n] * coef[j];
-      mu = glm_linkinv(eta);
+      mu = glm_linkinv(eta, link);
     }
     loc[0] += 2.0 * w * (y_log_y(y, mu) + y_log_y(1.0 - y, 1.0 - mu));
     if (w > 0.0) {
-      const double me = glm_mu_eta(eta);
+      const double me = glm_mu_eta(eta, link);
       const double z = eta + (y - mu) / me;
       const double ww = w * me * me / (mu * (1.0 - mu));   // (sqrt-weight)^2
       int k = 1;

@@ -10,7 +10,7 @@
 //   unif_rand     MT19937 word * 2^-32, fixup() into the open interval (0, 1)
 //   unif_index    R_unif_index: rejection over rbits(ceil(log2 n)), 16 bits per draw
 //   sample        do_sample, uniform without replacement: x = 0..n-1, j = unif_index(n),
-//                 take x[j], x[j] = x[--n]
+//                 take x[j], x[j] = x[--n]; with replacement: unif_index(n) + 1 per draw
 // The partition is a sequential RNG stream, so it stays on the host: per subset O(|a|)
 // (the selection plus an order-keeping compaction for setdiff), 1.25e8 simple steps at
 // n = 500k, K = 250.
@@ -110,6 +110,15 @@ extern "C" int mk_r_sample(int32_t seed, int32_t n, int32_t size, int32_t* out) 
   RRng rng(seed);
   std::vector<int32_t> x((size_t)n);
   sample_noreplace(rng, n, size, x, out);
+  return MK_OK;
+}
+
+// sample(x, size, replace = TRUE) with length(x) = n > 1 (MK.R:141: sample(seq(1, length(Xout), 1),
+// samplesize, replace=TRUE)): do_sample's with-replacement branch, iy[i] = R_unif_index(n) + 1.
+extern "C" int mk_r_sample_replace(int32_t seed, int32_t n, int32_t size, int32_t* out) {
+  if (n < 1 || size < 0 || (size > 0 && !out)) return rs_fail("invalid arguments");
+  RRng rng(seed);
+  for (int32_t i = 0; i < size; ++i) out[i] = (int32_t)(rng.unif_index(n) + 1);
   return MK_OK;
 }
 

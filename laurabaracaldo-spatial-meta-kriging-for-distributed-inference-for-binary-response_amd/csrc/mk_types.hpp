@@ -25,6 +25,7 @@ namespace mk {
 
 struct Model {
   int S, q, p, n_pad, Np, nt, ntri, n_theta, cov_model;
+  int link;                               // MK_LINK_LOGIT | MK_LINK_PROBIT
   int o_A, o_phi, o_nu, o_w, n_mh_max;   // MH parameter offsets (spBayes order)
   int n_batch, batch_length, n_samples, kept0, n_kept;
   int n_test, n_test_pad, ntt;

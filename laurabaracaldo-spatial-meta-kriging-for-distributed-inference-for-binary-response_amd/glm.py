@@ -17,8 +17,12 @@ from . import _lib
 from ._lib import check, dptr, iptr
 
 
-def glm_binomial(y, x, weights, epsilon=1e-8, maxit=25, device=0):
-    """Returns (coefficients, vcov, beta_tuning = t(chol(vcov))) -- y are counts, weights trials."""
+def glm_binomial(y, x, weights, epsilon=1e-8, maxit=25, device=0, link="logit"):
+    """Returns (coefficients, vcov, beta_tuning = t(chol(vcov))) -- y are counts, weights trials.
+    link="probit": binomial(link = "probit") (north-star extension; the reference fits logit)."""
+    from .session import LINKS
+    if link not in LINKS:
+        raise ValueError(f"error: link must be 'logit' or 'probit', not '{link}'")
     lib = _lib.load()
     x = np.asarray(x, dtype=np.float64)
     n, p = x.shape
@@ -28,7 +32,7 @@ def glm_binomial(y, x, weights, epsilon=1e-8, maxit=25, device=0):
     coef = np.zeros(p)
     vcov = np.zeros(p * p)
     it = np.zeros(1, dtype=np.int32)
-    check(lib.mk_glm_binomial(dptr(y), dptr(wt), dptr(xf), n, p, float(epsilon), int(maxit), dptr(coef), dptr(vcov),
-                              iptr(it), int(device)))
+    check(lib.mk_glm_binomial_link(dptr(y), dptr(wt), dptr(xf), n, p, LINKS[link], float(epsilon), int(maxit),
+                                   dptr(coef), dptr(vcov), iptr(it), int(device)))
     vcov = vcov.reshape(p, p, order="F")
     return coef, vcov, np.linalg.cholesky(vcov)

@@ -71,12 +71,21 @@ def default_config(q, p, beta_starting, beta_tuning, cov_model="exponential", n_
                          batch_length=batch_length, accept_rate=0.43, seed=seed, **kw)
 
 
-def start_values(y, x, weight, q, device=0):
+def start_values(y, x, weight, q, device=0, link="logit"):
     """MK.R:53-55 on the full data, once, on device: beta.starting and t(chol(vcov))."""
     n_tot = len(y)
     wt = np.broadcast_to(np.asarray(weight, float), (n_tot,))
-    coef, vcov, bt = glm_binomial(y, x, wt, device=device)
+    coef, vcov, bt = glm_binomial(y, x, wt, device=device, link=link)
     return coef, bt
+
+
+def r_sample_replace(n, size, seed):
+    """sample.int(n, size, replace=TRUE) as R draws it right after set.seed(seed) (1-based),
+    e.g. MK.R:141's sampleparIndex with n = length(Xout) = 996."""
+    lib = load()
+    out = np.empty(int(size), dtype=np.int32)
+    check(lib.mk_r_sample_replace(int(seed), int(n), int(size), out.ctypes.data_as(_ip)))
+    return out
 
 
 def meta_fit(y, x, weight, coords, q, index_part, coords_test=None, cfg=None, subset_base=0, device=0,
@@ -122,8 +131,12 @@ def combine_results(obj, device=0, method="mean"):
     return result, result2
 
 
-def posterior_summary(result, result2, x_test, q=None, samplesize=1000, seed=20250114, device=0):
+def posterior_summary(result, result2, x_test, q=None, samplesize=1000, seed=20250114, device=0, rng="philox",
+                      index=None, link="logit"):
     """MK.R:136-165 on device: interpolate both combined grids to Xout (996 levels), one shared
     resample index vector (comonotone draws, MK.R:141), p(y=1) = logistic(x.test B + w) and the
-    median / 2.5% / 97.5% summaries (post.posterior_summary)."""
-    return _post_summary(result, result2, x_test, samplesize=samplesize, seed=seed, device=device)
+    median / 2.5% / 97.5% summaries (post.posterior_summary).  rng="R": sampleparIndex is R's
+    sample(seq(1, length(Xout), 1), samplesize, replace=TRUE) right after set.seed(seed);
+    index: a 1-based index vector drawn by the caller (R's own stream)."""
+    return _post_summary(result, result2, x_test, samplesize=samplesize, seed=seed, device=device, rng=rng,
+                         index=index, link=link)

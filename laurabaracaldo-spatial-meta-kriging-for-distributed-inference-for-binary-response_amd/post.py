@@ -28,11 +28,31 @@ def combine_median(grids, max_iter=100, tol=1e-12, device=0):
     return out.reshape(L, C, order="F").reshape(g.shape[1:]), it
 
 
-def posterior_summary(result, result2, x_test, q=None, samplesize=1000, seed=20250114, device=0, p_sample=True):
+def posterior_summary(result, result2, x_test, q=None, samplesize=1000, seed=20250114, device=0, p_sample=True,
+                      rng="philox", index=None, link="logit"):
     """MK.R:136-165 on device.  result: 200 x P combined parameter grid (betas first, MK.R:159);
     result2: 200 x C combined w.predict grid; x_test: C x p.  Returns SamplePar, Samplew,
-    p_sample (samplesize x ...), w_quant (3 x C), param_quant (3 x P), p_quant (3 x C), index."""
+    p_sample (samplesize x ...), w_quant (3 x C), param_quant (3 x P), p_quant (3 x C), index
+    (0-based rows of the 996-level grid).
+
+    sampleparIndex (MK.R:141): rng="philox" draws it from Philox(seed); rng="R" replays R's
+    sample(seq(1, 996, 1), samplesize, replace=TRUE) right after set.seed(seed)
+    (mk_r_sample_replace); index= takes a caller-drawn 1-based vector (R's own stream).
+    link="probit" evaluates p(y=1) = Phi(x.test B + w) (extension; MK.R:160 is logistic)."""
+    from .session import LINKS
     lib = _lib.load()
+    if link not in LINKS:
+        raise ValueError(f"error: link must be 'logit' or 'probit', not '{link}'")
+    if index is None and rng == "R":
+        index = np.empty(int(samplesize), dtype=np.int32)
+        check(lib.mk_r_sample_replace(int(seed), 996, int(samplesize), iptr(index)))
+    elif index is None and rng != "philox":
+        raise ValueError(f"error: rng must be 'philox' or 'R', not '{rng}'")
+    idx_in = None
+    if index is not None:
+        idx_in = np.ascontiguousarray(np.asarray(index), dtype=np.int32)
+        if idx_in.shape != (int(samplesize),):
+            raise ValueError("error: index must have samplesize entries")
     result = np.asarray(result, dtype=np.float64)
     P = result.shape[1]
     res = _f64(result.ravel(order="F"))
@@ -51,8 +71,8 @@ def posterior_summary(result, result2, x_test, q=None, samplesize=1000, seed=202
         if p_sample:
             out["p_sample"] = np.zeros(S * C)
             o.p_sample = dptr(out["p_sample"])
-    check(lib.mk_posterior_summary(dptr(res), P, dptr(res2), C, dptr(xtf), p, S, int(seed) & 0xFFFFFFFFFFFFFFFF, o,
-                                   int(device)))
+    check(lib.mk_posterior_summary_ex(dptr(res), P, dptr(res2), C, dptr(xtf), p, S, int(seed) & 0xFFFFFFFFFFFFFFFF,
+                                      iptr(idx_in) if idx_in is not None else None, LINKS[link], o, int(device)))
     shapes = dict(SamplePar=(S, P), param_quant=(3, P), Samplew=(S, C), w_quant=(3, C), p_quant=(3, C),
                   p_sample=(S, C))
     for k, shp in shapes.items():

@@ -12,6 +12,7 @@ from . import _lib
 from ._lib import Config, Outputs, Problem, check, dptr, iptr
 
 COV_MODELS = {"exponential": _lib.MK_COV_EXPONENTIAL, "matern": _lib.MK_COV_MATERN}
+LINKS = {"logit": _lib.MK_LINK_LOGIT, "probit": _lib.MK_LINK_PROBIT}
 
 # kernel-stat ids (mk_api.hip)
 KS_CHOL_UPDATE, KS_CHOL_DIAG, KS_CHOL_TRSM, KS_SWEEP, KS_LAUUM, KS_ITER, KS_INV = range(7)
@@ -27,9 +28,13 @@ class SamplerConfig:
     def __init__(self, q, p, beta_starting, beta_tuning, cov_model="exponential", n_batch=100, batch_length=50,
                  accept_rate=0.43, burn_in=None, phi_starting=None, phi_tuning=None, phi_unif=None,
                  A_starting=None, A_tuning=None, w_starting=0.0, w_tuning=0.5, nu_starting=None, nu_tuning=None,
-                 nu_unif=None, K_IW_df=None, K_IW_S=None, seed=20250114, n_streams=0, predict_tile=0):
+                 nu_unif=None, K_IW_df=None, K_IW_S=None, seed=20250114, n_streams=0, predict_tile=0,
+                 link="logit"):
         if cov_model not in COV_MODELS:
             raise ValueError(f"error: specified cov.model '{cov_model}' is not a valid option")
+        if link not in LINKS:
+            raise ValueError(f"error: link must be 'logit' (the reference) or 'probit', not '{link}'")
+        self.link = link
         self.q, self.p = int(q), int(p)
         self.cov_model = cov_model
         self.n_batch, self.batch_length = int(n_batch), int(batch_length)
@@ -112,6 +117,7 @@ class SamplerConfig:
         c.device = int(device)
         c.n_streams = self.n_streams
         c.predict_tile = self.predict_tile
+        c.link = LINKS[self.link]
         return c, keep
 
 
@@ -249,13 +255,15 @@ class Session:
         self.close()
 
 
-def combine(grids, device=0):
-    """MK.R:123-133 on device: (grid_1 + ... + grid_K)/K in the reference's sequential order."""
+def combine(grids, device=0, mean=True):
+    """MK.R:123-133 on device: (grid_1 + ... + grid_K)/K in the reference's sequential order
+    (mean=False: the sum only -- a shard's term of the combine)."""
     lib = _lib.load()
     g = _f64(np.stack([np.asarray(x, float) for x in grids]))
     K = g.shape[0]
     out = np.zeros(g.shape[1:])
-    check(lib.mk_combine(dptr(g.reshape(K, -1)), K, int(np.prod(g.shape[1:])), dptr(out), int(device)))
+    fn = lib.mk_combine if mean else lib.mk_combine_sum
+    check(fn(dptr(g.reshape(K, -1)), K, int(np.prod(g.shape[1:])), dptr(out), int(device)))
     return out
 
 

@@ -8,7 +8,7 @@ from the spBayes ``spMvGLM`` help-page recipe.  This module is that driver
   coords ~ U[0,1]^2; per outcome X_a = [1, N(0,1)]; block-diagonal design
   beta = (1,-1) | (1,-1,-1,1) | (1,-1,-1,1,0.5,-0.5); phi = 6; K = A A'
   w ~ GP(0, LMC(exponential|Matern)); exact Cholesky draw for n_total <= 6000,
-  random Fourier features (M features) above; y ~ Binomial(weight, logistic(X beta + w)).
+  random Fourier features (M = 4096) above; y ~ Binomial(weight, logistic(X beta + w)).
 
 Layout produced (R conventions): y, weight location-major (site i, outcome a at
 i*q + a); x (n*q, p) block-diagonal; coords (n, 2).  Test sites: coords_test
@@ -53,9 +53,11 @@ def _exact_field(coords, A, phi, nu, cov_model, rng):
     return W @ A.T
 
 
-def _rff_field(coords, A, phi, nu, cov_model, rng, M=1024, chunk=65536):
+def _rff_field(coords, A, phi, nu, cov_model, rng, M=4096, chunk=8192):
     """Random Fourier features: exponential -> omega = phi*z/sqrt(u), u~chi2_1 (Cauchy-type);
-    Matern -> multivariate-t(2 nu) frequencies scaled by phi."""
+    Matern -> multivariate-t(2 nu) frequencies scaled by phi.  M = 4096 features (SURVEY.md 8d);
+    the n x M cosines (2e9 at configs[2]) run as multithreaded torch CPU ops in row chunks."""
+    import torch
     n = coords.shape[0]
     q = A.shape[0]
     W = np.zeros((n, q))
@@ -66,14 +68,18 @@ def _rff_field(coords, A, phi, nu, cov_model, rng, M=1024, chunk=65536):
         omega = phi * z / np.sqrt(u)[:, None]
         b = rng.uniform(0, 2 * np.pi, size=M)
         c = rng.standard_normal(M)
+        om_t = torch.from_numpy(np.ascontiguousarray(omega.T))
+        b_t, c_t = torch.from_numpy(b), torch.from_numpy(c)
         for s in range(0, n, chunk):
-            proj = coords[s:s + chunk] @ omega.T + b
-            W[s:s + chunk, h] = np.sqrt(2.0 / M) * (np.cos(proj) @ c)
+            proj = torch.from_numpy(np.ascontiguousarray(coords[s:s + chunk])) @ om_t
+            proj += b_t
+            torch.cos_(proj)
+            W[s:s + chunk, h] = np.sqrt(2.0 / M) * (proj @ c_t).numpy()
     return W @ A.T
 
 
 def generate(n, q=1, n_test=1000, weight=1, cov_model=0, phi=6.0, nu=0.5, seed=20250114,
-             exact_max=6000):
+             exact_max=6000, link="logit"):
     rng = np.random.default_rng(seed)
     A = np.array(TRUE_A[q])
     beta = np.array(TRUE_BETA[q])
@@ -85,7 +91,11 @@ def generate(n, q=1, n_test=1000, weight=1, cov_model=0, phi=6.0, nu=0.5, seed=2
     xcov = rng.standard_normal((n + n_test, q))
     X_all = block_design(xcov, q)
     eta = X_all @ beta + W.reshape(-1)
-    prob = 1.0 / (1.0 + np.exp(-eta))
+    if link == "probit":      # extension: y ~ Binomial(weight, Phi(eta))
+        from scipy.special import ndtr
+        prob = ndtr(eta)
+    else:
+        prob = 1.0 / (1.0 + np.exp(-eta))
     y_all = rng.binomial(weight, prob).astype(np.float64)
     N = n * q
     return dict(

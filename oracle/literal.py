@@ -43,7 +43,7 @@ def log_posterior(params, coords, y, wt, X, cfg):
     if matern:
         out += np.sum(unif_jacobian(np.asarray(nu), cfg.nu_a, cfg.nu_b))
     eta = X @ beta + w
-    out += np.sum(loglik_terms(y, wt, eta))
+    out += np.sum(loglik_terms(y, wt, eta, getattr(cfg, "link", 0)))
     return out
 
 

@@ -11,10 +11,11 @@ Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import 
                         NOT in the reference (which averages, MK.R:123-133): parity unpinned, this
                         restatement is the spec the device kernel is checked against.
 
-Resample index (build decision): R's sample() (Mersenne-Twister) cannot be
-replayed, so draw j uses Philox key (seed, 0), counter (j, 0, TAG_RESAMPLE, 0):
-idx_j = min(floor(u_j * 996), 995) -- uniform over the 996 Xout levels with replacement, like
-sample(seq(1, length(Xout), 1), samplesize, replace=TRUE).
+Resample index (MK.R:141, sample(seq(1, length(Xout), 1), samplesize, replace=TRUE)): either
+R's own draws -- a caller-given 1-based index, e.g. rrng.RRng(seed).sample_int_replace(996, S)
+for an R session that called set.seed(seed) just before -- or, by default, Philox: draw j uses
+key (seed, 0), counter (j, 0, TAG_RESAMPLE, 0), idx_j = min(floor(u_j * 996), 995), uniform
+over the 996 Xout levels with replacement like R's.
 """
 import numpy as np
 
@@ -31,14 +32,15 @@ def resample_index(samplesize, seed, n_levels=len(XOUT996)):
     return np.minimum(np.floor(u * n_levels).astype(np.int64), n_levels - 1)
 
 
-def posterior_summary(result, result2, x_test, samplesize=1000, seed=20250114):
+def posterior_summary(result, result2, x_test, samplesize=1000, seed=20250114, index=None, link="logit"):
     """MK.R:136-165.  result: 200 x P combined parameter grid (betas first, MK.R:159);
     result2: 200 x C combined w.predict grid; x_test: C x p.  Returns the reference's
     SamplePar, Samplew, p.sample, w.quant (3 x C), param.quant (3 x P), plus p.quant (3 x C)."""
     result = np.asarray(result, dtype=np.float64)
     result2 = np.asarray(result2, dtype=np.float64)
     x_test = np.asarray(x_test, dtype=np.float64)
-    idx = resample_index(samplesize, seed)
+    # index: caller-drawn 1-based sampleparIndex (e.g. R's stream, rrng.RRng(seed).sample_int_replace)
+    idx = resample_index(samplesize, seed) if index is None else np.asarray(index, dtype=np.int64) - 1
     sample_par = r_approx(PROBS200, result, XOUT996)[idx]          # Result.Inter[sampleparIndex,]
     sample_w = r_approx(PROBS200, result2, XOUT996)[idx]           # Result.Inter2[sampleparIndex,]
     p = x_test.shape[1]
@@ -46,7 +48,12 @@ def posterior_summary(result, result2, x_test, samplesize=1000, seed=20250114):
     xb = np.zeros((samplesize, x_test.shape[0]))
     for m in range(p):
         xb = xb + sample_par[:, m:m + 1] * x_test[:, m][None, :]
-    p_sample = 1.0 / (1.0 + np.exp(-(xb + sample_w)))
+    eta = xb + sample_w
+    if link == "probit":                      # extension: Phi(eta) = erfc(-eta/sqrt2)/2 (device formula)
+        from scipy.special import erfc
+        p_sample = 0.5 * erfc(-eta * 0.7071067811865476)
+    else:
+        p_sample = 1.0 / (1.0 + np.exp(-eta))
     return dict(index=idx, SamplePar=sample_par, Samplew=sample_w, p_sample=p_sample,
                 w_quant=r_quantile7(sample_w, SUMMARY_PROBS, axis=0),
                 param_quant=r_quantile7(sample_par, SUMMARY_PROBS, axis=0),

@@ -14,6 +14,7 @@ this restates R >= 3.6.0's published algorithms for the defaults RNGkind("Mersen
                    unif_rand draw (floor(u * 65536))
   sample_int    -- do_sample, uniform without replacement: x = 0..n-1; j = unif_index(n);
                    pick x[j]; x[j] = x[--n]
+  sample_int_replace -- do_sample with replacement: unif_index(n) + 1 per draw (MK.R:141)
   partition     -- MK.R:15-41 verbatim (1-based indices, setdiff keeps a's order)
 Pinned by R's published known answers (tests/test_rrng.py): set.seed(1); runif(3) and
 set.seed(42|123|1); sample(1:10).  The product implementation is `mk_partition_r` in libmk.
@@ -91,6 +92,11 @@ class RRng:
             n -= 1
             x[j] = x[n]
         return out
+
+    def sample_int_replace(self, n, size):
+        """sample.int(n, size, replace=TRUE), 1-based: do_sample's R_unif_index(n) + 1 per draw
+        (MK.R:141 draws sampleparIndex this way)."""
+        return [self.unif_index(n) + 1 for _ in range(size)]
 
     def runif(self, k):
         return [self.unif_rand() for _ in range(k)]

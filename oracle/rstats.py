@@ -106,22 +106,38 @@ def _binom_dev(y, mu, wt):
     return np.sum(2.0 * wt * (_y_log_y(y, mu) + _y_log_y(1.0 - y, 1.0 - mu)))
 
 
-def glm_binomial(yprop, X, prior_w, epsilon=1e-8, maxit=25):
+_PROBIT_THRESH = 8.125890664701906     # -qnorm(.Machine$double.eps)
+
+
+def _probit_linkinv(eta):
+    from scipy.special import ndtr
+    return ndtr(np.clip(eta, -_PROBIT_THRESH, _PROBIT_THRESH))
+
+
+def _probit_mu_eta(eta):
+    return np.maximum(np.exp(-0.5 * eta * eta) / np.sqrt(2.0 * np.pi), _DBL_EPS)
+
+
+def glm_binomial(yprop, X, prior_w, epsilon=1e-8, maxit=25, link="logit"):
     """glm.fit IRLS for family=binomial(logit); returns (coef, vcov).
 
     vcov = chol2inv(R) of the final weighted QR (dispersion 1), as summary.glm.
     MK.R:53-55 then uses coef as beta.starting and t(chol(vcov)) as beta.tuning.
+    link="probit": make.link("probit") (linkinv pnorm of eta clamped to +-qnorm(eps),
+    mu.eta max(dnorm, eps), linkfun qnorm) -- the extension's start values.
     """
+    from scipy.special import ndtri
+    linkinv, mu_eta_f = (_logit_linkinv, _logit_mu_eta) if link == "logit" else (_probit_linkinv, _probit_mu_eta)
     X = np.asarray(X, dtype=np.float64)
     y = np.asarray(yprop, dtype=np.float64)
     wt = np.asarray(prior_w, dtype=np.float64)
     mu = (wt * y + 0.5) / (wt + 1.0)                  # binomial()$initialize
-    eta = np.log(mu / (1.0 - mu))
+    eta = np.log(mu / (1.0 - mu)) if link == "logit" else ndtri(mu)
     devold = _binom_dev(y, mu, wt)
     coef = None
     R = None
     for _ in range(maxit):
-        mu_eta = _logit_mu_eta(eta)
+        mu_eta = mu_eta_f(eta)
         varmu = mu * (1.0 - mu)
         good = (wt > 0) & (mu_eta != 0)
         z = eta[good] + (y[good] - mu[good]) / mu_eta[good]
@@ -130,7 +146,7 @@ def glm_binomial(yprop, X, prior_w, epsilon=1e-8, maxit=25):
         Qm, R = np.linalg.qr(Xw)
         coef = np.linalg.solve(R, Qm.T @ (z * w))
         eta = X @ coef
-        mu = _logit_linkinv(eta)
+        mu = linkinv(eta)
         dev = _binom_dev(y, mu, wt)
         if abs(dev - devold) / (abs(dev) + 0.1) < epsilon:
             break

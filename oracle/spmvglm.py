@@ -60,8 +60,28 @@ def softplus(x):
     return np.maximum(x, 0.0) + np.log1p(np.exp(-np.abs(x)))
 
 
-def loglik_terms(y, wt, eta):
-    """Binomial-logit log-likelihood per observation: y*eta - wt*log(1+exp(eta))."""
+LINK_LOGIT, LINK_PROBIT = 0, 1
+
+
+def log_ndtr(x):
+    """log Phi(x), the device's formula (csrc/mk_common.hpp log_norm_cdf): log1p(-erfc(x/sqrt2)/2)
+    for x >= 0, log(erfcx(-x/sqrt2)/2) - x^2/2 below (no underflow)."""
+    x = np.asarray(x, dtype=np.float64)
+    r = 0.7071067811865476
+    pos = x >= 0.0
+    out = np.empty_like(x)
+    out[pos] = np.log1p(-0.5 * ssp.erfc(x[pos] * r))
+    xn = x[~pos]
+    out[~pos] = np.log(0.5 * ssp.erfcx(-xn * r)) - 0.5 * xn * xn
+    return out
+
+
+def loglik_terms(y, wt, eta, link=LINK_LOGIT):
+    """Binomial log-likelihood per observation (constants dropped).  logit (spMvGLM's binomial
+    family, MK.R:80-84): y*eta - wt*log(1+exp(eta)); probit (north-star extension, no reference
+    parity target): y log Phi(eta) + (wt - y) log Phi(-eta)."""
+    if link == LINK_PROBIT:
+        return y * log_ndtr(eta) + (wt - y) * log_ndtr(-eta)
     return y * eta - wt * softplus(eta)
 
 
@@ -158,8 +178,9 @@ class Config:
                  phi_starting=None, phi_tuning=None, phi_unif=None,
                  A_starting=None, A_tuning=None, w_starting=0.0, w_tuning=0.5,
                  nu_starting=None, nu_tuning=None, nu_unif=None,
-                 K_IW_df=None, K_IW_S=None, burn_in=None, seed=20250114):
+                 K_IW_df=None, K_IW_S=None, burn_in=None, seed=20250114, link=LINK_LOGIT):
         self.q, self.p = q, p
+        self.link = int(link)
         self.cov_model = cov_model
         self.n_batch, self.batch_length = n_batch, batch_length
         self.n_samples = n_batch * batch_length
@@ -297,7 +318,7 @@ def fit_subset(coords, y, wt, X, cfg, subset=0, coords_test=None, record_w=False
         for j in range(p):
             delta = np.exp(tune[o_beta + j]) * zs[o_beta + j]
             eta_c = eta + delta * X[:, j]
-            ratio = np.sum(loglik_terms(y, wt, eta_c) - loglik_terms(y, wt, eta))
+            ratio = np.sum(loglik_terms(y, wt, eta_c, cfg.link) - loglik_terms(y, wt, eta, cfg.link))
             if logus[o_beta + j] <= ratio:
                 beta[j] += delta
                 eta = eta_c
@@ -372,7 +393,7 @@ def fit_subset(coords, y, wt, X, cfg, subset=0, coords_test=None, record_w=False
 
         # ---------------- 5. single-site w sweep (site-major, outcome-minor)
         delta_w = np.exp(tune[o_w:o_w + N]) * zs[o_w:o_w + N]
-        dll = loglik_terms(y, wt, eta + delta_w) - loglik_terms(y, wt, eta)
+        dll = loglik_terms(y, wt, eta + delta_w, cfg.link) - loglik_terms(y, wt, eta, cfg.link)
         lu = logus[o_w:o_w + N]
         Qdiag = np.stack([np.diag(Q[h]) for h in range(q)], axis=1)      # (n,q)
         for k in range(N):

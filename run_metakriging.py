@@ -88,24 +88,38 @@ def main():
 
     t2 = time.perf_counter()
     big = cfg.predict_tile > 0 and cfg.predict_tile < c["n_test"]
-    with mk.Session(subs, cfg, coords_test=d["coords_test"], subset_base=lo, device=local) as ses:   # MK.R:108
-        for b in range(cfg.n_batch):          # progress every n.report = 10 batches (MK.R:84)
-            ses.run(cfg.batch_length)
-            if rank == 0 and (b + 1) % 10 == 0:
-                print(f"batch {b + 1}/{cfg.n_batch}  {time.perf_counter() - t2:.1f}s", file=sys.stderr, flush=True)
+    C = q * c["n_test"]
+    P = cfg.P
+    if subs:
+        with mk.Session(subs, cfg, coords_test=d["coords_test"], subset_base=lo, device=local) as ses:   # MK.R:108
+            for b in range(cfg.n_batch):          # progress every n.report = 10 batches (MK.R:84)
+                ses.run(cfg.batch_length)
+                if rank == 0 and (b + 1) % 10 == 0:
+                    print(f"batch {b + 1}/{cfg.n_batch}  {time.perf_counter() - t2:.1f}s", file=sys.stderr, flush=True)
+            t3 = time.perf_counter()
+            # 1M sites: per-subset parameter grids, w.predict only as this shard's partial sum
+            out = ses.outputs(quantiles=True, w_predict=not big, w_predict_sum=big)
+    else:                                         # K < world: this rank has no subsets, it joins the exchange
         t3 = time.perf_counter()
-        # 1M sites: per-subset parameter grids, w.predict only as this shard's partial sum
-        out = ses.outputs(quantiles=True, w_predict=not big, w_predict_sum=big)
+        out = {"parameters": [], "w_predict": [], "w_predict_sum": np.zeros((200, C))}
     t["fit_s"] = t3 - t2
     t["predict_quantiles_s"] = time.perf_counter() - t3
 
     t4 = time.perf_counter()
-    if world > 1 and not big:
+    par = np.stack(out["parameters"]) if out["parameters"] else np.zeros((0, 200, P))
+    if world > 1:
         import torch
         dev = torch.device("cuda", local)
-        par = np.stack(out["parameters"])
         result = dmod.combine_sharded(par, K, dist, method=a.combine, device=dev, gpu=local)   # MK.R:123-127
-        result2 = dmod.combine_sharded(np.stack(out["w_predict"]), K, dist, method=a.combine, device=dev, gpu=local)
+        if not big:
+            wp = np.stack(out["w_predict"]) if out["w_predict"] else np.zeros((0, 200, C))
+            result2 = dmod.combine_sharded(wp, K, dist, method=a.combine, device=dev, gpu=local)
+        else:
+            # tiled kriging (cfg5): every rank holds only its shard's partial sum of w.predict;
+            # result2 = (S_0 + S_1 + ...) / K with the rank terms added in rank order
+            if a.combine != "mean":
+                raise SystemExit("error: --combine median needs the per-subset grids (not available with predict_tile)")
+            result2 = dmod.combine_partial_sums(out["w_predict_sum"], K, dist, device=dev, gpu=local)
     elif not big:
         obj = [{"parameters": out["parameters"][i], "w.predict": out["w_predict"][i]} for i in range(len(subs))]
         result, result2 = mk.combine_results(obj, device=local, method=a.combine)             # MK.R:123-133

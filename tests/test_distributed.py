@@ -128,3 +128,73 @@ def test_col_blocks_cover_columns():
         for world in (1, 2, 3, 8):
             b = dmod.col_blocks(C, world)
             assert b[0][0] == 0 and b[-1][1] == C and all(x[1] == y[0] for x, y in zip(b, b[1:]))
+
+
+def test_shard_range_balanced():
+    """Balanced contiguous shards (ADVICE: ceil blocks left ranks empty, e.g. K=5 on 8 GPUs):
+    sizes differ by at most one and no rank is empty while K >= world."""
+    dmod = importlib.import_module(PKG + ".distributed")
+    for K in (1, 5, 8, 20, 250):
+        for world in (1, 2, 3, 8):
+            sizes = [hi - lo for lo, hi in (dmod.shard_range(K, world, r) for r in range(world))]
+            assert sum(sizes) == K and max(sizes) - min(sizes) <= 1
+            if K >= world:
+                assert min(sizes) >= 1
+    assert [dmod.shard_range(250, 8, r) for r in (0, 7)] == [(0, 31), (218, 250)]
+
+
+def _seq_sum(grids):
+    acc = np.array(grids[0], copy=True)
+    for g in grids[1:]:
+        acc = acc + g
+    return acc
+
+
+def _partial_worker(rank, world, port, K, C, out_q):
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    dmod = importlib.import_module(PKG + ".distributed")
+    lo, hi = dmod.shard_range(K, world, rank)
+    # this rank's term of the combine: its subsets' grids summed in subset order (w_predict_sum)
+    part = _seq_sum([_grid_wide(k, C) for k in range(lo, hi)]) if hi > lo else np.zeros((200, C))
+    full = dmod.combine_partial_sums(part, K, dist, combine_fn=_seq_sum)
+    # an empty shard (K < world) still joins the column-sharded exchange
+    k_small = world - 1
+    lo2, hi2 = dmod.shard_range(k_small, world, rank)
+    local = np.stack([_grid_wide(k, C) for k in range(lo2, hi2)]) if hi2 > lo2 else np.zeros((0, 200, C))
+    from oracle.spmvglm import combine_mean
+    small = dmod.combine_sharded(local, k_small, dist, combine_fn=combine_mean)
+    out_q.put((rank, full, small))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("K,C,world", [(7, 9, 2), (10, 4, 3)])
+def test_partial_sums_and_empty_shards(K, C, world):
+    """cfg5 path (ADVICE high): per-rank partial sums of w.predict combined in rank order,
+    result2 = (S_0 + S_1 + ...) / K on every rank; and a K < world exchange with an empty rank."""
+    import torch.multiprocessing as mp
+    from oracle.spmvglm import combine_mean
+    dmod = importlib.import_module(PKG + ".distributed")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_partial_worker, args=(r, world, port, K, C, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    terms = []
+    for r in range(world):
+        lo, hi = dmod.shard_range(K, world, r)
+        terms.append(_seq_sum([_grid_wide(k, C) for k in range(lo, hi)]))
+    ref = _seq_sum(terms) / K
+    one_gpu = combine_mean([_grid_wide(k, C) for k in range(K)])
+    small_ref = combine_mean([_grid_wide(k, C) for k in range(world - 1)])
+    for rank, full, small in res:
+        assert np.array_equal(full, ref)
+        np.testing.assert_allclose(full, one_gpu, rtol=1e-13, atol=1e-13)   # re-association only
+        assert np.array_equal(small, small_ref)

@@ -36,6 +36,28 @@ def test_posterior_summary_matches_oracle(mk, C, p, S):
     np.testing.assert_allclose(dev["p_quant"], ref["p_quant"], rtol=1e-14, atol=0)
 
 
+@pytest.mark.parametrize("link", ["logit", "probit"])
+def test_posterior_summary_r_stream_index(mk, link):
+    """MK.R:141 on R's stream: rng="R" draws sampleparIndex as sample(seq(1, 996, 1), S, replace=TRUE)
+    right after set.seed(seed) (mk_r_sample_replace); the summaries then match the oracle given
+    R's index.  link="probit": p(y=1) = Phi(eta)."""
+    from oracle.rrng import RRng
+    C, p, S, seed = 40, 2, 1000, 20250114
+    g = _grids(1, C=4 + C, seed=3)[0]
+    res, res2 = g[:, :4], g[:, 4:]
+    x_test = np.random.default_rng(2).normal(size=(C, p))
+    dev = mk.posterior_summary(res, res2, x_test, samplesize=S, seed=seed, rng="R", link=link)
+    r_idx = RRng(seed).sample_int_replace(996, S)
+    ref = post.posterior_summary(res, res2, x_test, samplesize=S, index=r_idx, link=link)
+    assert np.array_equal(dev["index"], np.asarray(r_idx) - 1)
+    assert np.array_equal(dev["SamplePar"], ref["SamplePar"])
+    assert np.array_equal(dev["Samplew"], ref["Samplew"])
+    np.testing.assert_allclose(dev["p_sample"], ref["p_sample"], rtol=1e-14, atol=1e-300)
+    assert np.array_equal(dev["w_quant"], ref["w_quant"])
+    dev2 = mk.posterior_summary(res, res2, x_test, samplesize=S, index=r_idx, link=link)
+    assert np.array_equal(dev2["SamplePar"], dev["SamplePar"])
+
+
 def test_posterior_summary_parameters_only(mk):
     res = _grids(1, C=3, seed=9)[0]
     dev = mk.posterior_summary(res, None, None, samplesize=500, seed=2)
@@ -70,6 +92,16 @@ def test_glm_start_values_match_oracle(mk, q, n):
     np.testing.assert_allclose(bt @ bt.T, vcov, rtol=1e-12)        # t(chol(vcov)) is lower
 
 
+@pytest.mark.parametrize("q,n", [(1, 20000), (2, 6000)])
+def test_glm_probit_start_values_match_oracle(mk, q, n):
+    """binomial(link = "probit") IRLS (extension's start values) vs the QR oracle."""
+    d = mk.synthetic.generate(n, q=q, n_test=0, seed=9, link="probit")
+    coef, vcov, bt = mk.glm_binomial(d["y"], d["x"], np.ones(n * q), link="probit")
+    rc, rv = rstats.glm_binomial(d["y"], d["x"], np.ones(n * q), link="probit")
+    np.testing.assert_allclose(coef, rc, rtol=1e-10)
+    np.testing.assert_allclose(vcov, rv, rtol=1e-8)
+
+
 def test_glm_binomial_trials(mk):
     """weights > 1: glm((y/weight) ~ x - 1, weights = weight) on counts."""
     rng = np.random.default_rng(3)
@@ -98,3 +130,20 @@ def test_stream_grouping_does_not_change_the_chains(mk):
             assert np.array_equal(o["samples"][s], outs[0]["samples"][s])
             assert np.array_equal(o["w_pred_samples"][s], outs[0]["w_pred_samples"][s])
             assert np.array_equal(o["w_predict"][s], outs[0]["w_predict"][s])
+
+
+def test_torch_first_process_rccl_combine(mk):
+    """Multi-GPU launch order (torch's HIP runtime + an RCCL group initialised before libmk loads,
+    as bench.py / run_metakriging.py do under torch.distributed.run), in a fresh process: a chain
+    replays the oracle and the device-resident column-sharded combine -- mean, sum, Weiszfeld
+    median, rank-ordered partial sums -- matches the CPU restatements (MK.R:123-133)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    r = subprocess.run([sys.executable, os.path.join(here, "gpu_torch_first.py")], capture_output=True, text=True,
+                       timeout=240, env=dict(os.environ, MASTER_ADDR="127.0.0.1"))
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert r.returncode == 0 and lines, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
+    assert json.loads(lines[-1])["ok"]

@@ -13,16 +13,17 @@ TOL = 1e-8
 
 
 def _run_both(mk, n, q, cov, n_test=12, n_batch=3, batch_length=4, burn_in=7, seed=9, subset_base=0, S=2,
-              sizes=None):
+              sizes=None, link="logit"):
     sizes = list(sizes) if sizes is not None else [n] * S
     off = np.concatenate([[0], np.cumsum(sizes)])
-    d = mk.synthetic.generate(int(off[-1]), q=q, n_test=n_test, seed=seed + q, cov_model=cov)
+    d = mk.synthetic.generate(int(off[-1]), q=q, n_test=n_test, seed=seed + q, cov_model=cov, link=link)
     ct = d["coords_test"] if n_test else None
     p = 2 * q
     kw = dict(n_batch=n_batch, batch_length=batch_length, burn_in=burn_in, seed=seed)
     cfg = mk.SamplerConfig(q, p, beta_starting=np.zeros(p), beta_tuning=np.full(p, 0.05),
-                           cov_model="matern" if cov else "exponential", **kw)
-    ocfg = om.Config(q, p, beta_starting=np.zeros(p), beta_tuning=np.full(p, 0.05), cov_model=cov, **kw)
+                           cov_model="matern" if cov else "exponential", link=link, **kw)
+    ocfg = om.Config(q, p, beta_starting=np.zeros(p), beta_tuning=np.full(p, 0.05), cov_model=cov,
+                     link=om.LINK_PROBIT if link == "probit" else om.LINK_LOGIT, **kw)
     subs = []
     for s, m in enumerate(sizes):
         sl = slice(off[s], off[s] + m)
@@ -113,6 +114,14 @@ def test_replay_lmc_ragged_multi_tile(mk):
     for q, sizes in ((2, [700, 513]), (3, [600, 129])):
         dev, refs = _run_both(mk, None, q, 0, sizes=sizes, n_test=24, n_batch=2, batch_length=2, burn_in=3)
         _check(dev, refs)
+
+
+@pytest.mark.parametrize("n,q,cov", [(150, 1, 0), (48, 2, 0), (100, 1, 1), (40, 3, 0)])
+def test_replay_probit_matches_oracle(mk, n, q, cov):
+    """Probit link (north-star "logit/probit"; the reference is logit, so the oracle's probit
+    likelihood is the spec): y log Phi(eta) + (wt - y) log Phi(-eta) in the beta and w steps."""
+    dev, refs = _run_both(mk, n, q, cov, link="probit")
+    _check(dev, refs)
 
 
 def test_replay_subset_beyond_2048_sites(mk):

@@ -50,6 +50,7 @@ def test_no_gpu_errors_cleanly(mk):
     cfg = mk.SamplerConfig(1, 2, [0, 0], [0.1, 0.1], n_batch=1, batch_length=2)
     with pytest.raises(mk.MkError):
         mk.Session([dict(coords=d["coords"], y=d["y"], weights=np.ones(20), x=d["x"])], cfg)
+    assert lib.mk_session_count() == 0             # nothing left behind by the failed create
 
 
 def test_partition_sizes_follow_reference(mk):

@@ -167,3 +167,40 @@ def test_posterior_recovers_truth():
 def test_combine_mean_sequential_order():
     g = [np.full((2, 2), v) for v in (0.1, 0.2, 0.3)]
     np.testing.assert_array_equal(om.combine_mean(g), ((g[0] + g[1]) + g[2]) / 3)
+
+
+def test_log_ndtr_matches_scipy():
+    """The probit log-likelihood's log Phi (device formula restated) vs scipy.special.log_ndtr."""
+    import scipy.special as ssp
+    x = np.concatenate([np.linspace(-60, 40, 20001), [-1e-300, 0.0, 1e-300, -8.3, 8.3]])
+    np.testing.assert_allclose(om.log_ndtr(x), ssp.log_ndtr(x), rtol=2e-14, atol=1e-300)
+
+
+def test_probit_glm_solves_score_equations():
+    """binomial(link = "probit") IRLS: the MLE's score sum_i (y - mu) phi(eta) / (mu (1 - mu)) x_i is ~0,
+    and it recovers the generating coefficients of a large probit sample."""
+    from scipy.special import ndtr
+    from oracle import rstats
+    rng = np.random.default_rng(5)
+    n = 20000
+    X = np.column_stack([np.ones(n), rng.normal(size=n)])
+    y = (rng.uniform(size=n) < ndtr(X @ np.array([0.4, -0.7]))).astype(float)
+    coef, vcov = rstats.glm_binomial(y, X, np.ones(n), link="probit")
+    eta = X @ coef
+    mu = ndtr(eta)
+    score = X.T @ ((y - mu) * np.exp(-0.5 * eta * eta) / np.sqrt(2 * np.pi) / (mu * (1 - mu)))
+    assert np.max(np.abs(vcov @ score)) < 1e-6      # remaining Newton step (glm.fit stops on deviance)
+    assert np.all(np.abs(coef - [0.4, -0.7]) < 4 * np.sqrt(np.diag(vcov)))
+
+
+def test_probit_chain_matches_literal():
+    """The incremental probit chain equals the literal full-recompute restatement (q = 1, 2)."""
+    from oracle import literal
+    for q, n in ((1, 25), (2, 12)):
+        d = syn.generate(n, q=q, n_test=0, seed=40 + q, link="probit")
+        p = 2 * q
+        cfg = om.Config(q, p, beta_starting=np.zeros(p), beta_tuning=np.full(p, 0.05), n_batch=2, batch_length=3,
+                        burn_in=4, seed=3, link=om.LINK_PROBIT)
+        a = om.fit_subset(d["coords"], d["y"], np.ones(n * q), d["x"], cfg, subset=1)
+        b = literal.fit_subset_literal(d["coords"], d["y"], np.ones(n * q), d["x"], cfg, subset=1)
+        np.testing.assert_allclose(a["samples"], b["samples"], rtol=0, atol=1e-9)

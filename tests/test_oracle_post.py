@@ -81,3 +81,21 @@ def test_weiszfeld_small_K(K):
     assert med.shape == (200, 3) and np.all(np.isfinite(med)) and it.min() >= 1
     if K <= 2:                                     # any point of the segment is a median; we stay at the mean
         np.testing.assert_allclose(med, combine_mean(list(g)), rtol=1e-12, atol=1e-12)
+
+
+def test_posterior_summary_r_index_and_probit():
+    """A caller-given (R-stream) 1-based sampleparIndex is used as is; link="probit" gives
+    p(y=1) = Phi(eta) (extension; MK.R:160 is logistic)."""
+    from scipy.special import ndtr
+    from oracle.rrng import RRng
+    g = _grids(1, C=7, seed=4)[0]
+    res, res2 = g[:, :4], g[:, 4:]
+    x_test = np.column_stack([np.ones(3), np.linspace(-1, 1, 3)])
+    idx1 = RRng(20250114).sample_int_replace(996, 800)
+    out = post.posterior_summary(res, res2, x_test, samplesize=800, index=idx1, link="probit")
+    assert np.array_equal(out["index"], np.asarray(idx1) - 1)
+    interp = lambda y: np.stack([np.interp(rstats.XOUT996, rstats.PROBS200, y[:, c])   # noqa: E731
+                                 for c in range(y.shape[1])], axis=1)
+    np.testing.assert_allclose(out["SamplePar"], interp(res)[np.asarray(idx1) - 1], rtol=1e-14, atol=1e-14)
+    eta = out["SamplePar"][:, :2] @ x_test.T + out["Samplew"]
+    np.testing.assert_allclose(out["p_sample"], ndtr(eta), rtol=1e-14)

@@ -82,3 +82,27 @@ def test_partition_errors(mk):
         mk.metakriging.partition(0, 3, seed=1, method="R")
     with pytest.raises(ValueError):
         mk.metakriging.partition(10, 3, seed=1, method="bogus")
+
+
+# sample(1:n, size, replace = TRUE) after set.seed(seed), R >= 3.6.0 console output
+KNOWN_SAMPLE_REPLACE = {(123, 6, 10): [3, 6, 3, 2, 2, 6, 3, 5, 4, 6],
+                        (42, 10, 5): [1, 5, 1, 9, 10]}
+
+
+@pytest.mark.parametrize("key", sorted(KNOWN_SAMPLE_REPLACE))
+def test_oracle_sample_replace_known_answers(key):
+    seed, n, size = key
+    assert rrng.RRng(seed).sample_int_replace(n, size) == KNOWN_SAMPLE_REPLACE[key]
+
+
+@pytest.mark.parametrize("key", sorted(KNOWN_SAMPLE_REPLACE) + [(20250114, 996, 1000), (7, 70000, 50)])
+def test_lib_sample_replace_matches_oracle(mk, key):
+    """mk_r_sample_replace: MK.R:141's sampleparIndex (sample(seq(1, 996, 1), 1000, replace=TRUE))
+    as R draws it right after set.seed(seed); n > 2^16 takes the two-draw rbits path."""
+    seed, n, size = key
+    lib = mk._lib.load()
+    out = np.zeros(size, dtype=np.int32)
+    mk._lib.check(lib.mk_r_sample_replace(seed, n, size, mk._lib.iptr(out)))
+    assert out.tolist() == rrng.RRng(seed).sample_int_replace(n, size)
+    if key in KNOWN_SAMPLE_REPLACE:
+        assert out.tolist() == KNOWN_SAMPLE_REPLACE[key]
