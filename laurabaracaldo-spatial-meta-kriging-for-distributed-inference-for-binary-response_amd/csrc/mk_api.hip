@@ -14,11 +14,14 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
+#include <utility>
 #include <memory>
 #include <string>
 #include <vector>
 #include "../../include/mk.h"
 #include "mk_kernels.hpp"
+#include "mk_gemm.hpp"
 
 using namespace mk;
 
@@ -228,13 +231,35 @@ static void drain_timers(mk_session* s) {
 
 static inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
 
-// Every tile-GEMM kernel takes MK_GD_LDS_BYTES (> 64 KiB) of dynamic LDS: two DMA stages.
+// Every tile-GEMM kernel takes gb_lds_bytes(TM, TN) of dynamic LDS: two DMA stages (> 64 KiB at 128 x 128).
+static constexpr size_t LDS_128 = gb_lds_bytes(128, 128), LDS_64 = gb_lds_bytes(64, 64),
+                        LDS_64x128 = gb_lds_bytes(64, 128);
 static bool set_gemm_lds() {
-  for (const void* kfn : {(const void*)k_chol_update, (const void*)k_chol_trsm, (const void*)k_inv_level,
-                          (const void*)k_qblocks, (const void*)k_lauum, (const void*)k_pred_var})
-    if (hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, MK_GD_LDS_BYTES) != hipSuccess)
+  const std::pair<const void*, size_t> fns[] = {
+      {(const void*)k_chol_update<128>, LDS_128}, {(const void*)k_chol_update<64>, LDS_64},
+      {(const void*)k_chol_trsm<128>, LDS_128},   {(const void*)k_chol_trsm<64>, LDS_64x128},
+      {(const void*)k_inv_level<128>, LDS_128},   {(const void*)k_inv_level<64>, LDS_64},
+      {(const void*)k_qblocks, LDS_64},           {(const void*)k_lauum, LDS_128},
+      {(const void*)k_pred_var, LDS_128}};
+  for (const auto& f : fns)
+    if (hipFuncSetAttribute(f.first, hipFuncAttributeMaxDynamicSharedMemorySize, (int)f.second) != hipSuccess)
       return false;
   return true;
+}
+
+// Tile shape of a GEMM launch: 64-sub-tiles (bit-identical, mk_gemm.hpp) when the 128-tile grid
+// would leave the chip short of work -- fewer than MK_TILE_THRESH workgroups (default 512, two
+// per CU).  MK_TILE=64 / 128 forces one shape (tests compare them).
+static int tile_env(const char* name, int dflt) {
+  const char* v = std::getenv(name);
+  return (v && *v) ? std::atoi(v) : dflt;
+}
+static bool use_sub_tiles(long wg128) {
+  static const int force = tile_env("MK_TILE", 0);
+  static const int thresh = tile_env("MK_TILE_THRESH", 512);
+  if (force == 64) return true;
+  if (force == 128) return false;
+  return wg128 < thresh;
 }
 
 // ------------------------------------------------------------------ Cholesky of all candidates of outcome h
@@ -267,8 +292,12 @@ static void launch_cholesky(mk_session* s, Group& g, int h0, int hc, const int* 
     if (k > 0) {
       // rows below the panel start x panel columns x K, per factor
       timed(s, g.stream, KS_CHOL_UPDATE, panel_flops(k, false), [&] {
-        hipLaunchKernelGGL(k_chol_update, dim3(xcd_grid_h(E, nt - k)), dim3(256), MK_GD_LDS_BYTES, g.stream, g.ms, S, h0, hc, k,
-                           slist, scount);
+        if (use_sub_tiles((long)E * (nt - k)))
+          hipLaunchKernelGGL(k_chol_update<64>, dim3(xcd_grid_h(E, (nt - k) * 4)), dim3(256), LDS_64, g.stream, g.ms, S, h0,
+                             hc, k, slist, scount);
+        else
+          hipLaunchKernelGGL(k_chol_update<128>, dim3(xcd_grid_h(E, nt - k)), dim3(256), LDS_128, g.stream, g.ms, S, h0,
+                             hc, k, slist, scount);
       });
     }
     timed(s, g.stream, KS_CHOL_DIAG, 0.0, [&] {
@@ -277,8 +306,12 @@ static void launch_cholesky(mk_session* s, Group& g, int h0, int hc, const int* 
     });
     if (k < nt - 1) {
       timed(s, g.stream, KS_CHOL_TRSM, panel_flops(k, true), [&] {
-        hipLaunchKernelGGL(k_chol_trsm, dim3(xcd_grid_h(E, nt - k - 1)), dim3(256), MK_GD_LDS_BYTES, g.stream, g.ms, S, h0, hc, k,
-                           slist, scount);
+        if (use_sub_tiles((long)E * (nt - k - 1)))
+          hipLaunchKernelGGL(k_chol_trsm<64>, dim3(xcd_grid_h(E, (nt - k - 1) * 2)), dim3(256), LDS_64x128, g.stream, g.ms,
+                             S, h0, hc, k, slist, scount);
+        else
+          hipLaunchKernelGGL(k_chol_trsm<128>, dim3(xcd_grid_h(E, nt - k - 1)), dim3(256), LDS_128, g.stream, g.ms, S, h0,
+                             hc, k, slist, scount);
       });
     }
   }
@@ -290,11 +323,15 @@ static void launch_trinv(mk_session* s, Group& g, int max_entries, const int* li
   hipLaunchKernelGGL(k_inv_copydiag, dim3(max_entries * nt), dim3(256), 0, g.stream, g.ms, list, count);
   for (int sz = 1; sz < nt; sz *= 2) {
     const int npairs = (nt + 2 * sz - 1) / (2 * sz);
+    const bool sub = use_sub_tiles((long)max_entries * npairs * sz * sz);
     for (int phase = 0; phase < 2; ++phase)
       timed(s, g.stream, KS_INV, 0.0, [&] {
-        hipLaunchKernelGGL(k_inv_level, dim3(xcd_grid_h(max_entries, npairs * sz * sz)), dim3(256), MK_GD_LDS_BYTES,
-                           g.stream, g.ms,
-                           list, count, sz, phase);
+        if (sub)
+          hipLaunchKernelGGL(k_inv_level<64>, dim3(xcd_grid_h(max_entries, npairs * sz * sz * 4)), dim3(256), LDS_64,
+                             g.stream, g.ms, list, count, sz, phase);
+        else
+          hipLaunchKernelGGL(k_inv_level<128>, dim3(xcd_grid_h(max_entries, npairs * sz * sz)), dim3(256), LDS_128,
+                             g.stream, g.ms, list, count, sz, phase);
       });
   }
 }
@@ -304,8 +341,8 @@ static void launch_inverse(mk_session* s, Group& g) {
   const int nt = s->nt, max_entries = g.S * s->q;
   launch_trinv(s, g, max_entries, g.d_list, g.d_count);
   timed(s, g.stream, KS_LAUUM, 0.0, [&] {
-    hipLaunchKernelGGL(k_qblocks, dim3(xcd_grid_h(max_entries, nt)), dim3(256), MK_GD_LDS_BYTES, g.stream, g.ms, g.md.n_s, g.d_list,
-                       g.d_count);
+    hipLaunchKernelGGL(k_qblocks, dim3(xcd_grid_h(max_entries, nt * 2)), dim3(256), LDS_64, g.stream, g.ms, g.md.n_s,
+                       g.d_list, g.d_count);
   });
   hipLaunchKernelGGL(k_take_border, dim3(max_entries * ((s->n_pad + 255) / 256)), dim3(256), 0, g.stream, g.md, g.ms,
                      g.d_list, g.d_count);
@@ -317,7 +354,7 @@ static void launch_pred_refresh(mk_session* s, Group& g) {
   if (md.n_test <= 0) return;
   const int nt = s->nt, max_entries = g.S * s->q;
   hipLaunchKernelGGL(pred_PT_kernel(md.cov_model), dim3(max_entries * md.n_pad), dim3(256), 0, g.stream, md, g.d_plist, g.d_pcount);
-  hipLaunchKernelGGL(k_pred_var, dim3(xcd_grid_h(max_entries, nt * md.ntt)), dim3(256), MK_GD_LDS_BYTES, g.stream, md, g.ms,
+  hipLaunchKernelGGL(k_pred_var, dim3(xcd_grid_h(max_entries, nt * md.ntt)), dim3(256), LDS_128, g.stream, md, g.ms,
                      g.d_plist, g.d_pcount);
   hipLaunchKernelGGL(k_pred_var_reduce, dim3(max_entries * (md.n_test_pad / 256)), dim3(256), 0, g.stream, md, nt,
                      g.d_plist, g.d_pcount);
@@ -1309,7 +1346,7 @@ extern "C" int mk_cholesky_batched(const double* A, int32_t S, int32_t n, double
                        a.d_count);
     const int ntiles = nt * (nt + 1) / 2;
     launch_trinv(s, a, S, a.d_list, a.d_count);
-    hipLaunchKernelGGL(k_lauum, dim3(S * ntiles), dim3(256), MK_GD_LDS_BYTES, s->stream, ms, md.n_s, a.d_list, a.d_count);
+    hipLaunchKernelGGL(k_lauum, dim3(S * ntiles), dim3(256), LDS_128, s->stream, ms, md.n_s, a.d_list, a.d_count);
     hipLaunchKernelGGL(k_extract_L, dim3(2048), dim3(256), 0, s->stream, ms, n, S, dL, 1);
     if (hipMemcpyAsync(inv_out, dL, (size_t)S * n * n * 8, hipMemcpyDeviceToHost, s->stream) != hipSuccess)
       return fail(set_err(MK_E_HIP, "inverse download"));

@@ -12,11 +12,14 @@ typedef void (*CovCandidateKernel)(Model, MatSet, int, int, int, int, const int*
 inline CovCandidateKernel cov_candidate_kernel(int model) {
   return model == MK_COV_EXPONENTIAL ? k_cov_candidate<MK_COV_EXPONENTIAL> : k_cov_candidate<MK_COV_MATERN>;
 }
+template <int TM>
 __global__ void k_chol_update(MatSet ms, int S, int h0, int hc, int k, const int* slist, const int* scount);
+template <int TM>
 __global__ void k_chol_trsm(MatSet ms, int S, int h0, int hc, int k, const int* slist, const int* scount);
 __global__ void k_chol_diag(MatSet ms, const int* n_s, int h0, int hc, int k, double* ld_part, double* quad_c, int* info,
                             const int* slist, const int* scount);
 __global__ void k_inv_copydiag(MatSet ms, const int* list, const int* count);
+template <int TM>
 __global__ void k_inv_level(MatSet ms, const int* list, const int* count, int sz, int phase);
 __global__ void k_lauum(MatSet ms, const int* n_s, const int* list, const int* count);
 __global__ void k_qblocks(MatSet ms, const int* n_s, const int* list, const int* count);

@@ -264,43 +264,65 @@ template __global__ void k_cov_candidate<MK_COV_MATERN>(Model, MatSet, int, int,
 // (Generating C(i,k) from coordinates at its first touch inside this kernel was measured
 // slower on cfg3 and its code path made the kernel spill 80 VGPRs: candidates come from
 // k_cov_candidate.)
+// TM = 128: one workgroup per 128-tile.  TM = 64: four per tile (small shards: late panels have
+// few tiles and long K), bit-identical (mk_gemm.hpp); the upper quadrant of the diagonal tile is
+// skipped -- k_chol_diag reads the lower triangle only.
+template <int TM>
 __global__ __launch_bounds__(256, 2) void k_chol_update(MatSet ms, int S, int h0, int hc, int k, const int* slist,
                                                        const int* scount) {
-  extern __shared__ __attribute__((aligned(16))) double lds[];   // GD_LDS_BYTES (two DMA stages)
+  extern __shared__ __attribute__((aligned(16))) double lds[];   // gb_lds_bytes(TM, TM) (two DMA stages)
+  constexpr int SUB = (MK_NB / TM) * (MK_NB / TM);
   const int ntk = ms.nt - k;
   int e, t, s, h;
-  if (!xcd_map(active_pairs(slist, scount, S, hc), ntk, &e, &t) || !pick_pair(slist, scount, e, h0, hc, &s, &h)) return;
+  if (!xcd_map(active_pairs(slist, scount, S, hc), ntk * SUB, &e, &t) || !pick_pair(slist, scount, e, h0, hc, &s, &h))
+    return;
+  const int st = t % SUB;
+  t /= SUB;
+  const int sr = st & 1, sc = st >> 1;   // (0, 0) when TM = 128
   const int i = k + t;
+  if (i == k && sc > sr) return;
   const int sh = s * ms.q + h;
   double* M = mat_slot(ms, sh, 1 - ms.cur[sh]);
   const long ld = ms.ld;
-  double* C = M + i * MK_NB + (long)k * MK_NB * ld;
-  Acc acc;
+  double* C = M + i * MK_NB + sr * TM + (long)(k * MK_NB + sc * TM) * ld;
+  AccT<TM / 32, TM / 32> acc;
   acc_load(acc, C, ld);
   // (Skipping the diagonal tiles' unused upper quadrant -- per MFMA or per chunk -- measured slower.)
-  gemm_128<true, true, true>(M + i * MK_NB, ld, M + k * MK_NB, ld, k * MK_NB, k * MK_NB, acc, lds);
+  gemm_tile<TM, TM, true, true, true>(M + i * MK_NB + sr * TM, ld, M + k * MK_NB + sc * TM, ld, k * MK_NB, k * MK_NB,
+                                      acc, lds);
   store_tile(C, ld, acc);
 }
+template __global__ void k_chol_update<128>(MatSet, int, int, int, int, const int*, const int*);
+template __global__ void k_chol_update<64>(MatSet, int, int, int, int, const int*, const int*);
 
+// TM = 64: the tile's two row halves on two workgroups (in place: each reads and writes its own
+// rows only), bit-identical.
+template <int TM>
 __global__ __launch_bounds__(256, 2) void k_chol_trsm(MatSet ms, int S, int h0, int hc, int k, const int* slist,
                                                      const int* scount) {
-  extern __shared__ __attribute__((aligned(16))) double lds[];   // MK_GD_LDS_BYTES
+  extern __shared__ __attribute__((aligned(16))) double lds[];   // gb_lds_bytes(TM, 128)
+  constexpr int SUB = MK_NB / TM;
   const int ntk = ms.nt - k - 1;
   int e, t, s, h;
-  if (!xcd_map(active_pairs(slist, scount, S, hc), ntk, &e, &t) || !pick_pair(slist, scount, e, h0, hc, &s, &h)) return;
+  if (!xcd_map(active_pairs(slist, scount, S, hc), ntk * SUB, &e, &t) || !pick_pair(slist, scount, e, h0, hc, &s, &h))
+    return;
+  const int sr = t % SUB;
+  t /= SUB;
   const int i = k + 1 + t;
   const int sh = s * ms.q + h;
   const int slot = 1 - ms.cur[sh];
   double* M = mat_slot(ms, sh, slot);
   const double* W = winv_slot(ms, sh, slot, k);
   const long ld = ms.ld;
-  double* C = M + i * MK_NB + (long)k * MK_NB * ld;
-  Acc acc;
+  double* C = M + i * MK_NB + sr * TM + (long)k * MK_NB * ld;
+  AccT<TM / 32, 4> acc;
   acc_zero(acc);
   // Winv_k lower triangular: (C Winv^T)(m, n) = sum_{j <= n} C(m, j) Winv(n, j)
-  gemm_128<true, true, false, false, false, SKIP_TRI_B>(C, ld, W, MK_NB, MK_NB, MK_NB, acc, lds);
+  gemm_tile<TM, 128, true, true, false, false, false, SKIP_TRI_B>(C, ld, W, MK_NB, MK_NB, MK_NB, acc, lds);
   store_tile(C, ld, acc);
 }
+template __global__ void k_chol_trsm<128>(MatSet, int, int, int, int, const int*, const int*);
+template __global__ void k_chol_trsm<64>(MatSet, int, int, int, int, const int*, const int*);
 
 // ---------------------------------------------------------------- diagonal tile: factor + invert in LDS
 // 128x128 tile T (column-major, stride TLD) in LDS, 256 threads, blocked by 16 (see
@@ -613,13 +635,19 @@ __global__ __launch_bounds__(256) void k_inv_copydiag(MatSet ms, const int* __re
 //   phase 0: Y_BT = L_BT W_TT        (Y kept in the free factor slot)
 //   phase 1: W_BT = -W_BB Y_BT
 // with W_TT, W_BB complete from the lower levels.  Triangularity bounds every K range.
+// TM = 64: each 128-tile on four workgroups (small shards), bit-identical.
+template <int TM>
 __global__ __launch_bounds__(256, 2) void k_inv_level(MatSet ms, const int* __restrict__ list,
                                                       const int* __restrict__ count, int sz, int phase) {
-  extern __shared__ __attribute__((aligned(16))) double lds[];   // MK_GD_LDS_BYTES
+  extern __shared__ __attribute__((aligned(16))) double lds[];   // gb_lds_bytes(TM, TM)
+  constexpr int SUB = (MK_NB / TM) * (MK_NB / TM);
   const int npairs = (ms.nt + 2 * sz - 1) / (2 * sz);
   const int per = npairs * sz * sz;
   int e, t;
-  if (!xcd_map(*count, per, &e, &t)) return;
+  if (!xcd_map(*count, per * SUB, &e, &t)) return;
+  const int st = t % SUB;
+  t /= SUB;
+  const int sr = st & 1, sc = st >> 1;
   const int p = t / (sz * sz);
   t %= sz * sz;
   const int T0 = 2 * p * sz, B0 = T0 + sz;
@@ -632,22 +660,26 @@ __global__ __launch_bounds__(256, 2) void k_inv_level(MatSet ms, const int* __re
   const long ld = ms.ld;
   double* Wm = wmat(ms, sh);
   double* Y = mat_slot(ms, sh, 1 - cur);
-  Acc acc;
+  const int ro = sr * TM;             // sub-tile row / column offsets in the 128-tile
+  const long co = (long)sc * TM * ld;
+  AccT<TM / 32, TM / 32> acc;
   acc_zero(acc);
   if (phase == 0) {
     const double* Lm = mat_slot(ms, sh, cur);
     const int K = (B0 - j) * MK_NB;
     // K ranges [j, B0) share their end: descending chunks keep the tiles of a subset in step (L2 reuse)
-    gemm_128<true, false, false, true>(Lm + i * MK_NB + (long)j * MK_NB * ld, ld, Wm + j * MK_NB + (long)j * MK_NB * ld,
-                                       ld, K, K, acc, lds);
-    store_tile(Y + i * MK_NB + (long)j * MK_NB * ld, ld, acc);
+    gemm_tile<TM, TM, true, false, false, true>(Lm + i * MK_NB + ro + (long)j * MK_NB * ld, ld,
+                                                Wm + j * MK_NB + (long)j * MK_NB * ld + co, ld, K, K, acc, lds);
+    store_tile(Y + i * MK_NB + ro + (long)j * MK_NB * ld + co, ld, acc);
   } else {
     const int K = (i - B0 + 1) * MK_NB;
-    gemm_128<true, false, true>(Wm + i * MK_NB + (long)B0 * MK_NB * ld, ld, Y + B0 * MK_NB + (long)j * MK_NB * ld, ld,
-                                K, K, acc, lds);
-    store_tile(Wm + i * MK_NB + (long)j * MK_NB * ld, ld, acc);
+    gemm_tile<TM, TM, true, false, true>(Wm + i * MK_NB + ro + (long)B0 * MK_NB * ld, ld,
+                                         Y + B0 * MK_NB + (long)j * MK_NB * ld + co, ld, K, K, acc, lds);
+    store_tile(Wm + i * MK_NB + ro + (long)j * MK_NB * ld + co, ld, acc);
   }
 }
+template __global__ void k_inv_level<128>(MatSet, const int*, const int*, int, int);
+template __global__ void k_inv_level<64>(MatSet, const int*, const int*, int, int);
 
 // Tiles (i,j), i >= j, of R^-1 = sum over rows l < n_s of W(l,i)^T W(l,j) (drops the bordered
 // row and the padding).  diag_only: tiles (i,i) into QB; otherwise the full symmetric Q.
@@ -683,15 +715,29 @@ __global__ __launch_bounds__(256, 2) void k_lauum(MatSet ms, const int* __restri
   store_tile(Q + i * MK_NB + (long)j * MK_NB * ld, ld, acc, Ct);
 }
 
+// Only the two diagonal 64-quadrants of each 128-tile of R^-1 are consumed (k_sweep reads the
+// 64 x 64 block of its 64-site block), so each is one 64-sub-tile workgroup (the same bits as
+// the 128-tile product) and the off-diagonal quadrants are never computed.
 __global__ __launch_bounds__(256, 2) void k_qblocks(MatSet ms, const int* __restrict__ n_s, const int* __restrict__ list,
                                                  const int* __restrict__ count) {
-  extern __shared__ __attribute__((aligned(16))) double lds[];   // MK_GD_LDS_BYTES
-  int e, i;
-  if (!xcd_map(*count, ms.nt, &e, &i)) return;
+  extern __shared__ __attribute__((aligned(16))) double lds[];   // gb_lds_bytes(64, 64)
+  int e, t;
+  if (!xcd_map(*count, ms.nt * 2, &e, &t)) return;
+  const int i = t >> 1, sd = t & 1;
   const int sh = list[e];
-  Acc acc;
-  wtw_tile<true>(ms, sh, n_s[sh / ms.q], i, i, acc, lds);
-  store_tile(ms.QB + ((long)sh * ms.nt + i) * MK_NB * MK_NB, MK_NB, acc);
+  const int ns = n_s[sh / ms.q];
+  const double* X = wmat(ms, sh);
+  const long ld = ms.ld;
+  const int K = (ms.nt - i) * MK_NB;
+  const int kvalid = ns - i * MK_NB;
+  AccT<2, 2> acc;
+  acc_zero(acc);
+  // both operands are the panel W(i:, 128 i + 64 sd : +64) -- loaded once
+  if (kvalid > 0)
+    gemm_tile<64, 64, false, false, false, false, true, SKIP_NONE, true>(
+        X + i * MK_NB + (long)(i * MK_NB + 64 * sd) * ld, ld, X + i * MK_NB + (long)(i * MK_NB + 64 * sd) * ld, ld,
+        K, kvalid, acc, lds);
+  store_tile(ms.QB + ((long)sh * ms.nt + i) * MK_NB * MK_NB + 64 * sd + 64 * sd * MK_NB, MK_NB, acc);
 }
 
 // z_h = border row of the accepted factor = L^-1 u_h (exact for the u_h the candidate was built with).

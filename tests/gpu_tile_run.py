@@ -1,0 +1,43 @@
+"""Helper run as a subprocess by tests/test_gpu_linalg.py (not a test module): a short chain
+under the tile shape the environment forces (MK_TILE=64 | 128, read once per process), outputs
+saved to the .npz named on the command line."""
+import importlib
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+PKG = "laurabaracaldo-spatial-meta-kriging-for-distributed-inference-for-binary-response_amd"
+
+
+def main(path):
+    mk = importlib.import_module(PKG)
+    out = {}
+    for q, sizes, cov in ((1, [700, 640, 333], 0), (2, [300, 257], 0), (1, [500, 260], 1)):
+        d = mk.synthetic.generate(sum(sizes), q=q, n_test=20, seed=71 + q + cov, cov_model=cov)
+        p = 2 * q
+        cfg = mk.SamplerConfig(q, p, np.zeros(p), np.full(p, 0.05), cov_model="matern" if cov else "exponential",
+                               n_batch=2, batch_length=3, burn_in=4, seed=5)
+        subs, off = [], 0
+        for m in sizes:
+            rows = slice(off * q, (off + m) * q)
+            subs.append(dict(coords=d["coords"][off:off + m], y=d["y"][rows], weights=np.ones(m * q), x=d["x"][rows]))
+            off += m
+        with mk.Session(subs, cfg, coords_test=d["coords_test"], record_w=True) as ses:
+            ses.run(cfg.n_samples)
+            o = ses.outputs(samples=True, w_samples=True, w_pred_samples=True)
+        for s in range(len(sizes)):
+            out[f"q{q}c{cov}_samples_{s}"] = o["samples"][s]
+            out[f"q{q}c{cov}_w_{s}"] = o["w_samples"][s]
+            out[f"q{q}c{cov}_pred_{s}"] = o["w_pred_samples"][s]
+    L, ld = mk.cholesky_batched(np.stack([np.eye(300) + 0.5 * np.exp(-np.abs(np.subtract.outer(np.arange(300.0),
+                                                                                               np.arange(300.0))) / 7)
+                                          for _ in range(2)]), inverse=False)
+    out["chol_L"], out["chol_ld"] = L, ld
+    np.savez(path, **out)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])

@@ -78,3 +78,24 @@ def test_combine_is_sequential_mean(mk):
     out = mk.combine(grids)
     ref = om.combine_mean(grids)
     assert np.array_equal(out, ref)          # same summation order -> bit identical
+
+
+def test_sub_tile_gemm_is_bit_identical(tmp_path):
+    """The 64-sub-tile GEMMs (small shards: Cholesky update / trsm, inverse levels) give exactly
+    the 128-tile results (mk_gemm.hpp: same MFMA sequence per element): chains, latent w,
+    kriging draws and a plain factorisation, with each shape forced in its own process."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    res = {}
+    for shape in ("64", "128"):
+        path = str(tmp_path / f"tile{shape}.npz")
+        r = subprocess.run([sys.executable, os.path.join(here, "gpu_tile_run.py"), path], capture_output=True,
+                           text=True, timeout=240, env=dict(os.environ, MK_TILE=shape))
+        assert r.returncode == 0, r.stderr[-4000:]
+        z = np.load(path)
+        res[shape] = {k: z[k] for k in z.files}
+    assert res["64"].keys() == res["128"].keys()
+    for k in res["64"]:
+        assert np.array_equal(res["64"][k], res["128"][k]), k
