@@ -111,9 +111,10 @@ def load():
     global _LIB
     if _LIB is not None:
         return _LIB
-    if not os.path.exists(LIB_PATH):
-        raise MkError(MK_E_ARG, f"{LIB_PATH} not built; run __graft_entry__.build()")
-    lib = ctypes.CDLL(LIB_PATH)
+    path = os.environ.get("MK_LIB") or LIB_PATH      # MK_LIB: a development build (tools/ probes)
+    if not os.path.exists(path):
+        raise MkError(MK_E_ARG, f"{path} not built; run __graft_entry__.build()")
+    lib = ctypes.CDLL(path)
     for name, (res, args) in EXPORTS.items():
         fn = getattr(lib, name)
         fn.restype = res

@@ -163,6 +163,13 @@ struct mk_session {
   int* d_slist = nullptr;         // tiled replay: per-outcome subset lists [q][S] + counts [q]
   int* d_scount = nullptr;
   std::vector<Group> groups;      // the run-time split, one stream each
+  // multi-workgroup sweep (k_sweep_mg, small shards): partial dots, per-block counters, error flag
+  bool sweep_mg = false;
+  size_t sweep_mg_lds = 0;
+  double* sw_part = nullptr;
+  int* sw_cnt = nullptr;
+  int* sw_xcc = nullptr;
+  int* sw_err = nullptr;
   double* d_probs = nullptr;
   std::vector<int> n_part;
   std::vector<void*> allocs;
@@ -360,6 +367,32 @@ static void launch_pred_refresh(mk_session* s, Group& g) {
                      g.d_plist, g.d_pcount);
 }
 
+// The latent-w sweep: the cooperative multi-workgroup kernel when the session chose it (small
+// shard, one stream), else one workgroup per subset; both give the same bits (mk_mcmc.hip).
+static void launch_sweep(mk_session* s, Group& g, int it) {
+  const int q = s->q;
+  if (s->sweep_mg && s->groups.size() == 1) {
+    hipMemsetAsync(s->sw_cnt, 0, (size_t)g.S * (s->n_pad / 64) * sizeof(int), g.stream);
+    Model md = g.md;
+    MatSet ms = g.ms;
+    int iter = it;
+    double* part = s->sw_part;
+    int* cnt = s->sw_cnt;
+    int* xcc = s->sw_xcc;
+    int* err = s->sw_err;
+    void* args[] = {&md, &ms, &iter, &part, &cnt, &xcc, &err};
+    hipLaunchCooperativeKernel(sweep_kernel(q, true), dim3(xcd_grid(g.S, s->nt)), dim3(256), args,
+                               (unsigned)s->sweep_mg_lds, g.stream);
+    return;
+  }
+  const size_t sw_lds = (size_t)q * (64 * 64 + 2 * 64) * sizeof(double);
+  Model md = g.md;
+  MatSet ms = g.ms;
+  int iter = it;
+  void* args[] = {&md, &ms, &iter};
+  hipLaunchKernel(sweep_kernel(q, false), dim3(g.S), dim3(MK_SW_T), args, sw_lds, g.stream);
+}
+
 static void run_iteration(mk_session* s, Group& g, int it) {
   Model& md = g.md;
   const int S = g.S, q = s->q;
@@ -381,8 +414,7 @@ static void run_iteration(mk_session* s, Group& g, int it) {
                      g.d_plist, g.d_pcount);
   launch_inverse(s, g);
   if (kept && !s->tiled) launch_pred_refresh(s, g);
-  const size_t sw_lds = (size_t)q * (64 * 64 + 2 * 64) * sizeof(double);
-  timed(s, st, KS_SWEEP, 0.0, [&] { hipLaunchKernelGGL(k_sweep, dim3(S), dim3(MK_SW_T), sw_lds, st, md, g.ms, it); });
+  timed(s, st, KS_SWEEP, 0.0, [&] { launch_sweep(s, g, it); });
   if (s->record_samples) hipLaunchKernelGGL(k_record, dim3((S + 63) / 64), dim3(64), 0, st, md, it);
   if (s->record_w) hipLaunchKernelGGL(k_record_w, dim3((md.Np + 255) / 256, S), dim3(256), 0, st, md, it);
   if (kept && md.n_test > 0 && !s->tiled) {
@@ -684,8 +716,30 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
   HIPCHK(hipFuncSetAttribute((const void*)k_chol_diag, hipFuncAttributeMaxDynamicSharedMemorySize,
                              MK_DIAG_LDS_BYTES));
   if (!set_gemm_lds()) return set_err(MK_E_HIP, "gemm lds attribute");
-  HIPCHK(hipFuncSetAttribute((const void*)k_sweep, hipFuncAttributeMaxDynamicSharedMemorySize,
+  HIPCHK(hipFuncSetAttribute(sweep_kernel(q, false), hipFuncAttributeMaxDynamicSharedMemorySize,
                              q * (64 * 64 + 2 * 64) * 8));
+  // multi-workgroup sweep: chosen when the cooperative grid (S x nt workgroups) fits on the chip
+  // at once and the shard runs on one stream; MK_SWEEP=1 forces the one-workgroup kernel, 2 the
+  // multi-workgroup one (when it fits)
+  {
+    s->sweep_mg_lds = (size_t)q * (64 * 64 + 2 * 64) * 8 + 4 * MK_NB * 8;
+    const void* fn = sweep_kernel(q, true);
+    HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)s->sweep_mg_lds));
+    int per_cu = 0, n_cu = 0, coop = 0;
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, s->sweep_mg_lds));
+    HIPCHK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, c->device));
+    HIPCHK(hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, c->device));
+    const long grid = xcd_grid(S, nt);
+    const int mode = tile_env("MK_SWEEP", 0);
+    const bool fits = coop && grid <= (long)per_cu * n_cu && s->groups.size() == 1 && nt <= 32;
+    s->sweep_mg = fits && (mode == 2 || (mode == 0 && (long)S * 4 <= n_cu));
+    if (s->sweep_mg) {
+      if ((rc = s->alloc(&s->sw_part, (size_t)S * 2 * nt * q * 64)) || (rc = s->alloc(&s->sw_cnt, (size_t)S * (n_pad / 64))) ||
+          (rc = s->alloc(&s->sw_xcc, (size_t)S * nt)) || (rc = s->alloc(&s->sw_err, 1)))
+        return rc;
+      HIPCHK(hipMemsetAsync(s->sw_err, 0, sizeof(int), s->stream));
+    }
+  }
 
   // ---------------- initial state: eta, u, factor every R_h at the starting values, W, z (whole shard)
   Group& a = s->all;
@@ -716,6 +770,12 @@ extern "C" int mk_session_run(mk_session* s, int32_t n_iter) {
     HIPCHK(hipGetLastError());
   }
   for (auto& g : s->groups) HIPCHK(hipStreamSynchronize(g.stream));
+  if (s->sweep_mg) {
+    int e = 0;
+    HIPCHK(hipMemcpy(&e, s->sw_err, sizeof(int), hipMemcpyDeviceToHost));
+    if (e & 2) return set_err(MK_E_HIP, "latent sweep: a subset's workgroups ran on different XCDs (set MK_SWEEP=1)");
+    if (e) return set_err(MK_E_HIP, "latent sweep: workgroup barrier timed out");
+  }
   if (s->prof) {
     s->stats[KS_ITER].launches += n_iter;
     s->stats[KS_ITER].ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();

@@ -38,7 +38,19 @@ __global__ void k_beta(Model md, int iter);
 __global__ void k_Aphase(Model md, int iter);
 __global__ void k_theta_mh(Model md, MatSet ms, int h0, int hc, int which, int iter);
 __global__ void k_dirty_list(Model md, int force, int* list_inv, int* count_inv, int* list_pred, int* count_pred);
+template <int Q>
 __global__ void k_sweep(Model md, MatSet ms, int iter);
+template <int Q>
+__global__ void k_sweep_mg(Model md, MatSet ms, int iter, double* part, int* cnt, int* xcc, int* err);
+// the sweep kernels specialised for the session's number of outcomes
+inline const void* sweep_kernel(int q, bool mg) {
+  switch (q) {
+    case 1: return mg ? (const void*)k_sweep_mg<1> : (const void*)k_sweep<1>;
+    case 2: return mg ? (const void*)k_sweep_mg<2> : (const void*)k_sweep<2>;
+    case 3: return mg ? (const void*)k_sweep_mg<3> : (const void*)k_sweep<3>;
+    default: return mg ? (const void*)k_sweep_mg<4> : (const void*)k_sweep<4>;
+  }
+}
 __global__ void k_record(Model md, int iter);
 __global__ void k_record_w(Model md, int iter);
 __global__ void k_adapt(Model md, int b);

@@ -69,25 +69,6 @@ __device__ inline CandGen make_gen(const Model& md, int s, int h, int which, int
   return g;
 }
 
-// XCD-aware block -> (entry, tile) map.  Blocks are dealt round-robin over the 8 XCDs
-// (block b runs on XCD b % 8); the S*T work items are cut into 8 contiguous chunks and XCD x
-// takes chunk x in order, so the tiles of one entry (subset) run on one XCD and share its L2
-// (its shared panel is fetched once), and every XCD gets an equal share however few entries
-// are active (a short list of changed subsets no longer leaves XCDs idle).  S is the number of
-// ACTIVE entries; the grid (xcd_grid of the maximum) covers any S up to that maximum.  Speed
-// only; any placement is correct.
-__device__ inline bool xcd_map(int S, int T, int* s, int* t) {
-  const int W = S * T, C = (W + 7) >> 3;
-  const int x = blockIdx.x & 7, j = blockIdx.x >> 3;
-  if (j >= C) return false;
-  const int w = x * C + j;
-  if (w >= W) return false;
-  *s = w / T;
-  *t = w % T;
-  return true;
-}
-__host__ inline int xcd_grid(int S, int T) { return 8 * ((S + 7) / 8) * T; }
-
 // Lower tiles (i >= j) of every candidate of outcome h (tiles with j < jmin are skipped).
 // Generating tiles inside k_chol_update at their first touch (gen = 1) was measured
 // slower on cfg3 (+3.5 ms of exp work at 2 waves/SIMD vs 1.7 ms for this pass).

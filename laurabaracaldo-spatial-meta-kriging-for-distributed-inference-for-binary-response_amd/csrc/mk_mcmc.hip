@@ -259,7 +259,19 @@ __global__ __launch_bounds__(256) void k_dirty_list(Model md, int force, int* li
 // Sites in blocks of 64.  For block B: g_B = W[:,B]' z (dots over rows >= b0), then the
 // sequential MH steps inside the block use the 64x64 tile Q_BB of R^-1 (from QB) to carry
 // accepted moves forward (g_i += delta'_k Q_ik), then z += W[:,B] delta'_B (rows >= b0).
-// W panels are streamed twice per sweep (dots, update) -> n^2 doubles per subset per sweep.
+//
+// Two kernels, bit-identical by construction (the chains do not depend on which one runs):
+//   k_sweep     one 1024-thread workgroup per subset, W panels streamed twice (dots, update):
+//               large shards (every CU already has a subset);
+//   k_sweep_mg  one 256-thread workgroup per (subset, 128-row tile) in a cooperative grid: the
+//               workgroup keeps its tile's 128 x 64 panel of W in registers from the dots to
+//               the update (one pass over W), the tiles' partial dots meet through a per-subset
+//               counter barrier and every workgroup runs the block's MH steps itself: small
+//               shards (32 subsets on 256 CUs).
+// The shared summation order: dot g_i = sum over 128-row tiles t = b0/128, ... in tile order of
+// p_t = wave-xor-reduce(a0 + a1), lane l holding rows 128t + 2l, +1 (a0, a1 masked to
+// b0 <= row < n_s); update z_r += ((s0 + s1) + s2) + s3, s_w = fma chain over the block's columns
+// i = w, w + 4, ... (ascending).
 #define SW_B 64
 #define SW_T MK_SW_T
 // Lane i's value (i wave-uniform) as a scalar: two v_readlane_b32.
@@ -269,31 +281,55 @@ __device__ inline double rlane_u(double v, int i) {
   const int hi = __builtin_amdgcn_readlane((int)(b >> 32), i);
   return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
-__global__ __launch_bounds__(SW_T) void k_sweep(Model md, MatSet ms, int iter) {
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  const int q = md.q;
-  double* Qb = smem;                              // [q][SW_B*SW_B] column-major
-  double* gb = smem + q * SW_B * SW_B;            // [q][SW_B]
-  double* dacc = gb + q * SW_B;                   // [q][SW_B]
-  __shared__ int any_acc;
-  __shared__ double Ai[MK_QMAX * MK_QMAX];
-  const int s = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int ns = md.n_s[s], Ns = ns * q;
+
+// 64-bit DPP move as two 32-bit halves (gfx950's 64-bit DPP takes row_newbcast only).
+template <int CTRL>
+__device__ inline double dpp_f64(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffll), CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xf, 0xf, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+// Sum of the 64 lanes' values, the same in every lane: within each 16-lane row by DPP (quad
+// xor 1, quad xor 2, half-row mirror, row mirror -- VALU only, no LDS crossbar), then the four
+// row sums as ((r0 + r1) + (r2 + r3)) from lanes 0, 16, 32, 48.  The sweep's dot products use
+// this tree in both kernels.
+__device__ inline double wave_sum_dpp(double x) {
+  x += dpp_f64<0xB1>(x);    // quad_perm [1,0,3,2]
+  x += dpp_f64<0x4E>(x);    // quad_perm [2,3,0,1]
+  x += dpp_f64<0x141>(x);   // row_half_mirror
+  x += dpp_f64<0x140>(x);   // row_mirror
+  return (rlane_u(x, 0) + rlane_u(x, 16)) + (rlane_u(x, 32) + rlane_u(x, 48));
+}
+
+// Data the multi-workgroup sweep exchanges between the workgroups of one subset -- which all
+// run on one XCD (k_sweep_mg's block map; checked at run time) -- moves through that XCD's L2:
+// plain stores (the vector L1 writes through), s_waitcnt for their completion before the
+// barrier counter's atomic increment, and L1-bypassing loads (buffer loads with sc0) on the
+// reader's side.  No cache-wide release / acquire fence (an L2 write-back / invalidate per
+// workgroup) is needed.  COH = false: ordinary loads (the one-workgroup kernel).
+typedef unsigned int u2v __attribute__((ext_vector_type(2)));
+template <bool COH>
+__device__ inline double ld_l2(const double* base, long idx) {
+  if (!COH) return base[idx];
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7fffffff, 0x00020000);
+  const u2v v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)(idx * 8), 0, 1);   // aux 1: sc0 (bypass L1)
+  return __builtin_bit_cast(double, v);
+}
+
+// Proposals, likelihood differences and accept draws of sites [k0, k1) (location-major entries):
+// independent of the sweep order.
+__device__ inline void sweep_precompute(const Model& md, int s, int iter, int k0, int k1, int t0, int nthr) {
   const Key key = subset_key(md, s);
-  const long ld = ms.ld;
   const double* y = md.y + (long)s * md.Np;
   const double* wt = md.wt + (long)s * md.Np;
-  double* eta = md.eta + (long)s * md.Np;
-  double* w = md.w + (long)s * md.Np;
+  const double* eta = md.eta + (long)s * md.Np;
+  const double* tune = md.tune + (long)s * md.n_mh_max + md.o_w;
   double* dl = md.sw_delta + (long)s * md.Np;
   double* dll = md.sw_dll + (long)s * md.Np;
   double* lgu = md.sw_logu + (long)s * md.Np;
   int* sacc = md.sw_acc + (long)s * md.Np;
-  double* z = md.z + (long)s * q * md.n_pad;
-  const double* tune = md.tune + (long)s * md.n_mh_max + md.o_w;
-  if (tid < q * q) Ai[tid] = md.Ainv[(long)s * q * q + tid];
-  // ---- proposals, likelihood differences and accept draws: independent of the sweep order
-  for (int k = tid; k < Ns; k += SW_T) {
+  for (int k = k0 + t0; k < k1; k += nthr) {
     const int j = md.o_w + k;
     const double zz = proposal_normal(key, j, iter);
     const double d = exp(tune[k]) * zz;
@@ -302,22 +338,145 @@ __global__ __launch_bounds__(SW_T) void k_sweep(Model md, MatSet ms, int iter) {
     lgu[k] = accept_log_uniform(key, j, iter);
     sacc[k] = 0;
   }
+}
+
+// The sequential Metropolis steps of one block (wave 0 only).  Lane i preloads site b0+i's
+// proposal d, likelihood difference, accept draw and the step's g-independent term
+// 0.5 d^2 sum_h A^-1_ha^2 Q_ii; each step reads them (and the carried g) by readlane with the
+// uniform step index, the LDS column of Q_BB it may need was requested one step earlier, and an
+// accepted move updates g by a select rather than a branch -- the step's dependent chain is
+// readlane, three multiply-adds, a compare and a select.  Lane i collects site b0+i's
+// coefficients and accept flags; they leave after the loop.
+// gb [q][64] dots, Qb [q][64*64], Ai [q*q]; out: dacc [q][64] coefficients, accept flags
+// (write_acc) into sw_acc.  Returns whether any site moved (the same in every lane).
+// Accept iff log U <= dll - (d c + 0.5 d^2 dd), c = sum_h A^-1_ha g_h, dd = sum_h (A^-1_ha)^2 Q_ii.
+template <int Q, bool COH>
+__device__ inline int sweep_block_mh_q(const Model& md, int s, int b0, int nb, const double* gb, const double* Qb,
+                                       const double* Ai, double* dacc, bool write_acc) {
+  constexpr int q = Q;   // outcomes, at compile time: every loop below unrolls without branches
+  const int lane = threadIdx.x & 63;
+  const double* dl = md.sw_delta + (long)s * md.Np;
+  const double* dll = md.sw_dll + (long)s * md.Np;
+  const double* lgu = md.sw_logu + (long)s * md.Np;
+  int* sacc = md.sw_acc + (long)s * md.Np;
+  double gl[Q], dlr[Q], dllr[Q], lgr[Q], hdd[Q], dsum[Q], qn[Q], ai[Q * Q];
+  const int ls = (lane < nb) ? lane : 0;
+#pragma unroll
+  for (int e = 0; e < Q * Q; ++e) ai[e] = Ai[e];
+#pragma unroll
+  for (int h = 0; h < Q; ++h) {
+    gl[h] = (lane < nb) ? gb[h * SW_B + lane] : 0.0;
+    const int k = (b0 + ls) * q + h;
+    dlr[h] = ld_l2<COH>(dl, k);
+    dllr[h] = ld_l2<COH>(dll, k);
+    lgr[h] = ld_l2<COH>(lgu, k);
+    dsum[h] = 0.0;
+    qn[h] = Qb[h * SW_B * SW_B + lane];
+  }
+#pragma unroll
+  for (int a = 0; a < Q; ++a) {
+    double dd = 0.0;
+#pragma unroll
+    for (int h = 0; h < Q; ++h) {
+      const double aih = ai[h + a * q];
+      dd += (aih * aih) * Qb[h * SW_B * SW_B + ls * SW_B + ls];
+    }
+    const double d = dlr[a];
+    hdd[a] = 0.5 * d * d * dd;
+  }
+  int flags = 0, anyl = 0;
+  for (int i = 0; i < nb; ++i) {
+    const int iu = __builtin_amdgcn_readfirstlane(i);
+    const int inext = __builtin_amdgcn_readfirstlane(min(i + 1, nb - 1));   // next step's column (clamped)
+    double qc[Q];
+#pragma unroll
+    for (int h = 0; h < Q; ++h) {
+      qc[h] = qn[h];
+      qn[h] = Qb[h * SW_B * SW_B + inext * SW_B + lane];
+    }
+#pragma unroll
+    for (int a = 0; a < Q; ++a) {
+      const double d = rlane_u(dlr[a], iu);
+      double c = ai[a * q] * rlane_u(gl[0], iu);
+#pragma unroll
+      for (int h = 1; h < Q; ++h) c += ai[h + a * q] * rlane_u(gl[h], iu);
+      const double ratio = rlane_u(dllr[a], iu) - (d * c + rlane_u(hdd[a], iu));
+      const bool acc = rlane_u(lgr[a], iu) <= ratio;     // uniform
+#pragma unroll
+      for (int h = 0; h < Q; ++h) {
+        const double coef = d * ai[h + a * q];
+        const double gn = gl[h] + coef * qc[h];
+        gl[h] = acc ? gn : gl[h];
+        const double ds = dsum[h] + coef;
+        dsum[h] = (acc && lane == iu) ? ds : dsum[h];
+      }
+      flags |= (acc && lane == iu) ? (1 << a) : 0;
+      anyl |= acc ? 1 : 0;
+    }
+  }
+#pragma unroll
+  for (int h = 0; h < Q; ++h) dacc[h * SW_B + lane] = dsum[h];
+  if (write_acc && lane < nb)
+    for (int a = 0; a < q; ++a)
+      if ((flags >> a) & 1) sacc[(b0 + lane) * q + a] = 1;
+  return anyl;
+}
+
+// Accepted moves of sites [i0, i1) into w, eta, u and the batch accept counts.
+__device__ inline void sweep_apply(const Model& md, int s, int i0, int i1, const double* Ai, int t0, int nthr) {
+  const int q = md.q;
+  double* w = md.w + (long)s * md.Np;
+  double* eta = md.eta + (long)s * md.Np;
+  double* u = md.u + (long)s * q * md.n_pad;
+  double* acc = md.acc + (long)s * md.n_mh_max + md.o_w;
+  const double* dl = md.sw_delta + (long)s * md.Np;
+  const int* sacc = md.sw_acc + (long)s * md.Np;
+  for (int i = i0 + t0; i < i1; i += nthr) {
+    for (int a = 0; a < q; ++a) {
+      const int k = i * q + a;
+      if (sacc[k]) {
+        w[k] += dl[k];
+        eta[k] += dl[k];
+        acc[k] += 1.0;
+        for (int h = 0; h < q; ++h) u[(long)h * md.n_pad + i] += dl[k] * Ai[h + a * q];
+      }
+    }
+  }
+}
+
+template <int Q>
+__global__ __launch_bounds__(SW_T) void k_sweep(Model md, MatSet ms, int iter) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  constexpr int q = Q;
+  double* Qb = smem;                              // [q][SW_B*SW_B] column-major
+  double* gb = smem + q * SW_B * SW_B;            // [q][SW_B]
+  double* dacc = gb + q * SW_B;                   // [q][SW_B]
+  __shared__ int any_acc;
+  __shared__ double Ai[MK_QMAX * MK_QMAX];
+  const int s = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int ns = md.n_s[s];
+  const long ld = ms.ld;
+  double* z = md.z + (long)s * q * md.n_pad;
+  if (tid < q * q) Ai[tid] = md.Ainv[(long)s * q * q + tid];
+  sweep_precompute(md, s, iter, 0, ns * q, tid, SW_T);
   if (tid == 0) any_acc = 0;
   __syncthreads();
+  const int tl = (ns - 1) / MK_NB;                // last tile holding sites
   int p0 = 0, pnb = 0;
   for (int b0 = 0; b0 < ns + SW_B; b0 += SW_B) {
     const int nb = min(SW_B, ns - b0);
     // ---- (a) z += W[:, prev block] delta'_prev   (rows >= p0)
     // Thread t owns the row pair p0 + 2t, p0 + 2t + 1 (16-byte loads; p0 is even, ld even) and
     // issues the 16 column loads of a group before using them: unconditional loads (clamped
-    // column; W is finite everywhere), the short-block tail masked by a zero coefficient.
+    // column; W is finite everywhere), the short-block tail masked by a zero coefficient.  Four
+    // accumulators by column residue mod 4 (the shared order).
     if (pnb > 0 && any_acc) {
       for (int h = 0; h < q; ++h) {
         for (int r = p0 + 2 * tid; r < ns; r += 2 * SW_T) {
           const double* Wp = ms.W + ((long)s * q + h) * (ld * ld) + (long)p0 * ld + r;
           const double* da = dacc + h * SW_B;
           double* zh = z + (long)h * md.n_pad;
-          d2 v = {0.0, 0.0};
+          d2 v4[4] = {{0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}};
           for (int k0 = 0; k0 < pnb; k0 += 16) {
             d2 wv2[16];
 #pragma unroll
@@ -326,12 +485,14 @@ __global__ __launch_bounds__(SW_T) void k_sweep(Model md, MatSet ms, int iter) {
 #pragma unroll
             for (int u = 0; u < 16; ++u) {
               const double c = (k0 + u < pnb) ? da[k0 + u] : 0.0;
-              v.x = fma(wv2[u].x, c, v.x);
-              v.y = fma(wv2[u].y, c, v.y);
+              v4[u & 3].x = fma(wv2[u].x, c, v4[u & 3].x);
+              v4[u & 3].y = fma(wv2[u].y, c, v4[u & 3].y);
             }
           }
-          zh[r] += v.x;
-          if (r + 1 < ns) zh[r + 1] += v.y;
+          const double vx = ((v4[0].x + v4[1].x) + v4[2].x) + v4[3].x;
+          const double vy = ((v4[0].y + v4[1].y) + v4[2].y) + v4[3].y;
+          zh[r] += vx;
+          if (r + 1 < ns) zh[r + 1] += vy;
         }
       }
     }
@@ -347,82 +508,38 @@ __global__ __launch_bounds__(SW_T) void k_sweep(Model md, MatSet ms, int iter) {
         const double v = QBt[(off + r) + (off + c) * MK_NB];   // in the tile: off + 63 < 128
         Qb[h * SW_B * SW_B + e] = (r < nb && c < nb) ? v : 0.0;  // (a masked load would serialise)
       }
-      if (tid < SW_B) dacc[h * SW_B + tid] = 0.0;
       const double* Wb = ms.W + ((long)s * q + h) * (ld * ld) + (long)b0 * ld;
       const double* zh = z + (long)h * md.n_pad;
-      // one wave per column; lane l reads rows b0 + 2l + 128j (16-byte loads, 8 in flight,
-      // clamped inside the padded column and masked by a select)
-      const int nj = (ns - b0 + 127) / 128;
+      // one wave per column; lane l reads rows 128t + 2l, +1 of tiles t = tile .. tl (16-byte loads,
+      // 8 tiles in flight, clamped to the last tile and masked by selects), one reduction per tile
       for (int i = wv; i < nb; i += SW_T / 64) {
         const double* col = Wb + (long)i * ld;
-        double a0 = 0.0, a1 = 0.0;
-        for (int j0 = 0; j0 < nj; j0 += 8) {
+        double g = 0.0;
+        for (int t0 = tile; t0 <= tl; t0 += 8) {
           d2 wv2[8], zv2[8];
 #pragma unroll
           for (int u = 0; u < 8; ++u) {
-            const int rc = min(b0 + 2 * lane + 128 * (j0 + u), md.n_pad - 2);
+            const int rc = MK_NB * min(t0 + u, tl) + 2 * lane;
             wv2[u] = *reinterpret_cast<const d2*>(col + rc);
             zv2[u] = *reinterpret_cast<const d2*>(zh + rc);
           }
 #pragma unroll
           for (int u = 0; u < 8; ++u) {
-            const int rr = b0 + 2 * lane + 128 * (j0 + u);
-            a0 = (rr < ns) ? fma(wv2[u].x, zv2[u].x, a0) : a0;
-            a1 = (rr + 1 < ns) ? fma(wv2[u].y, zv2[u].y, a1) : a1;
+            if (t0 + u > tl) break;
+            const int r0 = MK_NB * (t0 + u) + 2 * lane;
+            const double a0 = (r0 >= b0 && r0 < ns) ? wv2[u].x * zv2[u].x : 0.0;
+            const double a1 = (r0 + 1 >= b0 && r0 + 1 < ns) ? wv2[u].y * zv2[u].y : 0.0;
+            const double p = wave_sum_dpp(a0 + a1);
+            g = (t0 + u == tile) ? p : g + p;
           }
         }
-        double acc = a0 + a1;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
-        if (lane == 0) gb[h * SW_B + i] = acc;
+        if (lane == 0) gb[h * SW_B + i] = g;
       }
     }
     __syncthreads();
-    // ---- (c) sequential Metropolis steps of the block (wave 0).  Lane i preloads site b0+i's
-    // proposal, likelihood difference, accept draw and Q diagonal; each step reads them (and
-    // the carried g) by readlane with the uniform step index: no memory round trip per step.
+    // ---- (c) sequential Metropolis steps of the block (wave 0)
     if (wv == 0) {
-      // (register arrays indexed by compile-time constants only: loops over MK_QMAX, q-guarded)
-      double gl[MK_QMAX], qd[MK_QMAX], dlr[MK_QMAX], dllr[MK_QMAX], lgr[MK_QMAX];
-      const int ls = (lane < nb) ? lane : 0;
-#pragma unroll
-      for (int h = 0; h < MK_QMAX; ++h) {
-        gl[h] = (h < q && lane < nb) ? gb[h * SW_B + lane] : 0.0;
-        qd[h] = (h < q) ? Qb[h * SW_B * SW_B + ls * SW_B + ls] : 0.0;
-        const int k = (b0 + ls) * q + h;
-        dlr[h] = (h < q) ? dl[k] : 0.0;
-        dllr[h] = (h < q) ? dll[k] : 0.0;
-        lgr[h] = (h < q) ? lgu[k] : 0.0;
-      }
-      int anyl = 0;
-      for (int i = 0; i < nb; ++i) {
-#pragma unroll
-        for (int a = 0; a < MK_QMAX; ++a) {
-          if (a >= q) break;
-          const int k = (b0 + i) * q + a;
-          const double d = rlane_u(dlr[a], i);
-          double c = 0.0, dd = 0.0;
-#pragma unroll
-          for (int h = 0; h < MK_QMAX; ++h) {
-            if (h >= q) break;
-            const double aih = Ai[h + a * q];
-            c += aih * rlane_u(gl[h], i);
-            dd += (aih * aih) * rlane_u(qd[h], i);
-          }
-          const double ratio = rlane_u(dllr[a], i) - (d * c + 0.5 * d * d * dd);
-          if (rlane_u(lgr[a], i) <= ratio) {
-#pragma unroll
-            for (int h = 0; h < MK_QMAX; ++h) {
-              if (h >= q) break;
-              const double coef = d * Ai[h + a * q];
-              gl[h] = gl[h] + coef * Qb[h * SW_B * SW_B + i * SW_B + lane];
-              if (lane == 0) dacc[h * SW_B + i] += coef;
-            }
-            if (lane == 0) sacc[k] = 1;
-            anyl = 1;
-          }
-        }
-      }
+      const int anyl = sweep_block_mh_q<Q, false>(md, s, b0, nb, gb, Qb, Ai, dacc, true);
       if (lane == 0) any_acc = anyl;
     }
     __syncthreads();
@@ -430,20 +547,203 @@ __global__ __launch_bounds__(SW_T) void k_sweep(Model md, MatSet ms, int iter) {
     pnb = nb;
   }
   // ---- apply accepted moves to w, eta, u and the batch accept counts
-  double* u = md.u + (long)s * q * md.n_pad;
-  double* acc = md.acc + (long)s * md.n_mh_max + md.o_w;
-  for (int i = tid; i < ns; i += SW_T) {
-    for (int a = 0; a < q; ++a) {
-      const int k = i * q + a;
-      if (sacc[k]) {
-        w[k] += dl[k];
-        eta[k] += dl[k];
-        acc[k] += 1.0;
-        for (int h = 0; h < q; ++h) u[(long)h * md.n_pad + i] += dl[k] * Ai[h + a * q];
+  sweep_apply(md, s, 0, ns, Ai, tid, SW_T);
+}
+
+// Multi-workgroup sweep (small shards).  Grid: xcd_grid(S, nt) workgroups of 256 threads,
+// cooperative (all co-resident); workgroup (s, t) owns rows [128t, 128t + 128) of subset s
+// (its z rows in registers, replicated in the four waves; its sites' proposals and final
+// moves) and takes part in blocks b0 < min(n_s, 128t + 128).  Per block: partial dots of its
+// tile for every column (wave w: columns w + 4j, lane l: rows 2l, 2l+1) into part[s][B & 1][t],
+// arrive on cnt[s][B], prefetch Q_BB, wait for the block's tiles tf..tl, sum the partials in
+// tile order, run the MH steps, update z from the same registers.  REG (q == 1): the panel
+// stays in registers across the wait; else it is reloaded for the update.  The partial dots and
+// the sites' proposals move through the subset's XCD L2 (ld_l2); the counters are atomics.  A
+// barrier wait gives up after ~2^22 sleeps (err |= 1) and a subset split over XCDs sets err |= 2;
+// the host reports either, and every wave always exits.
+// Q_BB of the block at b0 (q 64 x 64 column-major tiles of R_h^-1) straight into LDS by
+// LDS-DMA: one wave instruction moves two columns (lanes 0-31 column 2j, 32-63 column 2j+1),
+// no registers; completion is covered by the s_waitcnt before the next barrier arrival.  Entries
+// beyond the block's last site are copied as they are (finite, and never read by the MH steps).
+__device__ inline void qbb_dma(const Model& md, const MatSet& ms, int s, int b0, double* Qb) {
+  const int q = md.q, tile = b0 / MK_NB, off = b0 % MK_NB;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int col = lane >> 5, row = 2 * (lane & 31);
+  for (int h = 0; h < q; ++h) {
+    const double* QBt = ms.QB + (((long)s * q + h) * ms.nt + tile) * MK_NB * MK_NB;
+    for (int j = w; j < SW_B / 2; j += 4)
+      __builtin_amdgcn_global_load_lds((const void*)(QBt + (off + row) + (long)(off + 2 * j + col) * MK_NB),
+                                       (void*)(Qb + h * SW_B * SW_B + 2 * j * SW_B), 16, 0, 0);
+  }
+}
+
+#define MK_NT_MAX_MG 32   // tiles per subset the multi-workgroup sweep supports (n_s <= 4095)
+#ifdef MK_SWEEP_PROBE     // development probe only (tools/sweep_probe.py): per-phase clock of subset 0, tile 0
+__device__ long long mk_sweep_ts[64 * 8];
+#define SW_STAMP(B, i) do { if (s == 0 && t == tl && threadIdx.x == 0 && (B) < 64) mk_sweep_ts[(B) * 8 + (i)] = wall_clock64(); } while (0)
+}  // namespace mk
+extern "C" int mk_debug_sweep_probe(long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(mk::mk_sweep_ts), sizeof(long long) * 64 * 8) == hipSuccess ? 0 : -2;
+}
+namespace mk {
+#else
+#define SW_STAMP(B, i) do { } while (0)
+#endif
+template <int Q>
+__global__ __launch_bounds__(256) void k_sweep_mg(Model md, MatSet ms, int iter, double* __restrict__ part,
+                                                  int* __restrict__ cnt, int* __restrict__ xcc, int* __restrict__ err) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  constexpr int q = Q;
+  constexpr bool REG = (Q == 1);
+  const int nt = ms.nt;
+  double* Qb = smem;                              // [q][SW_B*SW_B]
+  double* gb = Qb + q * SW_B * SW_B;              // [q][SW_B]
+  double* dacc = gb + q * SW_B;                   // [q][SW_B]
+  double* red = dacc + q * SW_B;                  // [4][MK_NB] per-wave update sums
+  __shared__ double Ai[MK_QMAX * MK_QMAX];
+  __shared__ int any_acc;
+  // block map: block b runs on XCD b % 8 (the dispatch order every kernel here relies on); subset
+  // s takes slots (s / 8) * nt ... of XCD s % 8, so all of its tiles share one L2
+  const int j = blockIdx.x >> 3;
+  const int s = (blockIdx.x & 7) + 8 * (j / nt), t = j % nt;
+  if (s >= md.S) return;
+  const int ns = md.n_s[s];
+  const int tl = (ns - 1) / MK_NB;
+  if (t > tl) return;                             // rows >= n_s only: no sites, no dots
+  // the exchange through L2 is sound only if the subset's workgroups share an XCD: each
+  // publishes its XCC id (device-coherent atomic), checked against the others after block 0
+  const unsigned my_xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);   // hwreg(HW_REG_XCC_ID, 0, 4)
+  if (threadIdx.x == 0)
+    __hip_atomic_store(xcc + (long)s * nt + t, (int)my_xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const long ld = ms.ld;
+  const int r0 = MK_NB * t + 2 * lane;            // this lane's rows r0, r0 + 1
+  if (tid < q * q) Ai[tid] = md.Ainv[(long)s * q * q + tid];
+  // own sites' proposals (read by the MH of blocks 2t, 2t+1 after barrier 2t)
+  sweep_precompute(md, s, iter, MK_NB * t * q, min(MK_NB * (t + 1), ns) * q, tid, 256);
+  d2 zr[Q];
+#pragma unroll
+  for (int h = 0; h < Q; ++h) zr[h] = *reinterpret_cast<const d2*>(md.z + ((long)s * q + h) * md.n_pad + r0);
+  const long pstride = (long)nt * q * SW_B;       // one parity buffer of a subset
+  double* ps = part + (long)s * 2 * pstride;
+  int* cs = cnt + (long)s * (md.n_pad / SW_B);
+  const int last_b = min(ns - 1, MK_NB * t + MK_NB - 1) / SW_B;
+  qbb_dma(md, ms, s, 0, Qb);                      // block 0's Q_BB lands while the dots run
+  for (int B = 0; B <= last_b; ++B) {
+    const int b0 = B * SW_B, nb = min(SW_B, ns - b0), tf = b0 / MK_NB;
+    double* pb = ps + (B & 1) * pstride;
+    SW_STAMP(B, 0);
+    // ---- partial dots of tile t for every column of the block
+    d2 wreg[16];
+    for (int h = 0; h < q; ++h) {
+      const double* Wt = ms.W + ((long)s * q + h) * (ld * ld) + (long)b0 * ld + r0;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) wreg[j] = *reinterpret_cast<const d2*>(Wt + (long)(wv + 4 * j) * ld);
+      d2 zz = zr[0];
+#pragma unroll
+      for (int hh = 1; hh < Q; ++hh)
+        if (hh == h) zz = zr[hh];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const double a0 = (r0 >= b0 && r0 < ns) ? wreg[j].x * zz.x : 0.0;
+        const double a1 = (r0 + 1 >= b0 && r0 + 1 < ns) ? wreg[j].y * zz.y : 0.0;
+        const double p = wave_sum_dpp(a0 + a1);
+        if (lane == 0) pb[((long)t * q + h) * SW_B + wv + 4 * j] = p;
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0);                // this wave's stores have reached L2
+    __syncthreads();
+    SW_STAMP(B, 1);
+    if (tid == 0) __hip_atomic_fetch_add(cs + B, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    SW_STAMP(B, 2);
+    if (tid == 0) {
+      const int target = tl - tf + 1;
+      int spins = 0;
+      while (__hip_atomic_load(cs + B, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > (1 << 22)) {
+          __hip_atomic_fetch_or(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+    }
+    __syncthreads();
+    SW_STAMP(B, 3);
+    if (B == 0 && threadIdx.x <= tl) {              // every tile of the subset has arrived: same XCD?
+      const int other = __hip_atomic_load(xcc + (long)s * nt + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (other != (int)my_xcc) __hip_atomic_fetch_or(err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // ---- dots: partials of tiles tf .. tl summed in tile order (every workgroup, same bits);
+    // L1-bypassing loads, all issued before the adds
+    for (int e = tid; e < q * SW_B; e += 256) {
+      const int h = e / SW_B, i = e % SW_B;
+      double pv[MK_NT_MAX_MG];
+#pragma unroll
+      for (int u = 0; u < MK_NT_MAX_MG; ++u) pv[u] = ld_l2<true>(pb, ((long)min(tf + u, tl) * q + h) * SW_B + i);
+      double g = pv[0];
+#pragma unroll
+      for (int u = 1; u < MK_NT_MAX_MG; ++u)
+        if (tf + u <= tl) g = g + pv[u];
+      gb[e] = g;
+    }
+    __syncthreads();
+    SW_STAMP(B, 4);
+    // ---- the block's MH steps (wave 0 of every workgroup; the sites' owner records them)
+    if (wv == 0) {
+      const int anyl = sweep_block_mh_q<Q, true>(md, s, b0, nb, gb, Qb, Ai, dacc, t == tf);
+      if (lane == 0) any_acc = anyl;
+    }
+    __syncthreads();
+    SW_STAMP(B, 5);
+    if (B < last_b) qbb_dma(md, ms, s, b0 + SW_B, Qb);   // next block's Q_BB behind the update and dots
+    // ---- z rows of tile t (rows >= b0) += W[:, B] delta'_B
+    if (any_acc) {
+      for (int h = 0; h < q; ++h) {
+        if (!REG) {
+          const double* Wt = ms.W + ((long)s * q + h) * (ld * ld) + (long)b0 * ld + r0;
+#pragma unroll
+          for (int j = 0; j < 16; ++j) wreg[j] = *reinterpret_cast<const d2*>(Wt + (long)(wv + 4 * j) * ld);
+        }
+        d2 sw = {0.0, 0.0};
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const int i = wv + 4 * j;
+          const double c = (i < nb) ? dacc[h * SW_B + i] : 0.0;
+          sw.x = fma(wreg[j].x, c, sw.x);
+          sw.y = fma(wreg[j].y, c, sw.y);
+        }
+        red[wv * MK_NB + 2 * lane] = sw.x;
+        red[wv * MK_NB + 2 * lane + 1] = sw.y;
+        __syncthreads();
+        const double vx = ((red[2 * lane] + red[MK_NB + 2 * lane]) + red[2 * MK_NB + 2 * lane]) + red[3 * MK_NB + 2 * lane];
+        const double vy = ((red[2 * lane + 1] + red[MK_NB + 2 * lane + 1]) + red[2 * MK_NB + 2 * lane + 1]) +
+                          red[3 * MK_NB + 2 * lane + 1];
+        __syncthreads();
+#pragma unroll
+        for (int hh = 0; hh < Q; ++hh) {
+          if (hh != h) continue;
+          if (r0 >= b0 && r0 < ns) zr[hh].x += vx;
+          if (r0 + 1 >= b0 && r0 + 1 < ns) zr[hh].y += vy;
+        }
       }
     }
   }
+  // ---- write back z rows; apply this tile's accepted moves
+  if (wv == 0) {
+#pragma unroll
+    for (int h = 0; h < Q; ++h) *reinterpret_cast<d2*>(md.z + ((long)s * q + h) * md.n_pad + r0) = zr[h];
+  }
+  __syncthreads();
+  sweep_apply(md, s, MK_NB * t, min(MK_NB * (t + 1), ns), Ai, tid, 256);
 }
+template __global__ void k_sweep<1>(Model, MatSet, int);
+template __global__ void k_sweep<2>(Model, MatSet, int);
+template __global__ void k_sweep<3>(Model, MatSet, int);
+template __global__ void k_sweep<4>(Model, MatSet, int);
+template __global__ void k_sweep_mg<1>(Model, MatSet, int, double*, int*, int*, int*);
+template __global__ void k_sweep_mg<2>(Model, MatSet, int, double*, int*, int*, int*);
+template __global__ void k_sweep_mg<3>(Model, MatSet, int, double*, int*, int*, int*);
+template __global__ void k_sweep_mg<4>(Model, MatSet, int, double*, int*, int*, int*);
 
 // ---------------------------------------------------------------- 6. record / adapt
 __global__ __launch_bounds__(64) void k_record(Model md, int iter) {

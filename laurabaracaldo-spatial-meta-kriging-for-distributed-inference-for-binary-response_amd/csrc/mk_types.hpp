@@ -102,4 +102,24 @@ __device__ inline double* winv_slot(const MatSet& m, int sh, int slot, int k) {
 }
 __device__ inline Key subset_key(const Model& md, int s) { return make_key(md.seed, (uint32_t)(md.subset_base + s)); }
 
+// XCD-aware block -> (entry, tile) map.  Blocks are dealt round-robin over the 8 XCDs
+// (block b runs on XCD b % 8); the S*T work items are cut into 8 contiguous chunks and XCD x
+// takes chunk x in order, so the tiles of one entry (subset) run on one XCD and share its L2
+// (its shared panel is fetched once), and every XCD gets an equal share however few entries
+// are active (a short list of changed subsets no longer leaves XCDs idle).  S is the number of
+// ACTIVE entries; the grid (xcd_grid of the maximum) covers any S up to that maximum.  Speed
+// only; any placement is correct.
+__device__ inline bool xcd_map(int S, int T, int* s, int* t) {
+  const int W = S * T, C = (W + 7) >> 3;
+  const int x = blockIdx.x & 7, j = blockIdx.x >> 3;
+  if (j >= C) return false;
+  const int w = x * C + j;
+  if (w >= W) return false;
+  *s = w / T;
+  *t = w % T;
+  return true;
+}
+__host__ inline int xcd_grid(int S, int T) { return 8 * ((S + 7) / 8) * T; }
+
+
 }  // namespace mk

@@ -80,22 +80,26 @@ def test_combine_is_sequential_mean(mk):
     assert np.array_equal(out, ref)          # same summation order -> bit identical
 
 
-def test_sub_tile_gemm_is_bit_identical(tmp_path):
-    """The 64-sub-tile GEMMs (small shards: Cholesky update / trsm, inverse levels) give exactly
-    the 128-tile results (mk_gemm.hpp: same MFMA sequence per element): chains, latent w,
-    kriging draws and a plain factorisation, with each shape forced in its own process."""
+def test_sub_tile_gemm_and_multi_wg_sweep_are_bit_identical(tmp_path):
+    """Small-shard code paths give exactly the large-shard results: the 64-sub-tile GEMMs
+    (Cholesky update / trsm, inverse levels; mk_gemm.hpp: same MFMA sequence per element) and the
+    cooperative multi-workgroup latent sweep (k_sweep_mg; same summation order as k_sweep).
+    Chains, latent w, kriging draws and a plain factorisation, each configuration forced in its
+    own process (MK_TILE, MK_SWEEP are read once per process)."""
     import os
     import subprocess
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     res = {}
-    for shape in ("64", "128"):
-        path = str(tmp_path / f"tile{shape}.npz")
+    for tile, sweep in (("64", "2"), ("128", "1"), ("64", "1")):
+        path = str(tmp_path / f"tile{tile}_sweep{sweep}.npz")
         r = subprocess.run([sys.executable, os.path.join(here, "gpu_tile_run.py"), path], capture_output=True,
-                           text=True, timeout=240, env=dict(os.environ, MK_TILE=shape))
+                           text=True, timeout=240, env=dict(os.environ, MK_TILE=tile, MK_SWEEP=sweep))
         assert r.returncode == 0, r.stderr[-4000:]
         z = np.load(path)
-        res[shape] = {k: z[k] for k in z.files}
-    assert res["64"].keys() == res["128"].keys()
-    for k in res["64"]:
-        assert np.array_equal(res["64"][k], res["128"][k]), k
+        res[(tile, sweep)] = {k: z[k] for k in z.files}
+    ref = res[("128", "1")]
+    for key, got in res.items():
+        assert got.keys() == ref.keys()
+        for k in ref:
+            assert np.array_equal(got[k], ref[k]), (key, k)
