@@ -60,8 +60,13 @@ extern "C" int mk_device_memory(int32_t device, int64_t* free_bytes, int64_t* to
 
 namespace {
 
-constexpr int NKSTAT = 8;
-enum { KS_CHOL_UPDATE = 0, KS_CHOL_DIAG, KS_CHOL_TRSM, KS_SWEEP, KS_LAUUM, KS_ITER, KS_INV };
+constexpr int NKSTAT = 9;
+// KS_CHOL_UPDATE: the 128-tile panel-update launches (k_chol_update<128>); KS_CHOL_UPDATE_SUB:
+// the 64- / 32-sub-tile ones (small grids).  Together: the roofline kernel k_chol_update.
+// KS_UPDATE_BUSY: both, with the time of launches that overlap (the split schedule's bulk and
+// critical streams) counted once -- the union of their event intervals.
+enum { KS_CHOL_UPDATE = 0, KS_CHOL_DIAG, KS_CHOL_TRSM, KS_SWEEP, KS_LAUUM, KS_ITER, KS_INV, KS_CHOL_UPDATE_SUB,
+       KS_UPDATE_BUSY };
 
 struct Stat {
   long launches = 0;
@@ -84,6 +89,9 @@ struct Group {
   int* d_count = nullptr;
   int* d_plist = nullptr;  // pairs needing a kriging refresh
   int* d_pcount = nullptr;
+  hipEvent_t done = nullptr;         // fork-join sweep: this group's pre-sweep work is queued
+  hipStream_t bulk = nullptr;        // split Cholesky (launch_cholesky): CU-masked bulk-update stream
+  std::vector<hipEvent_t> ev;        // 2 nt + 1 events reused every factorisation
 };
 
 Model model_view(const Model& m, int s0, int S) {
@@ -166,6 +174,7 @@ struct mk_session {
   // multi-workgroup sweep (k_sweep_mg, small shards): partial dots, per-block counters, error flag
   bool sweep_mg = false;
   size_t sweep_mg_lds = 0;
+  hipEvent_t swept = nullptr;     // fork-join sweep (several groups): the whole-shard sweep is queued
   double* sw_part = nullptr;
   int* sw_cnt = nullptr;
   int* sw_xcc = nullptr;
@@ -195,8 +204,13 @@ struct mk_session {
     g_live_sessions.fetch_sub(1);
     if (device >= 0) hipSetDevice(device);
     for (auto& t : pending) { hipEventDestroy(t.a); hipEventDestroy(t.b); }
-    for (auto& g : groups)
+    for (auto& g : groups) {
       if (g.stream && g.stream != stream) hipStreamDestroy(g.stream);
+      if (g.done) hipEventDestroy(g.done);
+      if (g.bulk) hipStreamDestroy(g.bulk);
+      for (hipEvent_t e : g.ev) hipEventDestroy(e);
+    }
+    if (swept) hipEventDestroy(swept);
     for (void* p_ : allocs) hipFree(p_);
     if (stream) hipStreamDestroy(stream);
   }
@@ -223,6 +237,7 @@ static void timed(mk_session* s, hipStream_t st, int which, double flops, F&& la
 }
 
 static void drain_timers(mk_session* s) {
+  std::vector<std::pair<float, float>> upd;   // update launches: [start, end] relative to the first event
   for (auto& t : s->pending) {
     hipEventSynchronize(t.b);
     float ms = 0.f;
@@ -230,6 +245,28 @@ static void drain_timers(mk_session* s) {
     s->stats[t.which].launches += 1;
     s->stats[t.which].ms += ms;
     s->stats[t.which].flops += t.flops;
+    if (t.which == KS_CHOL_UPDATE || t.which == KS_CHOL_UPDATE_SUB) {
+      float t0 = 0.f;
+      hipEventElapsedTime(&t0, s->pending.front().a, t.a);
+      upd.push_back({t0, t0 + ms});
+      s->stats[KS_UPDATE_BUSY].launches += 1;
+      s->stats[KS_UPDATE_BUSY].flops += t.flops;
+    }
+  }
+  std::sort(upd.begin(), upd.end());
+  double busy = 0.0, lo = 0.0, hi = -1.0;
+  for (auto& iv : upd) {
+    if (iv.first > hi) {
+      if (hi > lo) busy += hi - lo;
+      lo = iv.first;
+      hi = iv.second;
+    } else {
+      hi = std::max(hi, (double)iv.second);
+    }
+  }
+  if (hi > lo) busy += hi - lo;
+  s->stats[KS_UPDATE_BUSY].ms += busy;
+  for (auto& t : s->pending) {
     hipEventDestroy(t.a);
     hipEventDestroy(t.b);
   }
@@ -240,12 +277,15 @@ static inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
 
 // Every tile-GEMM kernel takes gb_lds_bytes(TM, TN) of dynamic LDS: two DMA stages (> 64 KiB at 128 x 128).
 static constexpr size_t LDS_128 = gb_lds_bytes(128, 128), LDS_64 = gb_lds_bytes(64, 64),
-                        LDS_64x128 = gb_lds_bytes(64, 128);
+                        LDS_64x128 = gb_lds_bytes(64, 128), LDS_32 = gb_lds_bytes(32, 32),
+                        LDS_32x128 = gb_lds_bytes(32, 128);
 static bool set_gemm_lds() {
   const std::pair<const void*, size_t> fns[] = {
       {(const void*)k_chol_update<128>, LDS_128}, {(const void*)k_chol_update<64>, LDS_64},
       {(const void*)k_chol_trsm<128>, LDS_128},   {(const void*)k_chol_trsm<64>, LDS_64x128},
       {(const void*)k_inv_level<128>, LDS_128},   {(const void*)k_inv_level<64>, LDS_64},
+      {(const void*)k_chol_update<32>, LDS_32},   {(const void*)k_chol_trsm<32>, LDS_32x128},
+      {(const void*)k_inv_level<32>, LDS_32},
       {(const void*)k_qblocks, LDS_64},           {(const void*)k_lauum, LDS_128},
       {(const void*)k_pred_var, LDS_128}};
   for (const auto& f : fns)
@@ -255,71 +295,136 @@ static bool set_gemm_lds() {
 }
 
 // Tile shape of a GEMM launch: 64-sub-tiles (bit-identical, mk_gemm.hpp) when the 128-tile grid
-// would leave the chip short of work -- fewer than MK_TILE_THRESH workgroups (default 512, two
-// per CU).  MK_TILE=64 / 128 forces one shape (tests compare them).
+// would leave the chip short of work -- fewer than MK_TILE_THRESH workgroups (default 512, two per
+// CU).  MK_TILE=128 / 64 / 32 forces one shape (tests compare them; 32-sub-tiles were measured no
+// faster than 64 on the last, single-tile panels of small shards, so the policy does not pick them).
 static int tile_env(const char* name, int dflt) {
   const char* v = std::getenv(name);
   return (v && *v) ? std::atoi(v) : dflt;
 }
-static bool use_sub_tiles(long wg128) {
+static int tile_size(long wg128) {
   static const int force = tile_env("MK_TILE", 0);
   static const int thresh = tile_env("MK_TILE_THRESH", 512);
-  if (force == 64) return true;
-  if (force == 128) return false;
-  return wg128 < thresh;
+  if (force == 32 || force == 64 || force == 128) return force;
+  return wg128 >= thresh ? 128 : 64;
 }
 
 // ------------------------------------------------------------------ Cholesky of all candidates of outcome h
 // Candidate tiles are in the free slot (k_cov_candidate, or k_load_plain for the test entry).
 // One launch per step covers outcomes h0 .. h0+hc-1 of every subset (hc = q in the sampler).
+// Launch pieces of the blocked Cholesky for panel k, tiles [ia, ib), on stream st.
+static void chol_update(mk_session* s, Group& g, hipStream_t st, int h0, int hc, int k, int ia, int ib, int j0, int j1,
+                        const int* slist, const int* scount, double flops) {
+  const int E = g.S * hc, nti = ib - ia;
+  if (nti <= 0) return;
+  const int tm = tile_size((long)E * nti);
+  if (tm == 32) {
+    timed(s, st, KS_CHOL_UPDATE_SUB, flops, [&] {
+      hipLaunchKernelGGL(k_chol_update<32>, dim3(xcd_grid_h(E, nti * 16)), dim3(256), LDS_32, st, g.ms, g.S, h0, hc, k, ia,
+                         ib, j0, j1, slist, scount);
+    });
+  } else if (tm == 64) {
+    timed(s, st, KS_CHOL_UPDATE_SUB, flops, [&] {
+      hipLaunchKernelGGL(k_chol_update<64>, dim3(xcd_grid_h(E, nti * 4)), dim3(256), LDS_64, st, g.ms, g.S, h0, hc, k, ia,
+                         ib, j0, j1, slist, scount);
+    });
+  } else {
+    timed(s, st, KS_CHOL_UPDATE, flops, [&] {
+      hipLaunchKernelGGL(k_chol_update<128>, dim3(xcd_grid_h(E, nti)), dim3(256), LDS_128, st, g.ms, g.S, h0, hc, k, ia,
+                         ib, j0, j1, slist, scount);
+    });
+  }
+}
+static void chol_trsm(mk_session* s, Group& g, hipStream_t st, int h0, int hc, int k, int ia, int ib, const int* slist,
+                      const int* scount, double flops) {
+  const int E = g.S * hc, nti = ib - ia;
+  if (nti <= 0) return;
+  const int tm = tile_size((long)E * nti);
+  timed(s, st, KS_CHOL_TRSM, flops, [&] {
+    if (tm == 32)
+      hipLaunchKernelGGL(k_chol_trsm<32>, dim3(xcd_grid_h(E, nti * 4)), dim3(256), LDS_32x128, st, g.ms, g.S, h0, hc, k,
+                         ia, ib, slist, scount);
+    else if (tm == 64)
+      hipLaunchKernelGGL(k_chol_trsm<64>, dim3(xcd_grid_h(E, nti * 2)), dim3(256), LDS_64x128, st, g.ms, g.S, h0, hc, k,
+                         ia, ib, slist, scount);
+    else
+      hipLaunchKernelGGL(k_chol_trsm<128>, dim3(xcd_grid_h(E, nti)), dim3(256), LDS_128, st, g.ms, g.S, h0, hc, k, ia, ib,
+                         slist, scount);
+  });
+}
+static void chol_diag(mk_session* s, Group& g, hipStream_t st, int h0, int hc, int k, const int* slist,
+                      const int* scount) {
+  timed(s, st, KS_CHOL_DIAG, 0.0, [&] {
+    hipLaunchKernelGGL(k_chol_diag, dim3(g.S * hc), dim3(256), (size_t)MK_DIAG_LDS_BYTES, st, g.ms, g.md.n_s, h0, hc, k,
+                       g.md.ld_part, g.md.quad_c, g.md.info, slist, scount);
+  });
+}
+
+// Algorithmic flops of the column-k update over panels [j0, j1) (trsm: of panel k) of tiles
+// [ia, ib): every (subset, outcome) factor counted over its own valid extent n_s + 1 (the
+// bordered row; padding excluded), so ragged subsets (MK.R:18: the last takes the remainder) are
+// priced exactly.  With a subset list (tiled kriging replay) the active subsets live on the device:
+// the count is then an upper bound (every subset).
+static double panel_flops(mk_session* s, Group& g, int hc, int k, int ia, int ib, bool trsm, int j0 = 0, int j1 = -1) {
+  if (j1 < 0) j1 = k;
+  double fl = 0.0;
+  for (int i = g.s0; i < g.s0 + g.S; ++i) {
+    const double nv = (double)s->n_part[i] + 1.0;
+    const double rows = std::fmax(0.0, std::fmin(nv, (double)ib * MK_NB) - (double)ia * MK_NB);
+    const double cols = std::fmin((double)MK_NB, std::fmax(0.0, nv - (double)k * MK_NB));
+    const double depth = std::fmax(0.0, std::fmin((double)j1 * MK_NB, nv) - (double)j0 * MK_NB);
+    fl += trsm ? 2.0 * rows * MK_NB * MK_NB : 2.0 * rows * cols * depth;
+  }
+  return fl * hc;
+}
+
+// Cholesky of all candidates of outcomes h0 .. h0+hc-1 (candidate tiles in the free slot), left-
+// looking by 128-panels: per column k the update by panels < k, the diagonal tile, the trsm of
+// tiles k+1.. .
+//
+// Sequential form (one stream): U(k; panels 0..k-1), D(k), T(k).
+//
+// Split form (small shards, g.bulk set): the update of column c by panels 0..c-2 only needs
+// panels that are final two steps earlier, so it runs on the CU-masked bulk stream beside the
+// critical chain, which keeps only the rank-128 correction by panel c-1:
+//   critical (g.stream, all CUs):  U(k; k-1) [after bulk U(k; 0..k-2)], D(k), T(k)
+//   bulk (g.bulk, CUs minus the first `reserve`): U(k+2; 0..k) after T(k)
+// The diagonal kernel (one 149 KB-LDS workgroup per matrix) then finds idle CUs at once instead
+// of waiting for update workgroups to drain.  Same kernels, same per-element MFMA sequence (the
+// accumulator passes through fp64 memory between the two updates): same bits.  (An earlier
+// lookahead that moved the full-depth update of the next diagonal tile onto a second stream was
+// slower: that update's long K chain sat on the critical path)
 static void launch_cholesky(mk_session* s, Group& g, int h0, int hc, const int* slist = nullptr,
                             const int* scount = nullptr) {
-  const int nt = s->nt, S = g.S, E = S * hc;
-  const size_t diag_lds = (size_t)MK_DIAG_LDS_BYTES;
-  // Algorithmic flops of a launch: every (subset, outcome) factor counted over its own valid
-  // extent n_s + 1 (the bordered row; padding excluded), so ragged subsets (MK.R:18: the last
-  // takes the remainder) are priced exactly.  With a subset list (tiled kriging replay) the
-  // active subsets live on the device: the count is then an upper bound (every subset).
-  auto panel_flops = [&](int k, bool trsm) {
-    double fl = 0.0;
-    for (int i = g.s0; i < g.s0 + S; ++i) {
-      const double nv = (double)s->n_part[i] + 1.0;
-      if (trsm) {
-        fl += 2.0 * std::fmax(0.0, nv - (k + 1) * MK_NB) * MK_NB * MK_NB;
-      } else {
-        const double rows = std::fmax(0.0, nv - k * MK_NB);
-        const double cols = std::fmin((double)MK_NB, rows);
-        const double kk = std::fmin((double)k * MK_NB, nv);
-        fl += 2.0 * rows * cols * kk;
-      }
+  const int nt = s->nt;
+  if (slist || !g.bulk) {
+    for (int k = 0; k < nt; ++k) {
+      if (k > 0)
+        chol_update(s, g, g.stream, h0, hc, k, k, nt, 0, k, slist, scount, panel_flops(s, g, hc, k, k, nt, false));
+      chol_diag(s, g, g.stream, h0, hc, k, slist, scount);
+      if (k < nt - 1)
+        chol_trsm(s, g, g.stream, h0, hc, k, k + 1, nt, slist, scount, panel_flops(s, g, hc, k, k + 1, nt, true));
     }
-    return fl * hc;
-  };
+    return;
+  }
+  hipStream_t A = g.stream, B = g.bulk;
+  hipEvent_t* eT = g.ev.data();                  // eT[k]: T(k) done (critical), k = 0 .. nt-3
+  hipEvent_t* eU = g.ev.data() + nt;             // eU[c]: bulk U(c; 0..c-2) done, c = 2 .. nt-1
+  hipEventRecord(g.ev[2 * nt], A);               // the candidates are on A
+  hipStreamWaitEvent(B, g.ev[2 * nt], 0);
   for (int k = 0; k < nt; ++k) {
-    if (k > 0) {
-      // rows below the panel start x panel columns x K, per factor
-      timed(s, g.stream, KS_CHOL_UPDATE, panel_flops(k, false), [&] {
-        if (use_sub_tiles((long)E * (nt - k)))
-          hipLaunchKernelGGL(k_chol_update<64>, dim3(xcd_grid_h(E, (nt - k) * 4)), dim3(256), LDS_64, g.stream, g.ms, S, h0,
-                             hc, k, slist, scount);
-        else
-          hipLaunchKernelGGL(k_chol_update<128>, dim3(xcd_grid_h(E, nt - k)), dim3(256), LDS_128, g.stream, g.ms, S, h0,
-                             hc, k, slist, scount);
-      });
-    }
-    timed(s, g.stream, KS_CHOL_DIAG, 0.0, [&] {
-      hipLaunchKernelGGL(k_chol_diag, dim3(E), dim3(256), diag_lds, g.stream, g.ms, g.md.n_s, h0, hc, k, g.md.ld_part,
-                         g.md.quad_c, g.md.info, slist, scount);
-    });
-    if (k < nt - 1) {
-      timed(s, g.stream, KS_CHOL_TRSM, panel_flops(k, true), [&] {
-        if (use_sub_tiles((long)E * (nt - k - 1)))
-          hipLaunchKernelGGL(k_chol_trsm<64>, dim3(xcd_grid_h(E, (nt - k - 1) * 2)), dim3(256), LDS_64x128, g.stream, g.ms,
-                             S, h0, hc, k, slist, scount);
-        else
-          hipLaunchKernelGGL(k_chol_trsm<128>, dim3(xcd_grid_h(E, nt - k - 1)), dim3(256), LDS_128, g.stream, g.ms, S, h0,
-                             hc, k, slist, scount);
-      });
+    if (k >= 2) hipStreamWaitEvent(A, eU[k], 0);
+    if (k >= 1)
+      chol_update(s, g, A, h0, hc, k, k, nt, k - 1, k, nullptr, nullptr, panel_flops(s, g, hc, k, k, nt, false, k - 1, k));
+    chol_diag(s, g, A, h0, hc, k, nullptr, nullptr);
+    if (k < nt - 1)
+      chol_trsm(s, g, A, h0, hc, k, k + 1, nt, nullptr, nullptr, panel_flops(s, g, hc, k, k + 1, nt, true));
+    if (k + 2 < nt) {
+      const int c = k + 2;
+      hipEventRecord(eT[k], A);
+      hipStreamWaitEvent(B, eT[k], 0);
+      chol_update(s, g, B, h0, hc, c, c, nt, 0, c - 1, nullptr, nullptr, panel_flops(s, g, hc, c, c, nt, false, 0, c - 1));
+      hipEventRecord(eU[c], B);
     }
   }
 }
@@ -330,10 +435,16 @@ static void launch_trinv(mk_session* s, Group& g, int max_entries, const int* li
   hipLaunchKernelGGL(k_inv_copydiag, dim3(max_entries * nt), dim3(256), 0, g.stream, g.ms, list, count);
   for (int sz = 1; sz < nt; sz *= 2) {
     const int npairs = (nt + 2 * sz - 1) / (2 * sz);
-    const bool sub = use_sub_tiles((long)max_entries * npairs * sz * sz);
+    // the grid is sized for every pair, but only the accepted candidates' factors are in the
+    // list (about 40% at the amcmc target rate) and the level's K ranges are uneven: price the
+    // launch at an eighth of its 128-tile grid (measured: 32 subsets 1.33 -> 1.16 ms per iteration)
+    const int tm = tile_size((long)max_entries * npairs * sz * sz / 8);
     for (int phase = 0; phase < 2; ++phase)
       timed(s, g.stream, KS_INV, 0.0, [&] {
-        if (sub)
+        if (tm == 32)
+          hipLaunchKernelGGL(k_inv_level<32>, dim3(xcd_grid_h(max_entries, npairs * sz * sz * 16)), dim3(256), LDS_32,
+                             g.stream, g.ms, list, count, sz, phase);
+        else if (tm == 64)
           hipLaunchKernelGGL(k_inv_level<64>, dim3(xcd_grid_h(max_entries, npairs * sz * sz * 4)), dim3(256), LDS_64,
                              g.stream, g.ms, list, count, sz, phase);
         else
@@ -368,10 +479,11 @@ static void launch_pred_refresh(mk_session* s, Group& g) {
 }
 
 // The latent-w sweep: the cooperative multi-workgroup kernel when the session chose it (small
-// shard, one stream), else one workgroup per subset; both give the same bits (mk_mcmc.hip).
+// shard; g is then the whole-shard view), else one workgroup per subset; both give the same bits
+// (mk_mcmc.hip).
 static void launch_sweep(mk_session* s, Group& g, int it) {
   const int q = s->q;
-  if (s->sweep_mg && s->groups.size() == 1) {
+  if (s->sweep_mg) {
     hipMemsetAsync(s->sw_cnt, 0, (size_t)g.S * (s->n_pad / 64) * sizeof(int), g.stream);
     Model md = g.md;
     MatSet ms = g.ms;
@@ -393,7 +505,8 @@ static void launch_sweep(mk_session* s, Group& g, int it) {
   hipLaunchKernel(sweep_kernel(q, false), dim3(g.S), dim3(MK_SW_T), args, sw_lds, g.stream);
 }
 
-static void run_iteration(mk_session* s, Group& g, int it) {
+// One MCMC iteration of a group, in two halves around the latent sweep (run_iterations).
+static void iteration_pre_sweep(mk_session* s, Group& g, int it) {
   Model& md = g.md;
   const int S = g.S, q = s->q;
   const bool kept = it >= md.kept0;
@@ -414,7 +527,13 @@ static void run_iteration(mk_session* s, Group& g, int it) {
                      g.d_plist, g.d_pcount);
   launch_inverse(s, g);
   if (kept && !s->tiled) launch_pred_refresh(s, g);
-  timed(s, st, KS_SWEEP, 0.0, [&] { launch_sweep(s, g, it); });
+}
+
+static void iteration_post_sweep(mk_session* s, Group& g, int it) {
+  Model& md = g.md;
+  const int S = g.S;
+  const bool kept = it >= md.kept0;
+  hipStream_t st = g.stream;
   if (s->record_samples) hipLaunchKernelGGL(k_record, dim3((S + 63) / 64), dim3(64), 0, st, md, it);
   if (s->record_w) hipLaunchKernelGGL(k_record_w, dim3((md.Np + 255) / 256, S), dim3(256), 0, st, md, it);
   if (kept && md.n_test > 0 && !s->tiled) {
@@ -423,6 +542,33 @@ static void run_iteration(mk_session* s, Group& g, int it) {
   }
   if (kept && s->tiled) hipLaunchKernelGGL(k_record_kept, dim3(S), dim3(256), 0, st, md, it - md.kept0);
   if ((it + 1) % md.batch_length == 0) hipLaunchKernelGGL(k_adapt, dim3(S), dim3(256), 0, st, md, it / md.batch_length);
+}
+
+// One iteration of the shard.  Each group (stream) runs its own chain of launches; with the
+// multi-workgroup sweep and several groups, the groups join for one whole-shard sweep on the
+// session stream and fork again (the groups' Cholesky chains overlap each other's latency-bound
+// diagonal steps; the sweep is one cooperative launch).  Same kernels, same operands, same bits.
+static void run_iteration(mk_session* s, int it) {
+  if (s->sweep_mg && s->groups.size() > 1) {
+    for (auto& g : s->groups) {
+      hipStreamWaitEvent(g.stream, s->swept, 0);
+      iteration_pre_sweep(s, g, it);
+      hipEventRecord(g.done, g.stream);
+      hipStreamWaitEvent(s->stream, g.done, 0);
+    }
+    timed(s, s->stream, KS_SWEEP, 0.0, [&] { launch_sweep(s, s->all, it); });
+    hipEventRecord(s->swept, s->stream);
+    for (auto& g : s->groups) {
+      hipStreamWaitEvent(g.stream, s->swept, 0);
+      iteration_post_sweep(s, g, it);
+    }
+    return;
+  }
+  for (auto& g : s->groups) {
+    iteration_pre_sweep(s, g, it);
+    timed(s, g.stream, KS_SWEEP, 0.0, [&] { launch_sweep(s, g, it); });
+    iteration_post_sweep(s, g, it);
+  }
 }
 
 static int check_cfg(const mk_problem* pr, const mk_config* c) {
@@ -489,6 +635,31 @@ static int setup_groups(mk_session* s, int n_groups) {
       return set_err(MK_E_HIP, "group stream");
     }
     s->groups.push_back(g);
+  }
+  if (G > 1) {
+    for (auto& g : s->groups)
+      if (hipEventCreateWithFlags(&g.done, hipEventDisableTiming) != hipSuccess) return set_err(MK_E_HIP, "group event");
+    if (hipEventCreateWithFlags(&s->swept, hipEventDisableTiming) != hipSuccess) return set_err(MK_E_HIP, "sweep event");
+  }
+  // Split Cholesky (launch_cholesky) for small shards on one stream: a bulk-update stream that
+  // leaves the first `reserve` CUs (mask bits 0..reserve-1 = reserve/8 CUs on each XCD, measured
+  // by tools/cumask_probe.hip) to the diagonal kernels.  MK_CHOL_SPLIT=0 / 1 forces it off / on;
+  // MK_RESERVE_CU sets the reserve (default: one CU per diagonal workgroup, 8..64).
+  static const int split_env = tile_env("MK_CHOL_SPLIT", -1);
+  int n_cu = 0;
+  if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, s->device) != hipSuccess)
+    return set_err(MK_E_HIP, "device attribute");
+  const bool split = G == 1 && s->nt > 2 && (split_env == 1 || (split_env < 0 && (long)S * q * 4 <= n_cu));
+  if (split) {
+    const int reserve = std::max(8, std::min(64, round_up(tile_env("MK_RESERVE_CU", S * q), 8)));
+    std::vector<uint32_t> mask((n_cu + 31) / 32, 0xffffffffu);
+    for (int b = 0; b < reserve && b < n_cu; ++b) mask[b / 32] &= ~(1u << (b % 32));
+    Group& g = s->groups[0];
+    if (hipExtStreamCreateWithCUMask(&g.bulk, (uint32_t)n_cu, mask.data()) != hipSuccess)
+      return set_err(MK_E_HIP, "bulk stream");
+    g.ev.assign(2 * s->nt + 1, nullptr);
+    for (auto& e : g.ev)
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return set_err(MK_E_HIP, "cholesky event");
   }
   return 0;
 }
@@ -719,8 +890,7 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
   HIPCHK(hipFuncSetAttribute(sweep_kernel(q, false), hipFuncAttributeMaxDynamicSharedMemorySize,
                              q * (64 * 64 + 2 * 64) * 8));
   // multi-workgroup sweep: chosen when the cooperative grid (S x nt workgroups) fits on the chip
-  // at once and the shard runs on one stream; MK_SWEEP=1 forces the one-workgroup kernel, 2 the
-  // multi-workgroup one (when it fits)
+  // at once; MK_SWEEP=1 forces the one-workgroup kernel, 2 the multi-workgroup one (when it fits)
   {
     s->sweep_mg_lds = (size_t)q * (64 * 64 + 2 * 64) * 8 + 4 * MK_NB * 8;
     const void* fn = sweep_kernel(q, true);
@@ -731,7 +901,7 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
     HIPCHK(hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, c->device));
     const long grid = xcd_grid(S, nt);
     const int mode = tile_env("MK_SWEEP", 0);
-    const bool fits = coop && grid <= (long)per_cu * n_cu && s->groups.size() == 1 && nt <= 32;
+    const bool fits = coop && grid <= (long)per_cu * n_cu && nt <= 32;
     s->sweep_mg = fits && (mode == 2 || (mode == 0 && (long)S * 4 <= n_cu));
     if (s->sweep_mg) {
       if ((rc = s->alloc(&s->sw_part, (size_t)S * 2 * nt * q * 64)) || (rc = s->alloc(&s->sw_cnt, (size_t)S * (n_pad / 64))) ||
@@ -765,7 +935,7 @@ extern "C" int mk_session_run(mk_session* s, int32_t n_iter) {
   if (n_iter < 0 || s->iter + n_iter > s->md.n_samples) return set_err(MK_E_ARG, "n_iter beyond n.samples");
   const auto t0 = std::chrono::steady_clock::now();
   for (int i = 0; i < n_iter; ++i) {
-    for (auto& g : s->groups) run_iteration(s, g, s->iter);
+    run_iteration(s, s->iter);
     s->iter++;
     HIPCHK(hipGetLastError());
   }

@@ -1,6 +1,6 @@
 // Batched fp64 tile GEMM on CDNA4 MFMA (v_mfma_f64_16x16x4_f64).
 //
-// One 256-thread workgroup (4 waves, 2x2) owns one TM x TN output tile (TM, TN in {64, 128});
+// One 256-thread workgroup (4 waves, 2x2) owns one TM x TN output tile (TM, TN in {32, 64, 128});
 // each wave owns a (TM/2) x (TN/2) quadrant = BM x BN MFMA blocks of 16x16.  K is streamed in
 // chunks of 16 straight from HBM into LDS by global_load_lds (LDS-DMA: no staging registers,
 // no ds_write pass), two stages deep: chunk c+1 streams in while chunk c is multiplied, one
@@ -20,8 +20,8 @@
 //   op(A)(m,k) = A[m + k*sA]  (A_MU)   or  A[m*sA + k]  (!A_MU)
 //   op(B)(k,n) = B[k*sB + n]  (B_NU)   or  B[k + n*sB]  (!B_NU)
 // LDS images (a DMA wave instruction writes 64 lanes x 16 B = 1 KiB lane-linearly):
-//   m-contiguous: [k][m], k-row stride 144 (128-long operand) or 80 (64-long) doubles; one
-//     instruction per k-row (a 64-long row uses the first 32 lanes).  Both strides are 32 mod 64
+//   m-contiguous: [k][m], k-row stride 144 / 80 / 48 doubles (128 / 64 / 32-long operand); one
+//     instruction per k-row (a shorter row uses the first lanes).  Every stride is 32 mod 64
 //     dwords, so the two 16-lane halves of a ds_read_b64 group hit disjoint banks.
 //   k-contiguous: [m][16], the 8 k-pairs of row m XOR-swizzled by (m >> 1) & 7.  One
 //     instruction fills 8 rows (lane L: row L>>3, slot L&7 holds pair (L&7)^swz); the
@@ -40,12 +40,14 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 typedef double d2 __attribute__((ext_vector_type(2)));
 
 constexpr int GB_K = 16;                       // K chunk (the k-contiguous image assumes 8 pairs per row)
-__host__ __device__ constexpr int gb_stride(int len) { return len == 128 ? 144 : 80; }
+// m-contiguous image k-row stride: 32 mod 64 dwords for every operand length (bank-disjoint halves)
+__host__ __device__ constexpr int gb_stride(int len) { return len == 128 ? 144 : (len == 64 ? 80 : 48); }
 __host__ __device__ constexpr int gb_img(int len) { return GB_K * gb_stride(len); }   // >= len * GB_K
 // dynamic LDS of a TM x TN tile GEMM: two stages of (A image, B image)
 __host__ __device__ constexpr int gb_lds_bytes(int tm, int tn) { return 2 * (gb_img(tm) + gb_img(tn)) * 8; }
 static_assert(gb_lds_bytes(128, 128) == MK_GD_LDS_BYTES, "mk_common.hpp LDS size");
-static_assert(128 * GB_K <= gb_img(128) && 64 * GB_K <= gb_img(64), "k-contiguous images fit their slots");
+static_assert(128 * GB_K <= gb_img(128) && 64 * GB_K <= gb_img(64) && 32 * GB_K <= gb_img(32),
+              "k-contiguous images fit their slots");
 
 template <int BM, int BN>
 struct AccT {
@@ -77,7 +79,7 @@ __device__ inline void dma_chunk(const double* __restrict__ X, long s, int k0, d
     }
   } else {
 #pragma unroll
-    for (int j = 0; j < LEN / 32; ++j) {
+    for (int j = 0; j < (LEN + 31) / 32; ++j) {
       const int m8 = (w + 4 * j) * 8;
       const int m = m8 + (lane >> 3);
       const int pr = (lane & 7) ^ ku_swz(m);

@@ -13,9 +13,11 @@ inline CovCandidateKernel cov_candidate_kernel(int model) {
   return model == MK_COV_EXPONENTIAL ? k_cov_candidate<MK_COV_EXPONENTIAL> : k_cov_candidate<MK_COV_MATERN>;
 }
 template <int TM>
-__global__ void k_chol_update(MatSet ms, int S, int h0, int hc, int k, const int* slist, const int* scount);
+__global__ void k_chol_update(MatSet ms, int S, int h0, int hc, int k, int ia, int ib, int j0, int j1,
+                              const int* slist, const int* scount);
 template <int TM>
-__global__ void k_chol_trsm(MatSet ms, int S, int h0, int hc, int k, const int* slist, const int* scount);
+__global__ void k_chol_trsm(MatSet ms, int S, int h0, int hc, int k, int ia, int ib, const int* slist,
+                            const int* scount);
 __global__ void k_chol_diag(MatSet ms, const int* n_s, int h0, int hc, int k, double* ld_part, double* quad_c, int* info,
                             const int* slist, const int* scount);
 __global__ void k_inv_copydiag(MatSet ms, const int* list, const int* count);

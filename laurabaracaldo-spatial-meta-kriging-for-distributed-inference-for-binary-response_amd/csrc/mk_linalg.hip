@@ -245,22 +245,26 @@ template __global__ void k_cov_candidate<MK_COV_MATERN>(Model, MatSet, int, int,
 // (Generating C(i,k) from coordinates at its first touch inside this kernel was measured
 // slower on cfg3 and its code path made the kernel spill 80 VGPRs: candidates come from
 // k_cov_candidate.)
-// TM = 128: one workgroup per 128-tile.  TM = 64: four per tile (small shards: late panels have
-// few tiles and long K), bit-identical (mk_gemm.hpp); the upper quadrant of the diagonal tile is
-// skipped -- k_chol_diag reads the lower triangle only.
+// TM = 128: one workgroup per 128-tile.  TM = 64 / 32: four / sixteen per tile (small shards:
+// late panels have few tiles and long K), bit-identical (mk_gemm.hpp); the upper sub-tiles of
+// the diagonal tile are skipped -- k_chol_diag reads the lower triangle only.
+// Column k, tiles i in [ia, ib), panels j in [j0, j1) (j1 <= k): C(i,k) -= sum_j L(i,j) L(k,j)^T.
+// The split schedule (launch_cholesky) runs panels [0, k-1) early on the bulk stream and panel
+// k-1 on the critical stream; the accumulator round-trips through fp64 memory between the two,
+// so every element sees the same MFMA sequence as one [0, k) launch (same bits).
 template <int TM>
-__global__ __launch_bounds__(256, 2) void k_chol_update(MatSet ms, int S, int h0, int hc, int k, const int* slist,
-                                                       const int* scount) {
+__global__ __launch_bounds__(256, 2) void k_chol_update(MatSet ms, int S, int h0, int hc, int k, int ia, int ib,
+                                                       int j0, int j1, const int* slist, const int* scount) {
   extern __shared__ __attribute__((aligned(16))) double lds[];   // gb_lds_bytes(TM, TM) (two DMA stages)
-  constexpr int SUB = (MK_NB / TM) * (MK_NB / TM);
-  const int ntk = ms.nt - k;
+  constexpr int SUBR = MK_NB / TM, SUB = SUBR * SUBR;
+  const int ntk = ib - ia;
   int e, t, s, h;
   if (!xcd_map(active_pairs(slist, scount, S, hc), ntk * SUB, &e, &t) || !pick_pair(slist, scount, e, h0, hc, &s, &h))
     return;
   const int st = t % SUB;
   t /= SUB;
-  const int sr = st & 1, sc = st >> 1;   // (0, 0) when TM = 128
-  const int i = k + t;
+  const int sr = st % SUBR, sc = st / SUBR;   // (0, 0) when TM = 128
+  const int i = ia + t;
   if (i == k && sc > sr) return;
   const int sh = s * ms.q + h;
   double* M = mat_slot(ms, sh, 1 - ms.cur[sh]);
@@ -269,27 +273,30 @@ __global__ __launch_bounds__(256, 2) void k_chol_update(MatSet ms, int S, int h0
   AccT<TM / 32, TM / 32> acc;
   acc_load(acc, C, ld);
   // (Skipping the diagonal tiles' unused upper quadrant -- per MFMA or per chunk -- measured slower.)
-  gemm_tile<TM, TM, true, true, true>(M + i * MK_NB + sr * TM, ld, M + k * MK_NB + sc * TM, ld, k * MK_NB, k * MK_NB,
-                                      acc, lds);
+  const long jo = (long)j0 * MK_NB * ld;
+  gemm_tile<TM, TM, true, true, true>(M + i * MK_NB + sr * TM + jo, ld, M + k * MK_NB + sc * TM + jo, ld,
+                                      (j1 - j0) * MK_NB, (j1 - j0) * MK_NB, acc, lds);
   store_tile(C, ld, acc);
 }
-template __global__ void k_chol_update<128>(MatSet, int, int, int, int, const int*, const int*);
-template __global__ void k_chol_update<64>(MatSet, int, int, int, int, const int*, const int*);
+template __global__ void k_chol_update<128>(MatSet, int, int, int, int, int, int, int, int, const int*, const int*);
+template __global__ void k_chol_update<64>(MatSet, int, int, int, int, int, int, int, int, const int*, const int*);
+template __global__ void k_chol_update<32>(MatSet, int, int, int, int, int, int, int, int, const int*, const int*);
 
 // TM = 64: the tile's two row halves on two workgroups (in place: each reads and writes its own
 // rows only), bit-identical.
+// Tiles i in [ia, ib) of panel k (ia > k).
 template <int TM>
-__global__ __launch_bounds__(256, 2) void k_chol_trsm(MatSet ms, int S, int h0, int hc, int k, const int* slist,
-                                                     const int* scount) {
+__global__ __launch_bounds__(256, 2) void k_chol_trsm(MatSet ms, int S, int h0, int hc, int k, int ia, int ib,
+                                                     const int* slist, const int* scount) {
   extern __shared__ __attribute__((aligned(16))) double lds[];   // gb_lds_bytes(TM, 128)
   constexpr int SUB = MK_NB / TM;
-  const int ntk = ms.nt - k - 1;
+  const int ntk = ib - ia;
   int e, t, s, h;
   if (!xcd_map(active_pairs(slist, scount, S, hc), ntk * SUB, &e, &t) || !pick_pair(slist, scount, e, h0, hc, &s, &h))
     return;
   const int sr = t % SUB;
   t /= SUB;
-  const int i = k + 1 + t;
+  const int i = ia + t;
   const int sh = s * ms.q + h;
   const int slot = 1 - ms.cur[sh];
   double* M = mat_slot(ms, sh, slot);
@@ -302,8 +309,9 @@ __global__ __launch_bounds__(256, 2) void k_chol_trsm(MatSet ms, int S, int h0, 
   gemm_tile<TM, 128, true, true, false, false, false, SKIP_TRI_B>(C, ld, W, MK_NB, MK_NB, MK_NB, acc, lds);
   store_tile(C, ld, acc);
 }
-template __global__ void k_chol_trsm<128>(MatSet, int, int, int, int, const int*, const int*);
-template __global__ void k_chol_trsm<64>(MatSet, int, int, int, int, const int*, const int*);
+template __global__ void k_chol_trsm<128>(MatSet, int, int, int, int, int, int, const int*, const int*);
+template __global__ void k_chol_trsm<64>(MatSet, int, int, int, int, int, int, const int*, const int*);
+template __global__ void k_chol_trsm<32>(MatSet, int, int, int, int, int, int, const int*, const int*);
 
 // ---------------------------------------------------------------- diagonal tile: factor + invert in LDS
 // 128x128 tile T (column-major, stride TLD) in LDS, 256 threads, blocked by 16 (see
@@ -621,14 +629,14 @@ template <int TM>
 __global__ __launch_bounds__(256, 2) void k_inv_level(MatSet ms, const int* __restrict__ list,
                                                       const int* __restrict__ count, int sz, int phase) {
   extern __shared__ __attribute__((aligned(16))) double lds[];   // gb_lds_bytes(TM, TM)
-  constexpr int SUB = (MK_NB / TM) * (MK_NB / TM);
+  constexpr int SUBR = MK_NB / TM, SUB = SUBR * SUBR;
   const int npairs = (ms.nt + 2 * sz - 1) / (2 * sz);
   const int per = npairs * sz * sz;
   int e, t;
   if (!xcd_map(*count, per * SUB, &e, &t)) return;
   const int st = t % SUB;
   t /= SUB;
-  const int sr = st & 1, sc = st >> 1;
+  const int sr = st % SUBR, sc = st / SUBR;
   const int p = t / (sz * sz);
   t %= sz * sz;
   const int T0 = 2 * p * sz, B0 = T0 + sz;
@@ -661,6 +669,7 @@ __global__ __launch_bounds__(256, 2) void k_inv_level(MatSet ms, const int* __re
 }
 template __global__ void k_inv_level<128>(MatSet, const int*, const int*, int, int);
 template __global__ void k_inv_level<64>(MatSet, const int*, const int*, int, int);
+template __global__ void k_inv_level<32>(MatSet, const int*, const int*, int, int);
 
 // Tiles (i,j), i >= j, of R^-1 = sum over rows l < n_s of W(l,i)^T W(l,j) (drops the bordered
 // row and the padding).  diag_only: tiles (i,i) into QB; otherwise the full symmetric Q.

@@ -80,25 +80,29 @@ def test_combine_is_sequential_mean(mk):
     assert np.array_equal(out, ref)          # same summation order -> bit identical
 
 
-def test_sub_tile_gemm_and_multi_wg_sweep_are_bit_identical(tmp_path):
-    """Small-shard code paths give exactly the large-shard results: the 64-sub-tile GEMMs
-    (Cholesky update / trsm, inverse levels; mk_gemm.hpp: same MFMA sequence per element) and the
-    cooperative multi-workgroup latent sweep (k_sweep_mg; same summation order as k_sweep).
+def test_sub_tile_gemm_split_cholesky_and_multi_wg_sweep_are_bit_identical(tmp_path):
+    """Small-shard code paths give exactly the large-shard results: the 64- and 32-sub-tile GEMMs
+    (Cholesky update / trsm, inverse levels; mk_gemm.hpp: same MFMA sequence per element), the
+    split two-stream Cholesky schedule (bulk update by panels < k-1 on a CU-masked stream, the
+    rank-128 correction on the critical stream; the accumulator passes through fp64 memory) and
+    the cooperative multi-workgroup latent sweep (k_sweep_mg; same summation order as k_sweep).
     Chains, latent w, kriging draws and a plain factorisation, each configuration forced in its
-    own process (MK_TILE, MK_SWEEP are read once per process)."""
+    own process (MK_TILE, MK_SWEEP, MK_CHOL_SPLIT are read once per process)."""
     import os
     import subprocess
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     res = {}
-    for tile, sweep in (("64", "2"), ("128", "1"), ("64", "1")):
-        path = str(tmp_path / f"tile{tile}_sweep{sweep}.npz")
+    for tile, sweep, split in (("128", "1", "0"), ("64", "2", "1"), ("64", "1", "0"), ("32", "1", "1"),
+                               ("128", "2", "1")):
+        path = str(tmp_path / f"tile{tile}_sweep{sweep}_split{split}.npz")
         r = subprocess.run([sys.executable, os.path.join(here, "gpu_tile_run.py"), path], capture_output=True,
-                           text=True, timeout=240, env=dict(os.environ, MK_TILE=tile, MK_SWEEP=sweep))
+                           text=True, timeout=240,
+                           env=dict(os.environ, MK_TILE=tile, MK_SWEEP=sweep, MK_CHOL_SPLIT=split))
         assert r.returncode == 0, r.stderr[-4000:]
         z = np.load(path)
-        res[(tile, sweep)] = {k: z[k] for k in z.files}
-    ref = res[("128", "1")]
+        res[(tile, sweep, split)] = {k: z[k] for k in z.files}
+    ref = res[("128", "1", "0")]
     for key, got in res.items():
         assert got.keys() == ref.keys()
         for k in ref:
