@@ -247,7 +247,9 @@ def main():
                      "sub_tile_launch_share": sub_share,
                      "busy_ms_union": st["ms"], "launch_ms_summed": summed_ms,
                      "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved / FP64_PEAK_TFLOPS, "traffic": _pmc_traffic(),
+                     "frac": achieved / FP64_PEAK_TFLOPS,
+                     # PMC bytes per launch, profiled on the default workload (N=1, n=500k, K=250) only
+                     "traffic": _pmc_traffic() if (world == 1 and K == 250 and n == 500_000) else None,
                      "avg_launch_ms": avg_ms, "launches": st["launches"],
                      "algorithmic_flops_per_launch": st["flops"] / max(1, st["launches"])},
         "kernels_ms_per_step": {k: v["ms"] / n_post for k, v in kern.items()},

@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--kept", type=int, default=6)
     ap.add_argument("--burn", type=int, default=14)
     ap.add_argument("--tile", type=int, default=65536)
+    ap.add_argument("--kernel-events", type=int, default=1, help="HIP events around k_pred_var (0: off)")
     a = ap.parse_args()
     mk = importlib.import_module(PKG)
     S, ns = a.subsets, a.n_sub
@@ -50,8 +51,11 @@ def main():
         t0 = time.perf_counter()
         ses.run(n_samples)
         t1 = time.perf_counter()
+        if a.kernel_events:   # HIP events around every k_pred_var launch (the kriging GEMM)
+            ses.profile(True, kinds=[mk.session.KS_PRED_VAR])
         out = ses.outputs(quantiles=False, samples=True, w_predict_sum=True)
         t2 = time.perf_counter()
+        pv = ses.kernel_stats(mk.session.KS_PRED_VAR)
     kept_phi = np.stack([smp[a.burn:, 3] for smp in out["samples"]])          # phi column of p.beta.theta.samples
     runs = int(sum(1 + np.count_nonzero(np.diff(r)) for r in kept_phi))
     pred_s = t2 - t1
@@ -75,6 +79,16 @@ def main():
                                "assumes": f"phi runs per kept sample {run_frac:.3f} as measured here"},
         "w_predict_sum_finite": bool(np.isfinite(out["w_predict_sum"]).all()),
     }
+    if a.kernel_events and pv["ms"] > 0:
+        gemm_flops = runs * ns * ns * a.n_test   # X = W P^T, W lower-triangular, per (subset, phi run)
+        tf = gemm_flops / (pv["ms"] * 1e-3) / 1e12
+        gen = os.environ.get("MK_PRED_GEN", "0") not in ("", "0")
+        res["k_pred_var"] = {"launches": pv["launches"], "ms": pv["ms"], "avg_launch_ms": pv["ms"] / pv["launches"],
+                             "algorithmic_flops": gemm_flops, "achieved": tf, "unit": "TFLOP/s",
+                             "frac": tf / FP64_PEAK_TFLOPS, "p_t": "generated in LDS" if gen else "stored",
+                             "algorithmic_bytes": runs * (ns * ns / 2 + (1 if gen else 2) * ns * a.n_test) * 8.0,
+                             "bytes_note": "per (subset, phi run): W (lower) read once, X written once"
+                                           + ("" if gen else ", P^T read once")}
     print(json.dumps(res), flush=True)
 
 

@@ -60,13 +60,15 @@ extern "C" int mk_device_memory(int32_t device, int64_t* free_bytes, int64_t* to
 
 namespace {
 
-constexpr int NKSTAT = 9;
+constexpr int NKSTAT = 10;
 // KS_CHOL_UPDATE: the 128-tile panel-update launches (k_chol_update<128>); KS_CHOL_UPDATE_SUB:
 // the 64- / 32-sub-tile ones (small grids).  Together: the roofline kernel k_chol_update.
 // KS_UPDATE_BUSY: both, with the time of launches that overlap (the split schedule's bulk and
 // critical streams) counted once -- the union of their event intervals.
+// KS_PRED_VAR: the kriging GEMM k_pred_var; its flops assume every pair is refreshed (an upper
+// bound: only the pairs whose factor changed are in the list -- bench_kriging counts exactly).
 enum { KS_CHOL_UPDATE = 0, KS_CHOL_DIAG, KS_CHOL_TRSM, KS_SWEEP, KS_LAUUM, KS_ITER, KS_INV, KS_CHOL_UPDATE_SUB,
-       KS_UPDATE_BUSY };
+       KS_UPDATE_BUSY, KS_PRED_VAR };
 
 struct Stat {
   long launches = 0;
@@ -164,6 +166,7 @@ struct mk_session {
   int S = 0, q = 1, p = 0, n_pad = 0, nt = 0, P = 0;
   int iter = 0;
   bool matern = false, record_samples = true, record_w = false;
+  bool pred_gen = false;          // kriging P^T generated inside k_pred_var (exponential; no P^T buffer)
   Group all;                      // the whole shard on `stream`
   bool tiled = false;             // kriging after the fit over test-site tiles (predict_tile)
   int pred_tile = 0, n_test_all = 0, n_test_pad_all = 0;
@@ -287,7 +290,7 @@ static bool set_gemm_lds() {
       {(const void*)k_chol_update<32>, LDS_32},   {(const void*)k_chol_trsm<32>, LDS_32x128},
       {(const void*)k_inv_level<32>, LDS_32},
       {(const void*)k_qblocks, LDS_64},           {(const void*)k_lauum, LDS_128},
-      {(const void*)k_pred_var, LDS_128}};
+      {(const void*)k_pred_var<true>, LDS_128},   {(const void*)k_pred_var<false>, LDS_128}};
   for (const auto& f : fns)
     if (hipFuncSetAttribute(f.first, hipFuncAttributeMaxDynamicSharedMemorySize, (int)f.second) != hipSuccess)
       return false;
@@ -466,14 +469,27 @@ static void launch_inverse(mk_session* s, Group& g) {
                      g.d_list, g.d_count);
 }
 
-// Kriging refresh (kept iterations): P^T, X = W P^T and s = |X_t|^2 for the pairs in the pred list.
+// Algorithmic flops of k_pred_var over every pair of the group: 2 n_s^2 / 2 per test site (W
+// lower-triangular) -- an upper bound, the list holds the pairs whose factor changed.
+static double pred_flops(mk_session* s, Group& g) {
+  double fl = 0.0;
+  for (int i = g.s0; i < g.s0 + g.S; ++i) fl += (double)s->n_part[i] * s->n_part[i] * g.md.n_test;
+  return fl * s->q;
+}
+
+// Kriging refresh (kept iterations): X = W P^T and s = |X_t|^2 for the pairs in the pred list
+// (P^T generated in the GEMM for the exponential model, else stored first by k_pred_PT).
 static void launch_pred_refresh(mk_session* s, Group& g) {
   Model& md = g.md;
   if (md.n_test <= 0) return;
   const int nt = s->nt, max_entries = g.S * s->q;
-  hipLaunchKernelGGL(pred_PT_kernel(md.cov_model), dim3(max_entries * md.n_pad), dim3(256), 0, g.stream, md, g.d_plist, g.d_pcount);
-  hipLaunchKernelGGL(k_pred_var, dim3(xcd_grid_h(max_entries, nt * md.ntt)), dim3(256), LDS_128, g.stream, md, g.ms,
-                     g.d_plist, g.d_pcount);
+  if (!s->pred_gen)
+    hipLaunchKernelGGL(pred_PT_kernel(md.cov_model), dim3(max_entries * md.n_pad), dim3(256), 0, g.stream, md, g.d_plist,
+                       g.d_pcount);
+  timed(s, g.stream, KS_PRED_VAR, pred_flops(s, g), [&] {
+    hipLaunchKernelGGL(s->pred_gen ? k_pred_var<true> : k_pred_var<false>, dim3(xcd_grid_h(max_entries, nt * md.ntt)),
+                       dim3(256), LDS_128, g.stream, md, g.ms, g.d_plist, g.d_pcount);
+  });
   hipLaunchKernelGGL(k_pred_var_reduce, dim3(max_entries * (md.n_test_pad / 256)), dim3(256), 0, g.stream, md, nt,
                      g.d_plist, g.d_pcount);
 }
@@ -683,6 +699,10 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
   const int S = pr->n_subsets, q = pr->q, p = pr->p;
   s->S = S; s->q = q; s->p = p;
   s->matern = c->cov_model == MK_COV_MATERN;
+  // MK_PRED_GEN=1: P^T generated inside the kriging GEMM (exponential; no P^T buffer, half the
+  // kriging memory, but 0.52 vs 0.74 of fp64 peak: the exp/sqrt per element are recomputed for
+  // every row panel).  Default: stored P^T.
+  s->pred_gen = !s->matern && tile_env("MK_PRED_GEN", 0) != 0;
   s->n_part.assign(pr->n_part, pr->n_part + S);
   int nmax = 0;
   for (int i = 0; i < S; ++i) nmax = std::max(nmax, (int)pr->n_part[i]);
@@ -760,7 +780,7 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
     return rc;
   if ((rc = s->alloc(&md.s_pred, (size_t)S * q * n_test_pad)) ||
       (rc = s->alloc(&md.s_part, (size_t)S * q * nt * n_test_pad)) ||
-      (n_test > 0 && (rc = s->alloc(&md.PT, (size_t)S * q * n_pad * n_test_pad))) ||
+      (n_test > 0 && !s->pred_gen && (rc = s->alloc(&md.PT, (size_t)S * q * n_pad * n_test_pad))) ||
       (n_test > 0 && (rc = s->alloc(&md.XK, (size_t)S * q * n_pad * n_test_pad))) ||
       (rc = s->alloc(&md.w_pred, (size_t)S * n_kept * q * std::max(n_test, 1))))
     return rc;
@@ -1088,6 +1108,7 @@ extern "C" int mk_session_outputs(mk_session* s, mk_outputs* o) {
     HIPCHK(hipStreamSynchronize(s->stream));
     int rc = predict_tiled(s, o);
     if (rc) return rc;
+    if (s->prof) drain_timers(s);
   } else if ((o->w_predict || o->w_predict_sum) && n_test > 0) {
     const int C = q * n_test;
     double* dq = scratch.get<double>((size_t)S * C * MK_N_LEVELS);

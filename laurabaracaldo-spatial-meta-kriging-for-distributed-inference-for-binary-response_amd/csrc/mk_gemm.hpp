@@ -174,6 +174,34 @@ __device__ inline void gemm_tile(const double* __restrict__ A, long sA, const do
   }
 }
 
+// acc += op(A)[TM x K] * B[K x TN] with B GENERATED into LDS rather than streamed: gen(k0, img)
+// writes chunk k0's [16][TN] m-contiguous image (k-row stride gb_stride(TN)) with plain LDS stores.
+// A streams by LDS-DMA as in gemm_tile; chunk c+1's B is generated while chunk c multiplies (the
+// stage it overwrites was last read before the previous barrier).  Same MFMA sequence per element
+// as gemm_tile<..., A_MU, B_NU = true> on a stored copy of the same values.
+template <int TM, int TN, bool A_MU, class Gen>
+__device__ inline void gemm_tile_genb(const double* __restrict__ A, long sA, int K, AccT<TM / 32, TN / 32>& acc,
+                                      double* lds, Gen&& gen) {
+  constexpr int STAGE = gb_img(TM) + gb_img(TN);
+  if (K <= 0) return;
+  const int nch = K / GB_K;
+  dma_chunk<A_MU, TM>(A, sA, 0, lds);
+  gen(0, lds + gb_img(TM));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int c = 0; c < nch; ++c) {
+    const double* st = lds + (c & 1) * STAGE;
+    if (c + 1 < nch) {
+      double* nx = lds + ((c + 1) & 1) * STAGE;
+      dma_chunk<A_MU, TM>(A, sA, GB_K * (c + 1), nx);
+      gen(GB_K * (c + 1), nx + gb_img(TM));
+    }
+    mma_chunk<TM, TN, false, A_MU, true, SKIP_NONE, false>(st, st + gb_img(TM), acc, 0, GB_K, 0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+}
+
 // The 128 x 128 form every kernel started from.
 template <bool A_MU, bool B_NU, bool NEG = false, bool REV = false, bool SAME = false, int SKIP = SKIP_NONE,
           bool MASK = false>

@@ -33,6 +33,7 @@ typedef void (*PredPTKernel)(Model, const int*, const int*);
 inline PredPTKernel pred_PT_kernel(int model) {
   return model == MK_COV_EXPONENTIAL ? k_pred_PT<MK_COV_EXPONENTIAL> : k_pred_PT<MK_COV_MATERN>;
 }
+template <bool GEN>
 __global__ void k_pred_var(Model md, MatSet ms, const int* list, const int* count);
 __global__ void k_pred_var_reduce(Model md, int nt, const int* list, const int* count);
 // mk_mcmc.hip

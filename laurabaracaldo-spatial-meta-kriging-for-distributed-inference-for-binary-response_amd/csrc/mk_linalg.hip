@@ -843,6 +843,12 @@ template __global__ void k_pred_PT<MK_COV_MATERN>(Model, const int*, const int*)
 
 // X = W P^T (row tile i, test tile tb), stored column-major by test site (XK[t][row]);
 // partial column sums of squares over valid rows -> s_part[sh][i][t].
+// GEN (exponential model): the P^T tile is generated in LDS chunk by chunk -- exp(-phi d), the
+// expression k_pred_PT stores -- so P^T never exists in HBM: the kernel reads W (kept in L2 across
+// the test tiles of one row panel: consecutive workgroups of a pair share i) and writes X; a
+// stored P^T was re-read from HBM once per row panel (~8.5 x its size at n_s = 2000).
+// !GEN (Matern): P^T from k_pred_PT (its Bessel tables are too heavy to inline per element).
+template <bool GEN>
 __global__ __launch_bounds__(256, 2) void k_pred_var(Model md, MatSet ms, const int* __restrict__ list,
                                                   const int* __restrict__ count) {
   extern __shared__ __attribute__((aligned(16))) double lds[];   // MK_GD_LDS_BYTES
@@ -850,17 +856,53 @@ __global__ __launch_bounds__(256, 2) void k_pred_var(Model md, MatSet ms, const 
   const int per = ms.nt * md.ntt;
   int e, t_;
   if (!xcd_map(*count, per, &e, &t_)) return;
+  // i-major: consecutive workgroups share the W row panel (L2) and stream distinct P^T blocks
+  // (tb-major -- sharing the P^T block, re-reading W -- measured 0.65 vs 0.74 of peak)
   const int i = t_ / md.ntt, tb = t_ % md.ntt;
   const int sh = list[e];
   const int s = sh / md.q;
   const int ns = md.n_s[s];
   const long ld = ms.ld;
   const double* Wm = wmat(ms, sh);
-  const double* PT = md.PT + (long)sh * md.n_pad * md.n_test_pad + tb * MK_NB;
   Acc acc;
   acc_zero(acc);
   const int K = (i + 1) * MK_NB;   // W lower-triangular
-  gemm_128<true, true>(Wm + i * MK_NB, ld, PT, md.n_test_pad, K, K, acc, lds);
+  if (GEN) {
+    const int h = sh % md.q;
+    double phi, nu;
+    current_phi_nu(md, s, h, &phi, &nu);
+    // thread: k-row r of every chunk, 8 consecutive test sites c0 .. c0+7 of the tile
+    const int r = threadIdx.x >> 4, c0 = (threadIdx.x & 15) * 8;
+    const double* cx = md.coords + (long)s * 2 * md.n_pad;
+    double tx[8], ty[8];
+    bool tv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int t = tb * MK_NB + c0 + j;
+      tv[j] = t < md.n_test;
+      tx[j] = tv[j] ? md.coords_test[t] : 0.0;
+      ty[j] = tv[j] ? md.coords_test[md.n_test_pad + t] : 0.0;
+    }
+    gemm_tile_genb<128, 128, true>(Wm + i * MK_NB, ld, K, acc, lds, [&](int k0, double* img) {
+      const int k = k0 + r;
+      const bool kv = k < ns;
+      const double ox = cx[k], oy = cx[md.n_pad + k];
+      d2 v[4];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const double d = dist2d(ox, oy, tx[j], ty[j]);
+        const double x = (kv && tv[j]) ? exp(-phi * d) : 0.0;
+        if (j & 1) v[j >> 1].y = x;
+        else v[j >> 1].x = x;
+      }
+      d2* dst = reinterpret_cast<d2*>(img + r * gb_stride(128) + c0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) dst[j] = v[j];
+    });
+  } else {
+    const double* PT = md.PT + (long)sh * md.n_pad * md.n_test_pad + tb * MK_NB;
+    gemm_128<true, true>(Wm + i * MK_NB, ld, PT, md.n_test_pad, K, K, acc, lds);
+  }
   double* XK = md.XK + (long)sh * md.n_test_pad * md.n_pad + (long)tb * MK_NB * md.n_pad + i * MK_NB;
   store_tile(XK, md.n_pad, acc);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w & 1;
@@ -893,6 +935,8 @@ __global__ __launch_bounds__(256, 2) void k_pred_var(Model md, MatSet ms, const 
     md.s_part[((long)sh * ms.nt + i) * md.n_test_pad + tb * MK_NB + n] = red[0][n] + red[1][n];
   }
 }
+template __global__ void k_pred_var<true>(Model, MatSet, const int*, const int*);
+template __global__ void k_pred_var<false>(Model, MatSet, const int*, const int*);
 
 __global__ __launch_bounds__(256) void k_pred_var_reduce(Model md, int nt, const int* __restrict__ list,
                                                          const int* __restrict__ count) {

@@ -1,6 +1,9 @@
 """Fold two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) into profiles/pmc_chol_update.json.
 
-usage: python tools/pmc_summary.py <fetch_pass_dir> <write_pass_dir> <out.json> "<command profiled>"
+usage: python tools/pmc_summary.py <fetch_pass_dir> <write_pass_dir> <out.json> "<command profiled>" [kernel]
+
+[kernel] (default mk::k_chol_update) is a name prefix: template instances (k_chol_update<128>,
+<64>, ...) are folded into one launch-weighted entry.
 
 gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE reports half the bytes of
 16-B/lane coalesced reads -> x2; WRITE_SIZE as reported.  Both are in KB -> x1024.
@@ -26,6 +29,8 @@ def _per_kernel(d, counter):
             if row["Counter_Name"] != counter:
                 continue
             name = row["Kernel_Name"].split("(")[0]
+            if name.startswith("void "):
+                name = name[5:]
             acc[name][0] += 1
             acc[name][1] += float(row["Counter_Value"])
     return {k: (n, s / n) for k, (n, s) in acc.items()}
@@ -41,8 +46,15 @@ def main():
         wn, wkb = write.get(k, (0, 0.0))
         allk[k] = {"launches": max(fn, wn), "fetch_kb_avg": fkb, "write_kb_avg": wkb,
                    "hbm_bytes_per_launch_corrected": (2.0 * fkb + wkb) * 1024.0}
-    main_k = allk[KERNEL]
-    doc = {"kernel": KERNEL, "command": cmd,
+    kernel = sys.argv[5] if len(sys.argv) > 5 else KERNEL
+    inst = {k: v for k, v in allk.items() if k == kernel or k.startswith(kernel + "<")}
+    if not inst:
+        raise SystemExit(f"{kernel} not in the profile")
+    n = sum(v["launches"] for v in inst.values())
+    main_k = {"launches": n}
+    for f in ("fetch_kb_avg", "write_kb_avg", "hbm_bytes_per_launch_corrected"):
+        main_k[f] = sum(v[f] * v["launches"] for v in inst.values()) / n
+    doc = {"kernel": kernel, "instances": sorted(inst), "command": cmd,
            "correction": "gfx950: FETCH_SIZE counts half the bytes of 16-B/lane coalesced reads "
                          "(MI355X_MICROARCH.md HBM section) -> x2; WRITE_SIZE as reported; units KB -> x1024",
            "fetch_kb_per_launch": main_k["fetch_kb_avg"], "write_kb_per_launch": main_k["write_kb_avg"],
@@ -50,7 +62,7 @@ def main():
            "all_kernels": allk}
     with open(out, "w") as f:
         json.dump(doc, f, indent=1)
-    print(f"{KERNEL}: {doc['hbm_bytes_per_launch'] / 1e9:.3f} GB per launch over {doc['launches']} launches")
+    print(f"{kernel}: {doc['hbm_bytes_per_launch'] / 1e9:.3f} GB per launch over {doc['launches']} launches")
 
 
 if __name__ == "__main__":
