@@ -67,7 +67,7 @@ def _cpu_worker(args):
     cfg = om.Config(1, 2, beta_starting=[0.9, -0.9], beta_tuning=[0.01, 0.01], n_batch=100, batch_length=50,
                     burn_in=2, seed=seed)
     r = om.fit_subset(d["coords"], d["y"], np.ones(n_s), d["x"], cfg, subset=idx, coords_test=d["coords_test"],
-                      max_iter=iters, quantiles=False)
+                      max_iter=iters, quantiles=False, sweep="c")
     return r["loop_seconds"]       # the MCMC iterations only (set-up excluded, as on the GPU side)
 
 
@@ -91,8 +91,9 @@ def cpu_baseline(n_s, iters, workers):
     rate = workers * iters / max(per)
     return dict(value=rate, unit="subset-iters/s", cores=workers, kind="port",
                 sample=f"{workers} subsets x {iters} kept iterations (n_s={n_s}, 1000 kriging sites) of the same "
-                       f"workload, oracle/spmvglm.py (NumPy + OpenBLAS dpotrf/dpotri), one process and one BLAS "
-                       f"thread per core; wall {wall:.1f}s incl. start-up")
+                       f"workload, oracle/spmvglm.py: LAPACK dpotrf/dpotri (OpenBLAS), NumPy vector work and the "
+                       f"latent sweep in C (oracle/csrc/sweep.c), one process and one BLAS thread per core; "
+                       f"wall {wall:.1f}s incl. start-up")
 
 
 def host_cores():

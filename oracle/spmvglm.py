@@ -226,15 +226,40 @@ class Config:
 
 
 # ----------------------------------------------------------------- the sampler
+_SWEEP_LIB = None
+
+
+def _c_sweep():
+    """ctypes handle of oracle/_sweep.so (make -C oracle), built on first use."""
+    global _SWEEP_LIB
+    if _SWEEP_LIB is None:
+        import ctypes
+        import os
+        import subprocess
+        here = os.path.dirname(os.path.abspath(__file__))
+        so = os.path.join(here, "_sweep.so")
+        if not os.path.exists(so):
+            subprocess.check_call(["make", "-s", "-C", here, "_sweep.so"])
+        lib = ctypes.CDLL(so)
+        dp = ctypes.POINTER(ctypes.c_double)
+        lib.mk_oracle_sweep.argtypes = [ctypes.c_int, ctypes.c_int, dp, dp, dp, dp, dp, ctypes.POINTER(dp), dp, dp, dp,
+                                        dp, dp]
+        lib.mk_oracle_sweep.restype = None
+        _SWEEP_LIB = lib
+    return _SWEEP_LIB
+
+
 def fit_subset(coords, y, wt, X, cfg, subset=0, coords_test=None, record_w=False,
-               quantiles=True, max_iter=None):
+               quantiles=True, max_iter=None, sweep="py"):
     """One subset: spMvGLM amcmc fit with fused spPredict on kept iterations.
 
     coords (n,2); y, wt (N=n*q) location-major; X (N,p) block-diagonal design.
     Returns dict with 'samples' (n_samples,P) reported parameters, 'accept'
     (n_batch, n_mh) acceptance rates, 'tuning' final log-sd, 'w_pred' (kept,
     q*n_test) predictive draws, and (if quantiles) 'param_q' (200,P), 'w_q'
-    (200, q*n_test).  max_iter truncates the chain (bounded CPU timing).
+    (200, q*n_test).  max_iter truncates the chain (bounded CPU timing).  sweep="c" runs step 5
+    (the latent-w sweep) in oracle/csrc/sweep.c -- the same operations in the same order -- for
+    the CPU baseline's timing.
     """
     q, p = cfg.q, cfg.p
     n = coords.shape[0]
@@ -396,7 +421,21 @@ def fit_subset(coords, y, wt, X, cfg, subset=0, coords_test=None, record_w=False
         dll = loglik_terms(y, wt, eta + delta_w, cfg.link) - loglik_terms(y, wt, eta, cfg.link)
         lu = logus[o_w:o_w + N]
         Qdiag = np.stack([np.diag(Q[h]) for h in range(q)], axis=1)      # (n,q)
-        for k in range(N):
+        if sweep == "c":
+            import ctypes
+            dp = ctypes.POINTER(ctypes.c_double)
+            arrs = [np.ascontiguousarray(a_, dtype=np.float64) for a_ in (delta_w, dll, lu, Ainv, Qdiag)]
+            G, U = np.ascontiguousarray(G), np.ascontiguousarray(U)   # updated in place below
+            for a_ in (w, eta):
+                assert a_.flags["C_CONTIGUOUS"] and a_.dtype == np.float64
+            Qs = [np.ascontiguousarray(Q[h]) for h in range(q)]
+            qptr = (dp * q)(*[a_.ctypes.data_as(dp) for a_ in Qs])
+            acc_w = accept[o_w:o_w + N].copy()
+            _c_sweep().mk_oracle_sweep(n, q, *[a_.ctypes.data_as(dp) for a_ in arrs], qptr, G.ctypes.data_as(dp),
+                                       U.ctypes.data_as(dp), w.ctypes.data_as(dp), eta.ctypes.data_as(dp),
+                                       acc_w.ctypes.data_as(dp))
+            accept[o_w:o_w + N] = acc_w
+        for k in (range(N) if sweep != "c" else ()):
             i, a = divmod(k, q)
             dl = delta_w[k]
             c = Ainv[:, a] @ G[i]
