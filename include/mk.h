@@ -112,10 +112,19 @@ int32_t mk_session_iteration(const mk_session* s);
 /* Quantile summaries + optional sample copies (requires all iterations done
  * for parameters / w_predict). */
 int mk_session_outputs(mk_session* s, mk_outputs* out);
-/* Per-kernel timing (HIP events on the session stream): launches, total ms and
- * algorithmic flops per kernel kind (0 Cholesky panel update, 1 diagonal tile,
- * 2 panel trsm, 3 latent sweep, 4 R^-1 diagonal tiles, 5 whole iterations, 6
- * inverse levels).  mk_session_profile(s, enable) before mk_session_run:
+/* spPredict after spMvGLM without refitting (spPredict(m.1, coords.test, ...), MK.R:87): a session
+ * created with predict_tile > 0 keeps every kept chain state (burn_in = 1 keeps all of them);
+ * mk_session_set_test_sites replaces its test sites (n_test x 2 column-major) and
+ * mk_session_set_kept_window(first, last) restricts the kriging replay of the next
+ * mk_session_outputs to iterations first..last (1-based, burn_in <= first <= last <= n.samples;
+ * spPredict's start / end).  The draws are those a session with burn_in = first would make. */
+int mk_session_set_test_sites(mk_session* s, int32_t n_test, const double* coords_test);
+int mk_session_set_kept_window(mk_session* s, int32_t first, int32_t last);
+/* Per-kernel timing (HIP events on the launching streams): launches, total ms and
+ * algorithmic flops per kernel kind (0 Cholesky panel update, 128-tiles; 1 diagonal tile;
+ * 2 panel trsm; 3 latent sweep; 4 R^-1 diagonal tiles; 5 whole iterations; 6 inverse levels;
+ * 7 panel update, 64/32-sub-tiles; 8 kinds 0 + 7 with overlapping launches counted once;
+ * 9 kriging GEMM k_pred_var).  mk_session_profile(s, enable) before mk_session_run:
  * enable 0 = off, 1 = every kind, otherwise a mask with bit (1 + kind) per kind
  * bracketed (e.g. 2 << 0 = the panel update only; fewer events, less overhead). */
 int mk_session_profile(mk_session* s, int32_t enable);

@@ -170,6 +170,9 @@ struct mk_session {
   Group all;                      // the whole shard on `stream`
   bool tiled = false;             // kriging after the fit over test-site tiles (predict_tile)
   int pred_tile = 0, n_test_all = 0, n_test_pad_all = 0;
+  int tile_req = 0;               // predict_tile as configured
+  int win_lo = 0, win_n = -1;     // tiled kriging: kept states [win_lo, win_lo + win_n) (-1: all)
+  std::vector<void*> kbufs;       // the kriging buffers (re-sized by mk_session_set_test_sites)
   double* d_ct_all = nullptr;     // all test sites [2][n_test_pad_all] (tiled mode)
   int* d_slist = nullptr;         // tiled replay: per-outcome subset lists [q][S] + counts [q]
   int* d_scount = nullptr;
@@ -190,6 +193,16 @@ struct mk_session {
   std::vector<Timed> pending;
   Stat stats[NKSTAT];
 
+  // Free one buffer allocated by alloc().
+  void release(void* ptr) {
+    if (!ptr) return;
+    for (size_t i = 0; i < allocs.size(); ++i)
+      if (allocs[i] == ptr) {
+        hipFree(ptr);
+        allocs.erase(allocs.begin() + (long)i);
+        return;
+      }
+  }
   template <typename T>
   int alloc(T** p_, size_t n) {
     void* ptr = nullptr;
@@ -680,6 +693,70 @@ static int setup_groups(mk_session* s, int n_groups) {
   return 0;
 }
 
+// (Re)allocate the kriging buffers for n_test_all test sites (coords_test: n_test_all x 2
+// column-major) and upload the sites: all of them in d_ct_all, the fused path's copy in the tile
+// buffer d_ct.  Tiled sessions size the buffers for one tile.  Refreshes the group views.
+static int kriging_buffers(mk_session* s, int n_test_all, const double* coords_test) {
+  Model& md = s->md;
+  for (void* b : s->kbufs) s->release(b);
+  s->kbufs.clear();
+  md.PT = md.XK = md.s_pred = md.s_part = md.w_pred = nullptr;
+  const int S = s->S, q = s->q, nt = s->nt, n_pad = s->n_pad;
+  s->n_test_all = n_test_all;
+  s->n_test_pad_all = round_up(std::max(n_test_all, 1), 256);
+  s->pred_tile = s->tiled ? std::min(s->tile_req, std::max(n_test_all, 1)) : n_test_all;
+  const int n_test = n_test_all > 0 ? s->pred_tile : 0;
+  const int n_test_pad = round_up(std::max(n_test, 1), 256);
+  md.n_test = n_test;
+  md.n_test_pad = n_test_pad;
+  md.ntt = n_test_pad / MK_NB;
+  double* d_ct = nullptr;
+  int rc;
+  if ((rc = s->alloc(&d_ct, (size_t)2 * n_test_pad)) || (rc = s->alloc(&s->d_ct_all, (size_t)2 * s->n_test_pad_all)) ||
+      (rc = s->alloc(&md.s_pred, (size_t)S * q * n_test_pad)) ||
+      (rc = s->alloc(&md.s_part, (size_t)S * q * nt * n_test_pad)) ||
+      (n_test > 0 && !s->pred_gen && (rc = s->alloc(&md.PT, (size_t)S * q * n_pad * n_test_pad))) ||
+      (n_test > 0 && (rc = s->alloc(&md.XK, (size_t)S * q * n_pad * n_test_pad))) ||
+      (rc = s->alloc(&md.w_pred, (size_t)S * md.n_kept * q * std::max(n_test, 1))))
+    return rc;
+  md.coords_test = d_ct;
+  s->kbufs = {d_ct, s->d_ct_all, md.s_pred, md.s_part, md.PT, md.XK, md.w_pred};
+  HIPCHK(hipMemset(md.s_pred, 0, (size_t)S * q * n_test_pad * 8));
+  const int npa = s->n_test_pad_all;
+  std::vector<double> hct((size_t)2 * npa, 0.0);
+  for (int t = 0; t < n_test_all; ++t) {
+    hct[t] = coords_test[t];
+    hct[npa + t] = coords_test[n_test_all + t];
+  }
+  HIPCHK(hipMemcpy(s->d_ct_all, hct.data(), hct.size() * 8, hipMemcpyHostToDevice));
+  // fused kriging reads every site from d_ct ([2][n_test_pad]); tiled mode fills it per tile
+  if (!s->tiled) HIPCHK(hipMemcpy(d_ct, hct.data(), hct.size() * 8, hipMemcpyHostToDevice));
+  s->all.md = s->md;
+  for (auto& g : s->groups) g.md = model_view(s->md, g.s0, g.S);
+  return 0;
+}
+
+extern "C" int mk_session_set_test_sites(mk_session* s, int32_t n_test, const double* coords_test) {
+  if (!s) return set_err(MK_E_ARG, "null session");
+  if (!s->tiled)
+    return set_err(MK_E_ARG, "the session keeps no chain states: create it with predict_tile > 0 (and no test sites)");
+  if (n_test < 1 || !coords_test) return set_err(MK_E_ARG, "n_test must be >= 1 with coordinates");
+  HIPCHK(hipSetDevice(s->device));
+  HIPCHK(hipStreamSynchronize(s->stream));
+  return kriging_buffers(s, n_test, coords_test);
+}
+
+extern "C" int mk_session_set_kept_window(mk_session* s, int32_t first, int32_t last) {
+  if (!s) return set_err(MK_E_ARG, "null session");
+  if (!s->tiled) return set_err(MK_E_ARG, "kept windows need a session created with predict_tile > 0");
+  const int lo = s->md.kept0 + 1, hi = s->md.n_samples;
+  if (first < lo || last < first || last > hi)
+    return set_err(MK_E_ARG, "kept window must satisfy burn_in <= first <= last <= n.samples");
+  s->win_lo = first - lo;
+  s->win_n = last - first + 1;
+  return 0;
+}
+
 extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_session** out) {
   if (!out) return set_err(MK_E_ARG, "null out");
   *out = nullptr;
@@ -719,13 +796,11 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
   const int n_samples = c->n_batch * c->batch_length;
   const int kept0 = c->burn_in - 1;
   const int n_kept = n_samples - kept0;
-  // tiled kriging: device kriging buffers hold one tile of test sites; all sites stay in HBM
-  s->tiled = c->predict_tile > 0 && c->predict_tile < pr->n_test;
-  s->n_test_all = pr->n_test;
-  s->n_test_pad_all = round_up(std::max(pr->n_test, 1), 256);
-  s->pred_tile = s->tiled ? c->predict_tile : pr->n_test;
-  const int n_test = s->pred_tile;
-  const int n_test_pad = round_up(std::max(n_test, 1), 256);
+  // tiled kriging: device kriging buffers hold one tile of test sites; all sites stay in HBM.
+  // predict_tile > 0 without test sites records the kept states for a later
+  // mk_session_set_test_sites (spPredict after spMvGLM without refitting).
+  s->tiled = c->predict_tile > 0 && (pr->n_test == 0 || c->predict_tile < pr->n_test);
+  s->tile_req = c->predict_tile;
 
   Model& md = s->md;
   md.S = S; md.q = q; md.p = p; md.n_pad = n_pad; md.Np = Np; md.nt = nt; md.ntri = ntri; md.n_theta = n_theta;
@@ -734,7 +809,6 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
   md.o_A = p; md.o_phi = p + ntri; md.o_nu = p + ntri + q; md.o_w = o_w; md.n_mh_max = n_mh_max;
   md.n_batch = c->n_batch; md.batch_length = c->batch_length; md.n_samples = n_samples;
   md.kept0 = kept0; md.n_kept = n_kept;
-  md.n_test = n_test; md.n_test_pad = n_test_pad; md.ntt = n_test_pad / MK_NB;
   md.subset_base = pr->subset_base;
   md.S_all = S;
   md.t_off = 0;
@@ -752,13 +826,12 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
   s->record_w = c->record_w != 0;
 
   // ---------------- allocations
-  int* d_ns; double *d_coords, *d_y, *d_wt, *d_X, *d_ct;
+  int* d_ns; double *d_coords, *d_y, *d_wt, *d_X;
   if ((rc = s->alloc(&d_ns, S)) || (rc = s->alloc(&d_coords, (size_t)S * 2 * n_pad)) ||
       (rc = s->alloc(&d_y, (size_t)S * Np)) || (rc = s->alloc(&d_wt, (size_t)S * Np)) ||
-      (rc = s->alloc(&d_X, (size_t)S * p * Np)) || (rc = s->alloc(&d_ct, (size_t)2 * n_test_pad)) ||
-      (rc = s->alloc(&s->d_ct_all, (size_t)2 * s->n_test_pad_all)))
+      (rc = s->alloc(&d_X, (size_t)S * p * Np)))
     return rc;
-  md.n_s = d_ns; md.coords = d_coords; md.y = d_y; md.wt = d_wt; md.X = d_X; md.coords_test = d_ct;
+  md.n_s = d_ns; md.coords = d_coords; md.y = d_y; md.wt = d_wt; md.X = d_X;
   if ((rc = s->alloc(&md.beta, (size_t)S * p)) || (rc = s->alloc(&md.theta, (size_t)S * n_theta)) ||
       (rc = s->alloc(&md.w, (size_t)S * Np)) || (rc = s->alloc(&md.eta, (size_t)S * Np)) ||
       (rc = s->alloc(&md.tune, (size_t)S * n_mh_max)) || (rc = s->alloc(&md.acc, (size_t)S * n_mh_max)) ||
@@ -778,12 +851,7 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
                    (rc = s->alloc(&md.kA, (size_t)n_kept * S * q * q)) ||
                    (rc = s->alloc(&s->d_slist, (size_t)q * S)) || (rc = s->alloc(&s->d_scount, (size_t)q))))
     return rc;
-  if ((rc = s->alloc(&md.s_pred, (size_t)S * q * n_test_pad)) ||
-      (rc = s->alloc(&md.s_part, (size_t)S * q * nt * n_test_pad)) ||
-      (n_test > 0 && !s->pred_gen && (rc = s->alloc(&md.PT, (size_t)S * q * n_pad * n_test_pad))) ||
-      (n_test > 0 && (rc = s->alloc(&md.XK, (size_t)S * q * n_pad * n_test_pad))) ||
-      (rc = s->alloc(&md.w_pred, (size_t)S * n_kept * q * std::max(n_test, 1))))
-    return rc;
+  if ((rc = kriging_buffers(s, pr->n_test, pr->coords_test))) return rc;
   MatSet& ms = s->ms;
   ms.ld = n_pad; ms.nt = nt; ms.q = q;
   if ((rc = s->alloc(&ms.L, (size_t)S * q * 2 * n_pad * n_pad)) ||
@@ -818,20 +886,11 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
       off_site += ns;
     }
   }
-  const int npa = s->n_test_pad_all, nta = s->n_test_all;
-  std::vector<double> hct((size_t)2 * npa, 0.0);
-  for (int t = 0; t < nta; ++t) {
-    hct[t] = pr->coords_test[t];
-    hct[npa + t] = pr->coords_test[nta + t];
-  }
   HIPCHK(hipMemcpy(d_ns, pr->n_part, S * sizeof(int), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(d_coords, hc.data(), hc.size() * 8, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(d_y, hy.data(), hy.size() * 8, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(d_wt, hw.data(), hw.size() * 8, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(d_X, hX.data(), hX.size() * 8, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(s->d_ct_all, hct.data(), hct.size() * 8, hipMemcpyHostToDevice));
-  // fused kriging reads every site from d_ct ([2][n_test_pad]); tiled mode fills it per tile
-  if (!s->tiled) HIPCHK(hipMemcpy(d_ct, hct.data(), hct.size() * 8, hipMemcpyHostToDevice));
 
   // ---------------- starting values (identical for every subset, MK.R:54-62)
   std::vector<double> hb((size_t)S * p), hth((size_t)S * n_theta), hwv((size_t)S * Np, 0.0),
@@ -896,7 +955,6 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
   HIPCHK(hipMemsetAsync(md.u, 0, (size_t)S * q * n_pad * 8, s->stream));
   HIPCHK(hipMemsetAsync(md.z, 0, (size_t)S * q * n_pad * 8, s->stream));
   HIPCHK(hipMemsetAsync(md.Z, 0, (size_t)S * q * q * n_pad * 8, s->stream));
-  HIPCHK(hipMemsetAsync(md.s_pred, 0, (size_t)S * q * n_test_pad * 8, s->stream));
   HIPCHK(hipMemsetAsync(ms.W, 0, (size_t)S * q * n_pad * n_pad * 8, s->stream));
   {
     std::vector<double> probs(MK_N_LEVELS);
@@ -1021,7 +1079,8 @@ struct DevBufs {
 // per subset instead of q*n_test x kept.
 static int predict_tiled(mk_session* s, mk_outputs* o) {
   Model& md = s->md;
-  const int S = s->S, q = s->q, nt = s->nt, n_kept = md.n_kept;
+  const int S = s->S, q = s->q, nt = s->nt;
+  const int k_lo = s->win_lo, n_kept = s->win_n < 0 ? md.n_kept : s->win_n;   // kept states replayed
   const int T = s->pred_tile, T_pad = md.n_test_pad, n_test = s->n_test_all;
   const long C = (long)q * n_test;
   hipStream_t st = s->stream;
@@ -1039,15 +1098,17 @@ static int predict_tiled(mk_session* s, mk_outputs* o) {
     HIPCHK(hipMemcpyAsync((void*)(md.coords_test + T_pad), s->d_ct_all + s->n_test_pad_all + t0, (size_t)Tc * 8,
                           hipMemcpyDeviceToDevice, st));
     Model mt = md;
+    mt.n_kept = n_kept;   // w_pred holds the window's draws
     mt.n_test = Tc;
     mt.t_off = t0;
     mt.ntt = (Tc + MK_NB - 1) / MK_NB;   // a short last tile: only its valid 128-site column blocks
                                           // (strides stay those of the full tile, n_test_pad)
-    for (int k = 0; k < n_kept; ++k) {
+    for (int j = 0; j < n_kept; ++j) {
+      const int k = k_lo + j;   // kept state k = iteration kept0 + k
       mt.theta = md.kth + (long)k * S * md.n_theta;
       mt.z = md.kz + (long)k * S * q * md.n_pad;
       mt.A_full = md.kA + (long)k * S * q * q;
-      const double* prev = k ? md.kth + (long)(k - 1) * S * md.n_theta : nullptr;
+      const double* prev = j ? md.kth + (long)(k - 1) * S * md.n_theta : nullptr;
       hipLaunchKernelGGL(k_kept_dirty, dim3(1), dim3(256), 0, st, mt, prev, s->d_slist, s->d_scount, g.d_plist,
                          g.d_pcount);
       for (int h = 0; h < q; ++h) {
@@ -1060,7 +1121,7 @@ static int predict_tiled(mk_session* s, mk_outputs* o) {
       g.md = mt;
       launch_pred_refresh(s, g);
       const int per = (Tc + 3) / 4;
-      hipLaunchKernelGGL(k_pred_draw, dim3(S * per), dim3(256), 0, st, mt, md.kept0 + k, k);
+      hipLaunchKernelGGL(k_pred_draw, dim3(S * per), dim3(256), 0, st, mt, md.kept0 + k, j);
       HIPCHK(hipGetLastError());
     }
     hipLaunchKernelGGL(k_quantiles, dim3(S * Ct), dim3(256), 0, st, md.w_pred, (long)n_kept * Ct, (long)Ct, n_kept, Ct,

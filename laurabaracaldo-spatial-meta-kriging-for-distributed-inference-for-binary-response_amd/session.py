@@ -159,6 +159,19 @@ class Session:
     def run(self, n_iter):
         check(self._lib.mk_session_run(self._h, int(n_iter)))
 
+    def set_test_sites(self, coords_test):
+        """Kriging sites for the next outputs() of a session created with predict_tile > 0
+        (its kept chain states were recorded during the run): spPredict without refitting."""
+        ct = np.asarray(coords_test, float).reshape(-1, 2)
+        self.n_test = int(ct.shape[0])
+        self.coords_test = _f64(ct.ravel(order="F"))
+        check(self._lib.mk_session_set_test_sites(self._h, self.n_test, dptr(self.coords_test)))
+
+    def set_kept_window(self, first, last):
+        """Replay only iterations first..last (1-based; spPredict's start / end) in the next outputs()."""
+        check(self._lib.mk_session_set_kept_window(self._h, int(first), int(last)))
+        self._window = int(last) - int(first) + 1
+
     @property
     def iteration(self):
         return self._lib.mk_session_iteration(self._h)
@@ -205,7 +218,7 @@ class Session:
             res["_w_samples_flat"] = np.zeros(tot)
             o.w_samples = dptr(res["_w_samples_flat"])
         if w_pred_samples and self.n_test:
-            res["w_pred_samples"] = np.zeros((S, cfg.kept, q * self.n_test))
+            res["w_pred_samples"] = np.zeros((S, getattr(self, "_window", cfg.kept), q * self.n_test))
             o.w_pred_samples = dptr(res["w_pred_samples"])
         if acceptance:
             nrep = cfg.p + cfg.n_theta + 1

@@ -12,14 +12,18 @@ Argument names and meaning follow spBayes as called by the reference:
 design without intercept handling -- the ``Y ~ X - 1`` form of MK.R:80).
 Errors are raised as ValueError / MkError where spBayes would stop().
 
-spPredict on this build replays the fitted chain with the prediction sites
-attached (the MI355X design fuses kriging into the kept iterations): the chain
-is a deterministic function of the seed and every kriging draw uses its own
-Philox stream, so the replayed chain is identical to the fitted one.
+spMvGLM keeps its device session open with every chain state recorded
+(predict_tile mode, burn_in = 1); spPredict then only runs the kriging: it sets
+the prediction sites (mk_session_set_test_sites) and replays the kept states of
+iterations start..end (mk_session_set_kept_window) -- no refit.  Every kriging
+draw has its own Philox stream keyed by the iteration, so the draws equal those of
+a fit that fused the kriging into iterations start..end.
 """
 import numpy as np
 
 from .session import SamplerConfig, Session
+
+PREDICT_TILE = 65536   # test sites per kriging pass in spPredict (device buffers per pass)
 
 
 def _stack(formula, weights):
@@ -89,34 +93,36 @@ def spMvGLM(formula, coords, weights, starting, tuning, priors, amcmc, cov_model
         raise ValueError("error: family must be binomial (the reference's binary response)")
     q, p, n, y, X, wt = _stack(formula, weights)
     coords = np.asarray(coords, float).reshape(n, 2)
-    cfg = _config(q, p, starting, tuning, priors, amcmc, cov_model, seed=seed)
+    cfg = _config(q, p, starting, tuning, priors, amcmc, cov_model, burn_in=1, seed=seed)
+    cfg.predict_tile = PREDICT_TILE          # record every chain state for spPredict
     sub = dict(coords=coords, y=y, weights=wt, x=X)
-    with Session([sub], cfg, subset_base=subset_index, device=device, record_w=True) as ses:
+    ses = Session([sub], cfg, subset_base=subset_index, device=device, record_w=True)
+    try:
         ses.run(cfg.n_samples)
         out = ses.outputs(quantiles=False, samples=True, w_samples=True, acceptance=True)
+    except Exception:
+        ses.close()
+        raise
     fit = SpMvGLMFit()
     fit["p.beta.theta.samples"] = out["samples"][0]
     fit["p.w.samples"] = out["w_samples"][0]
     fit["acceptance"] = out["acceptance"][0]
-    fit["_inputs"] = dict(sub=sub, cfg_args=(q, p, starting, tuning, priors, amcmc, cov_model), seed=seed,
-                          device=device, subset_index=subset_index)
+    fit["_session"] = ses                    # closed when the fit object is collected
+    fit["_n_samples"] = cfg.n_samples
     return fit
 
 
 def spPredict(sp_obj, pred_coords, pred_covars=None, start=1, end=None, thin=1):
-    """p.w.predictive.samples ((q n_test) x kept) for kept iterations start..end (1-based, inclusive)."""
-    inp = sp_obj["_inputs"]
-    q, p, starting, tuning, priors, amcmc, cov_model = inp["cfg_args"]
-    n_samples = amcmc["n.batch"] * amcmc["batch.length"]
+    """p.w.predictive.samples ((q n_test) x kept) for kept iterations start..end (1-based,
+    inclusive; every thin-th), kriged from the chain states spMvGLM recorded (no refit)."""
+    ses = sp_obj["_session"]
+    n_samples = sp_obj["_n_samples"]
     end = n_samples if end is None else int(end)
     start = int(start)
     if not (1 <= start <= end <= n_samples):
         raise ValueError("error: invalid start/end")
-    cfg = _config(q, p, starting, tuning, priors, amcmc, cov_model, burn_in=start, seed=inp["seed"])
-    pred_coords = np.asarray(pred_coords, float).reshape(-1, 2)
-    with Session([inp["sub"]], cfg, coords_test=pred_coords, subset_base=inp["subset_index"],
-                 device=inp["device"]) as ses:
-        ses.run(cfg.n_samples)
-        out = ses.outputs(quantiles=False, w_pred_samples=True)
-    wp = out["w_pred_samples"][0]                  # (q n_test) x kept(start..n_samples)
-    return {"p.w.predictive.samples": wp[:, : end - start + 1: int(thin)]}
+    ses.set_test_sites(np.asarray(pred_coords, float).reshape(-1, 2))
+    ses.set_kept_window(start, end)
+    out = ses.outputs(quantiles=False, w_pred_samples=True)
+    wp = out["w_pred_samples"][0]                  # (q n_test) x (end - start + 1)
+    return {"p.w.predictive.samples": wp[:, ::int(thin)]}

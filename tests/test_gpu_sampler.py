@@ -182,3 +182,38 @@ def test_tiled_kriging_is_bit_identical_to_fused(mk, n, q, cov, tile):
     for s in range(1, S):
         seq = seq + fused["w_predict"][s]
     assert np.array_equal(fused["w_predict_sum"], seq)
+
+
+@pytest.mark.parametrize("q,cov", [(1, 0), (2, 0), (1, 1)])
+def test_sppredict_reuses_the_fit_without_refitting(mk, q, cov):
+    """spMvGLM keeps every chain state on the device; spPredict(start, end, thin) only krigs
+    (mk_session_set_test_sites + mk_session_set_kept_window).  Its draws equal those of a session
+    that fused the kriging into iterations start..n.samples (burn_in = start), and spMvGLM's
+    samples equal that session's chain (MK.R:80-87: spMvGLM then spPredict(start = burn.in))."""
+    n, n_test, start = 90, 11, 7
+    d = mk.synthetic.generate(n, q=q, n_test=n_test, seed=41 + q + cov, cov_model=cov)
+    p = 2 * q
+    formula = [(d["y"][a::q], d["x"][a::q, 2 * a:2 * a + 2]) for a in range(q)]
+    starting = {"beta": np.zeros(p), "phi": 3 / 0.5, "A": np.eye(q)[np.tril_indices(q)], "w": 0.0}
+    tuning = {"beta": np.full(p, 0.05), "phi": 1.0, "A": 0.1, "w": 0.5}
+    priors = {"phi.Unif": (3 / 0.75, 3 / 0.25), "K.IW": (q, 0.1 * np.eye(q))}
+    if cov:
+        starting["nu"], tuning["nu"], priors["nu.Unif"] = 0.5, 0.1, (0.1, 2.0)
+    amcmc = {"n.batch": 3, "batch.length": 4, "accept.rate": 0.43}
+    model = "matern" if cov else "exponential"
+    fit = mk.spMvGLM(formula, d["coords"], np.ones((n, q)), starting, tuning, priors, amcmc, cov_model=model, seed=9)
+    pred = mk.spPredict(fit, d["coords_test"], start=start)["p.w.predictive.samples"]
+    part = mk.spPredict(fit, d["coords_test"][:5], start=start + 2, end=10, thin=2)["p.w.predictive.samples"]
+    # reference: one session with the kriging fused into iterations start..12
+    from importlib import import_module
+    sb = import_module(mk.__name__ + ".spbayes")
+    cfg = sb._config(q, p, starting, tuning, priors, amcmc, model, burn_in=start, seed=9)
+    q_, p_, n_, y, X, wt = sb._stack(formula, np.ones((n, q)))
+    with mk.Session([dict(coords=d["coords"], y=y, weights=wt, x=X)], cfg, coords_test=d["coords_test"]) as ses:
+        ses.run(cfg.n_samples)
+        ref = ses.outputs(quantiles=False, samples=True, w_pred_samples=True)
+    assert np.array_equal(fit["p.beta.theta.samples"], ref["samples"][0])
+    assert np.array_equal(pred, ref["w_pred_samples"][0])
+    # start + 2 .. 10, every 2nd, first 5 sites: rows (site, outcome) location-major
+    sub = ref["w_pred_samples"][0][:5 * q, 2:10 - start + 1:2]
+    assert np.array_equal(part, sub)
