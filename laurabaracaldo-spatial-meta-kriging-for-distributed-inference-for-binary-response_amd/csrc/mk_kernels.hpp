@@ -12,7 +12,7 @@ typedef void (*CovCandidateKernel)(Model, MatSet, int, int, int, int, const int*
 inline CovCandidateKernel cov_candidate_kernel(int model) {
   return model == MK_COV_EXPONENTIAL ? k_cov_candidate<MK_COV_EXPONENTIAL> : k_cov_candidate<MK_COV_MATERN>;
 }
-template <int TM>
+template <int TM, int TN = TM>
 __global__ void k_chol_update(MatSet ms, int S, int h0, int hc, int k, int ia, int ib, int j0, int j1,
                               const int* slist, const int* scount);
 template <int TM>

@@ -245,42 +245,44 @@ template __global__ void k_cov_candidate<MK_COV_MATERN>(Model, MatSet, int, int,
 // (Generating C(i,k) from coordinates at its first touch inside this kernel was measured
 // slower on cfg3 and its code path made the kernel spill 80 VGPRs: candidates come from
 // k_cov_candidate.)
-// TM = 128: one workgroup per 128-tile.  TM = 64 / 32: four / sixteen per tile (small shards:
-// late panels have few tiles and long K), bit-identical (mk_gemm.hpp); the upper sub-tiles of
-// the diagonal tile are skipped -- k_chol_diag reads the lower triangle only.
+// TM x TN = 128 x 128: one workgroup per 128-tile; 64 x 64 / 32 x 32: four / sixteen per tile
+// (small shards: late panels have few tiles and long K), bit-identical (mk_gemm.hpp); sub-tiles
+// of the diagonal tile entirely above the diagonal are skipped -- k_chol_diag reads the lower
+// triangle only.  (64 x 128 row halves measured slower than 64 x 64 quarters at 32-63 subsets;
+// two alternating bulk streams for consecutive columns, no faster than one.)
 // Column k, tiles i in [ia, ib), panels j in [j0, j1) (j1 <= k): C(i,k) -= sum_j L(i,j) L(k,j)^T.
 // The split schedule (launch_cholesky) runs panels [0, k-1) early on the bulk stream and panel
 // k-1 on the critical stream; the accumulator round-trips through fp64 memory between the two,
 // so every element sees the same MFMA sequence as one [0, k) launch (same bits).
-template <int TM>
+template <int TM, int TN>
 __global__ __launch_bounds__(256, 2) void k_chol_update(MatSet ms, int S, int h0, int hc, int k, int ia, int ib,
                                                        int j0, int j1, const int* slist, const int* scount) {
-  extern __shared__ __attribute__((aligned(16))) double lds[];   // gb_lds_bytes(TM, TM) (two DMA stages)
-  constexpr int SUBR = MK_NB / TM, SUB = SUBR * SUBR;
+  extern __shared__ __attribute__((aligned(16))) double lds[];   // gb_lds_bytes(TM, TN) (two DMA stages)
+  constexpr int SUBR = MK_NB / TM, SUB = SUBR * (MK_NB / TN);
   const int ntk = ib - ia;
   int e, t, s, h;
   if (!xcd_map(active_pairs(slist, scount, S, hc), ntk * SUB, &e, &t) || !pick_pair(slist, scount, e, h0, hc, &s, &h))
     return;
   const int st = t % SUB;
   t /= SUB;
-  const int sr = st % SUBR, sc = st / SUBR;   // (0, 0) when TM = 128
+  const int sr = st % SUBR, sc = st / SUBR;   // (0, 0) when TM = TN = 128
   const int i = ia + t;
-  if (i == k && sc > sr) return;
+  if (i == k && sc * TN >= (sr + 1) * TM) return;   // entirely above the diagonal
   const int sh = s * ms.q + h;
   double* M = mat_slot(ms, sh, 1 - ms.cur[sh]);
   const long ld = ms.ld;
-  double* C = M + i * MK_NB + sr * TM + (long)(k * MK_NB + sc * TM) * ld;
-  AccT<TM / 32, TM / 32> acc;
+  double* C = M + i * MK_NB + sr * TM + (long)(k * MK_NB + sc * TN) * ld;
+  AccT<TM / 32, TN / 32> acc;
   acc_load(acc, C, ld);
   // (Skipping the diagonal tiles' unused upper quadrant -- per MFMA or per chunk -- measured slower.)
   const long jo = (long)j0 * MK_NB * ld;
-  gemm_tile<TM, TM, true, true, true>(M + i * MK_NB + sr * TM + jo, ld, M + k * MK_NB + sc * TM + jo, ld,
+  gemm_tile<TM, TN, true, true, true>(M + i * MK_NB + sr * TM + jo, ld, M + k * MK_NB + sc * TN + jo, ld,
                                       (j1 - j0) * MK_NB, (j1 - j0) * MK_NB, acc, lds);
   store_tile(C, ld, acc);
 }
-template __global__ void k_chol_update<128>(MatSet, int, int, int, int, int, int, int, int, const int*, const int*);
-template __global__ void k_chol_update<64>(MatSet, int, int, int, int, int, int, int, int, const int*, const int*);
-template __global__ void k_chol_update<32>(MatSet, int, int, int, int, int, int, int, int, const int*, const int*);
+template __global__ void k_chol_update<128, 128>(MatSet, int, int, int, int, int, int, int, int, const int*, const int*);
+template __global__ void k_chol_update<64, 64>(MatSet, int, int, int, int, int, int, int, int, const int*, const int*);
+template __global__ void k_chol_update<32, 32>(MatSet, int, int, int, int, int, int, int, int, const int*, const int*);
 
 // TM = 64: the tile's two row halves on two workgroups (in place: each reads and writes its own
 // rows only), bit-identical.
