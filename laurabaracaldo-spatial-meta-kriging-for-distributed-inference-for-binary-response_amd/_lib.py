@@ -66,6 +66,8 @@ EXPORTS = {
     "mk_session_create": (ctypes.c_int, [ctypes.POINTER(Problem), ctypes.POINTER(Config), ctypes.POINTER(ctypes.c_void_p)]),
     "mk_session_run": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32]),
     "mk_session_iteration": (ctypes.c_int32, [ctypes.c_void_p]),
+    "mk_session_set_lookahead": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32]),
+    "mk_session_lookahead": (ctypes.c_int32, [ctypes.c_void_p]),
     "mk_session_outputs": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Outputs)]),
     "mk_session_set_test_sites": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(ctypes.c_double)]),
     "mk_session_set_kept_window": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32]),

@@ -138,6 +138,8 @@ Model model_view(const Model& m, int s0, int S) {
   if (m.kz) v.kz = m.kz + s * q * np;
   if (m.kth) v.kth = m.kth + s * m.n_theta;
   if (m.kA) v.kA = m.kA + s * q * q;
+  if (m.bacc) v.bacc = m.bacc + s * q * np;
+  if (m.zc) v.zc = m.zc + s * q * np;
   return v;
 }
 
@@ -150,6 +152,7 @@ MatSet matset_view(const MatSet& m, int s0) {
   if (m.Q) v.Q = m.Q + sq * e;
   if (m.QB) v.QB = m.QB + sq * wt;
   v.cur = m.cur + sq;
+  if (m.Y) v.Y = m.Y + sq * e;
   return v;
 }
 
@@ -186,6 +189,17 @@ struct mk_session {
   int* sw_xcc = nullptr;
   int* sw_err = nullptr;
   double* d_probs = nullptr;
+  // Lookahead schedule (exponential model, one group; run_iteration_la): iteration t+1's phi
+  // candidates are factored on la_c while iteration t's inverse and sweep run on the main stream,
+  // and their z' = L'^-1 u is solved on la_x trailing the factorisation panel by panel.
+  int la_mode = -1;               // mk_session_set_lookahead: -1 auto, 0 off, 1 on
+  bool la_ok = false;             // eligible (buffers allocated)
+  bool la = false;                // in use
+  int la_next = -1;               // iteration whose candidates are queued on la_c (-1: none)
+  int la_enq = 0;                 // panels of those candidates enqueued so far
+  hipStream_t la_c = nullptr;     // created at the first lookahead run (an unused stream still takes a
+                                  // hardware queue, GPU_MAX_HW_QUEUES = 4, and slows the split Cholesky)
+  std::vector<hipEvent_t> la_ev;  // [nt] panel k final | decided (or adapted) | spare
   std::vector<int> n_part;
   std::vector<void*> allocs;
   bool prof = false;
@@ -227,6 +241,8 @@ struct mk_session {
       for (hipEvent_t e : g.ev) hipEventDestroy(e);
     }
     if (swept) hipEventDestroy(swept);
+    for (hipEvent_t e : la_ev) hipEventDestroy(e);
+    if (la_c) hipStreamDestroy(la_c);
     for (void* p_ : allocs) hipFree(p_);
     if (stream) hipStreamDestroy(stream);
   }
@@ -410,31 +426,44 @@ static double panel_flops(mk_session* s, Group& g, int hc, int k, int ia, int ib
 // accumulator passes through fp64 memory between the two updates): same bits.  (An earlier
 // lookahead that moved the full-depth update of the next diagonal tile onto a second stream was
 // slower: that update's long K chain sat on the critical path)
+//
+// crit: the critical stream (default g.stream; the lookahead schedule factors on its own stream).
+// evP (optional, nt events): evP[k] is recorded on it once panel k is final (after T(k); the last
+// after D(nt-1)), for the border solve that trails the factorisation.
+// [k_lo, k_hi): the panels to enqueue (the lookahead schedule enqueues a factorisation in two
+// pieces around the main stream's work, so the host does not hold back either stream).
 static void launch_cholesky(mk_session* s, Group& g, int h0, int hc, const int* slist = nullptr,
-                            const int* scount = nullptr) {
+                            const int* scount = nullptr, hipStream_t crit = nullptr, hipEvent_t* evP = nullptr,
+                            int k_lo = 0, int k_hi = -1) {
   const int nt = s->nt;
+  if (k_hi < 0) k_hi = nt;
+  hipStream_t A = crit ? crit : g.stream;
   if (slist || !g.bulk) {
-    for (int k = 0; k < nt; ++k) {
+    for (int k = k_lo; k < k_hi; ++k) {
       if (k > 0)
-        chol_update(s, g, g.stream, h0, hc, k, k, nt, 0, k, slist, scount, panel_flops(s, g, hc, k, k, nt, false));
-      chol_diag(s, g, g.stream, h0, hc, k, slist, scount);
+        chol_update(s, g, A, h0, hc, k, k, nt, 0, k, slist, scount, panel_flops(s, g, hc, k, k, nt, false));
+      chol_diag(s, g, A, h0, hc, k, slist, scount);
       if (k < nt - 1)
-        chol_trsm(s, g, g.stream, h0, hc, k, k + 1, nt, slist, scount, panel_flops(s, g, hc, k, k + 1, nt, true));
+        chol_trsm(s, g, A, h0, hc, k, k + 1, nt, slist, scount, panel_flops(s, g, hc, k, k + 1, nt, true));
+      if (evP) hipEventRecord(evP[k], A);
     }
     return;
   }
-  hipStream_t A = g.stream, B = g.bulk;
+  hipStream_t B = g.bulk;
   hipEvent_t* eT = g.ev.data();                  // eT[k]: T(k) done (critical), k = 0 .. nt-3
   hipEvent_t* eU = g.ev.data() + nt;             // eU[c]: bulk U(c; 0..c-2) done, c = 2 .. nt-1
-  hipEventRecord(g.ev[2 * nt], A);               // the candidates are on A
-  hipStreamWaitEvent(B, g.ev[2 * nt], 0);
-  for (int k = 0; k < nt; ++k) {
+  if (k_lo == 0) {
+    hipEventRecord(g.ev[2 * nt], A);             // the candidates are on A
+    hipStreamWaitEvent(B, g.ev[2 * nt], 0);
+  }
+  for (int k = k_lo; k < k_hi; ++k) {
     if (k >= 2) hipStreamWaitEvent(A, eU[k], 0);
     if (k >= 1)
       chol_update(s, g, A, h0, hc, k, k, nt, k - 1, k, nullptr, nullptr, panel_flops(s, g, hc, k, k, nt, false, k - 1, k));
     chol_diag(s, g, A, h0, hc, k, nullptr, nullptr);
     if (k < nt - 1)
       chol_trsm(s, g, A, h0, hc, k, k + 1, nt, nullptr, nullptr, panel_flops(s, g, hc, k, k + 1, nt, true));
+    if (evP) hipEventRecord(evP[k], A);
     if (k + 2 < nt) {
       const int c = k + 2;
       hipEventRecord(eT[k], A);
@@ -471,7 +500,7 @@ static void launch_trinv(mk_session* s, Group& g, int max_entries, const int* li
 }
 
 // W = L^-1 for the changed factors, diagonal tiles of R^-1, z from the bordered row.
-static void launch_inverse(mk_session* s, Group& g) {
+static void launch_inverse(mk_session* s, Group& g, bool from_zc = false) {
   const int nt = s->nt, max_entries = g.S * s->q;
   launch_trinv(s, g, max_entries, g.d_list, g.d_count);
   timed(s, g.stream, KS_LAUUM, 0.0, [&] {
@@ -479,7 +508,7 @@ static void launch_inverse(mk_session* s, Group& g) {
                        g.d_list, g.d_count);
   });
   hipLaunchKernelGGL(k_take_border, dim3(max_entries * ((s->n_pad + 255) / 256)), dim3(256), 0, g.stream, g.md, g.ms,
-                     g.d_list, g.d_count);
+                     g.d_list, g.d_count, from_zc ? (const double*)g.md.zc : nullptr);
 }
 
 // Algorithmic flops of k_pred_var over every pair of the group: 2 n_s^2 / 2 per test site (W
@@ -522,8 +551,18 @@ static void launch_sweep(mk_session* s, Group& g, int it) {
     int* xcc = s->sw_xcc;
     int* err = s->sw_err;
     void* args[] = {&md, &ms, &iter, &part, &cnt, &xcc, &err};
-    hipLaunchCooperativeKernel(sweep_kernel(q, true), dim3(xcd_grid(g.S, s->nt)), dim3(256), args,
-                               (unsigned)s->sweep_mg_lds, g.stream);
+    // A cooperative launch is not dispatched beside other queues' work; under the lookahead
+    // schedule the candidates' factorisation runs concurrently, so the grid goes out as a plain
+    // launch: the kernel's waits only need every workgroup resident eventually -- the other
+    // stream's kernels never wait on the sweep and drain -- and each wait has a time-out
+    // (MK_SWEEP_COOP=1 keeps the cooperative launch)
+    static const int coop_env = tile_env("MK_SWEEP_COOP", 0);
+    if (s->la && !coop_env)
+      hipLaunchKernel(sweep_kernel(q, true), dim3(xcd_grid(g.S, s->nt)), dim3(256), args, (unsigned)s->sweep_mg_lds,
+                      g.stream);
+    else
+      hipLaunchCooperativeKernel(sweep_kernel(q, true), dim3(xcd_grid(g.S, s->nt)), dim3(256), args,
+                                 (unsigned)s->sweep_mg_lds, g.stream);
     return;
   }
   const size_t sw_lds = (size_t)q * (64 * 64 + 2 * 64) * sizeof(double);
@@ -573,11 +612,86 @@ static void iteration_post_sweep(mk_session* s, Group& g, int it) {
   if ((it + 1) % md.batch_length == 0) hipLaunchKernelGGL(k_adapt, dim3(S), dim3(256), 0, st, md, it / md.batch_length);
 }
 
+// Lookahead schedule (exponential model, one group).  The phi proposal of iteration t+1 is known
+// once iteration t's phi step has decided (and, at a batch end, adapted), so its candidates
+// R(phi'_{t+1}) are assembled and factored on la_c while the main stream runs iteration t's
+// inverse, kriging and sweep -- at small shards both chains are latency-bound and overlap.  The
+// candidates carry no bordered row (u_{t+1} = A_{t+1}^-1 w_t does not exist yet): after the A step
+// the main stream solves z' = L'^-1 u one tile column per launch, each behind the factorisation's
+// panel (k_border_step), and |z'|^2 completes the phi ratio (k_border_quad).  The chain is the
+// sequential schedule's (same draws, same decisions); z' differs from the bordered factor's row
+// by rounding only (tests compare both schedules and the oracle).
+// Panels [0, k_hi) of iteration it's candidates (the assembly with the first piece); the rest by
+// enqueue_candidates_rest.  MK_LA_HEAD sets the first piece (default 3 panels: the GPU needs
+// ~0.2 ms per panel at small shards, the host ~10 us per launch for the main stream's ~30).
+static int la_head(mk_session* s) {
+  static const int head = tile_env("MK_LA_HEAD", 3);
+  return std::max(1, std::min(head, s->nt));
+}
+static void enqueue_candidates(mk_session* s, Group& g, int it, hipEvent_t after, int k_hi) {
+  const int S = g.S, q = s->q, nt = s->nt;
+  hipStreamWaitEvent(s->la_c, after, 0);
+  hipLaunchKernelGGL(cov_candidate_kernel(g.md.cov_model), dim3(xcd_grid_h(S * q, nt * (nt + 1) / 2)), dim3(256), 0,
+                     s->la_c, g.md, g.ms, 0, q, 0 | MK_CAND_NOBORDER, it, nullptr, nullptr);
+  launch_cholesky(s, g, 0, q, nullptr, nullptr, s->la_c, s->la_ev.data(), 0, k_hi);
+  s->la_next = it;
+  s->la_enq = k_hi;
+}
+static void enqueue_candidates_rest(mk_session* s, Group& g) {
+  if (s->la_enq < s->nt) launch_cholesky(s, g, 0, s->q, nullptr, nullptr, s->la_c, s->la_ev.data(), s->la_enq, s->nt);
+  s->la_enq = s->nt;
+}
+
+static void run_iteration_la(mk_session* s, int it) {
+  Group& g = s->groups[0];
+  Model& md = g.md;
+  const int S = g.S, q = s->q, nt = s->nt;
+  hipStream_t M = g.stream;
+  hipEvent_t* evP = s->la_ev.data();
+  hipEvent_t ev_d = evP[nt];
+  if (s->la_next != it) {   // first iteration of the session (or after a tiled replay reused the slots)
+    hipEventRecord(ev_d, M);
+    enqueue_candidates(s, g, it, ev_d, nt);
+  }
+  enqueue_candidates_rest(s, g);
+  hipLaunchKernelGGL(k_beta, dim3(S), dim3(256), 0, M, md, it);
+  if (q > 1) hipLaunchKernelGGL(k_trmv_Z, dim3(S * q * ((s->n_pad + 255) / 256)), dim3(256), 0, M, md, g.ms);
+  hipLaunchKernelGGL(k_Aphase, dim3(S), dim3(256), 0, M, md, it);
+  for (int k = 0; k < nt; ++k) {   // z' = L'^-1 u, trailing the candidates' panels
+    hipStreamWaitEvent(M, evP[k], 0);
+    hipLaunchKernelGGL(k_border_step, dim3(xcd_grid_h(S * q, std::max(1, nt - 1 - k))), dim3(256), 0, M, md, g.ms, k);
+  }
+  hipLaunchKernelGGL(k_border_quad, dim3(S * q), dim3(256), 0, M, md);
+  hipLaunchKernelGGL(k_theta_mh, dim3((S * q + 63) / 64), dim3(64), 0, M, md, g.ms, 0, q, 0, it);
+  const bool more = it + 1 < md.n_samples, batch_end = (it + 1) % md.batch_length == 0;
+  if (more && !batch_end) {   // the head now; the rest after the main stream's launches
+    hipEventRecord(ev_d, M);
+    enqueue_candidates(s, g, it + 1, ev_d, la_head(s));
+  }
+  hipLaunchKernelGGL(k_dirty_list, dim3(1), dim3(256), 0, M, md, (int)(it == md.kept0), g.d_list, g.d_count, g.d_plist,
+                     g.d_pcount);
+  launch_inverse(s, g, true);
+  const bool kept = it >= md.kept0;
+  if (kept && !s->tiled) launch_pred_refresh(s, g);
+  timed(s, M, KS_SWEEP, 0.0, [&] { launch_sweep(s, g, it); });
+  iteration_post_sweep(s, g, it);
+  if (more && batch_end) {   // the next proposal's scale is the adapted one
+    hipEventRecord(ev_d, M);
+    enqueue_candidates(s, g, it + 1, ev_d, nt);
+  }
+  enqueue_candidates_rest(s, g);
+  if (!more) s->la_next = -1;
+}
+
 // One iteration of the shard.  Each group (stream) runs its own chain of launches; with the
 // multi-workgroup sweep and several groups, the groups join for one whole-shard sweep on the
 // session stream and fork again (the groups' Cholesky chains overlap each other's latency-bound
 // diagonal steps; the sweep is one cooperative launch).  Same kernels, same operands, same bits.
 static void run_iteration(mk_session* s, int it) {
+  if (s->la) {
+    run_iteration_la(s, it);
+    return;
+  }
   if (s->sweep_mg && s->groups.size() > 1) {
     for (auto& g : s->groups) {
       hipStreamWaitEvent(g.stream, s->swept, 0);
@@ -860,6 +974,19 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
       (rc = s->alloc(&ms.QB, (size_t)S * q * nt * MK_NB * MK_NB)) || (rc = s->alloc(&ms.cur, (size_t)S * q)) ||
       (rc = s->alloc(&s->d_probs, MK_N_LEVELS)))
     return rc;
+  // lookahead schedule buffers (run_iteration_la): exponential model on one stream group
+  {
+    const int G = std::max(1, std::min(c->n_streams > 0 ? (int)c->n_streams : 1, S));
+    s->la_ok = !s->matern && G == 1;
+    if (s->la_ok) {
+      if ((rc = s->alloc(&md.bacc, (size_t)S * q * n_pad)) || (rc = s->alloc(&md.zc, (size_t)S * q * n_pad)) ||
+          (rc = s->alloc(&ms.Y, (size_t)S * q * n_pad * n_pad)))
+        return rc;
+      s->la_ev.assign(nt + 2, nullptr);
+      for (auto& e : s->la_ev)
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return set_err(MK_E_HIP, "lookahead event");
+    }
+  }
   if ((rc = setup_groups(s, c->n_streams > 0 ? c->n_streams : 1))) return rc;
 
   // ---------------- host staging (R layout -> padded device layout)
@@ -1003,6 +1130,9 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
   HIPCHK(hipStreamSynchronize(s->stream));
   drain_timers(s);
   for (auto& st : s->stats) st = Stat();
+  // default schedule: lookahead where eligible; MK_LOOKAHEAD=0 / 1 overrides (mk_session_set_lookahead too)
+  static const int la_env = tile_env("MK_LOOKAHEAD", -1);
+  s->la = s->la_ok && la_env != 0;
   *out = hold.release();
   return 0;
 }
@@ -1011,6 +1141,19 @@ extern "C" int mk_session_run(mk_session* s, int32_t n_iter) {
   if (!s) return set_err(MK_E_ARG, "null session");
   HIPCHK(hipSetDevice(s->device));
   if (n_iter < 0 || s->iter + n_iter > s->md.n_samples) return set_err(MK_E_ARG, "n_iter beyond n.samples");
+  if (s->la && !s->la_c) {
+    // the candidates' factorisation is the critical chain: its stream gets the device's highest
+    // priority, so its small diagonal / trsm grids are dispatched ahead of the main stream's
+    // inverse and sweep workgroups as CUs free up (MK_LA_PRIO=0: default priority)
+    static const int prio_env = tile_env("MK_LA_PRIO", 1);
+    int lo = 0, hi = 0;
+    if (prio_env && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess) {
+      if (hipStreamCreateWithPriority(&s->la_c, hipStreamNonBlocking, hi) != hipSuccess)
+        return set_err(MK_E_HIP, "lookahead stream");
+    } else if (hipStreamCreateWithFlags(&s->la_c, hipStreamNonBlocking) != hipSuccess) {
+      return set_err(MK_E_HIP, "lookahead stream");
+    }
+  }
   const auto t0 = std::chrono::steady_clock::now();
   for (int i = 0; i < n_iter; ++i) {
     run_iteration(s, s->iter);
@@ -1018,6 +1161,7 @@ extern "C" int mk_session_run(mk_session* s, int32_t n_iter) {
     HIPCHK(hipGetLastError());
   }
   for (auto& g : s->groups) HIPCHK(hipStreamSynchronize(g.stream));
+  if (s->la_c) HIPCHK(hipStreamSynchronize(s->la_c));   // the next iteration's candidates
   if (s->sweep_mg) {
     int e = 0;
     HIPCHK(hipMemcpy(&e, s->sw_err, sizeof(int), hipMemcpyDeviceToHost));
@@ -1033,6 +1177,19 @@ extern "C" int mk_session_run(mk_session* s, int32_t n_iter) {
 }
 
 extern "C" int32_t mk_session_iteration(const mk_session* s) { return s ? s->iter : -1; }
+
+extern "C" int mk_session_set_lookahead(mk_session* s, int32_t mode) {
+  if (!s) return set_err(MK_E_ARG, "null session");
+  if (mode < -1 || mode > 1) return set_err(MK_E_ARG, "lookahead mode must be -1 (auto), 0 or 1");
+  if (s->iter > 0) return set_err(MK_E_ARG, "the schedule is fixed once the chain has started");
+  if (mode == 1 && !s->la_ok)
+    return set_err(MK_E_ARG, "lookahead needs the exponential model on one stream group");
+  s->la_mode = mode;
+  s->la = s->la_ok && mode != 0;
+  return 0;
+}
+
+extern "C" int32_t mk_session_lookahead(const mk_session* s) { return (s && s->la) ? 1 : 0; }
 
 extern "C" int mk_session_profile(mk_session* s, int32_t enable) {
   if (!s) return set_err(MK_E_ARG, "null session");
@@ -1086,6 +1243,7 @@ static int predict_tiled(mk_session* s, mk_outputs* o) {
   hipStream_t st = s->stream;
   Group g = s->all;
   const int ntri_tiles = nt * (nt + 1) / 2;
+  s->la_next = -1;   // the replay factors into the free slots: a lookahead candidate is gone
   DevBufs scratch;
   double* dq = scratch.get<double>((size_t)S * q * T * MK_N_LEVELS);
   double* dsum = scratch.get<double>((size_t)q * T * MK_N_LEVELS);

@@ -25,7 +25,9 @@ template <int TM>
 __global__ void k_inv_level(MatSet ms, const int* list, const int* count, int sz, int phase);
 __global__ void k_lauum(MatSet ms, const int* n_s, const int* list, const int* count);
 __global__ void k_qblocks(MatSet ms, const int* n_s, const int* list, const int* count);
-__global__ void k_take_border(Model md, MatSet ms, const int* list, const int* count);
+__global__ void k_take_border(Model md, MatSet ms, const int* list, const int* count, const double* zc);
+__global__ void k_border_step(Model md, MatSet ms, int k);
+__global__ void k_border_quad(Model md);
 __global__ void k_trmv_Z(Model md, MatSet ms);
 template <int MODEL>
 __global__ void k_pred_PT(Model md, const int* list, const int* count);

@@ -27,6 +27,8 @@ namespace mk {
 // Candidate correlation matrix of outcome h for every subset, lower tiles only:
 //   R[i][j] = rho(|s_i - s_j|; phi', nu')  (i, j < n_s);  R[n_s][j] = u_h[j];  R[n_s][n_s] = 0;
 //   padding rows/cols: identity.  phi'/nu' = the Philox proposal of MH parameter j_mh.
+//   which | MK_CAND_NOBORDER: R[n_s][j] = 0 (the lookahead schedule factors the candidate before
+//   u is known and solves for z' afterwards, k_border_step).
 __device__ inline void candidate_theta(const Model& md, int s, int h, int which, int iter, double* phi, double* nu) {
   const Key key = subset_key(md, s);
   const double* th = md.theta + (long)s * md.n_theta;
@@ -52,7 +54,7 @@ struct CandGen {
   CorrFn rho;
   __device__ inline double operator()(int R, int C) const {
     if (R < ns && C < ns) return (R == C) ? 1.0 : rho(dist2d(cx[R], cy[R], cx[C], cy[C]));
-    if (R == ns && C < ns) return uh[C];
+    if (R == ns && C < ns) return uh ? uh[C] : 0.0;
     return (R == C && R != ns) ? 1.0 : 0.0;
   }
 };
@@ -103,7 +105,7 @@ __device__ inline double cand_value(const CandGen& g, int R, int C) {
     const double d = dist2d(g.cx[R], g.cy[R], g.cx[C], g.cy[C]);
     return (MODEL == MK_COV_EXPONENTIAL) ? exp(-g.rho.phi * d) : g.rho(d);
   }
-  if (R == g.ns && C < g.ns) return g.uh[C];
+  if (R == g.ns && C < g.ns) return g.uh ? g.uh[C] : 0.0;
   return (R == C && R != g.ns) ? 1.0 : 0.0;
 }
 
@@ -209,7 +211,8 @@ __global__ __launch_bounds__(256) void k_cov_candidate(Model md, MatSet ms, int 
   while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
   const int tj = t - ti * (ti + 1) / 2;
   const int sh = s * md.q + h;
-  CandGen g = make_gen(md, s, h, which, iter);
+  CandGen g = make_gen(md, s, h, which & 3, iter);
+  if (which & MK_CAND_NOBORDER) g.uh = nullptr;   // lookahead: u is not known yet (k_border_step)
   double* M = mat_slot(ms, sh, 1 - ms.cur[sh]);
   const long ld = ms.ld;
   if (MODEL == MK_COV_MATERN) {
@@ -650,7 +653,7 @@ __global__ __launch_bounds__(256, 2) void k_inv_level(MatSet ms, const int* __re
   const int cur = ms.cur[sh];
   const long ld = ms.ld;
   double* Wm = wmat(ms, sh);
-  double* Y = mat_slot(ms, sh, 1 - cur);
+  double* Y = ms.Y ? ms.Y + (long)sh * mat_elems(ms) : mat_slot(ms, sh, 1 - cur);
   const int ro = sr * TM;             // sub-tile row / column offsets in the 128-tile
   const long co = (long)sc * TM * ld;
   AccT<TM / 32, TM / 32> acc;
@@ -732,9 +735,10 @@ __global__ __launch_bounds__(256, 2) void k_qblocks(MatSet ms, const int* __rest
   store_tile(ms.QB + ((long)sh * ms.nt + i) * MK_NB * MK_NB + 64 * sd + 64 * sd * MK_NB, MK_NB, acc);
 }
 
-// z_h = border row of the accepted factor = L^-1 u_h (exact for the u_h the candidate was built with).
+// z_h = border row of the accepted factor = L^-1 u_h (exact for the u_h the candidate was built with),
+// or (lookahead schedule, zc set) the candidate's solved z'_h.
 __global__ __launch_bounds__(256) void k_take_border(Model md, MatSet ms, const int* __restrict__ list,
-                                                     const int* __restrict__ count) {
+                                                     const int* __restrict__ count, const double* __restrict__ zc) {
   const int per = (md.n_pad + 255) / 256;
   const int e = blockIdx.x / per;
   if (e >= *count) return;
@@ -743,8 +747,108 @@ __global__ __launch_bounds__(256) void k_take_border(Model md, MatSet ms, const 
   const int ns = md.n_s[s];
   const int j = (blockIdx.x % per) * 256 + threadIdx.x;
   if (j >= md.n_pad) return;
+  const long zo = ((long)s * md.q + h) * md.n_pad + j;
+  if (zc) {
+    md.z[zo] = (j < ns) ? zc[zo] : 0.0;
+    return;
+  }
   const double* M = mat_slot(ms, sh, ms.cur[sh]);
-  md.z[((long)s * md.q + h) * md.n_pad + j] = (j < ns) ? M[ns + (long)j * ms.ld] : 0.0;
+  md.z[zo] = (j < ns) ? M[ns + (long)j * ms.ld] : 0.0;
+}
+
+// ---------------------------------------------------------------- lookahead border solve
+// The lookahead schedule (mk_api.hip) factors iteration t+1's phi candidates while iteration t's
+// inverse and sweep run, before u_{t+1} = A_{t+1}^-1 w_t exists, so the candidate has no bordered
+// row and z'_h = L'_h^-1 u_h comes from a forward solve after the A step, one launch per tile
+// column k, each behind the factorisation's panel k (right-looking: every (pair, row tile) reads
+// its tile of L' once):
+//   z'_k = Winv_k (u_k - acc_k)   (every workgroup of the pair, redundantly; Winv_k from L2)
+//   acc_i += L'_ik z'_k           (workgroup t: row tile i = k+1+t; k = nt-1: z' only)
+// Lane l holds rows 2l, 2l+1; wave v columns v, v+4, ...; the four waves' partials are added in
+// wave order, acc's column sums in k order: deterministic.
+__device__ inline d2 gemv_tile(const double* A, long lda, const double* x, double* red) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  d2 acc = {0.0, 0.0};
+  const double* Ar = A + 2 * lane;
+#pragma unroll 2
+  for (int j0 = 0; j0 < 32; j0 += 8) {
+    d2 v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = *reinterpret_cast<const d2*>(Ar + (long)(wv + 4 * (j0 + j)) * lda);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const double xc = x[wv + 4 * (j0 + j)];
+      acc.x = fma(v[j].x, xc, acc.x);
+      acc.y = fma(v[j].y, xc, acc.y);
+    }
+  }
+  red[wv * MK_NB + 2 * lane] = acc.x;
+  red[wv * MK_NB + 2 * lane + 1] = acc.y;
+  __syncthreads();
+  d2 out;
+  out.x = ((red[2 * lane] + red[MK_NB + 2 * lane]) + red[2 * MK_NB + 2 * lane]) + red[3 * MK_NB + 2 * lane];
+  out.y = ((red[2 * lane + 1] + red[MK_NB + 2 * lane + 1]) + red[2 * MK_NB + 2 * lane + 1]) + red[3 * MK_NB + 2 * lane + 1];
+  return out;   // meaningful in every wave (each reads the same sums)
+}
+
+__global__ __launch_bounds__(256) void k_border_step(Model md, MatSet ms, int k) {
+  __shared__ double xs[MK_NB];
+  __shared__ double red[4 * MK_NB];
+  const int nt = ms.nt, T = max(1, nt - 1 - k);
+  int e, t;
+  if (!xcd_map(md.S * md.q, T, &e, &t)) return;
+  const int s = e / md.q;
+  const int ns = md.n_s[s];
+  const int i = k + 1 + t;
+  if (k * MK_NB >= ns) return;                          // z'_k = 0 (rows beyond the subset; never read)
+  const bool acc_work = k < nt - 1 && i * MK_NB < ns;   // tile i holds sites: accumulate into it
+  if (t > 0 && !acc_work) return;                       // (workgroup 0 always writes z'_k)
+  const int slot = 1 - ms.cur[e];
+  const long np = md.n_pad;
+  const double* u = md.u + (long)e * np;                // [S][q][n_pad]: pair e = s*q + h
+  double* zc = md.zc + (long)e * np;
+  double* bacc = md.bacc + (long)e * np;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (tid < MK_NB) {
+    const int row = k * MK_NB + tid;
+    xs[tid] = (row < ns) ? u[row] - (k > 0 ? bacc[row] : 0.0) : 0.0;
+  }
+  __syncthreads();
+  d2 y = gemv_tile(winv_slot(ms, e, slot, k), MK_NB, xs, red);
+  const int row = k * MK_NB + 2 * lane;
+  y.x = (row < ns) ? y.x : 0.0;
+  y.y = (row + 1 < ns) ? y.y : 0.0;
+  __syncthreads();                                      // every wave has read red and xs
+  if (wv == 0) {
+    xs[2 * lane] = y.x;
+    xs[2 * lane + 1] = y.y;
+    if (t == 0) *reinterpret_cast<d2*>(zc + row) = y;
+  }
+  __syncthreads();
+  if (!acc_work) return;
+  const d2 p = gemv_tile(mat_slot(ms, e, slot) + i * MK_NB + (long)k * MK_NB * ms.ld, ms.ld, xs, red);
+  if (wv == 0) {
+    d2* ap = reinterpret_cast<d2*>(bacc + i * MK_NB + 2 * lane);
+    d2 v = p;
+    if (k > 0) {
+      const d2 o = *ap;
+      v.x = o.x + v.x;
+      v.y = o.y + v.y;
+    }
+    *ap = v;
+  }
+}
+
+// quad_c = |z'_h|^2 (rows < n_s) for every pair: the candidate's u' R'^-1 u.
+__global__ __launch_bounds__(256) void k_border_quad(Model md) {
+  __shared__ double red[8];
+  const int e = blockIdx.x, s = e / md.q;
+  const int ns = md.n_s[s];
+  const double* zc = md.zc + (long)e * md.n_pad;
+  double loc = 0.0;
+  for (int r = threadIdx.x; r < ns; r += 256) loc += zc[r] * zc[r];
+  const double tot = block_sum<256>(loc, red);
+  if (threadIdx.x == 0) md.quad_c[e] = tot;
 }
 
 // Z_{h,c} = W_h u_c for every subset, outcome h and c (q > 1, start of the A phase).

@@ -12,6 +12,8 @@
 //   QB      [S*q][nt][128^2]         diagonal 128-tiles of R_h^-1 = W'W (rows < n_s)
 //   u, z    [S][q][n_pad]            u = (I (x) A^-1) w, z_h = W_h u_h  (so u_h'R_h^-1 u_h = |z_h|^2)
 //   Z       [S][q][q][n_pad]         Z_{h,c} = W_h u_c (q > 1 only)
+//   bacc,zc [S][q][n_pad]            lookahead: border-solve partial sums, z'_h = L'_h^-1 u_h
+//   Y       [S*q][n_pad^2]           lookahead: inverse-level scratch (else the free factor slot)
 //   PT, XK  [S*q][n_pad][n_test_pad] kriging: P^T = rho(obs, test) and X = W P^T
 // All matrices of one (subset, outcome) pair are contiguous; every kernel finds
 // its pair from blockIdx and the cur[] slot table, so no host round trip is
@@ -80,6 +82,9 @@ struct Model {
   double* kz;          // z_h = W_h u_h   (q*n_pad)
   double* kth;         // theta           (n_theta)
   double* kA;          // A               (q*q)
+  // lookahead schedule (mk_api.hip): border solve of the candidate factored ahead of its iteration
+  double* bacc;        // [S][q][n_pad]     right-looking partial sums of the border solve
+  double* zc;          // [S][q][n_pad]     z'_h = L'_h^-1 u_h of the candidate
   int P;               // reported columns
 };
 
@@ -90,6 +95,7 @@ struct MatSet {
   double* Q;   // [S*q][ld*ld] full inverse (parity-test entry point only)
   double* QB;  // [S*q][nt][128*128] diagonal tiles of the inverse
   int* cur;    // [S*q]
+  double* Y;   // [S*q][ld*ld] inverse-level scratch (lookahead schedule; else the free factor slot)
   int ld, nt, q;
 };
 

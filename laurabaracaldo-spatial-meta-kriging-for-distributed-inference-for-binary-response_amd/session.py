@@ -128,7 +128,7 @@ class Session:
     subsets: list of dicts with 'coords' (n_s,2), 'y' (n_s*q,), 'weights' (n_s*q,), 'x' (n_s*q, p).
     """
 
-    def __init__(self, subsets, cfg, coords_test=None, subset_base=0, device=0, record_w=False):
+    def __init__(self, subsets, cfg, coords_test=None, subset_base=0, device=0, record_w=False, lookahead=None):
         lib = _lib.load()
         self.cfg = cfg
         self.q, self.p = cfg.q, cfg.p
@@ -155,6 +155,8 @@ class Session:
         check(lib.mk_session_create(ctypes.byref(pr), ctypes.byref(c), ctypes.byref(h)))
         self._h = h
         self._lib = lib
+        if lookahead is not None:
+            self.set_lookahead(lookahead)
 
     def run(self, n_iter):
         check(self._lib.mk_session_run(self._h, int(n_iter)))
@@ -171,6 +173,16 @@ class Session:
         """Replay only iterations first..last (1-based; spPredict's start / end) in the next outputs()."""
         check(self._lib.mk_session_set_kept_window(self._h, int(first), int(last)))
         self._window = int(last) - int(first) + 1
+
+    def set_lookahead(self, mode):
+        """Launch schedule before the first run: True / 1 lookahead (the next iteration's phi
+        candidates factored while this iteration's inverse and sweep run), False / 0 sequential,
+        -1 the library default.  The chain is the same either way (to rounding)."""
+        check(self._lib.mk_session_set_lookahead(self._h, int(mode)))
+
+    @property
+    def lookahead(self):
+        return bool(self._lib.mk_session_lookahead(self._h))
 
     @property
     def iteration(self):

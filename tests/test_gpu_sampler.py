@@ -13,7 +13,7 @@ TOL = 1e-8
 
 
 def _run_both(mk, n, q, cov, n_test=12, n_batch=3, batch_length=4, burn_in=7, seed=9, subset_base=0, S=2,
-              sizes=None, link="logit"):
+              sizes=None, link="logit", lookahead=None, chunks=None):
     sizes = list(sizes) if sizes is not None else [n] * S
     off = np.concatenate([[0], np.cumsum(sizes)])
     d = mk.synthetic.generate(int(off[-1]), q=q, n_test=n_test, seed=seed + q, cov_model=cov, link=link)
@@ -29,8 +29,11 @@ def _run_both(mk, n, q, cov, n_test=12, n_batch=3, batch_length=4, burn_in=7, se
         sl = slice(off[s], off[s] + m)
         rows = slice(off[s] * q, (off[s] + m) * q)
         subs.append(dict(coords=d["coords"][sl], y=d["y"][rows], weights=np.ones(m * q), x=d["x"][rows]))
-    with mk.Session(subs, cfg, coords_test=ct, subset_base=subset_base, record_w=True) as ses:
-        ses.run(cfg.n_samples)
+    with mk.Session(subs, cfg, coords_test=ct, subset_base=subset_base, record_w=True, lookahead=lookahead) as ses:
+        if lookahead is not None:
+            assert ses.lookahead == bool(lookahead)
+        for c in (chunks or [cfg.n_samples]):
+            ses.run(c)
         dev = ses.outputs(samples=True, w_samples=True, w_pred_samples=True, acceptance=True)
     refs = [om.fit_subset(sb["coords"], sb["y"], sb["weights"], sb["x"], ocfg, subset=subset_base + s,
                           coords_test=ct, record_w=True) for s, sb in enumerate(subs)]
@@ -129,6 +132,58 @@ def test_replay_subset_beyond_2048_sites(mk):
     threads) and the diagonal-tile kernel runs past 16 pivots; replayed against the oracle."""
     dev, refs = _run_both(mk, 2200, 1, 0, n_test=16, n_batch=2, batch_length=2, burn_in=3, S=1)
     _check(dev, refs)
+
+
+@pytest.mark.parametrize("n,q,sizes", [(150, 1, None), (None, 1, [700, 333]), (64, 2, None), (None, 3, [300, 129]),
+                                       (None, 1, [1, 2, 3])])
+def test_replay_sequential_schedule(mk, n, q, sizes):
+    """The sequential launch schedule (bordered candidates: z' is the factor's row n_s) replays the
+    oracle too; the default for the exponential model is the lookahead schedule."""
+    dev, refs = _run_both(mk, n, q, 0, sizes=sizes, lookahead=0)
+    _check(dev, refs)
+
+
+@pytest.mark.parametrize("n,q,sizes", [(150, 1, None), (None, 1, [1300, 700, 129]), (None, 2, [400, 257]),
+                                       (None, 3, [300, 2, 129])])
+def test_lookahead_schedule_replays_oracle(mk, n, q, sizes):
+    """Lookahead schedule: iteration t+1's phi candidates are factored without a
+    bordered row while iteration t's inverse and sweep run, and z' = L'^-1 u comes from the
+    trailing border solve (k_border_step / k_border_combine).  Replayed against the oracle across
+    batch ends (adapted proposal scales) and across mk_session_run calls that stop mid-batch (the
+    candidate queued by one call is used by the next)."""
+    dev, refs = _run_both(mk, n, q, 0, sizes=sizes, lookahead=1, chunks=[1, 4, 2, 5])
+    _check(dev, refs)
+
+
+def test_lookahead_equals_sequential_schedule(mk):
+    """Both schedules run the same chain: every decision agrees and the states differ by rounding
+    only (z' from a forward solve instead of the bordered factor row)."""
+    a, _ = _run_both(mk, None, 1, 0, sizes=[900, 650], n_batch=4, batch_length=3, burn_in=9, lookahead=1)
+    b, _ = _run_both(mk, None, 1, 0, sizes=[900, 650], n_batch=4, batch_length=3, burn_in=9, lookahead=0)
+    for s in range(2):
+        np.testing.assert_allclose(a["samples"][s], b["samples"][s], rtol=0, atol=1e-10)
+        np.testing.assert_allclose(a["w_samples"][s], b["w_samples"][s], rtol=0, atol=1e-10)
+        np.testing.assert_allclose(a["w_pred_samples"][s], b["w_pred_samples"][s], rtol=0, atol=1e-10)
+        assert np.array_equal(a["acceptance"][s], b["acceptance"][s])
+
+
+def test_lookahead_is_rejected_where_ineligible(mk):
+    """The Matern model (nu's candidate depends on the same iteration's phi decision) keeps the
+    sequential schedule; asking for lookahead is an argument error, as is changing the schedule
+    after the chain has started."""
+    d = mk.synthetic.generate(60, q=1, n_test=3, seed=3, cov_model=1)
+    sub = [dict(coords=d["coords"], y=d["y"], weights=np.ones(60), x=d["x"])]
+    cfg = mk.SamplerConfig(1, 2, [0, 0], [0.05, 0.05], cov_model="matern", n_batch=1, batch_length=3, burn_in=2)
+    with mk.Session(sub, cfg) as ses:
+        assert not ses.lookahead
+        with pytest.raises(mk.MkError):
+            ses.set_lookahead(1)
+    cfg = mk.SamplerConfig(1, 2, [0, 0], [0.05, 0.05], n_batch=1, batch_length=3, burn_in=2)
+    with mk.Session(sub, cfg) as ses:
+        assert ses.lookahead
+        ses.run(1)
+        with pytest.raises(mk.MkError):
+            ses.set_lookahead(0)
 
 
 def test_quantiles_bit_exact_on_device_samples(mk):
