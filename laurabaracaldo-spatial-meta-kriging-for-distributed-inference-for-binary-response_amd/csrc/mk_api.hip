@@ -181,7 +181,8 @@ struct mk_session {
   int* d_scount = nullptr;
   std::vector<Group> groups;      // the run-time split, one stream each
   // multi-workgroup sweep (k_sweep_mg, small shards): partial dots, per-block counters, error flag
-  bool sweep_mg = false;
+  bool sweep_mg = false;          // buffers allocated and chosen for the sequential schedule
+  bool sweep_mg_forced = false;   // MK_SWEEP=2: also under the lookahead schedule
   size_t sweep_mg_lds = 0;
   hipEvent_t swept = nullptr;     // fork-join sweep (several groups): the whole-shard sweep is queued
   double* sw_part = nullptr;
@@ -197,6 +198,7 @@ struct mk_session {
   bool la = false;                // in use
   int la_next = -1;               // iteration whose candidates are queued on la_c (-1: none)
   int la_enq = 0;                 // panels of those candidates enqueued so far
+  hipStream_t la_m = nullptr;     // MK_LA_MASK: CU-masked main stream of the lookahead iterations
   hipStream_t la_c = nullptr;     // created at the first lookahead run (an unused stream still takes a
                                   // hardware queue, GPU_MAX_HW_QUEUES = 4, and slows the split Cholesky)
   std::vector<hipEvent_t> la_ev;  // [nt] panel k final | decided (or adapted) | spare
@@ -243,6 +245,7 @@ struct mk_session {
     if (swept) hipEventDestroy(swept);
     for (hipEvent_t e : la_ev) hipEventDestroy(e);
     if (la_c) hipStreamDestroy(la_c);
+    if (la_m) hipStreamDestroy(la_m);
     for (void* p_ : allocs) hipFree(p_);
     if (stream) hipStreamDestroy(stream);
   }
@@ -327,8 +330,9 @@ static bool set_gemm_lds() {
 }
 
 // Tile shape of a GEMM launch: 64-sub-tiles (bit-identical, mk_gemm.hpp) when the 128-tile grid
-// would leave the chip short of work -- fewer than MK_TILE_THRESH workgroups (default 512, two per
-// CU).  MK_TILE=128 / 64 / 32 forces one shape (tests compare them; 32-sub-tiles were measured no
+// would leave the chip short of work -- fewer than MK_TILE_THRESH workgroups (default 256, one per
+// CU; 512 before the lookahead schedule, whose concurrent chain fills the rest: 32 subsets
+// 6,360 -> 6,546 subset-iters/s, 250 subsets unchanged).  MK_TILE=128 / 64 / 32 forces one shape (tests compare them; 32-sub-tiles were measured no
 // faster than 64 on the last, single-tile panels of small shards, so the policy does not pick them).
 static int tile_env(const char* name, int dflt) {
   const char* v = std::getenv(name);
@@ -336,7 +340,7 @@ static int tile_env(const char* name, int dflt) {
 }
 static int tile_size(long wg128) {
   static const int force = tile_env("MK_TILE", 0);
-  static const int thresh = tile_env("MK_TILE_THRESH", 512);
+  static const int thresh = tile_env("MK_TILE_THRESH", 256);
   if (force == 32 || force == 64 || force == 128) return force;
   return wg128 >= thresh ? 128 : 64;
 }
@@ -449,26 +453,33 @@ static void launch_cholesky(mk_session* s, Group& g, int h0, int hc, const int* 
     }
     return;
   }
+  // depth d (MK_CHOL_DEPTH, default 2): the bulk update of column c covers panels [0, c-d) and is
+  // launched after T(c-d-1), so it has d critical steps to finish; the critical correction is
+  // then rank-128d, U(k; k-d..k-1).  Same per-element MFMA sequence for any d (same bits).
+  static const int depth_env = tile_env("MK_CHOL_DEPTH", 2);
+  const int d = std::max(1, std::min(depth_env, 4));
   hipStream_t B = g.bulk;
-  hipEvent_t* eT = g.ev.data();                  // eT[k]: T(k) done (critical), k = 0 .. nt-3
-  hipEvent_t* eU = g.ev.data() + nt;             // eU[c]: bulk U(c; 0..c-2) done, c = 2 .. nt-1
+  hipEvent_t* eT = g.ev.data();                  // eT[k]: T(k) done (critical)
+  hipEvent_t* eU = g.ev.data() + nt;             // eU[c]: bulk U(c; 0..c-d-1) done, c = d+1 .. nt-1
   if (k_lo == 0) {
     hipEventRecord(g.ev[2 * nt], A);             // the candidates are on A
     hipStreamWaitEvent(B, g.ev[2 * nt], 0);
   }
   for (int k = k_lo; k < k_hi; ++k) {
-    if (k >= 2) hipStreamWaitEvent(A, eU[k], 0);
-    if (k >= 1)
-      chol_update(s, g, A, h0, hc, k, k, nt, k - 1, k, nullptr, nullptr, panel_flops(s, g, hc, k, k, nt, false, k - 1, k));
+    if (k > d) hipStreamWaitEvent(A, eU[k], 0);
+    if (k >= 1) {
+      const int j0 = std::max(0, k - d);
+      chol_update(s, g, A, h0, hc, k, k, nt, j0, k, nullptr, nullptr, panel_flops(s, g, hc, k, k, nt, false, j0, k));
+    }
     chol_diag(s, g, A, h0, hc, k, nullptr, nullptr);
     if (k < nt - 1)
       chol_trsm(s, g, A, h0, hc, k, k + 1, nt, nullptr, nullptr, panel_flops(s, g, hc, k, k + 1, nt, true));
     if (evP) hipEventRecord(evP[k], A);
-    if (k + 2 < nt) {
-      const int c = k + 2;
+    if (k + d + 1 < nt) {
+      const int c = k + d + 1;
       hipEventRecord(eT[k], A);
       hipStreamWaitEvent(B, eT[k], 0);
-      chol_update(s, g, B, h0, hc, c, c, nt, 0, c - 1, nullptr, nullptr, panel_flops(s, g, hc, c, c, nt, false, 0, c - 1));
+      chol_update(s, g, B, h0, hc, c, c, nt, 0, c - d, nullptr, nullptr, panel_flops(s, g, hc, c, c, nt, false, 0, c - d));
       hipEventRecord(eU[c], B);
     }
   }
@@ -539,9 +550,21 @@ static void launch_pred_refresh(mk_session* s, Group& g) {
 // The latent-w sweep: the cooperative multi-workgroup kernel when the session chose it (small
 // shard; g is then the whole-shard view), else one workgroup per subset; both give the same bits
 // (mk_mcmc.hip).
+// Default schedule: lookahead for shards of up to 192 (subset, outcome) pairs, where both chains are
+// latency-bound (measured: 32 subsets +20 %, 63 +21 %, 125 +8 %); at 250 subsets both saturate
+// the chip and the sequential schedule is as fast (8,529 vs 8,680, within run-to-run spread)
+// while its panel-update launches run alone (roofline timing 0.71 of peak vs 0.59 beside the
+// main stream's kernels).
+static bool la_auto(const mk_session* s) { return (long)s->S * s->q <= 192; }
+
+// Under the lookahead schedule the one-workgroup kernel is the default: the cooperative kernel's
+// gain (one W pass, 0.6 vs 1.2 ms at 32 subsets alone) is lost beside the concurrent factorisation
+// (measured 6,399 vs 6,546 subset-iters/s at 32 subsets), and it keeps no inter-workgroup waits.
+static bool use_sweep_mg(const mk_session* s) { return s->sweep_mg && (!s->la || s->sweep_mg_forced); }
+
 static void launch_sweep(mk_session* s, Group& g, int it) {
   const int q = s->q;
-  if (s->sweep_mg) {
+  if (use_sweep_mg(s)) {
     hipMemsetAsync(s->sw_cnt, 0, (size_t)g.S * (s->n_pad / 64) * sizeof(int), g.stream);
     Model md = g.md;
     MatSet ms = g.ms;
@@ -692,7 +715,7 @@ static void run_iteration(mk_session* s, int it) {
     run_iteration_la(s, it);
     return;
   }
-  if (s->sweep_mg && s->groups.size() > 1) {
+  if (use_sweep_mg(s) && s->groups.size() > 1) {
     for (auto& g : s->groups) {
       hipStreamWaitEvent(g.stream, s->swept, 0);
       iteration_pre_sweep(s, g, it);
@@ -1108,6 +1131,7 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
     const int mode = tile_env("MK_SWEEP", 0);
     const bool fits = coop && grid <= (long)per_cu * n_cu && nt <= 32;
     s->sweep_mg = fits && (mode == 2 || (mode == 0 && (long)S * 4 <= n_cu));
+    s->sweep_mg_forced = fits && mode == 2;
     if (s->sweep_mg) {
       if ((rc = s->alloc(&s->sw_part, (size_t)S * 2 * nt * q * 64)) || (rc = s->alloc(&s->sw_cnt, (size_t)S * (n_pad / 64))) ||
           (rc = s->alloc(&s->sw_xcc, (size_t)S * nt)) || (rc = s->alloc(&s->sw_err, 1)))
@@ -1132,7 +1156,7 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
   for (auto& st : s->stats) st = Stat();
   // default schedule: lookahead where eligible; MK_LOOKAHEAD=0 / 1 overrides (mk_session_set_lookahead too)
   static const int la_env = tile_env("MK_LOOKAHEAD", -1);
-  s->la = s->la_ok && la_env != 0;
+  s->la = s->la_ok && (la_env == 1 || (la_env < 0 && la_auto(s)));
   *out = hold.release();
   return 0;
 }
@@ -1153,13 +1177,32 @@ extern "C" int mk_session_run(mk_session* s, int32_t n_iter) {
     } else if (hipStreamCreateWithFlags(&s->la_c, hipStreamNonBlocking) != hipSuccess) {
       return set_err(MK_E_HIP, "lookahead stream");
     }
+    // MK_LA_MASK=R (experimental): the main stream's work runs on a stream that leaves the first R
+    // CUs (R/8 per XCD) to the candidates' factorisation
+    static const int mask_env = tile_env("MK_LA_MASK", 0);
+    int n_cu = 0;
+    if (mask_env > 0 && hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, s->device) == hipSuccess) {
+      std::vector<uint32_t> mask((n_cu + 31) / 32, 0xffffffffu);
+      for (int b = 0; b < mask_env && b < n_cu; ++b) mask[b / 32] &= ~(1u << (b % 32));
+      if (hipExtStreamCreateWithCUMask(&s->la_m, (uint32_t)n_cu, mask.data()) != hipSuccess)
+        return set_err(MK_E_HIP, "lookahead main stream");
+    }
+  }
+  const bool swap_m = s->la && s->la_m;
+  if (swap_m) {   // the iterations' main-stream work on la_m, after everything queued on the session stream
+    hipEventRecord(s->la_ev[s->nt + 1], s->stream);
+    hipStreamWaitEvent(s->la_m, s->la_ev[s->nt + 1], 0);
+    s->groups[0].stream = s->la_m;
   }
   const auto t0 = std::chrono::steady_clock::now();
   for (int i = 0; i < n_iter; ++i) {
     run_iteration(s, s->iter);
     s->iter++;
-    HIPCHK(hipGetLastError());
+    if (hipGetLastError() != hipSuccess) break;
   }
+  if (swap_m) s->groups[0].stream = s->stream;
+  HIPCHK(hipGetLastError());
+  if (swap_m) HIPCHK(hipStreamSynchronize(s->la_m));
   for (auto& g : s->groups) HIPCHK(hipStreamSynchronize(g.stream));
   if (s->la_c) HIPCHK(hipStreamSynchronize(s->la_c));   // the next iteration's candidates
   if (s->sweep_mg) {
@@ -1178,6 +1221,7 @@ extern "C" int mk_session_run(mk_session* s, int32_t n_iter) {
 
 extern "C" int32_t mk_session_iteration(const mk_session* s) { return s ? s->iter : -1; }
 
+
 extern "C" int mk_session_set_lookahead(mk_session* s, int32_t mode) {
   if (!s) return set_err(MK_E_ARG, "null session");
   if (mode < -1 || mode > 1) return set_err(MK_E_ARG, "lookahead mode must be -1 (auto), 0 or 1");
@@ -1185,7 +1229,7 @@ extern "C" int mk_session_set_lookahead(mk_session* s, int32_t mode) {
   if (mode == 1 && !s->la_ok)
     return set_err(MK_E_ARG, "lookahead needs the exponential model on one stream group");
   s->la_mode = mode;
-  s->la = s->la_ok && mode != 0;
+  s->la = s->la_ok && (mode == 1 || (mode == -1 && la_auto(s)));
   return 0;
 }
 

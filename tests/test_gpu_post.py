@@ -116,13 +116,17 @@ def test_glm_binomial_trials(mk):
 
 
 def test_stream_grouping_does_not_change_the_chains(mk):
+    """Subset groups on several HIP streams give the one-stream chains bit for bit (sequential
+    schedule: the lookahead schedule needs one group; its own equivalence is tested in
+    test_gpu_sampler.py)."""
     d = mk.synthetic.generate(5 * 90, q=1, n_test=6, seed=21)
     subs = [dict(coords=d["coords"][i * 90:(i + 1) * 90], y=d["y"][i * 90:(i + 1) * 90], weights=np.ones(90),
                  x=d["x"][i * 90:(i + 1) * 90]) for i in range(5)]
     outs = []
     for ns in (1, 2, 3, 5):
         cfg = mk.SamplerConfig(1, 2, [0, 0], [0.05, 0.05], n_batch=2, batch_length=5, burn_in=6, seed=4, n_streams=ns)
-        with mk.Session(subs, cfg, coords_test=d["coords_test"]) as ses:
+        with mk.Session(subs, cfg, coords_test=d["coords_test"], lookahead=0 if ns == 1 else None) as ses:
+            assert not ses.lookahead
             ses.run(cfg.n_samples)
             outs.append(ses.outputs(samples=True, w_pred_samples=True))
     for o in outs[1:]:
