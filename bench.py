@@ -21,9 +21,14 @@ roofline.traffic is the PMC-measured HBM traffic of the same kernel from profile
   python bench.py --gpus N --steps K --warmup W
 """
 import argparse
+import os
+
+# before HIP starts: libmk's lookahead schedule runs up to five HIP streams and HIP shares
+# hardware queues beyond GPU_MAX_HW_QUEUES (4 by default; DESIGN.md 4.2)
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 import importlib
 import json
-import os
 import sys
 import time
 

@@ -14,9 +14,14 @@ inverse (2 n_s^3 / 3) and the draws (2 n_s per draw) are counted too.
   python bench_kriging.py [--subsets 32] [--n-test 1000000] [--kept 6] [--tile 65536]
 """
 import argparse
+import os
+
+# before HIP starts: libmk's lookahead schedule runs up to five HIP streams and HIP shares
+# hardware queues beyond GPU_MAX_HW_QUEUES (4 by default; DESIGN.md 4.2)
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 import importlib
 import json
-import os
 import sys
 import time
 

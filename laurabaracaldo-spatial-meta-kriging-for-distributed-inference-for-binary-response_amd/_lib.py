@@ -116,6 +116,11 @@ def load():
     if _LIB is not None:
         return _LIB
     path = os.environ.get("MK_LIB") or LIB_PATH      # MK_LIB: a development build (tools/ probes)
+    # the lookahead schedule runs up to five HIP streams: give the process at least 8 hardware
+    # queues (read when HIP starts; a process that started HIP earlier keeps its count, and libmk
+    # then runs three streams)
+    if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
+        os.environ["GPU_MAX_HW_QUEUES"] = "8"
     if not os.path.exists(path):
         raise MkError(MK_E_ARG, f"{path} not built; run __graft_entry__.build()")
     lib = ctypes.CDLL(path)

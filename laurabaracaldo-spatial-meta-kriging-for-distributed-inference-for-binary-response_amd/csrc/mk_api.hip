@@ -201,7 +201,8 @@ struct mk_session {
   hipStream_t la_m = nullptr;     // MK_LA_MASK: CU-masked main stream of the lookahead iterations
   hipStream_t la_c = nullptr;     // created at the first lookahead run (an unused stream still takes a
                                   // hardware queue, GPU_MAX_HW_QUEUES = 4, and slows the split Cholesky)
-  std::vector<hipEvent_t> la_ev;  // [nt] panel k final | decided (or adapted) | spare
+  hipStream_t la_k = nullptr;     // kept iterations' kriging refresh beside the sweep (MK_LA_KRIG)
+  std::vector<hipEvent_t> la_ev;  // [nt] panel k final | decided (or adapted) | join | W ready | kriged
   std::vector<int> n_part;
   std::vector<void*> allocs;
   bool prof = false;
@@ -246,6 +247,7 @@ struct mk_session {
     for (hipEvent_t e : la_ev) hipEventDestroy(e);
     if (la_c) hipStreamDestroy(la_c);
     if (la_m) hipStreamDestroy(la_m);
+    if (la_k) hipStreamDestroy(la_k);
     for (void* p_ : allocs) hipFree(p_);
     if (stream) hipStreamDestroy(stream);
   }
@@ -465,6 +467,43 @@ static void launch_cholesky(mk_session* s, Group& g, int h0, int hc, const int* 
     hipEventRecord(g.ev[2 * nt], A);             // the candidates are on A
     hipStreamWaitEvent(B, g.ev[2 * nt], 0);
   }
+  static const int fine_env = tile_env("MK_CHOL_FINE", 0);
+  if (fine_env) {
+    // Fine split: the critical stream keeps only the diagonal tile's correction, the diagonal
+    // factor and the trsm; the off-diagonal tiles' correction of column k+1 runs on the bulk stream
+    // right after T(k), beside D(k+1).
+    //   A: [eU(k)] U(k; tile k; panels k-d..k-1), D(k), [eO(k)] T(k), evP(k)
+    //   B: [evP(k)] U(k+1; tiles > k+1; panels k+1-d..k) -> eO(k+1); U(k+d+1; panels < k+1) -> eU
+    hipEvent_t* eO = g.ev.data() + 2 * nt + 1;     // eO[c]: off-diagonal correction of column c done
+    for (int k = k_lo; k < k_hi; ++k) {
+      if (k > d) hipStreamWaitEvent(A, eU[k], 0);
+      const int j0 = std::max(0, k - d);
+      if (k >= 1)
+        chol_update(s, g, A, h0, hc, k, k, k + 1, j0, k, nullptr, nullptr, panel_flops(s, g, hc, k, k, k + 1, false, j0, k));
+      chol_diag(s, g, A, h0, hc, k, nullptr, nullptr);
+      if (k < nt - 1) {
+        if (k >= 1) hipStreamWaitEvent(A, eO[k], 0);
+        chol_trsm(s, g, A, h0, hc, k, k + 1, nt, nullptr, nullptr, panel_flops(s, g, hc, k, k + 1, nt, true));
+      }
+      hipEventRecord(eT[k], A);
+      if (evP) hipEventRecord(evP[k], A);
+      if (k + 1 < nt) {
+        hipStreamWaitEvent(B, eT[k], 0);
+        const int c = k + 1, jc = std::max(0, c - d);
+        if (c + 1 < nt) {
+          chol_update(s, g, B, h0, hc, c, c + 1, nt, jc, c, nullptr, nullptr, panel_flops(s, g, hc, c, c + 1, nt, false, jc, c));
+          hipEventRecord(eO[c], B);
+        }
+        if (k + d + 1 < nt) {
+          const int cb = k + d + 1;
+          chol_update(s, g, B, h0, hc, cb, cb, nt, 0, cb - d, nullptr, nullptr,
+                      panel_flops(s, g, hc, cb, cb, nt, false, 0, cb - d));
+          hipEventRecord(eU[cb], B);
+        }
+      }
+    }
+    return;
+  }
   for (int k = k_lo; k < k_hi; ++k) {
     if (k > d) hipStreamWaitEvent(A, eU[k], 0);
     if (k >= 1) {
@@ -532,18 +571,19 @@ static double pred_flops(mk_session* s, Group& g) {
 
 // Kriging refresh (kept iterations): X = W P^T and s = |X_t|^2 for the pairs in the pred list
 // (P^T generated in the GEMM for the exponential model, else stored first by k_pred_PT).
-static void launch_pred_refresh(mk_session* s, Group& g) {
+static void launch_pred_refresh(mk_session* s, Group& g, hipStream_t st = nullptr) {
   Model& md = g.md;
   if (md.n_test <= 0) return;
+  if (!st) st = g.stream;
   const int nt = s->nt, max_entries = g.S * s->q;
   if (!s->pred_gen)
-    hipLaunchKernelGGL(pred_PT_kernel(md.cov_model), dim3(max_entries * md.n_pad), dim3(256), 0, g.stream, md, g.d_plist,
+    hipLaunchKernelGGL(pred_PT_kernel(md.cov_model), dim3(max_entries * md.n_pad), dim3(256), 0, st, md, g.d_plist,
                        g.d_pcount);
-  timed(s, g.stream, KS_PRED_VAR, pred_flops(s, g), [&] {
+  timed(s, st, KS_PRED_VAR, pred_flops(s, g), [&] {
     hipLaunchKernelGGL(s->pred_gen ? k_pred_var<true> : k_pred_var<false>, dim3(xcd_grid_h(max_entries, nt * md.ntt)),
-                       dim3(256), LDS_128, g.stream, md, g.ms, g.d_plist, g.d_pcount);
+                       dim3(256), LDS_128, st, md, g.ms, g.d_plist, g.d_pcount);
   });
-  hipLaunchKernelGGL(k_pred_var_reduce, dim3(max_entries * (md.n_test_pad / 256)), dim3(256), 0, g.stream, md, nt,
+  hipLaunchKernelGGL(k_pred_var_reduce, dim3(max_entries * (md.n_test_pad / 256)), dim3(256), 0, st, md, nt,
                      g.d_plist, g.d_pcount);
 }
 
@@ -695,8 +735,19 @@ static void run_iteration_la(mk_session* s, int it) {
                      g.d_pcount);
   launch_inverse(s, g, true);
   const bool kept = it >= md.kept0;
-  if (kept && !s->tiled) launch_pred_refresh(s, g);
+  // kept iterations: the kriging refresh (X = W P^T of the changed pairs) only reads W, as the sweep
+  // does, and the draws after the sweep are its only consumer -- it runs on la_k beside the sweep
+  const bool side = kept && !s->tiled && md.n_test > 0 && s->la_k;
+  if (side) {
+    hipEventRecord(evP[nt + 2], M);
+    hipStreamWaitEvent(s->la_k, evP[nt + 2], 0);
+    launch_pred_refresh(s, g, s->la_k);
+    hipEventRecord(evP[nt + 3], s->la_k);
+  } else if (kept && !s->tiled) {
+    launch_pred_refresh(s, g);
+  }
   timed(s, M, KS_SWEEP, 0.0, [&] { launch_sweep(s, g, it); });
+  if (side) hipStreamWaitEvent(M, evP[nt + 3], 0);
   iteration_post_sweep(s, g, it);
   if (more && batch_end) {   // the next proposal's scale is the adapted one
     hipEventRecord(ev_d, M);
@@ -823,7 +874,7 @@ static int setup_groups(mk_session* s, int n_groups) {
     Group& g = s->groups[0];
     if (hipExtStreamCreateWithCUMask(&g.bulk, (uint32_t)n_cu, mask.data()) != hipSuccess)
       return set_err(MK_E_HIP, "bulk stream");
-    g.ev.assign(2 * s->nt + 1, nullptr);
+    g.ev.assign(3 * s->nt + 1, nullptr);
     for (auto& e : g.ev)
       if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return set_err(MK_E_HIP, "cholesky event");
   }
@@ -1005,7 +1056,7 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
       if ((rc = s->alloc(&md.bacc, (size_t)S * q * n_pad)) || (rc = s->alloc(&md.zc, (size_t)S * q * n_pad)) ||
           (rc = s->alloc(&ms.Y, (size_t)S * q * n_pad * n_pad)))
         return rc;
-      s->la_ev.assign(nt + 2, nullptr);
+      s->la_ev.assign(nt + 4, nullptr);
       for (auto& e : s->la_ev)
         if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return set_err(MK_E_HIP, "lookahead event");
     }
@@ -1177,13 +1228,27 @@ extern "C" int mk_session_run(mk_session* s, int32_t n_iter) {
     } else if (hipStreamCreateWithFlags(&s->la_c, hipStreamNonBlocking) != hipSuccess) {
       return set_err(MK_E_HIP, "lookahead stream");
     }
-    // MK_LA_MASK=R (experimental): the main stream's work runs on a stream that leaves the first R
-    // CUs (R/8 per XCD) to the candidates' factorisation
-    static const int mask_env = tile_env("MK_LA_MASK", 0);
+    // Two more streams when the process has the hardware queues for them (HIP maps streams onto
+    // GPU_MAX_HW_QUEUES queues, default 4, shared round-robin beyond that -- a shared queue
+    // serialises the split Cholesky's streams: measured 5,427 -> 4,087 subset-iters/s at 32
+    // subsets; the package and bench.py set 8 before HIP starts):
+    //  * la_k: the kept iterations' kriging refresh beside the sweep (MK_LA_KRIG=0: off);
+    //  * la_m: the iterations' main-stream work on a stream that leaves the first MK_LA_MASK CUs
+    //    (default 32: 4 per XCD, the split Cholesky's reserve) to the candidates' critical chain --
+    //    its diagonal-tile workgroups take a whole CU's LDS and otherwise wait behind the inverse
+    //    and kriging GEMMs (32 / 63 / 125 subsets: 6,669 -> 6,921, 7,550 -> 7,645, 8,062 -> 8,211).
+    const char* hwq = std::getenv("GPU_MAX_HW_QUEUES");
+    const bool queues = hwq && std::atoi(hwq) >= 8;
+    static const int krig_env = tile_env("MK_LA_KRIG", -1);
+    if ((krig_env == 1 || (krig_env < 0 && queues)) && s->md.n_test > 0 && !s->tiled &&
+        hipStreamCreateWithFlags(&s->la_k, hipStreamNonBlocking) != hipSuccess)
+      return set_err(MK_E_HIP, "lookahead kriging stream");
+    static const int mask_env = tile_env("MK_LA_MASK", -1);
+    const int mask_cu = mask_env >= 0 ? mask_env : (queues ? 32 : 0);
     int n_cu = 0;
-    if (mask_env > 0 && hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, s->device) == hipSuccess) {
+    if (mask_cu > 0 && hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, s->device) == hipSuccess) {
       std::vector<uint32_t> mask((n_cu + 31) / 32, 0xffffffffu);
-      for (int b = 0; b < mask_env && b < n_cu; ++b) mask[b / 32] &= ~(1u << (b % 32));
+      for (int b = 0; b < mask_cu && b < n_cu; ++b) mask[b / 32] &= ~(1u << (b % 32));
       if (hipExtStreamCreateWithCUMask(&s->la_m, (uint32_t)n_cu, mask.data()) != hipSuccess)
         return set_err(MK_E_HIP, "lookahead main stream");
     }
@@ -1205,6 +1270,7 @@ extern "C" int mk_session_run(mk_session* s, int32_t n_iter) {
   if (swap_m) HIPCHK(hipStreamSynchronize(s->la_m));
   for (auto& g : s->groups) HIPCHK(hipStreamSynchronize(g.stream));
   if (s->la_c) HIPCHK(hipStreamSynchronize(s->la_c));   // the next iteration's candidates
+  if (s->la_k) HIPCHK(hipStreamSynchronize(s->la_k));
   if (s->sweep_mg) {
     int e = 0;
     HIPCHK(hipMemcpy(&e, s->sw_err, sizeof(int), hipMemcpyDeviceToHost));

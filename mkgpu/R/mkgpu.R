@@ -88,3 +88,10 @@ mk_posterior_summary <- function(result, result2, x.test, samplesize = 1000, n.o
   names(res) <- c("SamplePar", "Samplew", "p.sample", "w.quant", "param.quant")
   res
 }
+
+# libmk's lookahead schedule runs up to five HIP streams; HIP reads its hardware-queue count
+# (default 4, streams beyond it share queues) when it starts, which is after this hook.
+.onLoad <- function(libname, pkgname) {
+  q <- suppressWarnings(as.integer(Sys.getenv("GPU_MAX_HW_QUEUES", "0")))
+  if (is.na(q) || q < 8L) Sys.setenv(GPU_MAX_HW_QUEUES = "8")
+}

@@ -16,9 +16,14 @@ Prints one JSON line with the wall-clock of every phase (rank 0).  Multi-GPU:
   python run_metakriging.py --config 3          # configs[2]: n=500k, K=250, exponential, q=1
 """
 import argparse
+import os
+
+# before HIP starts: libmk's lookahead schedule runs up to five HIP streams and HIP shares
+# hardware queues beyond GPU_MAX_HW_QUEUES (4 by default; DESIGN.md 4.2)
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 import importlib
 import json
-import os
 import sys
 import time
 

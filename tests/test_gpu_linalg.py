@@ -88,23 +88,28 @@ def test_sub_tile_gemm_split_cholesky_and_multi_wg_sweep_are_bit_identical(tmp_p
     the cooperative multi-workgroup latent sweep (k_sweep_mg; same summation order as k_sweep),
     and the kriging GEMM with P^T generated in LDS (MK_PRED_GEN=1, exponential model) against
     the default stored-P^T path (k_pred_PT writes the same exp(-phi d) values to HBM first).
-    Chains, latent w, kriging draws and a plain factorisation, each configuration forced in its
-    own process (MK_TILE, MK_SWEEP, MK_CHOL_SPLIT, MK_PRED_GEN are read once per process)."""
+    Also the split schedule's depth (MK_CHOL_DEPTH: the bulk update d critical steps ahead, the
+    critical correction rank-128d) and its fine form (MK_CHOL_FINE: the diagonal tile's correction
+    alone on the critical stream).  Chains, latent w, kriging draws and a plain factorisation, each
+    configuration forced in its own process (the MK_* switches are read once per process)."""
     import os
     import subprocess
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     res = {}
-    for tile, sweep, split, gen in (("128", "1", "0", "0"), ("64", "2", "1", "0"), ("64", "1", "0", "0"),
-                                    ("32", "1", "1", "0"), ("128", "2", "1", "0"), ("128", "1", "0", "1")):
-        path = str(tmp_path / f"tile{tile}_sweep{sweep}_split{split}_gen{gen}.npz")
+    for tile, sweep, split, gen, fine, depth in (("128", "1", "0", "0", "0", "2"), ("64", "2", "1", "0", "0", "1"),
+                                                 ("64", "1", "0", "0", "0", "2"), ("32", "1", "1", "0", "1", "2"),
+                                                 ("128", "2", "1", "0", "0", "3"), ("128", "1", "0", "1", "0", "2"),
+                                                 ("64", "1", "1", "0", "1", "1")):
+        path = str(tmp_path / f"tile{tile}_sweep{sweep}_split{split}_gen{gen}_fine{fine}_d{depth}.npz")
         r = subprocess.run([sys.executable, os.path.join(here, "gpu_tile_run.py"), path], capture_output=True,
                            text=True, timeout=240,
-                           env=dict(os.environ, MK_TILE=tile, MK_SWEEP=sweep, MK_CHOL_SPLIT=split, MK_PRED_GEN=gen))
+                           env=dict(os.environ, MK_TILE=tile, MK_SWEEP=sweep, MK_CHOL_SPLIT=split, MK_PRED_GEN=gen,
+                                    MK_CHOL_FINE=fine, MK_CHOL_DEPTH=depth))
         assert r.returncode == 0, r.stderr[-4000:]
         z = np.load(path)
-        res[(tile, sweep, split, gen)] = {k: z[k] for k in z.files}
-    ref = res[("128", "1", "0", "0")]
+        res[(tile, sweep, split, gen, fine, depth)] = {k: z[k] for k in z.files}
+    ref = res[("128", "1", "0", "0", "0", "2")]
     for key, got in res.items():
         assert got.keys() == ref.keys()
         for k in ref:
