@@ -590,12 +590,12 @@ static void launch_pred_refresh(mk_session* s, Group& g, hipStream_t st = nullpt
 // The latent-w sweep: the cooperative multi-workgroup kernel when the session chose it (small
 // shard; g is then the whole-shard view), else one workgroup per subset; both give the same bits
 // (mk_mcmc.hip).
-// Default schedule: lookahead for shards of up to 192 (subset, outcome) pairs, where both chains are
-// latency-bound (measured: 32 subsets +20 %, 63 +21 %, 125 +8 %); at 250 subsets both saturate
-// the chip and the sequential schedule is as fast (8,529 vs 8,680, within run-to-run spread)
-// while its panel-update launches run alone (roofline timing 0.71 of peak vs 0.59 beside the
-// main stream's kernels).
-static bool la_auto(const mk_session* s) { return (long)s->S * s->q <= 192; }
+// Default schedule: lookahead for shards of up to 224 (subset, outcome) pairs, where the chains
+// leave the chip room to overlap (measured vs sequential: 32 subsets 5,427 -> 6,972, 63 6,174 ->
+// 7,719, 125 7,486 -> 8,303, 188 8,071 -> 8,486 subset-iters/s); at 250 subsets both saturate the
+// chip and the sequential schedule is as fast (8,572 vs 8,553-8,565) while its panel-update
+// launches run alone (roofline timing 0.71 of peak vs 0.52-0.57 beside the main stream's kernels).
+static bool la_auto(const mk_session* s) { return (long)s->S * s->q <= 224; }
 
 // Under the lookahead schedule the one-workgroup kernel is the default: the cooperative kernel's
 // gain (one W pass, 0.6 vs 1.2 ms at 32 subsets alone) is lost beside the concurrent factorisation

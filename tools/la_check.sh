@@ -2,8 +2,9 @@
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/la
 mkdir -p $O
-echo "box GPU_MAX_HW_QUEUES=$GPU_MAX_HW_QUEUES" > $O/env.log
 B="python bench.py --no-cpu-baseline"
-for K in 32 63 125 250; do
-  timeout -k 10 200 $B --n $((K * 2000)) --subsets $K > $O/b$K.log 2>&1 || exit 1
-done
+MK_LOOKAHEAD=1 timeout -k 10 200 $B > $O/b250_la1.log 2>&1 || exit 1
+MK_LOOKAHEAD=1 MK_LA_MASK=0 timeout -k 10 200 $B > $O/b250_la1_m0.log 2>&1 || exit 1
+MK_LOOKAHEAD=1 MK_LA_MASK=16 timeout -k 10 200 $B > $O/b250_la1_m16.log 2>&1 || exit 1
+MK_LOOKAHEAD=1 timeout -k 10 200 $B --n 376000 --subsets 188 > $O/b188_la1.log 2>&1 || exit 1
+MK_LOOKAHEAD=0 timeout -k 10 200 $B --n 376000 --subsets 188 > $O/b188_la0.log 2>&1 || exit 1
