@@ -1003,6 +1003,8 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
   md.seed = c->seed;
   md.accept_rate = c->accept_rate;
   md.P = P;
+  // kriging GEMM raster (k_pred_var): row panels per group; placement only, same bits for any value
+  md.pred_gi = std::max(1, std::min(tile_env("MK_PRED_GI", 1), 64));
   for (int h = 0; h < q; ++h) {
     md.phi_a[h] = c->phi_unif_a[h]; md.phi_b[h] = c->phi_unif_b[h];
     md.nu_a[h] = s->matern ? c->nu_unif_a[h] : 0.0;

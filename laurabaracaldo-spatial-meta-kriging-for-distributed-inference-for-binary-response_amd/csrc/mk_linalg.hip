@@ -618,9 +618,21 @@ __global__ __launch_bounds__(256) void k_inv_copydiag(MatSet ms, const int* __re
   const double* Wd = winv_slot(ms, sh, ms.cur[sh], k);
   const long ld = ms.ld;
   double* Wt = wmat(ms, sh) + k * MK_NB + (long)k * MK_NB * ld;
-  for (int t = threadIdx.x; t < MK_NB * MK_NB; t += 256) {
-    const int r = t & 127, c = t >> 7;
-    Wt[r + (long)c * ld] = Wd[r + c * MK_NB];
+  // 16-byte row pairs, 16 loads in flight per thread (one dependent round trip per element made
+  // this copy 100-150 us per launch, on the main stream's critical path at small shards)
+#pragma unroll 1
+  for (int e0 = 0; e0 < MK_NB * MK_NB; e0 += 256 * 2 * 16) {
+    d2 v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int e = e0 + 2 * (threadIdx.x + 256 * j);
+      v[j] = *reinterpret_cast<const d2*>(Wd + e);
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int e = e0 + 2 * (threadIdx.x + 256 * j);
+      *reinterpret_cast<d2*>(Wt + (e & 127) + (long)(e >> 7) * ld) = v[j];
+    }
   }
 }
 
@@ -962,9 +974,20 @@ __global__ __launch_bounds__(256, 2) void k_pred_var(Model md, MatSet ms, const 
   const int per = ms.nt * md.ntt;
   int e, t_;
   if (!xcd_map(*count, per, &e, &t_)) return;
-  // i-major: consecutive workgroups share the W row panel (L2) and stream distinct P^T blocks
-  // (tb-major -- sharing the P^T block, re-reading W -- measured 0.65 vs 0.74 of peak)
-  const int i = t_ / md.ntt, tb = t_ % md.ntt;
+  // Grouped raster: groups of G = pred_gi row panels; inside a group the G row panels of one test
+  // block are consecutive, then the next test block.  The ~64 workgroups an XCD holds at once then
+  // cover G row panels x 64/G test blocks: each W row panel is shared by 64/G of them and each P^T
+  // block by G (through L2), where plain row-panel-major order (G = 1) shares W 64 ways and fetches
+  // every P^T block once per row panel (measured 8.7 x the P^T bytes).  (tb-major -- G = nt --
+  // re-reads W: 0.65 vs 0.74 of peak.)  Placement only: every tile's arithmetic is the same.
+  int i, tb;
+  {
+    const int G = md.pred_gi, gsz = G * md.ntt;
+    const int g0 = (t_ / gsz) * G, r = t_ % gsz;
+    const int ge = min(G, ms.nt - g0);      // short last group
+    tb = r / ge;
+    i = g0 + r % ge;
+  }
   const int sh = list[e];
   const int s = sh / md.q;
   const int ns = md.n_s[s];

@@ -86,6 +86,7 @@ struct Model {
   double* bacc;        // [S][q][n_pad]     right-looking partial sums of the border solve
   double* zc;          // [S][q][n_pad]     z'_h = L'_h^-1 u_h of the candidate
   int P;               // reported columns
+  int pred_gi;         // kriging GEMM raster: row panels per group (k_pred_var; 1 = row-panel-major)
 };
 
 struct MatSet {

@@ -1,5 +1,5 @@
 """Helper run as a subprocess by tests/test_gpu_linalg.py (not a test module): a short chain
-under the code paths the environment forces (MK_TILE, MK_SWEEP, MK_CHOL_SPLIT, MK_PRED_GEN; read once per process), outputs
+under the code paths the environment forces (MK_TILE, MK_SWEEP, MK_CHOL_SPLIT, MK_PRED_GEN, MK_PRED_GI; read once per process), outputs
 saved to the .npz named on the command line."""
 import importlib
 import os
@@ -16,7 +16,7 @@ def main(path):
     mk = importlib.import_module(PKG)
     out = {}
     for q, sizes, cov in ((1, [700, 640, 333], 0), (2, [300, 257], 0), (1, [500, 260], 1)):
-        d = mk.synthetic.generate(sum(sizes), q=q, n_test=20, seed=71 + q + cov, cov_model=cov)
+        d = mk.synthetic.generate(sum(sizes), q=q, n_test=300, seed=71 + q + cov, cov_model=cov)
         p = 2 * q
         cfg = mk.SamplerConfig(q, p, np.zeros(p), np.full(p, 0.05), cov_model="matern" if cov else "exponential",
                                n_batch=2, batch_length=3, burn_in=4, seed=5)

@@ -1,0 +1,8 @@
+#!/bin/bash
+# Round-2 (re-entry) check on one MI355X: GPU tests, smoke, default bench.
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/r02d
+mkdir -p $O
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > $O/gpu_tests.log 2>&1 || exit 1
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit 1
+timeout -k 10 300 python bench.py > $O/bench_default.log 2>&1 || exit 1
