@@ -111,7 +111,7 @@ int mk_session_run(mk_session* s, int32_t n_iter);
 int32_t mk_session_iteration(const mk_session* s);
 /* Launch schedule (results are the same chain either way): mode 1 = lookahead
  * (the next iteration's phi candidates are factored while this iteration's inverse and latent
- * sweep run; exponential model, n_streams <= 1), 0 = sequential, -1 = default (lookahead where
+ * sweep run; Matern: the nu step follows the phi decision; n_streams <= 1), 0 = sequential, -1 = default (lookahead where
  * eligible; env MK_LOOKAHEAD=0/1 overrides the default).  Before the first mk_session_run only.
  * mk_session_lookahead returns 1 when the lookahead schedule is in use. */
 int mk_session_set_lookahead(mk_session* s, int32_t mode);

@@ -140,6 +140,7 @@ Model model_view(const Model& m, int s0, int S) {
   if (m.kA) v.kA = m.kA + s * q * q;
   if (m.bacc) v.bacc = m.bacc + s * q * np;
   if (m.zc) v.zc = m.zc + s * q * np;
+  if (m.la_nu) v.la_nu = m.la_nu + s * q;
   return v;
 }
 
@@ -726,6 +727,21 @@ static void run_iteration_la(mk_session* s, int it) {
   }
   hipLaunchKernelGGL(k_border_quad, dim3(S * q), dim3(256), 0, M, md);
   hipLaunchKernelGGL(k_theta_mh, dim3((S * q + 63) / 64), dim3(64), 0, M, md, g.ms, 0, q, 0, it);
+  if (s->matern) {
+    // the nu step: its candidate R(phi_t, nu') needs this phi decision, so it is factored now, as in
+    // the sequential schedule (bordered row: u is known), on the idle high-priority candidate stream
+    // (all CUs; the main stream is CU-masked); where it is accepted its border row becomes z
+    // (k_nu_border into zc).  The next phi candidates follow on the same stream (they need nu_t).
+    hipEventRecord(ev_d, M);
+    hipStreamWaitEvent(s->la_c, ev_d, 0);
+    hipLaunchKernelGGL(cov_candidate_kernel(md.cov_model), dim3(xcd_grid_h(S * q, nt * (nt + 1) / 2)), dim3(256), 0,
+                       s->la_c, md, g.ms, 0, q, 1, it, nullptr, nullptr);
+    launch_cholesky(s, g, 0, q, nullptr, nullptr, s->la_c);
+    hipLaunchKernelGGL(k_theta_mh, dim3((S * q + 63) / 64), dim3(64), 0, s->la_c, md, g.ms, 0, q, 1, it);
+    hipLaunchKernelGGL(k_nu_border, dim3(S * q * ((s->n_pad + 255) / 256)), dim3(256), 0, s->la_c, md, g.ms);
+    hipEventRecord(evP[nt + 4], s->la_c);
+    hipStreamWaitEvent(M, evP[nt + 4], 0);
+  }
   const bool more = it + 1 < md.n_samples, batch_end = (it + 1) % md.batch_length == 0;
   if (more && !batch_end) {   // the head now; the rest after the main stream's launches
     hipEventRecord(ev_d, M);
@@ -1050,15 +1066,16 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
       (rc = s->alloc(&ms.QB, (size_t)S * q * nt * MK_NB * MK_NB)) || (rc = s->alloc(&ms.cur, (size_t)S * q)) ||
       (rc = s->alloc(&s->d_probs, MK_N_LEVELS)))
     return rc;
-  // lookahead schedule buffers (run_iteration_la): exponential model on one stream group
+  // lookahead schedule buffers (run_iteration_la): one stream group (either covariance model)
   {
     const int G = std::max(1, std::min(c->n_streams > 0 ? (int)c->n_streams : 1, S));
-    s->la_ok = !s->matern && G == 1;
+    s->la_ok = G == 1;
     if (s->la_ok) {
       if ((rc = s->alloc(&md.bacc, (size_t)S * q * n_pad)) || (rc = s->alloc(&md.zc, (size_t)S * q * n_pad)) ||
-          (rc = s->alloc(&ms.Y, (size_t)S * q * n_pad * n_pad)))
+          (rc = s->alloc(&ms.Y, (size_t)S * q * n_pad * n_pad)) || (rc = s->alloc(&md.la_nu, (size_t)S * q)))
         return rc;
-      s->la_ev.assign(nt + 4, nullptr);
+      HIPCHK(hipMemset(md.la_nu, 0, (size_t)S * q * sizeof(int)));
+      s->la_ev.assign(nt + 5, nullptr);
       for (auto& e : s->la_ev)
         if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return set_err(MK_E_HIP, "lookahead event");
     }

@@ -768,6 +768,22 @@ __global__ __launch_bounds__(256) void k_take_border(Model md, MatSet ms, const 
   md.z[zo] = (j < ns) ? M[ns + (long)j * ms.ld] : 0.0;
 }
 
+// Lookahead schedule, Matern: the nu candidate is factored after the phi decision with its bordered
+// row (u is known by then), so where the nu step accepted, z_h is that factor's border row; it
+// replaces the phi candidate's solved z'_h in zc (which k_take_border then copies for every
+// changed pair).
+__global__ __launch_bounds__(256) void k_nu_border(Model md, MatSet ms) {
+  const int per = (md.n_pad + 255) / 256;
+  const int e = blockIdx.x / per;
+  if (e >= md.S * md.q || !md.la_nu[e]) return;
+  const int s = e / md.q;
+  const int ns = md.n_s[s];
+  const int j = (blockIdx.x % per) * 256 + threadIdx.x;
+  if (j >= md.n_pad) return;
+  const double* M = mat_slot(ms, e, ms.cur[e]);
+  md.zc[(long)e * md.n_pad + j] = (j < ns) ? M[ns + (long)j * ms.ld] : 0.0;
+}
+
 // ---------------------------------------------------------------- lookahead border solve
 // The lookahead schedule (mk_api.hip) factors iteration t+1's phi candidates while iteration t's
 // inverse and sweep run, before u_{t+1} = A_{t+1}^-1 w_t exists, so the candidate has no bordered

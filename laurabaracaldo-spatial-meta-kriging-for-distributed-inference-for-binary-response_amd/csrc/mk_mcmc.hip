@@ -209,7 +209,8 @@ __global__ __launch_bounds__(64) void k_theta_mh(Model md, MatSet ms, int h0, in
   const double qc = md.quad_c[sh];
   const double ratio = -0.5 * (ldc - md.logdetR[sh]) - 0.5 * (qc - md.quad[sh]) + unif_jacobian(v_c, a, b) -
                        unif_jacobian(v_cur, a, b);
-  if (md.info[sh] == 0 && lu <= ratio) {
+  const bool accept = md.info[sh] == 0 && lu <= ratio;
+  if (accept) {
     th[idx] = th_c;
     ms.cur[sh] ^= 1;
     md.logdetR[sh] = ldc;
@@ -217,6 +218,7 @@ __global__ __launch_bounds__(64) void k_theta_mh(Model md, MatSet ms, int h0, in
     md.dirty[sh] = 1;
     md.acc[(long)s * md.n_mh_max + j_mh] += 1.0;
   }
+  if (which == 1 && md.la_nu) md.la_nu[sh] = accept ? 1 : 0;   // lookahead schedule: k_nu_border
   md.info[sh] = 0;
 }
 

@@ -85,6 +85,7 @@ struct Model {
   // lookahead schedule (mk_api.hip): border solve of the candidate factored ahead of its iteration
   double* bacc;        // [S][q][n_pad]     right-looking partial sums of the border solve
   double* zc;          // [S][q][n_pad]     z'_h = L'_h^-1 u_h of the candidate
+  int* la_nu;          // [S*q]             Matern: 1 where this iteration's nu step accepted (k_nu_border)
   int P;               // reported columns
   int pred_gi;         // kriging GEMM raster: row panels per group (k_pred_var; 1 = row-panel-major)
 };

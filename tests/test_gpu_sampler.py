@@ -134,32 +134,38 @@ def test_replay_subset_beyond_2048_sites(mk):
     _check(dev, refs)
 
 
-@pytest.mark.parametrize("n,q,sizes", [(150, 1, None), (None, 1, [700, 333]), (64, 2, None), (None, 3, [300, 129]),
-                                       (None, 1, [1, 2, 3])])
-def test_replay_sequential_schedule(mk, n, q, sizes):
+@pytest.mark.parametrize("n,q,sizes,cov", [(150, 1, None, 0), (None, 1, [700, 333], 0), (64, 2, None, 0),
+                                           (None, 3, [300, 129], 0), (None, 1, [1, 2, 3], 0), (100, 1, None, 1),
+                                           (None, 2, [130, 90], 1)])
+def test_replay_sequential_schedule(mk, n, q, sizes, cov):
     """The sequential launch schedule (bordered candidates: z' is the factor's row n_s) replays the
-    oracle too; the default for the exponential model is the lookahead schedule."""
-    dev, refs = _run_both(mk, n, q, 0, sizes=sizes, lookahead=0)
+    oracle too (exponential and Matern); the default for shards of up to 224 (subset, outcome)
+    pairs is the lookahead schedule."""
+    dev, refs = _run_both(mk, n, q, cov, sizes=sizes, lookahead=0)
     _check(dev, refs)
 
 
-@pytest.mark.parametrize("n,q,sizes", [(150, 1, None), (None, 1, [1300, 700, 129]), (None, 2, [400, 257]),
-                                       (None, 3, [300, 2, 129])])
-def test_lookahead_schedule_replays_oracle(mk, n, q, sizes):
+@pytest.mark.parametrize("n,q,sizes,cov", [(150, 1, None, 0), (None, 1, [1300, 700, 129], 0), (None, 2, [400, 257], 0),
+                                           (None, 3, [300, 2, 129], 0), (None, 1, [1000, 300], 1),
+                                           (48, 2, None, 1), (None, 1, [1, 3], 1)])
+def test_lookahead_schedule_replays_oracle(mk, n, q, sizes, cov):
     """Lookahead schedule: iteration t+1's phi candidates are factored without a
     bordered row while iteration t's inverse and sweep run, and z' = L'^-1 u comes from the
-    trailing border solve (k_border_step / k_border_combine).  Replayed against the oracle across
-    batch ends (adapted proposal scales) and across mk_session_run calls that stop mid-batch (the
-    candidate queued by one call is used by the next)."""
-    dev, refs = _run_both(mk, n, q, 0, sizes=sizes, lookahead=1, chunks=[1, 4, 2, 5])
+    trailing border solve (k_border_step / k_border_combine); Matern: the nu candidate follows the
+    phi decision with its bordered row, and its row replaces z' where nu is accepted (k_nu_border).
+    Replayed against the oracle across batch ends (adapted proposal scales) and across
+    mk_session_run calls that stop mid-batch (the candidate queued by one call is used by the
+    next); [1000, 300] is the configs[1] subset size."""
+    dev, refs = _run_both(mk, n, q, cov, sizes=sizes, lookahead=1, chunks=[1, 4, 2, 5])
     _check(dev, refs)
 
 
-def test_lookahead_equals_sequential_schedule(mk):
+@pytest.mark.parametrize("cov,sizes", [(0, [900, 650]), (1, [700, 400])])
+def test_lookahead_equals_sequential_schedule(mk, cov, sizes):
     """Both schedules run the same chain: every decision agrees and the states differ by rounding
     only (z' from a forward solve instead of the bordered factor row)."""
-    a, _ = _run_both(mk, None, 1, 0, sizes=[900, 650], n_batch=4, batch_length=3, burn_in=9, lookahead=1)
-    b, _ = _run_both(mk, None, 1, 0, sizes=[900, 650], n_batch=4, batch_length=3, burn_in=9, lookahead=0)
+    a, _ = _run_both(mk, None, 1, cov, sizes=sizes, n_batch=4, batch_length=3, burn_in=9, lookahead=1)
+    b, _ = _run_both(mk, None, 1, cov, sizes=sizes, n_batch=4, batch_length=3, burn_in=9, lookahead=0)
     for s in range(2):
         np.testing.assert_allclose(a["samples"][s], b["samples"][s], rtol=0, atol=1e-10)
         np.testing.assert_allclose(a["w_samples"][s], b["w_samples"][s], rtol=0, atol=1e-10)
@@ -168,22 +174,25 @@ def test_lookahead_equals_sequential_schedule(mk):
 
 
 def test_lookahead_is_rejected_where_ineligible(mk):
-    """The Matern model (nu's candidate depends on the same iteration's phi decision) keeps the
-    sequential schedule; asking for lookahead is an argument error, as is changing the schedule
-    after the chain has started."""
+    """Sessions that run their subsets as several stream groups (n_streams > 1) keep the
+    sequential schedule; asking for lookahead there is an argument error, as is changing the
+    schedule after the chain has started.  Both covariance models are eligible otherwise."""
     d = mk.synthetic.generate(60, q=1, n_test=3, seed=3, cov_model=1)
-    sub = [dict(coords=d["coords"], y=d["y"], weights=np.ones(60), x=d["x"])]
-    cfg = mk.SamplerConfig(1, 2, [0, 0], [0.05, 0.05], cov_model="matern", n_batch=1, batch_length=3, burn_in=2)
+    sub = [dict(coords=d["coords"][:30], y=d["y"][:30], weights=np.ones(30), x=d["x"][:30]),
+           dict(coords=d["coords"][30:], y=d["y"][30:], weights=np.ones(30), x=d["x"][30:])]
+    cfg = mk.SamplerConfig(1, 2, [0, 0], [0.05, 0.05], cov_model="matern", n_batch=1, batch_length=3, burn_in=2,
+                           n_streams=2)
     with mk.Session(sub, cfg) as ses:
         assert not ses.lookahead
         with pytest.raises(mk.MkError):
             ses.set_lookahead(1)
-    cfg = mk.SamplerConfig(1, 2, [0, 0], [0.05, 0.05], n_batch=1, batch_length=3, burn_in=2)
-    with mk.Session(sub, cfg) as ses:
-        assert ses.lookahead
-        ses.run(1)
-        with pytest.raises(mk.MkError):
-            ses.set_lookahead(0)
+    for cov in ("exponential", "matern"):
+        cfg = mk.SamplerConfig(1, 2, [0, 0], [0.05, 0.05], cov_model=cov, n_batch=1, batch_length=3, burn_in=2)
+        with mk.Session(sub, cfg) as ses:
+            assert ses.lookahead
+            ses.run(1)
+            with pytest.raises(mk.MkError):
+                ses.set_lookahead(0)
 
 
 def test_quantiles_bit_exact_on_device_samples(mk):
