@@ -141,6 +141,8 @@ Model model_view(const Model& m, int s0, int S) {
   if (m.bacc) v.bacc = m.bacc + s * q * np;
   if (m.zc) v.zc = m.zc + s * q * np;
   if (m.la_nu) v.la_nu = m.la_nu + s * q;
+  if (m.span) v.span = m.span + s;
+  if (m.span_pt) v.span_pt = m.span_pt + s;
   return v;
 }
 
@@ -177,6 +179,7 @@ struct mk_session {
   int tile_req = 0;               // predict_tile as configured
   int win_lo = 0, win_n = -1;     // tiled kriging: kept states [win_lo, win_lo + win_n) (-1: all)
   std::vector<void*> kbufs;       // the kriging buffers (re-sized by mk_session_set_test_sites)
+  std::vector<double> bbox;       // [S][4] xmin xmax ymin ymax of each subset's sites (Matern table ranges)
   double* d_ct_all = nullptr;     // all test sites [2][n_test_pad_all] (tiled mode)
   int* d_slist = nullptr;         // tiled replay: per-outcome subset lists [q][S] + counts [q]
   int* d_scount = nullptr;
@@ -577,7 +580,10 @@ static void launch_pred_refresh(mk_session* s, Group& g, hipStream_t st = nullpt
   if (md.n_test <= 0) return;
   if (!st) st = g.stream;
   const int nt = s->nt, max_entries = g.S * s->q;
-  if (!s->pred_gen)
+  if (md.cov_model == MK_COV_MATERN)
+    hipLaunchKernelGGL(k_pred_PT_matern, dim3(max_entries * (md.n_pad / MK_PT_RB)), dim3(256), 0, st, md, g.d_plist,
+                       g.d_pcount);
+  else if (!s->pred_gen)
     hipLaunchKernelGGL(pred_PT_kernel(md.cov_model), dim3(max_entries * md.n_pad), dim3(256), 0, st, md, g.d_plist,
                        g.d_pcount);
   timed(s, st, KS_PRED_VAR, pred_flops(s, g), [&] {
@@ -905,6 +911,7 @@ static int kriging_buffers(mk_session* s, int n_test_all, const double* coords_t
   for (void* b : s->kbufs) s->release(b);
   s->kbufs.clear();
   md.PT = md.XK = md.s_pred = md.s_part = md.w_pred = nullptr;
+  md.span_pt = nullptr;
   const int S = s->S, q = s->q, nt = s->nt, n_pad = s->n_pad;
   s->n_test_all = n_test_all;
   s->n_test_pad_all = round_up(std::max(n_test_all, 1), 256);
@@ -915,8 +922,10 @@ static int kriging_buffers(mk_session* s, int n_test_all, const double* coords_t
   md.n_test_pad = n_test_pad;
   md.ntt = n_test_pad / MK_NB;
   double* d_ct = nullptr;
+  double* d_spt = nullptr;
   int rc;
   if ((rc = s->alloc(&d_ct, (size_t)2 * n_test_pad)) || (rc = s->alloc(&s->d_ct_all, (size_t)2 * s->n_test_pad_all)) ||
+      (rc = s->alloc(&d_spt, (size_t)S)) ||
       (rc = s->alloc(&md.s_pred, (size_t)S * q * n_test_pad)) ||
       (rc = s->alloc(&md.s_part, (size_t)S * q * nt * n_test_pad)) ||
       (n_test > 0 && !s->pred_gen && (rc = s->alloc(&md.PT, (size_t)S * q * n_pad * n_test_pad))) ||
@@ -924,7 +933,26 @@ static int kriging_buffers(mk_session* s, int n_test_all, const double* coords_t
       (rc = s->alloc(&md.w_pred, (size_t)S * md.n_kept * q * std::max(n_test, 1))))
     return rc;
   md.coords_test = d_ct;
-  s->kbufs = {d_ct, s->d_ct_all, md.s_pred, md.s_part, md.PT, md.XK, md.w_pred};
+  s->kbufs = {d_ct, s->d_ct_all, md.s_pred, md.s_part, md.PT, md.XK, md.w_pred, d_spt};
+  {   // Matern kriging tables (k_pred_PT_matern): a bound on every subset-site to test-site distance
+    double t0 = 0.0, t1 = 0.0, t2 = 0.0, t3 = 0.0;
+    for (int t = 0; t < n_test_all; ++t) {
+      const double x = coords_test[t], y = coords_test[n_test_all + t];
+      if (t == 0 || x < t0) t0 = x;
+      if (t == 0 || x > t1) t1 = x;
+      if (t == 0 || y < t2) t2 = y;
+      if (t == 0 || y > t3) t3 = y;
+    }
+    std::vector<double> hs(S);
+    for (int i = 0; i < S; ++i) {
+      const double* b = s->bbox.data() + 4 * i;
+      hs[i] = n_test_all > 0 ? std::hypot(std::fmax(std::fabs(b[1] - t0), std::fabs(t1 - b[0])),
+                                          std::fmax(std::fabs(b[3] - t2), std::fabs(t3 - b[2])))
+                             : 0.0;
+    }
+    HIPCHK(hipMemcpy(d_spt, hs.data(), (size_t)S * 8, hipMemcpyHostToDevice));
+    md.span_pt = d_spt;
+  }
   HIPCHK(hipMemset(md.s_pred, 0, (size_t)S * q * n_test_pad * 8));
   const int npa = s->n_test_pad_all;
   std::vector<double> hct((size_t)2 * npa, 0.0);
@@ -985,6 +1013,22 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
   // every row panel).  Default: stored P^T.
   s->pred_gen = !s->matern && tile_env("MK_PRED_GEN", 0) != 0;
   s->n_part.assign(pr->n_part, pr->n_part + S);
+  s->bbox.assign((size_t)4 * S, 0.0);
+  {
+    long off = 0;
+    for (int i = 0; i < S; ++i) {
+      const int ns = pr->n_part[i];
+      const double* cs = pr->coords + 2 * off;
+      double* b = s->bbox.data() + 4 * i;
+      for (int r = 0; r < ns; ++r) {
+        if (r == 0 || cs[r] < b[0]) b[0] = cs[r];
+        if (r == 0 || cs[r] > b[1]) b[1] = cs[r];
+        if (r == 0 || cs[ns + r] < b[2]) b[2] = cs[ns + r];
+        if (r == 0 || cs[ns + r] > b[3]) b[3] = cs[ns + r];
+      }
+      off += ns;
+    }
+  }
   int nmax = 0;
   for (int i = 0; i < S; ++i) nmax = std::max(nmax, (int)pr->n_part[i]);
   const int n_pad = round_up(nmax + 1, MK_NB);
@@ -1058,6 +1102,15 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
                    (rc = s->alloc(&s->d_slist, (size_t)q * S)) || (rc = s->alloc(&s->d_scount, (size_t)q))))
     return rc;
   if ((rc = kriging_buffers(s, pr->n_test, pr->coords_test))) return rc;
+  {   // Matern candidate tables (k_cov_candidate): bounding-box diagonal of every subset
+    double* d_span = nullptr;
+    if ((rc = s->alloc(&d_span, (size_t)S))) return rc;
+    std::vector<double> hs(S);
+    for (int i = 0; i < S; ++i)
+      hs[i] = std::hypot(s->bbox[4 * i + 1] - s->bbox[4 * i], s->bbox[4 * i + 3] - s->bbox[4 * i + 2]);
+    HIPCHK(hipMemcpy(d_span, hs.data(), (size_t)S * 8, hipMemcpyHostToDevice));
+    md.span = d_span;
+  }
   MatSet& ms = s->ms;
   ms.ld = n_pad; ms.nt = nt; ms.q = q;
   if ((rc = s->alloc(&ms.L, (size_t)S * q * 2 * n_pad * n_pad)) ||

@@ -1,6 +1,7 @@
 // Kernel declarations shared by the launch code (mk_api.hip).
 #pragma once
 #include "mk_types.hpp"
+#include "mk_corr.hpp"
 
 namespace mk {
 inline int xcd_grid_h(int S, int T) { return 8 * ((S + 7) / 8) * T; }
@@ -32,6 +33,7 @@ __global__ void k_border_quad(Model md);
 __global__ void k_trmv_Z(Model md, MatSet ms);
 template <int MODEL>
 __global__ void k_pred_PT(Model md, const int* list, const int* count);
+__global__ void k_pred_PT_matern(Model md, const int* list, const int* count);
 typedef void (*PredPTKernel)(Model, const int*, const int*);
 inline PredPTKernel pred_PT_kernel(int model) {
   return model == MK_COV_EXPONENTIAL ? k_pred_PT<MK_COV_EXPONENTIAL> : k_pred_PT<MK_COV_MATERN>;

@@ -109,76 +109,48 @@ __device__ inline double cand_value(const CandGen& g, int R, int C) {
   return (R == C && R != g.ns) ? 1.0 : 0.0;
 }
 
-// Matern candidate tile.  K_nu costs a Temme series (x < 2) or Steed's CF2 (x >= 2) whose
-// length depends on x; with lanes mapped to rows nearly every wave holds both branches and a
-// spread of x, and pays for both branches at their longest.  Per 32-column chunk the elements
-// are binned by x (branch and convergence length: bins of MK_MT_EDGES), counted and placed with
-// wave ballots + one LDS atomic per wave and bin (order within a bin is arbitrary, every
-// element's value is not), and evaluated bin after bin, so a wave runs one branch over similar
-// lengths; results go through LDS and leave as the exponential path's 16-byte row-pair stores.
+// Matern candidate tile, per 32-column chunk: every off-diagonal element inside the chunk is
+// interpolated from the workgroup's Chebyshev table (cheb_eval); the few outside it (x = phi d
+// < 0.5, or beyond the table) are compacted into a list by wave ballots and evaluated exactly
+// afterwards, densely (an exact K_nu costs ~20x an interpolation: left in place, one such element
+// would hold up its whole wave).  Results go through LDS and leave as the exponential path's
+// 16-byte row-pair stores.
 #define MK_MT_COLS 32
-#define MK_MT_NBIN 10
-__device__ inline int matern_bin(double x) {
-  // 1..4: series (x < 2), 5..10: CF2
-  return (x < 1.0) ? ((x < 0.5) ? 1 : 2) : (x < 2.0) ? ((x < 1.5) ? 3 : 4)
-       : (x < 3.0) ? ((x < 2.5) ? 5 : 6) : (x < 5.0) ? ((x < 4.0) ? 7 : 8) : ((x < 7.0) ? 9 : 10);
-}
-__device__ inline void matern_tile(const CandGen& g, double* M, long ld, int ti, int tj, double* buf,
-                                   unsigned short* idx, unsigned char* binb, int* cnt) {
+__device__ inline void matern_tile(const CandGen& g, const double* chtab, int ni, double* M, long ld, int ti, int tj,
+                                   double* buf, unsigned short* idx, int* cnt) {
   const int tid = threadIdx.x, lane = tid & 63;
   constexpr int CH = MK_NB * MK_MT_COLS;   // elements per chunk
   constexpr int NJ = CH / 256;
-  int* cur = cnt + MK_MT_NBIN + 1;         // placement cursors
   for (int c0 = 0; c0 < MK_NB; c0 += MK_MT_COLS) {
-    if (tid <= MK_MT_NBIN) cnt[tid] = 0;
+    if (tid == 0) cnt[0] = 0;
     __syncthreads();
-#pragma unroll 1
+#pragma unroll 2
     for (int j = 0; j < NJ; ++j) {
       const int e = tid + 256 * j;
       const int r = e & (MK_NB - 1), cc = e >> 7;
       const int R = ti * MK_NB + r, C = tj * MK_NB + c0 + cc;
       const bool skip = (ti == tj) && ((R & ~1) + 1 < C);      // pair never stored (upper half)
-      int bin = 0;
+      bool exact = false;
       double v = 0.0;
       if (!skip) {
         if (R < g.ns && C < g.ns && R != C) {
-          v = dist2d(g.cx[R], g.cy[R], g.cx[C], g.cy[C]);     // distance; rho applied below
-          bin = matern_bin(v * g.rho.phi);
+          const double d = dist2d(g.cx[R], g.cy[R], g.cx[C], g.cy[C]);
+          if (!cheb_eval(chtab, ni, d * g.rho.phi, &v)) {
+            v = d;                                            // distance; rho applied below
+            exact = true;
+          }
         } else {
           v = cand_value<MK_COV_MATERN>(g, R, C);             // diagonal, border row, padding
         }
       }
       buf[e] = v;
-      binb[e] = (unsigned char)bin;
-#pragma unroll
-      for (int bb = 1; bb <= MK_MT_NBIN; ++bb) {
-        const unsigned long long m = __ballot(bin == bb);
-        if (m && lane == __ffsll((long long)m) - 1) atomicAdd(&cnt[bb], __popcll(m));
-      }
-    }
-    __syncthreads();
-    if (tid == 0) {                           // bin offsets (exclusive scan), cursors
-      int o = 0;
-      for (int bb = 1; bb <= MK_MT_NBIN; ++bb) {
-        cur[bb] = o;
-        o += cnt[bb];
-      }
-      cnt[0] = o;                             // total
-    }
-    __syncthreads();
-#pragma unroll 1
-    for (int j = 0; j < NJ; ++j) {
-      const int e = tid + 256 * j, bin = binb[e];
-#pragma unroll
-      for (int bb = 1; bb <= MK_MT_NBIN; ++bb) {
-        const unsigned long long m = __ballot(bin == bb);
-        if (m) {
-          const int leader = __ffsll((long long)m) - 1;
-          int base = 0;
-          if (lane == leader) base = atomicAdd(&cur[bb], __popcll(m));
-          base = __shfl(base, leader, 64);
-          if (bin == bb) idx[base + __popcll(m & ((1ull << lane) - 1ull))] = (unsigned short)e;
-        }
+      const unsigned long long m = __ballot(exact);
+      if (m) {
+        const int leader = __ffsll((long long)m) - 1;
+        int base = 0;
+        if (lane == leader) base = atomicAdd(cnt, __popcll(m));
+        base = __shfl(base, leader, 64);
+        if (exact) idx[base + __popcll(m & ((1ull << lane) - 1ull))] = (unsigned short)e;
       }
     }
     __syncthreads();
@@ -219,12 +191,16 @@ __global__ __launch_bounds__(256) void k_cov_candidate(Model md, MatSet ms, int 
     __shared__ double btab[5 * MK_BK_NTAB];
     __shared__ double buf[MK_NB * MK_MT_COLS];
     __shared__ unsigned short idx[MK_NB * MK_MT_COLS];
-    __shared__ int cnt[2 * (MK_MT_NBIN + 1)];
-    __shared__ unsigned char binb[MK_NB * MK_MT_COLS];
+    __shared__ int cnt[1];
+    __shared__ double chtab[MK_CH_NI_MAX * MK_CH_LD];
+    __shared__ double cosm[MK_CH_N * MK_CH_N];
     g.rho.fill_tables(btab, threadIdx.x, 256);
     __syncthreads();
     g.rho.tab = btab;
-    matern_tile(g, M, ld, ti, tj, buf, idx, binb, cnt);
+    // table over [0.5, phi x the subset's extent] (every pair distance is within it)
+    const int ni = cheb_count(md.span ? g.rho.phi * md.span[s] : INFINITY);
+    cheb_build(g.rho, ni, chtab, buf, cosm, threadIdx.x, 256);
+    matern_tile(g, chtab, ni, M, ld, ti, tj, buf, idx, cnt);
     return;
   }
   // two rows per lane, 16-byte stores; the upper half of a diagonal tile is never read (the
@@ -974,6 +950,83 @@ __global__ __launch_bounds__(256) void k_pred_PT(Model md, const int* __restrict
 }
 template __global__ void k_pred_PT<MK_COV_EXPONENTIAL>(Model, const int*, const int*);
 template __global__ void k_pred_PT<MK_COV_MATERN>(Model, const int*, const int*);
+
+// Matern P^T: one workgroup per (pair, MK_PT_RB observation rows) builds the Chebyshev table of
+// its pair's current (phi, nu) over [0.5, phi x the extent of subset + test sites] and
+// interpolates; elements outside the table are compacted per 4,096-site chunk and evaluated
+// exactly (as matern_tile).
+__global__ __launch_bounds__(256) void k_pred_PT_matern(Model md, const int* __restrict__ list,
+                                                        const int* __restrict__ count) {
+  constexpr int CHUNK = 4096;
+  __shared__ double btab[5 * MK_BK_NTAB];
+  __shared__ double chtab[MK_CH_NI_MAX * MK_CH_LD];
+  __shared__ double vals[MK_CH_NI_MAX * MK_CH_N];
+  __shared__ double cosm[MK_CH_N * MK_CH_N];
+  __shared__ unsigned short idx[CHUNK];
+  __shared__ int cnt;
+  const int per = md.n_pad / MK_PT_RB;
+  const int e = blockIdx.x / per;
+  if (e >= *count) return;
+  const int k0 = (blockIdx.x % per) * MK_PT_RB;
+  const int sh = list[e];
+  const int s = sh / md.q, h = sh % md.q;
+  const int ns = md.n_s[s];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int tlim = md.ntt * MK_NB;   // the column blocks k_pred_var reads
+  double* PT = md.PT + ((long)sh * md.n_pad + k0) * md.n_test_pad;
+  if (k0 >= ns) {                    // padding rows
+    for (int rr = 0; rr < MK_PT_RB; ++rr)
+      for (int t = tid; t < tlim; t += 256) PT[(long)rr * md.n_test_pad + t] = 0.0;
+    return;
+  }
+  double phi, nu;
+  current_phi_nu(md, s, h, &phi, &nu);
+  CorrFn rho;
+  rho.init(phi, nu, md.cov_model);
+  rho.fill_tables(btab, tid, 256);
+  __syncthreads();
+  rho.tab = btab;
+  const int ni = cheb_count(md.span_pt ? phi * md.span_pt[s] : INFINITY);
+  cheb_build(rho, ni, chtab, vals, cosm, tid, 256);
+  const double* cx = md.coords + (long)s * 2 * md.n_pad;
+  const double* tx = md.coords_test;
+  const double* ty = md.coords_test + md.n_test_pad;
+  for (int rr = 0; rr < MK_PT_RB; ++rr) {
+    const int k = k0 + rr;
+    double* row = PT + (long)rr * md.n_test_pad;
+    const bool kv = k < ns;
+    const double ox = cx[k], oy = cx[md.n_pad + k];
+    for (int t0 = 0; t0 < tlim; t0 += CHUNK) {
+      if (tid == 0) cnt = 0;
+      __syncthreads();
+      const int tend = min(tlim, t0 + CHUNK);
+      for (int t = t0 + tid; t < tend; t += 256) {   // tend - t0 is a multiple of 128: whole waves
+        double v = 0.0;
+        bool exact = false;
+        if (kv && t < md.n_test) {
+          const double d = dist2d(ox, oy, tx[t], ty[t]);
+          exact = !cheb_eval(chtab, ni, d * phi, &v);
+        }
+        if (!exact) row[t] = v;
+        const unsigned long long m = __ballot(exact);
+        if (m) {
+          const int leader = __ffsll((long long)m) - 1;
+          int base = 0;
+          if (lane == leader) base = atomicAdd(&cnt, __popcll(m));
+          base = __shfl(base, leader, 64);
+          if (exact) idx[base + __popcll(m & ((1ull << lane) - 1ull))] = (unsigned short)(t - t0);
+        }
+      }
+      __syncthreads();
+      const int n = cnt;
+      for (int p = tid; p < n; p += 256) {
+        const int t = t0 + idx[p];
+        row[t] = rho(dist2d(ox, oy, tx[t], ty[t]));
+      }
+      __syncthreads();
+    }
+  }
+}
 
 // X = W P^T (row tile i, test tile tb), stored column-major by test site (XK[t][row]);
 // partial column sums of squares over valid rows -> s_part[sh][i][t].

@@ -45,6 +45,8 @@ struct Model {
   const double* wt;
   const double* X;
   const double* coords_test;   // [2][n_test_pad]
+  const double* span;          // [S] bounding-box diagonal of the subset's sites (Matern tables)
+  const double* span_pt;       // [S] bound on the subset-to-test-site distances (Matern kriging tables)
   // state
   double* beta;      // [S][p]
   double* theta;     // [S][n_theta]: A lower-tri (log diag) | logit phi | logit nu
