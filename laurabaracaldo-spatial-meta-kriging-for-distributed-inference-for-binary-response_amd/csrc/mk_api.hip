@@ -143,6 +143,8 @@ Model model_view(const Model& m, int s0, int S) {
   if (m.la_nu) v.la_nu = m.la_nu + s * q;
   if (m.span) v.span = m.span + s;
   if (m.span_pt) v.span_pt = m.span_pt + s;
+  if (m.chtab) v.chtab = m.chtab + s * q * MK_CH_TAB;
+  if (m.chtab_p) v.chtab_p = m.chtab_p + s * q * MK_CH_TAB;
   return v;
 }
 
@@ -349,6 +351,18 @@ static int tile_size(long wg128) {
   static const int thresh = tile_env("MK_TILE_THRESH", 256);
   if (force == 32 || force == 64 || force == 128) return force;
   return wg128 >= thresh ? 128 : 64;
+}
+
+// ------------------------------------------------------------------ candidate assembly
+// Candidate matrices of n_entries (subset, outcome) entries (k_cov_candidate); Matern sessions
+// first store each entry's Chebyshev table (k_matern_table, one workgroup per entry), which the
+// tile workgroups then load.
+static void launch_candidates(const Model& md, const MatSet& ms, hipStream_t st, int n_entries, int h0, int hc,
+                              int which, int iter, const int* slist = nullptr, const int* scount = nullptr) {
+  if (md.cov_model == MK_COV_MATERN && md.chtab)
+    hipLaunchKernelGGL(k_matern_table, dim3(n_entries), dim3(256), 0, st, md, h0, hc, which, iter, slist, scount);
+  hipLaunchKernelGGL(cov_candidate_kernel(md.cov_model), dim3(xcd_grid_h(n_entries, ms.nt * (ms.nt + 1) / 2)),
+                     dim3(256), 0, st, md, ms, h0, hc, which, iter, slist, scount);
 }
 
 // ------------------------------------------------------------------ Cholesky of all candidates of outcome h
@@ -580,6 +594,8 @@ static void launch_pred_refresh(mk_session* s, Group& g, hipStream_t st = nullpt
   if (md.n_test <= 0) return;
   if (!st) st = g.stream;
   const int nt = s->nt, max_entries = g.S * s->q;
+  if (md.cov_model == MK_COV_MATERN && md.chtab_p)
+    hipLaunchKernelGGL(k_matern_table_list, dim3(max_entries), dim3(256), 0, st, md, g.d_plist, g.d_pcount);
   if (md.cov_model == MK_COV_MATERN)
     hipLaunchKernelGGL(k_pred_PT_matern, dim3(max_entries * (md.n_pad / MK_PT_RB)), dim3(256), 0, st, md, g.d_plist,
                        g.d_pcount);
@@ -653,11 +669,9 @@ static void iteration_pre_sweep(mk_session* s, Group& g, int it) {
   if (q > 1) hipLaunchKernelGGL(k_trmv_Z, dim3(S * q * ((s->n_pad + 255) / 256)), dim3(256), 0, st, md, g.ms);
   hipLaunchKernelGGL(k_Aphase, dim3(S), dim3(256), 0, st, md, it);
   const int nkinds = s->matern ? 2 : 1;
-  const int ntri_tiles = s->nt * (s->nt + 1) / 2;
   // the q outcomes' (phi_h, nu_h) steps are independent given u: one batched pass per kind
   for (int which = 0; which < nkinds; ++which) {
-    hipLaunchKernelGGL(cov_candidate_kernel(md.cov_model), dim3(xcd_grid_h(S * q, ntri_tiles)), dim3(256), 0, st, md, g.ms, 0, q, which,
-                       it, nullptr, nullptr);
+    launch_candidates(md, g.ms, st, S * q, 0, q, which, it);
     launch_cholesky(s, g, 0, q);
     hipLaunchKernelGGL(k_theta_mh, dim3((S * q + 63) / 64), dim3(64), 0, st, md, g.ms, 0, q, which, it);
   }
@@ -701,8 +715,7 @@ static int la_head(mk_session* s) {
 static void enqueue_candidates(mk_session* s, Group& g, int it, hipEvent_t after, int k_hi) {
   const int S = g.S, q = s->q, nt = s->nt;
   hipStreamWaitEvent(s->la_c, after, 0);
-  hipLaunchKernelGGL(cov_candidate_kernel(g.md.cov_model), dim3(xcd_grid_h(S * q, nt * (nt + 1) / 2)), dim3(256), 0,
-                     s->la_c, g.md, g.ms, 0, q, 0 | MK_CAND_NOBORDER, it, nullptr, nullptr);
+  launch_candidates(g.md, g.ms, s->la_c, S * q, 0, q, 0 | MK_CAND_NOBORDER, it);
   launch_cholesky(s, g, 0, q, nullptr, nullptr, s->la_c, s->la_ev.data(), 0, k_hi);
   s->la_next = it;
   s->la_enq = k_hi;
@@ -740,8 +753,7 @@ static void run_iteration_la(mk_session* s, int it) {
     // (k_nu_border into zc).  The next phi candidates follow on the same stream (they need nu_t).
     hipEventRecord(ev_d, M);
     hipStreamWaitEvent(s->la_c, ev_d, 0);
-    hipLaunchKernelGGL(cov_candidate_kernel(md.cov_model), dim3(xcd_grid_h(S * q, nt * (nt + 1) / 2)), dim3(256), 0,
-                       s->la_c, md, g.ms, 0, q, 1, it, nullptr, nullptr);
+    launch_candidates(md, g.ms, s->la_c, S * q, 0, q, 1, it);
     launch_cholesky(s, g, 0, q, nullptr, nullptr, s->la_c);
     hipLaunchKernelGGL(k_theta_mh, dim3((S * q + 63) / 64), dim3(64), 0, s->la_c, md, g.ms, 0, q, 1, it);
     hipLaunchKernelGGL(k_nu_border, dim3(S * q * ((s->n_pad + 255) / 256)), dim3(256), 0, s->la_c, md, g.ms);
@@ -1110,6 +1122,9 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
       hs[i] = std::hypot(s->bbox[4 * i + 1] - s->bbox[4 * i], s->bbox[4 * i + 3] - s->bbox[4 * i + 2]);
     HIPCHK(hipMemcpy(d_span, hs.data(), (size_t)S * 8, hipMemcpyHostToDevice));
     md.span = d_span;
+    if (s->matern && ((rc = s->alloc(&md.chtab, (size_t)S * q * MK_CH_TAB)) ||
+                      (rc = s->alloc(&md.chtab_p, (size_t)S * q * MK_CH_TAB))))
+      return rc;
   }
   MatSet& ms = s->ms;
   ms.ld = n_pad; ms.nt = nt; ms.q = q;
@@ -1266,9 +1281,7 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
   // ---------------- initial state: eta, u, factor every R_h at the starting values, W, z (whole shard)
   Group& a = s->all;
   hipLaunchKernelGGL(k_init_state, dim3(S), dim3(256), 0, s->stream, md);
-  const int ntri_tiles = nt * (nt + 1) / 2;
-  hipLaunchKernelGGL(cov_candidate_kernel(md.cov_model), dim3(xcd_grid_h(S * q, ntri_tiles)), dim3(256), 0, s->stream, md, ms, 0, q, 2,
-                     0, nullptr, nullptr);
+  launch_candidates(md, ms, s->stream, S * q, 0, q, 2, 0);
   launch_cholesky(s, a, 0, q);
   hipLaunchKernelGGL(k_theta_init, dim3((S * q + 63) / 64), dim3(64), 0, s->stream, md, ms, 0, q);
   hipLaunchKernelGGL(k_dirty_list, dim3(1), dim3(256), 0, s->stream, md, 0, a.d_list, a.d_count, a.d_plist, a.d_pcount);
@@ -1424,7 +1437,6 @@ static int predict_tiled(mk_session* s, mk_outputs* o) {
   const long C = (long)q * n_test;
   hipStream_t st = s->stream;
   Group g = s->all;
-  const int ntri_tiles = nt * (nt + 1) / 2;
   s->la_next = -1;   // the replay factors into the free slots: a lookahead candidate is gone
   DevBufs scratch;
   double* dq = scratch.get<double>((size_t)S * q * T * MK_N_LEVELS);
@@ -1452,8 +1464,7 @@ static int predict_tiled(mk_session* s, mk_outputs* o) {
       hipLaunchKernelGGL(k_kept_dirty, dim3(1), dim3(256), 0, st, mt, prev, s->d_slist, s->d_scount, g.d_plist,
                          g.d_pcount);
       for (int h = 0; h < q; ++h) {
-        hipLaunchKernelGGL(cov_candidate_kernel(mt.cov_model), dim3(xcd_grid_h(S, ntri_tiles)), dim3(256), 0, st, mt, g.ms, h, 1, 2, 0,
-                           s->d_slist + h * S, s->d_scount + h);
+        launch_candidates(mt, g.ms, st, S, h, 1, 2, 0, s->d_slist + h * S, s->d_scount + h);
         launch_cholesky(s, g, h, 1, s->d_slist + h * S, s->d_scount + h);
       }
       hipLaunchKernelGGL(k_flip_pairs, dim3((S * q + 255) / 256), dim3(256), 0, st, g.ms, g.d_plist, g.d_pcount);

@@ -217,6 +217,7 @@ struct CorrFn {
 #define MK_CH_NI_MAX 100                   // x < 2.384 + 0.5 * 93 = 48.88
 #define MK_CH_E7 2.384185791015625         // 0.5 * 1.25^7 (exact)
 #define MK_PT_RB 16                        // observation rows per workgroup of k_pred_PT_matern
+#define MK_CH_TAB (MK_CH_NI_MAX * MK_CH_LD + 1)   // one stored table: intervals, then the interval count
 
 // interval of x >= 0.5
 __device__ inline int cheb_interval(double x) {

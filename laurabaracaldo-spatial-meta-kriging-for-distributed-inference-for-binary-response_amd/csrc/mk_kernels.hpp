@@ -34,6 +34,8 @@ __global__ void k_trmv_Z(Model md, MatSet ms);
 template <int MODEL>
 __global__ void k_pred_PT(Model md, const int* list, const int* count);
 __global__ void k_pred_PT_matern(Model md, const int* list, const int* count);
+__global__ void k_matern_table(Model md, int h0, int hc, int which, int iter, const int* slist, const int* scount);
+__global__ void k_matern_table_list(Model md, const int* list, const int* count);
 typedef void (*PredPTKernel)(Model, const int*, const int*);
 inline PredPTKernel pred_PT_kernel(int model) {
   return model == MK_COV_EXPONENTIAL ? k_pred_PT<MK_COV_EXPONENTIAL> : k_pred_PT<MK_COV_MATERN>;

@@ -173,6 +173,39 @@ __device__ inline void matern_tile(const CandGen& g, const double* chtab, int ni
   }
 }
 
+// Matern tables in HBM: one workgroup per (subset, outcome) builds the Chebyshev table of its
+// candidate (the same (phi', nu') k_cov_candidate draws) or of its current (phi, nu) (kriging), so
+// the tile workgroups of a pair load it (11 KB, from L2) instead of each rebuilding it.
+__device__ inline void cheb_build_store(CorrFn rho, double x_hi, double* out) {
+  __shared__ double btab[5 * MK_BK_NTAB];
+  __shared__ double chtab[MK_CH_NI_MAX * MK_CH_LD];
+  __shared__ double vals[MK_CH_NI_MAX * MK_CH_N];
+  __shared__ double cosm[MK_CH_N * MK_CH_N];
+  rho.fill_tables(btab, threadIdx.x, 256);
+  __syncthreads();
+  rho.tab = btab;
+  const int ni = cheb_count(x_hi);
+  cheb_build(rho, ni, chtab, vals, cosm, threadIdx.x, 256);
+  for (int i = threadIdx.x; i < ni * MK_CH_LD; i += 256) out[i] = chtab[i];
+  if (threadIdx.x == 0) out[MK_CH_NI_MAX * MK_CH_LD] = (double)ni;
+}
+__global__ __launch_bounds__(256) void k_matern_table(Model md, int h0, int hc, int which, int iter, const int* slist,
+                                                      const int* scount) {
+  int s, h;
+  if (!pick_pair(slist, scount, blockIdx.x, h0, hc, &s, &h)) return;
+  double phi, nu;
+  candidate_theta(md, s, h, which & 3, iter, &phi, &nu);
+  CorrFn rho;
+  rho.init(phi, nu, MK_COV_MATERN);
+  cheb_build_store(rho, md.span ? phi * md.span[s] : INFINITY, md.chtab + ((long)s * md.q + h) * MK_CH_TAB);
+}
+// Load a stored table into LDS (returns the interval count; the caller synchronises).
+__device__ inline int cheb_load(const double* src, double* chtab) {
+  const int ni = (int)src[MK_CH_NI_MAX * MK_CH_LD];
+  for (int i = threadIdx.x; i < ni * MK_CH_LD; i += 256) chtab[i] = src[i];
+  return ni;
+}
+
 template <int MODEL>
 __global__ __launch_bounds__(256) void k_cov_candidate(Model md, MatSet ms, int h0, int hc, int which, int iter,
                                                        const int* slist, const int* scount) {
@@ -197,9 +230,16 @@ __global__ __launch_bounds__(256) void k_cov_candidate(Model md, MatSet ms, int 
     g.rho.fill_tables(btab, threadIdx.x, 256);
     __syncthreads();
     g.rho.tab = btab;
-    // table over [0.5, phi x the subset's extent] (every pair distance is within it)
-    const int ni = cheb_count(md.span ? g.rho.phi * md.span[s] : INFINITY);
-    cheb_build(g.rho, ni, chtab, buf, cosm, threadIdx.x, 256);
+    // table over [0.5, phi x the subset's extent] (every pair distance is within it): built by
+    // k_matern_table for the session's launches, here for the standalone parity entry point
+    int ni;
+    if (md.chtab) {
+      ni = cheb_load(md.chtab + (long)sh * MK_CH_TAB, chtab);
+      __syncthreads();
+    } else {
+      ni = cheb_count(md.span ? g.rho.phi * md.span[s] : INFINITY);
+      cheb_build(g.rho, ni, chtab, buf, cosm, threadIdx.x, 256);
+    }
     matern_tile(g, chtab, ni, M, ld, ti, tj, buf, idx, cnt);
     return;
   }
@@ -951,6 +991,19 @@ __global__ __launch_bounds__(256) void k_pred_PT(Model md, const int* __restrict
 template __global__ void k_pred_PT<MK_COV_EXPONENTIAL>(Model, const int*, const int*);
 template __global__ void k_pred_PT<MK_COV_MATERN>(Model, const int*, const int*);
 
+// Kriging tables: the current (phi, nu) of every listed pair over [0.5, phi x span_pt].
+__global__ __launch_bounds__(256) void k_matern_table_list(Model md, const int* __restrict__ list,
+                                                           const int* __restrict__ count) {
+  if ((int)blockIdx.x >= *count) return;
+  const int sh = list[blockIdx.x];
+  const int s = sh / md.q, h = sh % md.q;
+  double phi, nu;
+  current_phi_nu(md, s, h, &phi, &nu);
+  CorrFn rho;
+  rho.init(phi, nu, MK_COV_MATERN);
+  cheb_build_store(rho, md.span_pt ? phi * md.span_pt[s] : INFINITY, md.chtab_p + (long)sh * MK_CH_TAB);
+}
+
 // Matern P^T: one workgroup per (pair, MK_PT_RB observation rows) builds the Chebyshev table of
 // its pair's current (phi, nu) over [0.5, phi x the extent of subset + test sites] and
 // interpolates; elements outside the table are compacted per 4,096-site chunk and evaluated
@@ -986,8 +1039,14 @@ __global__ __launch_bounds__(256) void k_pred_PT_matern(Model md, const int* __r
   rho.fill_tables(btab, tid, 256);
   __syncthreads();
   rho.tab = btab;
-  const int ni = cheb_count(md.span_pt ? phi * md.span_pt[s] : INFINITY);
-  cheb_build(rho, ni, chtab, vals, cosm, tid, 256);
+  int ni;
+  if (md.chtab_p) {   // k_matern_table_list
+    ni = cheb_load(md.chtab_p + (long)sh * MK_CH_TAB, chtab);
+    __syncthreads();
+  } else {
+    ni = cheb_count(md.span_pt ? phi * md.span_pt[s] : INFINITY);
+    cheb_build(rho, ni, chtab, vals, cosm, tid, 256);
+  }
   const double* cx = md.coords + (long)s * 2 * md.n_pad;
   const double* tx = md.coords_test;
   const double* ty = md.coords_test + md.n_test_pad;

@@ -47,6 +47,8 @@ struct Model {
   const double* coords_test;   // [2][n_test_pad]
   const double* span;          // [S] bounding-box diagonal of the subset's sites (Matern tables)
   const double* span_pt;       // [S] bound on the subset-to-test-site distances (Matern kriging tables)
+  double* chtab;               // [S*q][MK_CH_TAB] Matern: Chebyshev tables of the pairs' candidates (k_matern_table)
+  double* chtab_p;             // [S*q][MK_CH_TAB] Matern: tables of the current (phi, nu), kriging (k_matern_table_list)
   // state
   double* beta;      // [S][p]
   double* theta;     // [S][n_theta]: A lower-tri (log diag) | logit phi | logit nu

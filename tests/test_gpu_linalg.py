@@ -28,6 +28,35 @@ def test_correlation_matches_oracle(mk, model, nu):
         assert np.max(np.abs(R[s] - ref)) <= REL * np.max(np.abs(ref))
 
 
+@pytest.mark.parametrize("nu", [0.05, 0.7, 3.4])
+def test_candidate_matern_table_ranges_vs_scipy(mk, nu):
+    """The Matern candidate kernel's Chebyshev tables (mk_corr.hpp cheb_*) at their edges: a tight
+    cluster (x = phi d < 0.5: exact series), a duplicated site (d = 0 off the diagonal: rho = 1),
+    sites spread over [0, 8]^2 so x runs past the last table interval (48.9: exact continued
+    fraction) and every interval in between; element by element vs scipy.special.kv, 1e-10
+    relative."""
+    import scipy.special as ssp
+    rng = np.random.default_rng(5)
+    n = 600
+    phi = np.array([6.5, 10.0])
+    c = np.empty((len(phi), n, 2))
+    for s in range(len(phi)):
+        c[s] = np.concatenate([rng.uniform(0, 0.02, size=(200, 2)), rng.uniform(0, 8.0, size=(n - 200, 2))])
+        c[s, 1] = c[s, 0]                                 # duplicated site
+    R = mk.correlation_batched(c, phi, nu=np.full(len(phi), nu), cov_model="matern")
+    for s in range(len(phi)):
+        x = phi[s] * om.distance_matrix(c[s], c[s])
+        assert x.max() > 60.0 and (x[x > 0] < 0.5).sum() > 1000
+        ref = np.ones_like(x)
+        m = x > 0
+        ref[m] = np.power(x[m], nu) / (2.0 ** (nu - 1.0) * ssp.gamma(nu)) * ssp.kv(nu, x[m])
+        np.fill_diagonal(ref, 1.0)
+        ok = ref > 1e-280
+        err = np.abs(R[s] - ref)[ok] / ref[ok]
+        assert np.max(err) <= REL, (s, np.max(err))
+        assert R[s][1, 0] == 1.0
+
+
 @pytest.mark.parametrize("nu", [0.21, 0.5, 1.3, 1.9])
 def test_candidate_matern_cfg2_geometry_vs_scipy(mk, nu):
     """configs[1] geometry (n_s = 1000, 8 tiles of 128): the sampler's binned Matern candidate
