@@ -195,6 +195,31 @@ def test_lookahead_is_rejected_where_ineligible(mk):
                 ses.set_lookahead(0)
 
 
+@pytest.mark.parametrize("shift", [(2.5, -1.0), (0.0, 0.0)])
+def test_matern_kriging_test_sites_outside_the_subsets(mk, shift):
+    """Matern kriging tables (k_matern_table_list / k_pred_PT_matern) span phi x the largest
+    subset-to-test-site distance (host bounding boxes): test sites moved outside the subsets'
+    extent still replay the oracle's kriging draws (sites beyond the table take the exact path)."""
+    sizes = [300, 170]
+    d = mk.synthetic.generate(sum(sizes), q=1, n_test=40, seed=31, cov_model=1)
+    ct = d["coords_test"] + np.asarray(shift)[None, :]
+    kw = dict(n_batch=2, batch_length=3, burn_in=4, seed=13)
+    cfg = mk.SamplerConfig(1, 2, beta_starting=np.zeros(2), beta_tuning=np.full(2, 0.05), cov_model="matern", **kw)
+    ocfg = om.Config(1, 2, beta_starting=np.zeros(2), beta_tuning=np.full(2, 0.05), cov_model=1, **kw)
+    subs, off = [], 0
+    for m in sizes:
+        subs.append(dict(coords=d["coords"][off:off + m], y=d["y"][off:off + m], weights=np.ones(m),
+                         x=d["x"][off:off + m]))
+        off += m
+    with mk.Session(subs, cfg, coords_test=ct) as ses:
+        ses.run(cfg.n_samples)
+        dev = ses.outputs(samples=True, w_pred_samples=True)
+    for s, sb in enumerate(subs):
+        ref = om.fit_subset(sb["coords"], sb["y"], sb["weights"], sb["x"], ocfg, subset=s, coords_test=ct)
+        np.testing.assert_allclose(dev["samples"][s], ref["samples"], rtol=0, atol=TOL)
+        np.testing.assert_allclose(dev["w_pred_samples"][s].T, ref["w_pred"], rtol=0, atol=TOL)
+
+
 def test_quantiles_bit_exact_on_device_samples(mk):
     dev, _ = _run_both(mk, 130, 1, 0, n_batch=4, batch_length=5, burn_in=3)
     for s in range(len(dev["samples"])):
