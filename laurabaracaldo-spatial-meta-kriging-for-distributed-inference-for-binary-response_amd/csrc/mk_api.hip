@@ -620,10 +620,16 @@ static void launch_pred_refresh(mk_session* s, Group& g, hipStream_t st = nullpt
 // launches run alone (roofline timing 0.71 of peak vs 0.52-0.57 beside the main stream's kernels).
 static bool la_auto(const mk_session* s) { return (long)s->S * s->q <= 224; }
 
-// Under the lookahead schedule the one-workgroup kernel is the default: the cooperative kernel's
-// gain (one W pass, 0.6 vs 1.2 ms at 32 subsets alone) is lost beside the concurrent factorisation
-// (measured 6,399 vs 6,546 subset-iters/s at 32 subsets), and it keeps no inter-workgroup waits.
-static bool use_sweep_mg(const mk_session* s) { return s->sweep_mg && (!s->la || s->sweep_mg_forced); }
+// Under the lookahead schedule the one-workgroup kernel is the default for q = 1: the cooperative
+// kernel's gain (one W pass, 0.6 vs 1.2 ms at 32 subsets alone) is lost beside the concurrent
+// factorisation (6,635 vs 6,892 subset-iters/s at 32 subsets; configs[1] 14,832 vs 15,074).  With
+// q >= 2 outcomes on a few subsets -- configs[3]'s per-GPU share on 8 GPUs -- the one-workgroup
+// sweep (q W panels per block, q x 64 MH steps) is the iteration's longest chain and the
+// cooperative kernel wins: q = 3, 7 subsets 1,050 -> 1,601, 13 subsets 1,553 -> 1,956 subset-iters/s
+// (25 subsets: equal).
+static bool use_sweep_mg(const mk_session* s) {
+  return s->sweep_mg && (!s->la || s->sweep_mg_forced || (s->q > 1 && s->S <= 16));
+}
 
 static void launch_sweep(mk_session* s, Group& g, int it) {
   const int q = s->q;
