@@ -273,6 +273,30 @@ def test_tiled_kriging_is_bit_identical_to_fused(mk, n, q, cov, tile):
     assert np.array_equal(fused["w_predict_sum"], seq)
 
 
+@pytest.mark.parametrize("cov", [0, 1])
+def test_tiled_kriging_at_the_cfg5_tile_size(mk, cov):
+    """configs[4]'s tile geometry: 70,000 test sites over tiles of 65,536 (run_metakriging.py's
+    predict_tile; a full tile and a short ragged one) give the fused path's draws and quantile
+    grids exactly (draws keyed by the global site index; Matern: the kriging tables per tile)."""
+    n, n_test = 300, 70_000
+    d = mk.synthetic.generate(2 * n, q=1, n_test=n_test, seed=77 + cov, cov_model=cov)
+    subs = [dict(coords=d["coords"][s * n:(s + 1) * n], y=d["y"][s * n:(s + 1) * n], weights=np.ones(n),
+                 x=d["x"][s * n:(s + 1) * n]) for s in range(2)]
+    outs = []
+    for pt in (0, 65536):
+        cfg = mk.SamplerConfig(1, 2, beta_starting=np.zeros(2), beta_tuning=np.full(2, 0.05),
+                               cov_model="matern" if cov else "exponential", n_batch=2, batch_length=3, burn_in=5,
+                               seed=3, predict_tile=pt)
+        with mk.Session(subs, cfg, coords_test=d["coords_test"]) as ses:
+            ses.run(cfg.n_samples)
+            outs.append(ses.outputs(w_pred_samples=True, w_predict_sum=True))
+    fused, tiled = outs
+    for s in range(2):
+        assert np.array_equal(tiled["w_pred_samples"][s], fused["w_pred_samples"][s])
+        assert np.array_equal(tiled["w_predict"][s], fused["w_predict"][s])
+    assert np.array_equal(tiled["w_predict_sum"], fused["w_predict_sum"])
+
+
 @pytest.mark.parametrize("q,cov", [(1, 0), (2, 0), (1, 1)])
 def test_sppredict_reuses_the_fit_without_refitting(mk, q, cov):
     """spMvGLM keeps every chain state on the device; spPredict(start, end, thin) only krigs
