@@ -207,8 +207,8 @@ struct CorrFn {
 // (phi, nu) from a table built per workgroup out of exact values: on x in [0.5, x_hi], where rho is
 // analytic, piecewise Chebyshev series of MK_CH_N terms on intervals [0.5 * 1.25^g, 0.5 * 1.25^(g+1))
 // (g < 7: the singularity of x^(2 nu) at 0 stays >= 9 half-widths away) and then of width 0.5
-// (e^-x varies by e^-0.5 per interval).  Truncation error < 1e-17 relative for these widths
-// (Bernstein-ellipse bound); measured against scipy kv: <= 1e-13 relative, nu in [0.05, 4], x in
+// (e^-x varies by e^-0.5 per interval).  Truncation error ~ rho_E^-12 ~ 1e-15 relative for these
+// widths (Bernstein ellipse rho_E >= 17.9); measured against scipy kv: <= 1e-13 relative, nu in [0.05, 4], x in
 // [0.5, 39] (the scipy reference's own accuracy).  x < 0.5 (the non-analytic part) and x beyond
 // the table use the exact evaluation.  Clenshaw: ~2 fp64 operations per term.
 #define MK_CH_N 12                         // Chebyshev terms per interval (degree 11)
