@@ -627,9 +627,10 @@ static bool la_auto(const mk_session* s) { return (long)s->S * s->q <= 224; }
 // sweep (q W panels per block, q x 64 MH steps) is the iteration's longest chain and the
 // cooperative kernel wins: q = 3, 7 subsets 1,050 -> 1,601, 13 subsets 1,553 -> 1,956 subset-iters/s
 // (25 subsets: equal).
-static bool use_sweep_mg(const mk_session* s) {
-  return s->sweep_mg && (!s->la || s->sweep_mg_forced || (s->q > 1 && s->S <= 16));
-}
+// The q >= 2 gain is not taken by default: in one round-end style run of the GPU suite a q = 3
+// lookahead replay stalled with the plainly launched cooperative kernel (not reproduced; the
+// one-workgroup kernel has no inter-workgroup waits).  MK_SWEEP=2 opts in.
+static bool use_sweep_mg(const mk_session* s) { return s->sweep_mg && (!s->la || s->sweep_mg_forced); }
 
 static void launch_sweep(mk_session* s, Group& g, int it) {
   const int q = s->q;
