@@ -180,6 +180,7 @@ def main():
                            n_streams=a.streams)
     subs = [mk.subset_data(d["y"], d["x"], 1.0, d["coords"], 1, idx[i]) for i in range(lo, hi)]
     ses = mk.Session(subs, cfg, coords_test=d["coords_test"], subset_base=base, device=local if world > 1 else 0)
+    la = ses.lookahead
     ses.run(W)                                    # warmup
     # timed window: HIP events bracket only the roofline kernel (k_chol_update) on its stream
     upd_kinds = [mk.session.KS_CHOL_UPDATE, mk.session.KS_CHOL_UPDATE_SUB]   # k_chol_update<128> + <64>/<32>
@@ -257,7 +258,12 @@ def main():
                      # PMC bytes per launch, profiled on the default workload (N=1, n=500k, K=250) only
                      "traffic": _pmc_traffic() if (world == 1 and K == 250 and n == 500_000) else None,
                      "avg_launch_ms": avg_ms, "launches": st["launches"],
-                     "algorithmic_flops_per_launch": st["flops"] / max(1, st["launches"])},
+                     "algorithmic_flops_per_launch": st["flops"] / max(1, st["launches"]),
+                     "schedule": "lookahead" if la else "sequential",
+                     "timing_note": ("update launches run beside the candidates' and main streams' other kernels "
+                                     "(lookahead schedule, DESIGN.md 4.2): their union interval includes time "
+                                     "shared with those kernels, so frac understates the kernel's own rate"
+                                     if la else "update launches run alone on the stream (sequential schedule)")},
         "kernels_ms_per_step": {k: v["ms"] / n_post for k, v in kern.items()},
         "kernels_ms_per_step_note": f"untimed post-window pass of {n_post} iterations, every kernel kind evented",
         "end_to_end_estimate_s": elapsed / a.steps * 5000,
