@@ -126,24 +126,33 @@ def test_sub_tile_gemm_split_cholesky_and_multi_wg_sweep_are_bit_identical(tmp_p
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     res = {}
-    # gi: the kriging GEMM raster (MK_PRED_GI row panels per group; placement only)
-    for tile, sweep, split, gen, fine, depth, gi in (("128", "1", "0", "0", "0", "2", "1"),
-                                                     ("64", "2", "1", "0", "0", "1", "4"),
-                                                     ("64", "1", "0", "0", "0", "2", "3"),
-                                                     ("32", "1", "1", "0", "1", "2", "4"),
-                                                     ("128", "2", "1", "0", "0", "3", "4"),
-                                                     ("128", "1", "0", "1", "0", "2", "2"),
-                                                     ("64", "1", "1", "0", "1", "1", "4")):
-        path = str(tmp_path / f"tile{tile}_sweep{sweep}_split{split}_gen{gen}_fine{fine}_d{depth}_gi{gi}.npz")
+    # gi: the kriging GEMM raster (MK_PRED_GI row panels per group; placement only).  la: the launch
+    # schedule -- the multi-workgroup sweep (sweep "2") runs on its default path, the sequential
+    # schedule (under lookahead it is opt-in only); the two schedules agree to
+    # rounding, not bit for bit, so each configuration is compared with the reference of its schedule.
+    configs = (("128", "1", "0", "0", "0", "2", "1", "1"),
+               ("64", "2", "1", "0", "0", "1", "4", "0"),
+               ("64", "1", "0", "0", "0", "2", "3", "1"),
+               ("32", "1", "1", "0", "1", "2", "4", "1"),
+               ("128", "2", "1", "0", "0", "3", "4", "0"),
+               ("128", "1", "0", "1", "0", "2", "2", "1"),
+               ("64", "1", "1", "0", "1", "1", "4", "1"),
+               ("128", "1", "0", "0", "0", "2", "1", "0"))
+    for cfg in configs:
+        tile, sweep, split, gen, fine, depth, gi, la = cfg
+        path = str(tmp_path / ("run_" + "_".join(cfg) + ".npz"))
         r = subprocess.run([sys.executable, os.path.join(here, "gpu_tile_run.py"), path], capture_output=True,
                            text=True, timeout=240,
                            env=dict(os.environ, MK_TILE=tile, MK_SWEEP=sweep, MK_CHOL_SPLIT=split, MK_PRED_GEN=gen,
-                                    MK_CHOL_FINE=fine, MK_CHOL_DEPTH=depth, MK_PRED_GI=gi))
+                                    MK_CHOL_FINE=fine, MK_CHOL_DEPTH=depth, MK_PRED_GI=gi,
+                                    **({} if la == "1" else {"MK_LOOKAHEAD": "0"})))
         assert r.returncode == 0, r.stderr[-4000:]
         z = np.load(path)
-        res[(tile, sweep, split, gen, fine, depth, gi)] = {k: z[k] for k in z.files}
-    ref = res[("128", "1", "0", "0", "0", "2", "1")]
-    for key, got in res.items():
+        res[cfg] = {k: z[k] for k in z.files}
+    refs = {"1": res[configs[0]], "0": res[configs[-1]]}
+    for cfg, got in res.items():
+        ref = refs[cfg[-1]]
         assert got.keys() == ref.keys()
         for k in ref:
-            assert np.array_equal(got[k], ref[k]), (key, k)
+            assert np.array_equal(got[k], ref[k]), (cfg, k)
+
