@@ -23,6 +23,7 @@ extern "C" {
 #define MK_E_HIP (-2)      /* HIP runtime failure */
 #define MK_E_NOMEM (-3)    /* device allocation failed */
 #define MK_E_NODEV (-4)    /* no HIP device */
+#define MK_E_INTERRUPT (-5) /* the progress callback asked to stop (R: a user interrupt) */
 
 #define MK_COV_EXPONENTIAL 0
 #define MK_COV_MATERN 1
@@ -143,6 +144,38 @@ int32_t mk_session_count(void);
 /* One-shot convenience: create, run n_batch*batch_length iterations, outputs, destroy. */
 int mk_fit_predict_batched(const mk_problem* prob, const mk_config* cfg, mk_outputs* out);
 
+/* ---- the whole node (replaces makeCluster + foreach %dopar% + the combine, MK.R:100-133) ----
+ * The K subsets of prob are cut into n_devices balanced contiguous blocks [floor(rK/G),
+ * floor((r+1)K/G)); block r runs as one session on devices[r], one host thread per block, with
+ * global subset indices (prob->subset_base + its first subset), so every chain equals the
+ * one-device chain.  The chains advance one amcmc batch at a time on every device; between
+ * batches the calling thread calls progress (if not NULL) -- spBayes's n.report output and R's
+ * interrupt check -- and stops the fit (MK_E_INTERRUPT, every device freed) when it returns
+ * nonzero.  cfg->device is ignored.
+ * The combine is device to device: every block's 200-level grids stay in HBM; an all-to-all hands
+ * device j all K subsets' grids for its block of columns (RCCL send/recv over xGMI when the devices
+ * are distinct; device copies when a device is listed more than once -- several shards on one GPU),
+ * device j combines them in global subset order -- MK.R:123-133's sequential mean, bit-identical
+ * to one device, or the Weiszfeld W2 median -- and its combined columns go to the host.  Tiled
+ * kriging (predict_tile) exchanges the grids of one test-site tile at a time, so the configs[4]
+ * combine of 1M sites needs K x 200 x q*tile doubles per device, not K x 200 x q*n_test.
+ * out (optional, any field NULL): the per-subset outputs of all K subsets as mk_session_outputs
+ * lays them out; out->w_predict_sum = the sequential sum of all K w.predict grids. */
+#define MK_COMBINE_MEAN 0     /* MK.R:123-133 */
+#define MK_COMBINE_MEDIAN 1   /* north-star extension: per column Weiszfeld geometric median in W2 */
+typedef struct mk_combined {
+  double* result;     /* 200 x P: the combined parameter grid (MK.R:127 result), or NULL            */
+  double* result2;    /* 200 x (q*n_test): the combined w.predict grid (MK.R:133 result2), or NULL  */
+  int32_t method;     /* MK_COMBINE_MEAN or MK_COMBINE_MEDIAN                                      */
+  int32_t max_iter;   /* MEDIAN: Weiszfeld iterations (<= 0: 100)                                   */
+  double tol;         /* MEDIAN: convergence tolerance (< 0: 1e-12)                                 */
+  int32_t exchange;   /* out: 1 = RCCL, 0 = device copies                                           */
+} mk_combined;
+/* Progress between batches: iterations done so far (a multiple of batch_length) of n_samples. */
+typedef int (*mk_progress_fn)(void* user, int32_t iterations, int32_t n_samples);
+int mk_meta_fit(const mk_problem* prob, const mk_config* cfg, const int32_t* devices, int32_t n_devices,
+                mk_progress_fn progress, void* user, mk_outputs* out, mk_combined* comb);
+
 /* ---- combine (MK.R:123-133): out = (grid_1 + ... + grid_K) / K, sequential order ---- */
 int mk_combine(const double* grids, int32_t K, int64_t grid_len, double* out, int32_t device);
 
@@ -222,6 +255,13 @@ int mk_correlation_batched(const double* coords, int32_t S, int32_t n, const dou
 /* Cholesky (lower) + log-determinant (+ optional inverse) of S SPD n x n matrices. */
 int mk_cholesky_batched(const double* A, int32_t S, int32_t n, double* L_out, double* logdet_out,
                         double* inv_out, int32_t device);
+
+/* Hardware queues the process's HIP runtime was started with (GPU_MAX_HW_QUEUES when HIP first
+ * initialised; HIP's default is 4).  The lookahead schedule adds a kriging stream and a CU-masked
+ * main stream only when there are >= 8 (streams beyond the queue count share queues and serialise,
+ * DESIGN.md 4.2).  A host that knows HIP started before its own setting took effect (e.g. torch
+ * first) passes the real count; n < 0 restores the default: GPU_MAX_HW_QUEUES from the environment. */
+int mk_set_hw_queues(int32_t n);
 
 const char* mk_last_error(void);
 int mk_device_count(void);

@@ -12,4 +12,5 @@ from .glm import glm_binomial  # noqa: F401
 from .post import combine_median  # noqa: F401
 from .metakriging import (combine_results, meta_fit, partition, partitioned_spMvGLM,  # noqa: F401
                           posterior_summary, start_values, subset_data)
+from .node import meta_fit_node  # noqa: F401
 from . import synthetic  # noqa: F401

@@ -6,8 +6,8 @@ import sys
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_PATH = os.path.join(PKG_DIR, "libmk.so")
-SOURCES = ["mk_linalg.hip", "mk_mcmc.hip", "mk_init.hip", "mk_post.hip", "mk_api.hip", "mk_rsample.cpp"]
-HEADERS = ["mk_common.hpp", "mk_types.hpp", "mk_gemm.hpp", "mk_corr.hpp", "mk_kernels.hpp"]
+SOURCES = ["mk_linalg.hip", "mk_mcmc.hip", "mk_init.hip", "mk_post.hip", "mk_api.hip", "mk_multi.hip", "mk_rsample.cpp"]
+HEADERS = ["mk_common.hpp", "mk_types.hpp", "mk_gemm.hpp", "mk_corr.hpp", "mk_kernels.hpp", "mk_internal.hpp"]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wno-unused-value",
          "-Wno-unused-result"]
 
@@ -40,7 +40,7 @@ def build(force=False, verbose=False):
         if verbose and out:
             sys.stderr.write(out.decode(errors="replace"))
     tmp = LIB_PATH + ".tmp"
-    cmd = [hipcc, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", tmp] + objs
+    cmd = [hipcc, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", tmp] + objs + ["-ldl"]
     subprocess.check_call(cmd)
     os.replace(tmp, LIB_PATH)
     for o in objs:

@@ -16,6 +16,9 @@ MK_E_ARG = -1
 MK_E_HIP = -2
 MK_E_NOMEM = -3
 MK_E_NODEV = -4
+MK_E_INTERRUPT = -5
+MK_COMBINE_MEAN = 0
+MK_COMBINE_MEDIAN = 1
 MK_COV_EXPONENTIAL = 0
 MK_COV_MATERN = 1
 MK_LINK_LOGIT = 0
@@ -62,7 +65,17 @@ class Summary(ctypes.Structure):
                 ("param_quant", _dp), ("p_quant", _dp), ("index", _ip)]
 
 
+class Combined(ctypes.Structure):
+    _fields_ = [("result", _dp), ("result2", _dp), ("method", ctypes.c_int32), ("max_iter", ctypes.c_int32),
+                ("tol", ctypes.c_double), ("exchange", ctypes.c_int32)]
+
+
+# int (*mk_progress_fn)(void* user, int32_t iterations, int32_t n_samples)
+PROGRESS_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32)
+
 EXPORTS = {
+    "mk_meta_fit": (ctypes.c_int, [ctypes.POINTER(Problem), ctypes.POINTER(Config), _ip, ctypes.c_int32,
+                                   PROGRESS_FN, ctypes.c_void_p, ctypes.POINTER(Outputs), ctypes.POINTER(Combined)]),
     "mk_session_create": (ctypes.c_int, [ctypes.POINTER(Problem), ctypes.POINTER(Config), ctypes.POINTER(ctypes.c_void_p)]),
     "mk_session_run": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32]),
     "mk_session_iteration": (ctypes.c_int32, [ctypes.c_void_p]),
@@ -102,25 +115,44 @@ EXPORTS = {
     "mk_partition_r": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _ip, _ip]),
     "mk_r_sample": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _ip]),
     "mk_r_sample_replace": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _ip]),
+    "mk_set_hw_queues": (ctypes.c_int, [ctypes.c_int32]),
     "mk_last_error": (ctypes.c_char_p, []),
     "mk_device_count": (ctypes.c_int, []),
     "mk_device_memory": (ctypes.c_int, [ctypes.c_int32, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
 }
 
 _LIB = None
+HW_QUEUES = None     # hardware queues of this process's HIP runtime, as passed to mk_set_hw_queues
+
+
+def _hip_started():
+    """True when this process's HIP runtime is already initialised (torch first): a
+    GPU_MAX_HW_QUEUES set now would no longer be read."""
+    import sys
+    torch = sys.modules.get("torch")
+    try:
+        return bool(torch is not None and torch.cuda.is_initialized())
+    except Exception:
+        return False
 
 
 def load():
     """Load libmk.so (raises MkError if it is absent -- no CPU fallback exists)."""
-    global _LIB
+    global _LIB, HW_QUEUES
     if _LIB is not None:
         return _LIB
     path = os.environ.get("MK_LIB") or LIB_PATH      # MK_LIB: a development build (tools/ probes)
-    # the lookahead schedule runs up to five HIP streams: give the process at least 8 hardware
-    # queues (read when HIP starts; a process that started HIP earlier keeps its count, and libmk
-    # then runs three streams)
-    if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
-        os.environ["GPU_MAX_HW_QUEUES"] = "8"
+    # the lookahead schedule runs up to five HIP streams: give the process 8 hardware queues when
+    # HIP has not started yet (the variable is read once, when HIP initialises).  If it has started
+    # (torch first), keep the count it started with and tell libmk, which then runs three streams
+    # instead of five on too few queues (DESIGN.md 4.2).
+    before = int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0)
+    if _hip_started():
+        HW_QUEUES = before if before > 0 else 4
+    else:
+        if before < 8:
+            os.environ["GPU_MAX_HW_QUEUES"] = "8"
+        HW_QUEUES = max(before, 8)
     if not os.path.exists(path):
         raise MkError(MK_E_ARG, f"{path} not built; run __graft_entry__.build()")
     lib = ctypes.CDLL(path)
@@ -128,6 +160,7 @@ def load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    lib.mk_set_hw_queues(HW_QUEUES)
     _LIB = lib
     return lib
 

@@ -22,6 +22,7 @@
 #include "../../include/mk.h"
 #include "mk_kernels.hpp"
 #include "mk_gemm.hpp"
+#include "mk_internal.hpp"
 
 using namespace mk;
 
@@ -164,6 +165,19 @@ MatSet matset_view(const MatSet& m, int s0) {
 }  // namespace
 
 static std::atomic<int> g_live_sessions{0};
+// Hardware queues of this process's HIP runtime (mk_set_hw_queues; -1: GPU_MAX_HW_QUEUES as set in
+// the environment, HIP's default 4 when unset).
+static std::atomic<int> g_hw_queues{-1};
+static int hw_queues() {
+  const int n = g_hw_queues.load();
+  if (n >= 0) return n;
+  const char* v = std::getenv("GPU_MAX_HW_QUEUES");
+  return (v && *v) ? std::atoi(v) : 4;
+}
+extern "C" int mk_set_hw_queues(int32_t n) {
+  g_hw_queues.store(n < 0 ? -1 : n);
+  return 0;
+}
 
 struct mk_session {
   mk_session() { g_live_sessions.fetch_add(1); }
@@ -190,6 +204,12 @@ struct mk_session {
   bool sweep_mg = false;          // buffers allocated and chosen for the sequential schedule
   bool sweep_mg_forced = false;   // MK_SWEEP=2: also under the lookahead schedule
   size_t sweep_mg_lds = 0;
+  // split-launch sweep (k_sweep_tiles / k_sweep_block, no inter-workgroup waits): partial dots
+  // [S][nt][q][64], the block's coefficients [S][q][64] and any-moved flags [S]
+  bool sweep_split = false;
+  double* sp_part = nullptr;
+  double* sp_dacc = nullptr;
+  int* sp_any = nullptr;
   hipEvent_t swept = nullptr;     // fork-join sweep (several groups): the whole-shard sweep is queued
   double* sw_part = nullptr;
   int* sw_cnt = nullptr;
@@ -209,6 +229,7 @@ struct mk_session {
                                   // hardware queue, GPU_MAX_HW_QUEUES = 4, and slows the split Cholesky)
   hipStream_t la_k = nullptr;     // kept iterations' kriging refresh beside the sweep (MK_LA_KRIG)
   std::vector<hipEvent_t> la_ev;  // [nt] panel k final | decided (or adapted) | join | W ready | kriged
+  hipError_t launch_err = hipSuccess;   // first failed hipLaunchKernel / cooperative launch of a run
   std::vector<int> n_part;
   std::vector<void*> allocs;
   bool prof = false;
@@ -239,23 +260,30 @@ struct mk_session {
     *p_ = (T*)ptr;
     return 0;
   }
+  // Teardown order: drain every stream first (no queued work may still reference an event or a
+  // buffer), then destroy the events the streams recorded, then the streams (CU-masked and
+  // priority queues included), then free the memory.
   ~mk_session() {
     g_live_sessions.fetch_sub(1);
     if (device >= 0) hipSetDevice(device);
+    std::vector<hipStream_t> streams;
+    for (auto& g : groups) {
+      if (g.stream && g.stream != stream) streams.push_back(g.stream);
+      if (g.bulk) streams.push_back(g.bulk);
+    }
+    for (hipStream_t st : {la_c, la_m, la_k, stream})
+      if (st) streams.push_back(st);
+    for (hipStream_t st : streams) hipStreamSynchronize(st);
     for (auto& t : pending) { hipEventDestroy(t.a); hipEventDestroy(t.b); }
     for (auto& g : groups) {
-      if (g.stream && g.stream != stream) hipStreamDestroy(g.stream);
       if (g.done) hipEventDestroy(g.done);
-      if (g.bulk) hipStreamDestroy(g.bulk);
       for (hipEvent_t e : g.ev) hipEventDestroy(e);
     }
     if (swept) hipEventDestroy(swept);
     for (hipEvent_t e : la_ev) hipEventDestroy(e);
-    if (la_c) hipStreamDestroy(la_c);
-    if (la_m) hipStreamDestroy(la_m);
-    if (la_k) hipStreamDestroy(la_k);
+    for (hipStream_t st : streams) hipStreamDestroy(st);
     for (void* p_ : allocs) hipFree(p_);
-    if (stream) hipStreamDestroy(stream);
+    (void)hipGetLastError();   // teardown errors are not the next call's
   }
 };
 
@@ -335,6 +363,21 @@ static bool set_gemm_lds() {
     if (hipFuncSetAttribute(f.first, hipFuncAttributeMaxDynamicSharedMemorySize, (int)f.second) != hipSuccess)
       return false;
   return true;
+}
+
+// Type-7 quantiles of n_rows kept values per (subset, column) (k_quantiles): the bitonic sort takes
+// the next power of two >= n_rows doubles of dynamic LDS (n_rows <= MK_QUANT_MAX).
+static int launch_quantiles(unsigned grid, hipStream_t st, const double* data, long subset_stride, long row_stride,
+                            int n_rows, int n_cols, const double* probs, int n_probs, double* out) {
+  HIPCHK(hipFuncSetAttribute((const void*)k_quantiles, hipFuncAttributeMaxDynamicSharedMemorySize, MK_QUANT_MAX * 8));
+  if (n_rows < 1 || n_rows > MK_QUANT_MAX)
+    return set_err(MK_E_ARG, "quantile summaries take 1 .. " + std::to_string(MK_QUANT_MAX) + " kept samples");
+  size_t n2 = 1;
+  while (n2 < (size_t)n_rows) n2 <<= 1;
+  hipLaunchKernelGGL(k_quantiles, dim3(grid), dim3(256), n2 * 8, st, data, subset_stride, row_stride, n_rows, n_cols,
+                     probs, n_probs, out);
+  HIPCHK(hipGetLastError());
+  return 0;
 }
 
 // Tile shape of a GEMM launch: 64-sub-tiles (bit-identical, mk_gemm.hpp) when the 128-tile grid
@@ -634,6 +677,31 @@ static bool use_sweep_mg(const mk_session* s) { return s->sweep_mg && (!s->la ||
 
 static void launch_sweep(mk_session* s, Group& g, int it) {
   const int q = s->q;
+  if (s->sweep_split) {   // two launches per 64-site block, ordered by the stream (no waits on the device)
+    int nmax = 1;
+    for (int i = g.s0; i < g.s0 + g.S; ++i) nmax = std::max(nmax, s->n_part[i]);
+    const int nblk = (nmax + 63) / 64, nt = s->nt;
+    Model md = g.md;
+    MatSet ms = g.ms;
+    int iter = it;
+    double* part = s->sp_part + (long)g.s0 * nt * q * 64;
+    double* dacc = s->sp_dacc + (long)g.s0 * q * 64;
+    int* any = s->sp_any + g.s0;
+    const size_t lds = (size_t)q * (64 * 64 + 2 * 64) * sizeof(double);
+    for (int B = 0; B <= nblk; ++B) {
+      void* ta[] = {&md, &ms, &iter, &B, &part, &dacc, &any};
+      hipError_t e = hipLaunchKernel(sweep_split_kernel(q, false), dim3(g.S * nt), dim3(256), ta, 0, g.stream);
+      if (e == hipSuccess && B < nblk) {
+        void* ba[] = {&md, &ms, &B, &part, &dacc, &any};
+        e = hipLaunchKernel(sweep_split_kernel(q, true), dim3(g.S), dim3(256), ba, lds, g.stream);
+      }
+      if (e != hipSuccess) {
+        if (s->launch_err == hipSuccess) s->launch_err = e;
+        return;
+      }
+    }
+    return;
+  }
   if (use_sweep_mg(s)) {
     hipMemsetAsync(s->sw_cnt, 0, (size_t)g.S * (s->n_pad / 64) * sizeof(int), g.stream);
     Model md = g.md;
@@ -650,12 +718,14 @@ static void launch_sweep(mk_session* s, Group& g, int it) {
     // stream's kernels never wait on the sweep and drain -- and each wait has a time-out
     // (MK_SWEEP_COOP=1 keeps the cooperative launch)
     static const int coop_env = tile_env("MK_SWEEP_COOP", 0);
+    hipError_t e;
     if (s->la && !coop_env)
-      hipLaunchKernel(sweep_kernel(q, true), dim3(xcd_grid(g.S, s->nt)), dim3(256), args, (unsigned)s->sweep_mg_lds,
-                      g.stream);
+      e = hipLaunchKernel(sweep_kernel(q, true), dim3(xcd_grid(g.S, s->nt)), dim3(256), args, (unsigned)s->sweep_mg_lds,
+                          g.stream);
     else
-      hipLaunchCooperativeKernel(sweep_kernel(q, true), dim3(xcd_grid(g.S, s->nt)), dim3(256), args,
-                                 (unsigned)s->sweep_mg_lds, g.stream);
+      e = hipLaunchCooperativeKernel(sweep_kernel(q, true), dim3(xcd_grid(g.S, s->nt)), dim3(256), args,
+                                     (unsigned)s->sweep_mg_lds, g.stream);
+    if (e != hipSuccess && s->launch_err == hipSuccess) s->launch_err = e;
     return;
   }
   const size_t sw_lds = (size_t)q * (64 * 64 + 2 * 64) * sizeof(double);
@@ -663,7 +733,8 @@ static void launch_sweep(mk_session* s, Group& g, int it) {
   MatSet ms = g.ms;
   int iter = it;
   void* args[] = {&md, &ms, &iter};
-  hipLaunchKernel(sweep_kernel(q, false), dim3(g.S), dim3(MK_SW_T), args, sw_lds, g.stream);
+  const hipError_t e = hipLaunchKernel(sweep_kernel(q, false), dim3(g.S), dim3(MK_SW_T), args, sw_lds, g.stream);
+  if (e != hipSuccess && s->launch_err == hipSuccess) s->launch_err = e;
 }
 
 // One MCMC iteration of a group, in two halves around the latent sweep (run_iterations).
@@ -840,7 +911,8 @@ static int check_cfg(const mk_problem* pr, const mk_config* c) {
   if (c->n_batch < 1 || c->batch_length < 1) return set_err(MK_E_ARG, "n.batch and batch.length must be >= 1");
   const int n_samples = c->n_batch * c->batch_length;
   if (c->burn_in < 1 || c->burn_in > n_samples) return set_err(MK_E_ARG, "burn_in must be in [1, n.samples]");
-  if (n_samples - c->burn_in + 1 > 2048) return set_err(MK_E_ARG, "at most 2048 kept samples supported");
+  if (n_samples - c->burn_in + 1 > MK_QUANT_MAX)
+    return set_err(MK_E_ARG, "at most " + std::to_string(MK_QUANT_MAX) + " kept samples supported");
   if (c->n_streams < 0 || c->n_streams > 8) return set_err(MK_E_ARG, "n_streams must be in [0, 8]");
   if (c->predict_tile < 0) return set_err(MK_E_ARG, "predict_tile must be >= 0");
   if (c->link != MK_LINK_LOGIT && c->link != MK_LINK_PROBIT) return set_err(MK_E_ARG, "link must be logit or probit");
@@ -1275,8 +1347,20 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
     const long grid = xcd_grid(S, nt);
     const int mode = tile_env("MK_SWEEP", 0);
     const bool fits = coop && grid <= (long)per_cu * n_cu && nt <= 32;
-    s->sweep_mg = fits && (mode == 2 || (mode == 0 && (long)S * 4 <= n_cu));
-    s->sweep_mg_forced = fits && mode == 2;
+    // MK_SWEEP: 1 one workgroup per subset, 2 cooperative multi-workgroup, 3 split launches;
+    // 0 (default): split launches for multi-outcome small shards (q >= 2, <= 16 subsets: the
+    // one-workgroup sweep's q x 64 MH steps and q W panels per block on one CU per subset are
+    // the iteration's longest chain), else the cooperative kernel on small sequential shards
+    s->sweep_split = mode == 3 || (mode == 0 && q >= 2 && S <= 16);
+    s->sweep_mg = !s->sweep_split && fits && (mode == 2 || (mode == 0 && (long)S * 4 <= n_cu));
+    s->sweep_mg_forced = s->sweep_mg && mode == 2;
+    if (s->sweep_split) {
+      HIPCHK(hipFuncSetAttribute(sweep_split_kernel(q, true), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 q * (64 * 64 + 2 * 64) * 8));
+      if ((rc = s->alloc(&s->sp_part, (size_t)S * nt * q * 64)) || (rc = s->alloc(&s->sp_dacc, (size_t)S * q * 64)) ||
+          (rc = s->alloc(&s->sp_any, (size_t)S)))
+        return rc;
+    }
     if (s->sweep_mg) {
       if ((rc = s->alloc(&s->sw_part, (size_t)S * 2 * nt * q * 64)) || (rc = s->alloc(&s->sw_cnt, (size_t)S * (n_pad / 64))) ||
           (rc = s->alloc(&s->sw_xcc, (size_t)S * nt)) || (rc = s->alloc(&s->sw_err, 1)))
@@ -1329,8 +1413,7 @@ extern "C" int mk_session_run(mk_session* s, int32_t n_iter) {
     //    (default 32: 4 per XCD, the split Cholesky's reserve) to the candidates' critical chain --
     //    its diagonal-tile workgroups take a whole CU's LDS and otherwise wait behind the inverse
     //    and kriging GEMMs (32 / 63 / 125 subsets: 6,669 -> 6,921, 7,550 -> 7,645, 8,062 -> 8,211).
-    const char* hwq = std::getenv("GPU_MAX_HW_QUEUES");
-    const bool queues = hwq && std::atoi(hwq) >= 8;
+    const bool queues = hw_queues() >= 8;
     static const int krig_env = tile_env("MK_LA_KRIG", -1);
     if ((krig_env == 1 || (krig_env < 0 && queues)) && s->md.n_test > 0 && !s->tiled &&
         hipStreamCreateWithFlags(&s->la_k, hipStreamNonBlocking) != hipSuccess)
@@ -1352,13 +1435,23 @@ extern "C" int mk_session_run(mk_session* s, int32_t n_iter) {
     s->groups[0].stream = s->la_m;
   }
   const auto t0 = std::chrono::steady_clock::now();
+  s->launch_err = hipSuccess;
+  hipError_t le = hipSuccess;
   for (int i = 0; i < n_iter; ++i) {
     run_iteration(s, s->iter);
     s->iter++;
-    if (hipGetLastError() != hipSuccess) break;
+    le = hipGetLastError();
+    if (le == hipSuccess) le = s->launch_err;
+    if (le != hipSuccess) break;
   }
   if (swap_m) s->groups[0].stream = s->stream;
-  HIPCHK(hipGetLastError());
+  // every stream is drained before an error returns: nothing of this run is left queued
+  if (le != hipSuccess) {
+    for (hipStream_t st : {s->la_m, s->la_c, s->la_k}) if (st) (void)hipStreamSynchronize(st);
+    for (auto& g : s->groups) (void)hipStreamSynchronize(g.stream);
+    return set_err(MK_E_HIP, std::string("kernel launch in iteration ") + std::to_string(s->iter - 1) + ": " +
+                                 hipGetErrorString(le));
+  }
   if (swap_m) HIPCHK(hipStreamSynchronize(s->la_m));
   for (auto& g : s->groups) HIPCHK(hipStreamSynchronize(g.stream));
   if (s->la_c) HIPCHK(hipStreamSynchronize(s->la_c));   // the next iteration's candidates
@@ -1436,55 +1529,78 @@ struct DevBufs {
 // fit (rows < n_s of a factor do not depend on its border row), so the draws, the quantiles and
 // their sum are bit-identical to the fused path.  Per tile the device holds q*T x kept draws
 // per subset instead of q*n_test x kept.
-static int predict_tiled(mk_session* s, mk_outputs* o) {
+// One tile [t0, t0 + Tc): the replay, then the tile's 200-level grids into dq ([S][q*Tc][200] in
+// HBM, on s->stream) and, if o->w_pred_samples, its draws to the host.  Returns after the stream
+// is idle.
+static int predict_tile(mk_session* s, int t0, double* dq, mk_outputs* o) {
   Model& md = s->md;
-  const int S = s->S, q = s->q, nt = s->nt;
+  const int S = s->S, q = s->q;
   const int k_lo = s->win_lo, n_kept = s->win_n < 0 ? md.n_kept : s->win_n;   // kept states replayed
   const int T = s->pred_tile, T_pad = md.n_test_pad, n_test = s->n_test_all;
   const long C = (long)q * n_test;
+  const int Tc = std::min(T, n_test - t0);
+  const int Ct = q * Tc;
   hipStream_t st = s->stream;
   Group g = s->all;
   s->la_next = -1;   // the replay factors into the free slots: a lookahead candidate is gone
+  HIPCHK(hipMemsetAsync((void*)md.coords_test, 0, (size_t)2 * T_pad * 8, st));
+  HIPCHK(hipMemcpyAsync((void*)md.coords_test, s->d_ct_all + t0, (size_t)Tc * 8, hipMemcpyDeviceToDevice, st));
+  HIPCHK(hipMemcpyAsync((void*)(md.coords_test + T_pad), s->d_ct_all + s->n_test_pad_all + t0, (size_t)Tc * 8,
+                        hipMemcpyDeviceToDevice, st));
+  Model mt = md;
+  mt.n_kept = n_kept;   // w_pred holds the window's draws
+  mt.n_test = Tc;
+  mt.t_off = t0;
+  mt.ntt = (Tc + MK_NB - 1) / MK_NB;   // a short last tile: only its valid 128-site column blocks
+                                        // (strides stay those of the full tile, n_test_pad)
+  for (int j = 0; j < n_kept; ++j) {
+    const int k = k_lo + j;   // kept state k = iteration kept0 + k
+    mt.theta = md.kth + (long)k * S * md.n_theta;
+    mt.z = md.kz + (long)k * S * q * md.n_pad;
+    mt.A_full = md.kA + (long)k * S * q * q;
+    const double* prev = j ? md.kth + (long)(k - 1) * S * md.n_theta : nullptr;
+    hipLaunchKernelGGL(k_kept_dirty, dim3(1), dim3(256), 0, st, mt, prev, s->d_slist, s->d_scount, g.d_plist,
+                       g.d_pcount);
+    for (int h = 0; h < q; ++h) {
+      launch_candidates(mt, g.ms, st, S, h, 1, 2, 0, s->d_slist + h * S, s->d_scount + h);
+      launch_cholesky(s, g, h, 1, s->d_slist + h * S, s->d_scount + h);
+    }
+    hipLaunchKernelGGL(k_flip_pairs, dim3((S * q + 255) / 256), dim3(256), 0, st, g.ms, g.d_plist, g.d_pcount);
+    launch_trinv(s, g, S * q, g.d_plist, g.d_pcount);
+    g.md = mt;
+    launch_pred_refresh(s, g);
+    const int per = (Tc + 3) / 4;
+    hipLaunchKernelGGL(k_pred_draw, dim3(S * per), dim3(256), 0, st, mt, md.kept0 + k, j);
+    HIPCHK(hipGetLastError());
+  }
+  if (dq) {
+    const int rq = launch_quantiles(S * Ct, st, md.w_pred, (long)n_kept * Ct, (long)Ct, n_kept, Ct, s->d_probs,
+                                    MK_N_LEVELS, dq);
+    if (rq) return rq;
+  }
+  if (o && o->w_pred_samples)   // per subset (C x kept) column-major
+    for (int i = 0; i < S; ++i)
+      HIPCHK(hipMemcpy2DAsync(o->w_pred_samples + (size_t)i * n_kept * C + (size_t)t0 * q, (size_t)C * 8,
+                              md.w_pred + (size_t)i * n_kept * Ct, (size_t)Ct * 8, (size_t)Ct * 8, n_kept,
+                              hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  return 0;
+}
+
+static int predict_tiled(mk_session* s, mk_outputs* o) {
+  const int S = s->S, q = s->q;
+  const int T = s->pred_tile, n_test = s->n_test_all;
+  const long C = (long)q * n_test;
+  hipStream_t st = s->stream;
   DevBufs scratch;
   double* dq = scratch.get<double>((size_t)S * q * T * MK_N_LEVELS);
   double* dsum = scratch.get<double>((size_t)q * T * MK_N_LEVELS);
   if (!dq || !dsum) return set_err(MK_E_NOMEM, "tiled kriging scratch");
+  const bool grids = o->w_predict || o->w_predict_sum;
   for (int t0 = 0; t0 < n_test; t0 += T) {
-    const int Tc = std::min(T, n_test - t0);
-    const int Ct = q * Tc;
-    HIPCHK(hipMemsetAsync((void*)md.coords_test, 0, (size_t)2 * T_pad * 8, st));
-    HIPCHK(hipMemcpyAsync((void*)md.coords_test, s->d_ct_all + t0, (size_t)Tc * 8, hipMemcpyDeviceToDevice, st));
-    HIPCHK(hipMemcpyAsync((void*)(md.coords_test + T_pad), s->d_ct_all + s->n_test_pad_all + t0, (size_t)Tc * 8,
-                          hipMemcpyDeviceToDevice, st));
-    Model mt = md;
-    mt.n_kept = n_kept;   // w_pred holds the window's draws
-    mt.n_test = Tc;
-    mt.t_off = t0;
-    mt.ntt = (Tc + MK_NB - 1) / MK_NB;   // a short last tile: only its valid 128-site column blocks
-                                          // (strides stay those of the full tile, n_test_pad)
-    for (int j = 0; j < n_kept; ++j) {
-      const int k = k_lo + j;   // kept state k = iteration kept0 + k
-      mt.theta = md.kth + (long)k * S * md.n_theta;
-      mt.z = md.kz + (long)k * S * q * md.n_pad;
-      mt.A_full = md.kA + (long)k * S * q * q;
-      const double* prev = j ? md.kth + (long)(k - 1) * S * md.n_theta : nullptr;
-      hipLaunchKernelGGL(k_kept_dirty, dim3(1), dim3(256), 0, st, mt, prev, s->d_slist, s->d_scount, g.d_plist,
-                         g.d_pcount);
-      for (int h = 0; h < q; ++h) {
-        launch_candidates(mt, g.ms, st, S, h, 1, 2, 0, s->d_slist + h * S, s->d_scount + h);
-        launch_cholesky(s, g, h, 1, s->d_slist + h * S, s->d_scount + h);
-      }
-      hipLaunchKernelGGL(k_flip_pairs, dim3((S * q + 255) / 256), dim3(256), 0, st, g.ms, g.d_plist, g.d_pcount);
-      launch_trinv(s, g, S * q, g.d_plist, g.d_pcount);
-      g.md = mt;
-      launch_pred_refresh(s, g);
-      const int per = (Tc + 3) / 4;
-      hipLaunchKernelGGL(k_pred_draw, dim3(S * per), dim3(256), 0, st, mt, md.kept0 + k, j);
-      HIPCHK(hipGetLastError());
-    }
-    hipLaunchKernelGGL(k_quantiles, dim3(S * Ct), dim3(256), 0, st, md.w_pred, (long)n_kept * Ct, (long)Ct, n_kept, Ct,
-                       s->d_probs, MK_N_LEVELS, dq);
-    HIPCHK(hipGetLastError());
+    const int Ct = q * std::min(T, n_test - t0);
+    int rc = predict_tile(s, t0, grids ? dq : nullptr, o);
+    if (rc) return rc;
     if (o->w_predict)   // per subset [C][200]: this tile's columns
       HIPCHK(hipMemcpy2DAsync(o->w_predict + (size_t)t0 * q * MK_N_LEVELS, (size_t)C * MK_N_LEVELS * 8, dq,
                               (size_t)Ct * MK_N_LEVELS * 8, (size_t)Ct * MK_N_LEVELS * 8, S, hipMemcpyDeviceToHost, st));
@@ -1494,15 +1610,59 @@ static int predict_tiled(mk_session* s, mk_outputs* o) {
       HIPCHK(hipMemcpyAsync(o->w_predict_sum + (size_t)t0 * q * MK_N_LEVELS, dsum, (size_t)Ct * MK_N_LEVELS * 8,
                             hipMemcpyDeviceToHost, st));
     }
-    if (o->w_pred_samples)   // per subset (C x kept) column-major
-      for (int i = 0; i < S; ++i)
-        HIPCHK(hipMemcpy2DAsync(o->w_pred_samples + (size_t)i * n_kept * C + (size_t)t0 * q, (size_t)C * 8,
-                                md.w_pred + (size_t)i * n_kept * Ct, (size_t)Ct * 8, (size_t)Ct * 8, n_kept,
-                                hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
   }
   return 0;
 }
+
+// ------------------------------------------------------------------ shard interface (mk_multi.hip)
+namespace mk {
+int session_info(const mk_session* s, ShardInfo* in) {
+  in->device = s->device;
+  in->S = s->S;
+  in->P = s->P;
+  in->q = s->q;
+  in->n_test = s->n_test_all;
+  in->tiled = s->tiled ? 1 : 0;
+  in->pred_tile = s->tiled ? s->pred_tile : s->n_test_all;
+  in->n_kept = s->md.n_kept;
+  in->stream = s->stream;
+  return 0;
+}
+// [S][P][200] parameter grids (obj[[i]]$parameters, MK.R:89) into d_out (HBM), on the session stream.
+int session_param_grids(mk_session* s, double* d_out) {
+  HIPCHK(hipSetDevice(s->device));
+  Model& md = s->md;
+  if (s->iter < md.n_samples) return set_err(MK_E_ARG, "quantile outputs need all n.samples iterations");
+  const int rq = launch_quantiles(s->S * s->P, s->stream, md.samples + (long)md.kept0 * s->P, (long)md.n_samples * s->P,
+                                  (long)s->P, md.n_kept, s->P, s->d_probs, MK_N_LEVELS, d_out);
+  if (rq) return rq;
+  HIPCHK(hipStreamSynchronize(s->stream));
+  return 0;
+}
+// [S][q n_test][200] w.predict grids of a fused session into d_out.
+int session_wpred_grids(mk_session* s, double* d_out) {
+  HIPCHK(hipSetDevice(s->device));
+  Model& md = s->md;
+  if (s->tiled) return set_err(MK_E_ARG, "tiled sessions produce their grids per tile");
+  if (s->iter < md.n_samples) return set_err(MK_E_ARG, "quantile outputs need all n.samples iterations");
+  const int C = s->q * md.n_test;
+  const int rq = launch_quantiles(s->S * C, s->stream, md.w_pred, (long)md.n_kept * C, (long)C, md.n_kept, C, s->d_probs,
+                                  MK_N_LEVELS, d_out);
+  if (rq) return rq;
+  HIPCHK(hipStreamSynchronize(s->stream));
+  return 0;
+}
+// Tiled session: the grids [S][q Tc][200] of test-site tile [t0, t0 + Tc) into d_out (and the
+// tile's draws into o->w_pred_samples when set).
+int session_tile_grids(mk_session* s, int t0, double* d_out, mk_outputs* o) {
+  HIPCHK(hipSetDevice(s->device));
+  if (!s->tiled) return set_err(MK_E_ARG, "not a tiled session");
+  if (s->iter < s->md.n_samples) return set_err(MK_E_ARG, "quantile outputs need all n.samples iterations");
+  if (t0 < 0 || t0 >= s->n_test_all || t0 % s->pred_tile) return set_err(MK_E_ARG, "bad tile offset");
+  return predict_tile(s, t0, d_out, o);
+}
+}  // namespace mk
 
 extern "C" int mk_session_outputs(mk_session* s, mk_outputs* o) {
   if (!s || !o) return set_err(MK_E_ARG, "null session/outputs");
@@ -1517,9 +1677,9 @@ extern "C" int mk_session_outputs(mk_session* s, mk_outputs* o) {
   if (o->parameters) {
     double* dq = scratch.get<double>((size_t)S * P * MK_N_LEVELS);
     if (!dq) return set_err(MK_E_NOMEM, "quantile scratch");
-    hipLaunchKernelGGL(k_quantiles, dim3(S * P), dim3(256), 0, s->stream, md.samples + (long)md.kept0 * P,
-                       (long)md.n_samples * P, (long)P, md.n_kept, P, s->d_probs, MK_N_LEVELS, dq);
-    HIPCHK(hipGetLastError());
+    int rq = launch_quantiles(S * P, s->stream, md.samples + (long)md.kept0 * P, (long)md.n_samples * P, (long)P,
+                              md.n_kept, P, s->d_probs, MK_N_LEVELS, dq);
+    if (rq) return rq;
     // device layout [S][P][200] == R's 200 x P column-major per subset
     HIPCHK(hipMemcpyAsync(o->parameters, dq, (size_t)S * P * MK_N_LEVELS * 8, hipMemcpyDeviceToHost, s->stream));
   }
@@ -1532,9 +1692,9 @@ extern "C" int mk_session_outputs(mk_session* s, mk_outputs* o) {
     const int C = q * n_test;
     double* dq = scratch.get<double>((size_t)S * C * MK_N_LEVELS);
     if (!dq) return set_err(MK_E_NOMEM, "quantile scratch");
-    hipLaunchKernelGGL(k_quantiles, dim3(S * C), dim3(256), 0, s->stream, md.w_pred, (long)md.n_kept * C, (long)C,
-                       md.n_kept, C, s->d_probs, MK_N_LEVELS, dq);
-    HIPCHK(hipGetLastError());
+    int rq = launch_quantiles(S * C, s->stream, md.w_pred, (long)md.n_kept * C, (long)C, md.n_kept, C, s->d_probs,
+                              MK_N_LEVELS, dq);
+    if (rq) return rq;
     if (o->w_predict)
       HIPCHK(hipMemcpyAsync(o->w_predict, dq, (size_t)S * C * MK_N_LEVELS * 8, hipMemcpyDeviceToHost, s->stream));
     if (o->w_predict_sum) {   // this shard's term of the combine: sequential sum over its subsets
@@ -1685,8 +1845,8 @@ extern "C" int mk_combine_median_device(const double* d_grids, int32_t K, int32_
 extern "C" int mk_posterior_summary_ex(const double* result, int32_t P, const double* result2, int64_t C,
                                        const double* x_test, int32_t p, int32_t S, uint64_t seed,
                                        const int32_t* index, int32_t link, mk_summary* o, int32_t device) {
-  if (!result || !o || P < 1 || C < 0 || p < 0 || p > P || S < 1 || S > 2048)
-    return set_err(MK_E_ARG, "bad posterior_summary arguments (P >= 1, 0 <= p <= P, 1 <= samplesize <= 2048)");
+  if (!result || !o || P < 1 || C < 0 || p < 0 || p > P || S < 1 || S > MK_QUANT_MAX)
+    return set_err(MK_E_ARG, "bad posterior_summary arguments (P >= 1, 0 <= p <= P, 1 <= samplesize <= 16384)");
   if (C > 0 && (!result2 || (p > 0 && !x_test))) return set_err(MK_E_ARG, "result2 / x_test missing");
   if (link != MK_LINK_LOGIT && link != MK_LINK_PROBIT) return set_err(MK_E_ARG, "link must be logit or probit");
   HIPCHK(hipSetDevice(device));
@@ -1764,8 +1924,8 @@ extern "C" int mk_posterior_summary_ex(const double* result, int32_t P, const do
   if (C > 0 && o->p_sample) HIPCHK(hipMemcpy(o->p_sample, d_p, (size_t)S * C * 8, hipMemcpyDeviceToHost));
   // type-7 (0.5, 0.025, 0.975) per column: each column is S contiguous rows -> 3 x ncol column-major
   auto quant = [&](const double* src, long ncol, double* dst) -> int {
-    hipLaunchKernelGGL(k_quantiles, dim3((unsigned)ncol), dim3(256), 0, st, src, (long)S, 1L, S, 1, d_pr, 3, d_q);
-    HIPCHK(hipGetLastError());
+    const int rq = launch_quantiles((unsigned)ncol, st, src, (long)S, 1L, S, 1, d_pr, 3, d_q);
+    if (rq) return rq;
     HIPCHK(hipMemcpy(dst, d_q, (size_t)ncol * 3 * 8, hipMemcpyDeviceToHost));
     return 0;
   };

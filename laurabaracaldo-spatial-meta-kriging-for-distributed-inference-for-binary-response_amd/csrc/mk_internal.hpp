@@ -1,0 +1,18 @@
+// Library-internal interface between the session (mk_api.hip) and the multi-device driver
+// (mk_multi.hip): a shard's quantile grids stay in HBM for the device-to-device combine.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <string>
+#include "../../include/mk.h"
+
+namespace mk {
+struct ShardInfo {
+  int device, S, P, q, n_test, tiled, pred_tile, n_kept;
+  hipStream_t stream;
+};
+int host_error(int code, const char* msg);   // sets mk_last_error()
+int session_info(const mk_session* s, ShardInfo* info);
+int session_param_grids(mk_session* s, double* d_out);                   // [S][P][200]
+int session_wpred_grids(mk_session* s, double* d_out);                   // fused: [S][q n_test][200]
+int session_tile_grids(mk_session* s, int t0, double* d_out, mk_outputs* o);   // tiled: [S][q Tc][200]
+}  // namespace mk

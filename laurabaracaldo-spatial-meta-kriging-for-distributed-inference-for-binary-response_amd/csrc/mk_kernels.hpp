@@ -52,6 +52,19 @@ template <int Q>
 __global__ void k_sweep(Model md, MatSet ms, int iter);
 template <int Q>
 __global__ void k_sweep_mg(Model md, MatSet ms, int iter, double* part, int* cnt, int* xcc, int* err);
+template <int Q>
+__global__ void k_sweep_tiles(Model md, MatSet ms, int iter, int B, double* part, const double* dacc_g, const int* any_g);
+template <int Q>
+__global__ void k_sweep_block(Model md, MatSet ms, int B, const double* part, double* dacc_g, int* any_g);
+// the split-launch sweep's two kernels for q outcomes
+inline const void* sweep_split_kernel(int q, bool block) {
+  switch (q) {
+    case 1: return block ? (const void*)k_sweep_block<1> : (const void*)k_sweep_tiles<1>;
+    case 2: return block ? (const void*)k_sweep_block<2> : (const void*)k_sweep_tiles<2>;
+    case 3: return block ? (const void*)k_sweep_block<3> : (const void*)k_sweep_tiles<3>;
+    default: return block ? (const void*)k_sweep_block<4> : (const void*)k_sweep_tiles<4>;
+  }
+}
 // the sweep kernels specialised for the session's number of outcomes
 inline const void* sweep_kernel(int q, bool mg) {
   switch (q) {

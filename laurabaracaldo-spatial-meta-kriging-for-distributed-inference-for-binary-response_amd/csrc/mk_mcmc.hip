@@ -659,7 +659,10 @@ __global__ __launch_bounds__(256) void k_sweep_mg(Model md, MatSet ms, int iter,
     if (tid == 0) __hip_atomic_fetch_add(cs + B, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     SW_STAMP(B, 2);
     if (tid == 0) {
-      const int target = tl - tf + 1;
+      // tiles tf .. tl arrive at every barrier; at an even B > 0 also tile tf - 1, which left after
+      // block B - 1 (its last) -- it arrives once it has read block B - 1's partials, so block B + 1
+      // cannot overwrite that parity buffer under its reads
+      const int target = tl - tf + 1 + ((B & 1) == 0 && B > 0 ? 1 : 0);
       int spins = 0;
       while (__hip_atomic_load(cs + B, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
         __builtin_amdgcn_s_sleep(1);
@@ -689,6 +692,8 @@ __global__ __launch_bounds__(256) void k_sweep_mg(Model md, MatSet ms, int iter,
       gb[e] = g;
     }
     __syncthreads();
+    if (B == last_b && t < tl && tid == 0)          // last read of this parity buffer by tile t
+      __hip_atomic_fetch_add(cs + B + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     SW_STAMP(B, 4);
     // ---- the block's MH steps (wave 0 of every workgroup; the sites' owner records them)
     if (wv == 0) {
@@ -738,6 +743,149 @@ __global__ __launch_bounds__(256) void k_sweep_mg(Model md, MatSet ms, int iter,
   __syncthreads();
   sweep_apply(md, s, MK_NB * t, min(MK_NB * (t + 1), ns), Ai, tid, 256);
 }
+// Split-launch sweep (small shards, no inter-workgroup waiting).  The sweep's only sequential
+// dependency -- block B's dots need z after block B-1's accepted moves -- is carried by stream
+// order instead of by barriers between co-resident workgroups: per 64-site block two launches,
+//   k_sweep_tiles(B): one 256-thread workgroup per (subset, 128-row tile): z rows of the tile
+//                     += W[:, B-1] delta'_{B-1} (if block B-1 moved a site), then the tile's partial
+//                     dots of block B's columns -> part[s][t][h][64]; B = 0 also computes the
+//                     tile's proposals, the launch after a subset's last block applies its moves;
+//   k_sweep_block(B): one workgroup per subset: the partials of tiles tf .. tl summed in tile
+//                     order, Q_BB, the block's MH steps (wave 0) -> delta' [s][h][64], any-moved.
+// A workgroup never waits on another, so nothing depends on co-residency, queue priority or CU
+// masks.  The arithmetic and its order are k_sweep's / k_sweep_mg's (per-tile DPP dot reductions
+// summed in tile order; per-wave column-residue FMA chains summed over the four waves): same bits.
+template <int Q>
+__global__ __launch_bounds__(256) void k_sweep_tiles(Model md, MatSet ms, int iter, int B, double* __restrict__ part,
+                                                     const double* __restrict__ dacc_g, const int* __restrict__ any_g) {
+  __shared__ double red[4 * MK_NB];
+  __shared__ double Ai[MK_QMAX * MK_QMAX];
+  constexpr int q = Q;
+  const int nt = ms.nt;
+  const int s = blockIdx.x / nt, t = blockIdx.x % nt;
+  const int ns = md.n_s[s];
+  const int tl = (ns - 1) / MK_NB;
+  if (t > tl) return;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const long ld = ms.ld;
+  const int r0 = MK_NB * t + 2 * lane;
+  const int n_blk = (ns + SW_B - 1) / SW_B;
+  if (B > n_blk) return;
+  if (B == 0) sweep_precompute(md, s, iter, MK_NB * t * q, min(MK_NB * (t + 1), ns) * q, tid, 256);
+  d2 zr[Q];
+#pragma unroll
+  for (int h = 0; h < Q; ++h) zr[h] = *reinterpret_cast<const d2*>(md.z + ((long)s * q + h) * md.n_pad + r0);
+  bool zdirty = false;
+  // ---- z rows of tile t (rows >= b0') += W[:, B-1] delta'_{B-1}
+  if (B > 0) {
+    const int bp = (B - 1) * SW_B, nbp = min(SW_B, ns - bp);
+    if (t >= bp / MK_NB && any_g[s]) {
+      zdirty = true;
+      for (int h = 0; h < q; ++h) {
+        const double* Wt = ms.W + ((long)s * q + h) * (ld * ld) + (long)bp * ld + r0;
+        const double* da = dacc_g + ((long)s * q + h) * SW_B;
+        d2 wreg[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) wreg[j] = *reinterpret_cast<const d2*>(Wt + (long)(wv + 4 * j) * ld);
+        d2 sw = {0.0, 0.0};
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const int i = wv + 4 * j;
+          const double c = (i < nbp) ? da[i] : 0.0;
+          sw.x = fma(wreg[j].x, c, sw.x);
+          sw.y = fma(wreg[j].y, c, sw.y);
+        }
+        red[wv * MK_NB + 2 * lane] = sw.x;
+        red[wv * MK_NB + 2 * lane + 1] = sw.y;
+        __syncthreads();
+        const double vx = ((red[2 * lane] + red[MK_NB + 2 * lane]) + red[2 * MK_NB + 2 * lane]) + red[3 * MK_NB + 2 * lane];
+        const double vy = ((red[2 * lane + 1] + red[MK_NB + 2 * lane + 1]) + red[2 * MK_NB + 2 * lane + 1]) +
+                          red[3 * MK_NB + 2 * lane + 1];
+        __syncthreads();
+#pragma unroll
+        for (int hh = 0; hh < Q; ++hh) {
+          if (hh != h) continue;
+          if (r0 >= bp && r0 < ns) zr[hh].x += vx;
+          if (r0 + 1 >= bp && r0 + 1 < ns) zr[hh].y += vy;
+        }
+      }
+    }
+  }
+  if (B < n_blk) {
+    // ---- partial dots of tile t for block B's columns (tiles >= the block's first tile)
+    const int b0 = B * SW_B;
+    if (t >= b0 / MK_NB) {
+      double* pb = part + (((long)s * nt + t) * q) * SW_B;
+      for (int h = 0; h < q; ++h) {
+        const double* Wt = ms.W + ((long)s * q + h) * (ld * ld) + (long)b0 * ld + r0;
+        d2 wreg[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) wreg[j] = *reinterpret_cast<const d2*>(Wt + (long)(wv + 4 * j) * ld);
+        d2 zz = zr[0];
+#pragma unroll
+        for (int hh = 1; hh < Q; ++hh)
+          if (hh == h) zz = zr[hh];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const double a0 = (r0 >= b0 && r0 < ns) ? wreg[j].x * zz.x : 0.0;
+          const double a1 = (r0 + 1 >= b0 && r0 + 1 < ns) ? wreg[j].y * zz.y : 0.0;
+          const double p = wave_sum_dpp(a0 + a1);
+          if (lane == 0) pb[h * SW_B + wv + 4 * j] = p;
+        }
+      }
+    }
+  }
+  if (zdirty && wv == 0) {
+#pragma unroll
+    for (int h = 0; h < Q; ++h) *reinterpret_cast<d2*>(md.z + ((long)s * q + h) * md.n_pad + r0) = zr[h];
+  }
+  if (B == n_blk) {   // the subset's last block is done: apply this tile's accepted moves
+    if (tid < q * q) Ai[tid] = md.Ainv[(long)s * q * q + tid];
+    __syncthreads();
+    sweep_apply(md, s, MK_NB * t, min(MK_NB * (t + 1), ns), Ai, tid, 256);
+  }
+}
+
+template <int Q>
+__global__ __launch_bounds__(256) void k_sweep_block(Model md, MatSet ms, int B, const double* __restrict__ part,
+                                                     double* __restrict__ dacc_g, int* __restrict__ any_g) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  constexpr int q = Q;
+  double* Qb = smem;                              // [q][SW_B*SW_B]
+  double* gb = Qb + q * SW_B * SW_B;              // [q][SW_B]
+  double* dacc = gb + q * SW_B;                   // [q][SW_B]
+  __shared__ double Ai[MK_QMAX * MK_QMAX];
+  const int s = blockIdx.x, tid = threadIdx.x;
+  const int ns = md.n_s[s];
+  const int b0 = B * SW_B;
+  if (b0 >= ns) return;
+  const int nb = min(SW_B, ns - b0), tf = b0 / MK_NB, tl = (ns - 1) / MK_NB, nt = ms.nt;
+  if (tid < q * q) Ai[tid] = md.Ainv[(long)s * q * q + tid];
+  const int tile = b0 / MK_NB, off = b0 % MK_NB;
+  for (int h = 0; h < q; ++h) {
+    const double* QBt = ms.QB + (((long)s * q + h) * nt + tile) * MK_NB * MK_NB;
+    for (int e = tid; e < SW_B * SW_B; e += 256) {
+      const int r = e & (SW_B - 1), c = e / SW_B;
+      Qb[h * SW_B * SW_B + e] = QBt[(off + r) + (off + c) * MK_NB];
+    }
+  }
+  // dots: partials of tiles tf .. tl summed in tile order
+  for (int e = tid; e < q * SW_B; e += 256) {
+    const int h = e / SW_B, i = e % SW_B;
+    const double* pp = part + ((long)s * nt * q + h) * SW_B + i;
+    double g = pp[(long)tf * q * SW_B];
+    for (int u = tf + 1; u <= tl; ++u) g = g + pp[(long)u * q * SW_B];
+    gb[e] = g;
+  }
+  __syncthreads();
+  if (tid < 64) {
+    const int anyl = sweep_block_mh_q<Q, false>(md, s, b0, nb, gb, Qb, Ai, dacc, true);
+#pragma unroll
+    for (int h = 0; h < Q; ++h) dacc_g[((long)s * q + h) * SW_B + tid] = dacc[h * SW_B + tid];
+    if (tid == 0) any_g[s] = anyl;
+  }
+}
+
 template __global__ void k_sweep<1>(Model, MatSet, int);
 template __global__ void k_sweep<2>(Model, MatSet, int);
 template __global__ void k_sweep<3>(Model, MatSet, int);
@@ -746,6 +894,13 @@ template __global__ void k_sweep_mg<1>(Model, MatSet, int, double*, int*, int*, 
 template __global__ void k_sweep_mg<2>(Model, MatSet, int, double*, int*, int*, int*);
 template __global__ void k_sweep_mg<3>(Model, MatSet, int, double*, int*, int*, int*);
 template __global__ void k_sweep_mg<4>(Model, MatSet, int, double*, int*, int*, int*);
+#define MK_INST_SPLIT(Q)                                                                                   \
+  template __global__ void k_sweep_tiles<Q>(Model, MatSet, int, int, double*, const double*, const int*); \
+  template __global__ void k_sweep_block<Q>(Model, MatSet, int, const double*, double*, int*);
+MK_INST_SPLIT(1)
+MK_INST_SPLIT(2)
+MK_INST_SPLIT(3)
+MK_INST_SPLIT(4)
 
 // ---------------------------------------------------------------- 6. record / adapt
 __global__ __launch_bounds__(64) void k_record(Model md, int iter) {
@@ -851,12 +1006,13 @@ __global__ __launch_bounds__(256) void k_pred_draw(Model md, int iter, int kidx)
 }
 
 // ---------------------------------------------------------------- 8. type-7 quantiles (MK.R:88-89)
-// One workgroup per (subset, column): bitonic sort of the kept values in LDS,
-// then R's quantile.default type 7: (1-h) x[lo] + h x[hi] (no FMA contraction).
+// One workgroup per (subset, column): bitonic sort of the kept values in LDS (dynamic: the next
+// power of two >= n_rows doubles, at most MK_QUANT_MAX = 128 KB), then R's quantile.default type 7:
+// (1-h) x[lo] + h x[hi] (no FMA contraction).
 __global__ __launch_bounds__(256) void k_quantiles(const double* __restrict__ data, long subset_stride, long row_stride,
                                                    int n_rows, int n_cols, const double* __restrict__ probs, int n_probs,
                                                    double* __restrict__ out /* [S][n_cols][n_probs] */) {
-  __shared__ double v[2048];
+  extern __shared__ double v[];
   const int s = blockIdx.x / n_cols, c = blockIdx.x % n_cols;
   const double* src = data + (long)s * subset_stride + c;
   int n2 = 1;

@@ -1,0 +1,429 @@
+// mk_meta_fit: the whole node in one call (include/mk.h) -- the subsets sharded over the GPUs of
+// one host, one host thread per shard, and the combine device to device.
+//
+// Replaces MK.R:100-114 (makeCluster(n.core) + foreach(i = 1:n.core) %dopar% partitioned_spMvGLM)
+// and the combine loop MK.R:119-133.  The fits exchange nothing: shard r is the
+// balanced contiguous block [floor(rK/G), floor((r+1)K/G)) of subsets with its global subset
+// indices, so its chains are the one-device chains.  The one exchange is the combine:
+//
+//   grids_r [S_r][C][200]  (HBM of device r; C = P parameter columns, or q*n_test kriging columns,
+//                           or q*tile per test-site tile)
+//   pack    send_r [G][S_r][per][200]  (column block j of each of its subsets; per = ceil(C/G))
+//   all-to-all: recv_j [K][per][200] <- send_r block j, at subset offset lo_r (global order)
+//   combine on device j: k_combine (sequential mean / sum over k = 0..K-1) or k_weiszfeld
+//   columns [a_j, a_j + c_j) of the combined grid -> host
+//
+// The all-to-all is RCCL send/recv in one group (xGMI) when the devices are distinct, and device
+// copies (hipMemcpyPeerAsync; same-device copies) when a device appears more than once -- RCCL
+// refuses two ranks on one GPU.  RCCL is loaded at run time (dlopen), so libmk has no link-time
+// dependency on it and a host that already loaded one (torch) shares it.
+#include <hip/hip_runtime.h>
+#include <dlfcn.h>
+#include <rccl/rccl.h>
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <thread>
+#include <vector>
+#include "../../include/mk.h"
+#include "mk_internal.hpp"
+#include "mk_kernels.hpp"
+
+using namespace mk;
+
+namespace {
+
+int fail(int code, const std::string& msg) { return host_error(code, msg.c_str()); }
+
+#define MHIP(x)                                                                                     \
+  do {                                                                                              \
+    hipError_t e_ = (x);                                                                            \
+    if (e_ != hipSuccess) return fail(MK_E_HIP, std::string(#x " -> ") + hipGetErrorString(e_));    \
+  } while (0)
+
+// ------------------------------------------------------------------ RCCL, resolved at run time
+struct Rccl {
+  bool ok = false;
+  std::string why;
+  ncclResult_t (*comm_init_all)(ncclComm_t*, int, const int*) = nullptr;
+  ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*group_start)() = nullptr;
+  ncclResult_t (*group_end)() = nullptr;
+  ncclResult_t (*send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  const char* (*error_string)(ncclResult_t) = nullptr;
+};
+
+const Rccl& rccl() {
+  static const Rccl r = [] {
+    Rccl x;
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL);
+    if (!h) {
+      const char* e = dlerror();
+      x.why = std::string("librccl not loadable: ") + (e ? e : "?");
+      return x;
+    }
+    x.comm_init_all = (decltype(x.comm_init_all))dlsym(h, "ncclCommInitAll");
+    x.comm_destroy = (decltype(x.comm_destroy))dlsym(h, "ncclCommDestroy");
+    x.group_start = (decltype(x.group_start))dlsym(h, "ncclGroupStart");
+    x.group_end = (decltype(x.group_end))dlsym(h, "ncclGroupEnd");
+    x.send = (decltype(x.send))dlsym(h, "ncclSend");
+    x.recv = (decltype(x.recv))dlsym(h, "ncclRecv");
+    x.error_string = (decltype(x.error_string))dlsym(h, "ncclGetErrorString");
+    x.ok = x.comm_init_all && x.comm_destroy && x.group_start && x.group_end && x.send && x.recv && x.error_string;
+    if (!x.ok) x.why = "librccl lacks a symbol";
+    return x;
+  }();
+  return r;
+}
+
+#define MNCCL(x)                                                                                    \
+  do {                                                                                              \
+    ncclResult_t e_ = (x);                                                                          \
+    if (e_ != ncclSuccess) return fail(MK_E_HIP, std::string(#x " -> ") + rccl().error_string(e_)); \
+  } while (0)
+
+// Runs f(r) for r in [0, n) on n threads and returns the first failure with its message (the
+// library's error text is thread-local: it is carried back to the calling thread).
+template <typename F>
+int parallel(int n, F&& f) {
+  std::vector<int> rc(n, 0);
+  std::vector<std::string> msg(n);
+  std::vector<std::thread> th;
+  th.reserve(n);
+  for (int r = 0; r < n; ++r)
+    th.emplace_back([&, r] {
+      rc[r] = f(r);
+      if (rc[r]) msg[r] = mk_last_error();
+    });
+  for (auto& t : th) t.join();
+  for (int r = 0; r < n; ++r)
+    if (rc[r]) return fail(rc[r], "device block " + std::to_string(r) + ": " + msg[r]);
+  return 0;
+}
+
+// Device buffer that grows on demand (freed on its device).
+struct DBuf {
+  int dev = 0;
+  double* p = nullptr;
+  size_t cap = 0;
+  int ensure(size_t n) {
+    if (n <= cap) return 0;
+    MHIP(hipSetDevice(dev));
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    if (hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(double)) != hipSuccess) {
+      (void)hipGetLastError();
+      p = nullptr;
+      return fail(MK_E_NOMEM, "combine buffer of " + std::to_string(n * 8) + " B");
+    }
+    cap = n;
+    return 0;
+  }
+  ~DBuf() {
+    if (p) {
+      (void)hipSetDevice(dev);
+      (void)hipFree(p);
+    }
+  }
+};
+
+// One device block: its session and its share of the exchange.
+struct Block {
+  int dev = 0, lo = 0, S = 0;
+  mk_session* ses = nullptr;
+  hipStream_t st = nullptr;
+  hipEvent_t packed = nullptr;
+  DBuf grids, send, recv, comb, sum, iters;   // iters: Weiszfeld iteration counts (as int)
+  ~Block() {
+    (void)hipSetDevice(dev);
+    if (st) (void)hipStreamSynchronize(st);
+    if (ses) mk_session_destroy(ses);
+    if (packed) (void)hipEventDestroy(packed);
+    if (st) (void)hipStreamDestroy(st);
+  }
+};
+
+struct Node {
+  int G = 0, K = 0;
+  std::vector<std::unique_ptr<Block>> b;
+  bool use_rccl = false;
+  std::vector<ncclComm_t> comms;
+  ~Node() {
+    for (ncclComm_t c : comms)
+      if (c) rccl().comm_destroy(c);
+  }
+};
+
+constexpr int L = MK_N_LEVELS;
+
+// The exchange + combine of one grid set: every block's grids [S_r][C][200] are in b.grids.
+// Writes (when not NULL) the combined columns: mean (or median) -> h_comb, sum -> h_sum, both
+// 200 x C column-major with column c at c*200.
+int exchange_combine(Node& nd, long C, const mk_combined* comb, double* h_comb, double* h_sum) {
+  if (!h_comb && !h_sum) return 0;
+  const int G = nd.G, K = nd.K;
+  const long per = std::max(1L, (C + G - 1) / G);
+  auto col0 = [&](int j) { return std::min(C, (long)j * per); };
+  auto ncol = [&](int j) { return std::min(C, (long)(j + 1) * per) - col0(j); };
+  const bool median = comb && comb->method == MK_COMBINE_MEDIAN;
+  // pack: column block j of every subset of block r
+  int rc = parallel(G, [&](int r) -> int {
+    Block& x = *nd.b[r];
+    MHIP(hipSetDevice(x.dev));
+    int e;
+    if ((e = x.send.ensure((size_t)G * x.S * per * L)) || (e = x.recv.ensure((size_t)K * per * L)) ||
+        (e = x.comb.ensure((size_t)per * L)) || (e = x.sum.ensure((size_t)per * L)) || (e = x.iters.ensure((size_t)per)))
+      return e;
+    MHIP(hipMemsetAsync(x.recv.p, 0, (size_t)K * per * L * 8, x.st));
+    if (x.S > 0) {
+      MHIP(hipMemsetAsync(x.send.p, 0, (size_t)G * x.S * per * L * 8, x.st));
+      for (int j = 0; j < G; ++j)
+        if (ncol(j) > 0)
+          MHIP(hipMemcpy2DAsync(x.send.p + (size_t)j * x.S * per * L, (size_t)per * L * 8, x.grids.p + col0(j) * L,
+                                (size_t)C * L * 8, (size_t)ncol(j) * L * 8, x.S, hipMemcpyDeviceToDevice, x.st));
+    }
+    MHIP(hipEventRecord(x.packed, x.st));
+    return 0;
+  });
+  if (rc) return rc;
+  // all-to-all: recv_j[lo_r ..] <- send_r[j]
+  if (nd.use_rccl) {
+    const Rccl& R = rccl();
+    MNCCL(R.group_start());
+    ncclResult_t first = ncclSuccess;
+    for (int r = 0; r < G; ++r)
+      for (int j = 0; j < G; ++j) {
+        Block &xr = *nd.b[r], &xj = *nd.b[j];
+        if (xr.S == 0 || ncol(j) == 0) continue;
+        const size_t cnt = (size_t)xr.S * per * L;
+        ncclResult_t e1 = R.send(xr.send.p + (size_t)j * xr.S * per * L, cnt, ncclFloat64, j, nd.comms[r], xr.st);
+        ncclResult_t e2 = R.recv(xj.recv.p + (size_t)xr.lo * per * L, cnt, ncclFloat64, r, nd.comms[j], xj.st);
+        if (first == ncclSuccess) first = e1 != ncclSuccess ? e1 : e2;
+      }
+    const ncclResult_t eg = R.group_end();
+    if (first != ncclSuccess) return fail(MK_E_HIP, std::string("ncclSend/ncclRecv -> ") + R.error_string(first));
+    if (eg != ncclSuccess) return fail(MK_E_HIP, std::string("ncclGroupEnd -> ") + R.error_string(eg));
+  } else {
+    for (int j = 0; j < G; ++j) {
+      Block& xj = *nd.b[j];
+      if (ncol(j) == 0) continue;
+      MHIP(hipSetDevice(xj.dev));
+      for (int r = 0; r < G; ++r) {
+        Block& xr = *nd.b[r];
+        if (xr.S == 0) continue;
+        MHIP(hipStreamWaitEvent(xj.st, xr.packed, 0));
+        const size_t bytes = (size_t)xr.S * per * L * 8;
+        const double* src = xr.send.p + (size_t)j * xr.S * per * L;
+        double* dst = xj.recv.p + (size_t)xr.lo * per * L;
+        if (xr.dev == xj.dev)
+          MHIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, xj.st));
+        else
+          MHIP(hipMemcpyPeerAsync(dst, xj.dev, src, xr.dev, bytes, xj.st));
+      }
+    }
+  }
+  // combine on the owner of each column block, in global subset order; columns to the host
+  return parallel(G, [&](int j) -> int {
+    Block& x = *nd.b[j];
+    MHIP(hipSetDevice(x.dev));
+    const long a = col0(j), cj = ncol(j);
+    if (cj > 0) {
+      const long g = per * L;
+      const unsigned nb = (unsigned)((g + 255) / 256);
+      if (h_comb) {
+        if (median) {
+          const int it = comb->max_iter > 0 ? comb->max_iter : 100;
+          const double tol = comb->tol >= 0.0 ? comb->tol : 1e-12;
+          hipLaunchKernelGGL(k_weiszfeld, dim3((unsigned)((per + 3) / 4)), dim3(256), 0, x.st, x.recv.p, K, L, per, it,
+                             tol, x.comb.p, (int*)x.iters.p);
+        } else {
+          hipLaunchKernelGGL(k_combine, dim3(nb), dim3(256), 0, x.st, x.recv.p, K, g, x.comb.p, 1);
+        }
+        MHIP(hipGetLastError());
+        MHIP(hipMemcpyAsync(h_comb + a * L, x.comb.p, (size_t)cj * L * 8, hipMemcpyDeviceToHost, x.st));
+      }
+      if (h_sum) {
+        hipLaunchKernelGGL(k_combine, dim3(nb), dim3(256), 0, x.st, x.recv.p, K, g, x.sum.p, 0);
+        MHIP(hipGetLastError());
+        MHIP(hipMemcpyAsync(h_sum + a * L, x.sum.p, (size_t)cj * L * 8, hipMemcpyDeviceToHost, x.st));
+      }
+    }
+    MHIP(hipStreamSynchronize(x.st));
+    return 0;
+  });
+}
+
+}  // namespace
+
+extern "C" int mk_meta_fit(const mk_problem* pr, const mk_config* c, const int32_t* devices, int32_t G,
+                           mk_progress_fn progress, void* user, mk_outputs* out, mk_combined* comb) {
+  if (!pr || !c) return fail(MK_E_ARG, "null problem/config");
+  if (!devices || G < 1) return fail(MK_E_ARG, "n_devices must be >= 1 with a device list");
+  const int K = pr->n_subsets;
+  if (K < 1) return fail(MK_E_ARG, "n_subsets must be >= 1");
+  if (pr->q < 1 || pr->q > 4 || pr->p < 1 || !pr->n_part) return fail(MK_E_ARG, "bad q / p / n_part");
+  if (comb && comb->method != MK_COMBINE_MEAN && comb->method != MK_COMBINE_MEDIAN)
+    return fail(MK_E_ARG, "combine method must be MK_COMBINE_MEAN or MK_COMBINE_MEDIAN");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(MK_E_NODEV, "no HIP device");
+  for (int r = 0; r < G; ++r)
+    if (devices[r] < 0 || devices[r] >= ndev) return fail(MK_E_ARG, "bad device ordinal in the device list");
+  for (int i = 0; i < K; ++i)
+    if (pr->n_part[i] < 1) return fail(MK_E_ARG, "every subset needs >= 1 site");
+  const int q = pr->q, p = pr->p, n_samples = c->n_batch * c->batch_length;
+  if (c->n_batch < 1 || c->batch_length < 1) return fail(MK_E_ARG, "n.batch and batch.length must be >= 1");
+
+  Node nd;
+  nd.G = G;
+  nd.K = K;
+  bool distinct = true;
+  for (int r = 0; r < G; ++r)
+    for (int j = 0; j < r; ++j) distinct = distinct && devices[r] != devices[j];
+  const char* xenv = std::getenv("MK_EXCHANGE");   // "copy": device copies even on distinct devices
+  nd.use_rccl = distinct && !(xenv && std::strcmp(xenv, "copy") == 0);
+  if (nd.use_rccl && !rccl().ok) return fail(MK_E_HIP, rccl().why);
+
+  // ---- blocks: balanced contiguous subset ranges, data pointers offset into the caller's arrays
+  std::vector<long> site0(K + 1, 0);
+  for (int i = 0; i < K; ++i) site0[i + 1] = site0[i] + pr->n_part[i];
+  for (int r = 0; r < G; ++r) {
+    auto x = std::make_unique<Block>();
+    x->dev = devices[r];
+    x->lo = (int)(((long)r * K) / G);
+    x->S = (int)(((long)(r + 1) * K) / G) - x->lo;
+    x->grids.dev = x->send.dev = x->recv.dev = x->comb.dev = x->sum.dev = x->iters.dev = x->dev;
+    nd.b.push_back(std::move(x));
+  }
+  int rc = parallel(G, [&](int r) -> int {
+    Block& x = *nd.b[r];
+    MHIP(hipSetDevice(x.dev));
+    MHIP(hipStreamCreateWithFlags(&x.st, hipStreamNonBlocking));
+    MHIP(hipEventCreateWithFlags(&x.packed, hipEventDisableTiming));
+    if (x.S == 0) return 0;
+    mk_problem sp = *pr;
+    const long s0 = site0[x.lo];
+    sp.n_subsets = x.S;
+    sp.subset_base = pr->subset_base + x.lo;
+    sp.n_part = pr->n_part + x.lo;
+    sp.coords = pr->coords + 2 * s0;
+    sp.y = pr->y + s0 * q;
+    sp.weights = pr->weights + s0 * q;
+    sp.x = pr->x + s0 * q * p;
+    mk_config sc = *c;
+    sc.device = x.dev;
+    return mk_session_create(&sp, &sc, &x.ses);
+  });
+  if (rc) return rc;
+  if (nd.use_rccl) {
+    nd.comms.assign(G, nullptr);
+    MNCCL(rccl().comm_init_all(nd.comms.data(), G, devices));
+  }
+  if (comb) comb->exchange = nd.use_rccl ? 1 : 0;
+
+  // ---- the chains, one amcmc batch at a time on every device; progress between batches
+  for (int it = 0; it < n_samples; it += c->batch_length) {
+    rc = parallel(G, [&](int r) -> int {
+      Block& x = *nd.b[r];
+      return x.ses ? mk_session_run(x.ses, c->batch_length) : 0;
+    });
+    if (rc) return rc;
+    if (progress && progress(user, it + c->batch_length, n_samples))
+      return fail(MK_E_INTERRUPT, "interrupted after " + std::to_string(it + c->batch_length) + " of " +
+                                      std::to_string(n_samples) + " iterations");
+  }
+
+  // ---- per-subset outputs other than the grids (samples, w, draws, acceptance): each block
+  // writes its subsets' slice of the caller's arrays
+  ShardInfo info0{};
+  for (auto& x : nd.b)
+    if (x->ses) {
+      session_info(x->ses, &info0);
+      break;
+    }
+  const int P = info0.P, n_test = info0.n_test, n_kept = info0.n_kept;
+  const long C = (long)q * n_test;
+  const int n_theta = P - p;
+  const bool tiled = info0.tiled != 0;
+  auto shard_out = [&](const Block& x) {
+    mk_outputs o{};
+    if (!out) return o;
+    const long s0 = site0[x.lo];
+    if (out->samples) o.samples = out->samples + (size_t)x.lo * n_samples * P;
+    if (out->w_samples) o.w_samples = out->w_samples + (size_t)s0 * q * n_samples;
+    if (out->w_pred_samples) o.w_pred_samples = out->w_pred_samples + (size_t)x.lo * C * n_kept;
+    if (out->acceptance) o.acceptance = out->acceptance + (size_t)x.lo * c->n_batch * (p + n_theta + 1);
+    return o;
+  };
+  rc = parallel(G, [&](int r) -> int {
+    Block& x = *nd.b[r];
+    if (!x.ses) return 0;
+    mk_outputs o = shard_out(x);
+    if (tiled) o.w_pred_samples = nullptr;   // written per tile below
+    if (!o.samples && !o.w_samples && !o.w_pred_samples && !o.acceptance) return 0;
+    return mk_session_outputs(x.ses, &o);
+  });
+  if (rc) return rc;
+
+  // ---- parameter grids (MK.R:89) -> out->parameters, combine -> comb->result (MK.R:127)
+  const bool want_par = (out && out->parameters) || (comb && comb->result);
+  if (want_par) {
+    rc = parallel(G, [&](int r) -> int {
+      Block& x = *nd.b[r];
+      if (!x.ses) return 0;
+      int e = x.grids.ensure((size_t)x.S * P * L);
+      if (e || (e = session_param_grids(x.ses, x.grids.p))) return e;
+      if (out && out->parameters)
+        MHIP(hipMemcpy(out->parameters + (size_t)x.lo * P * L, x.grids.p, (size_t)x.S * P * L * 8, hipMemcpyDeviceToHost));
+      return 0;
+    });
+    if (rc) return rc;
+    if (comb && comb->result && (rc = exchange_combine(nd, P, comb, comb->result, nullptr))) return rc;
+  }
+
+  // ---- w.predict grids (MK.R:87-89) -> out->w_predict; combine -> comb->result2 (MK.R:133) and
+  // the sequential sum -> out->w_predict_sum
+  if (n_test > 0) {
+    double* h_w = out ? out->w_predict : nullptr;
+    double* h_sum = out ? out->w_predict_sum : nullptr;
+    double* h_comb = comb ? comb->result2 : nullptr;
+    const bool want_w = h_w || h_sum || h_comb || (tiled && out && out->w_pred_samples);
+    if (want_w && !tiled) {
+      rc = parallel(G, [&](int r) -> int {
+        Block& x = *nd.b[r];
+        if (!x.ses) return 0;
+        int e = x.grids.ensure((size_t)x.S * C * L);
+        if (e || (e = session_wpred_grids(x.ses, x.grids.p))) return e;
+        if (h_w) MHIP(hipMemcpy(h_w + (size_t)x.lo * C * L, x.grids.p, (size_t)x.S * C * L * 8, hipMemcpyDeviceToHost));
+        return 0;
+      });
+      if (rc) return rc;
+      if ((rc = exchange_combine(nd, C, comb, h_comb, h_sum))) return rc;
+    } else if (want_w) {
+      const int T = info0.pred_tile;
+      for (int t0 = 0; t0 < n_test; t0 += T) {
+        const long Ct = (long)q * std::min(T, n_test - t0);
+        rc = parallel(G, [&](int r) -> int {
+          Block& x = *nd.b[r];
+          if (!x.ses) return 0;
+          mk_outputs o = shard_out(x);
+          int e = x.grids.ensure((size_t)x.S * Ct * L);
+          if (e || (e = session_tile_grids(x.ses, t0, x.grids.p, &o))) return e;
+          if (h_w)   // per subset [C][200]: this tile's columns
+            MHIP(hipMemcpy2D(h_w + (size_t)x.lo * C * L + (size_t)t0 * q * L, (size_t)C * L * 8, x.grids.p,
+                             (size_t)Ct * L * 8, (size_t)Ct * L * 8, x.S, hipMemcpyDeviceToHost));
+          return 0;
+        });
+        if (rc) return rc;
+        if ((rc = exchange_combine(nd, Ct, comb, h_comb ? h_comb + (size_t)t0 * q * L : nullptr,
+                                   h_sum ? h_sum + (size_t)t0 * q * L : nullptr)))
+          return rc;
+      }
+    }
+  }
+  return 0;
+}

@@ -122,16 +122,11 @@ class SamplerConfig:
         return c, keep
 
 
-class Session:
-    """One shard of subsets resident on one GPU.
+class PackedProblem:
+    """mk_problem of a list of subsets (the R layout libmk reads: per subset column-major coords,
+    location-major y / weights, (n_s q) x p design), with the arrays it points into kept alive."""
 
-    subsets: list of dicts with 'coords' (n_s,2), 'y' (n_s*q,), 'weights' (n_s*q,), 'x' (n_s*q, p).
-    """
-
-    def __init__(self, subsets, cfg, coords_test=None, subset_base=0, device=0, record_w=False, lookahead=None):
-        lib = _lib.load()
-        self.cfg = cfg
-        self.q, self.p = cfg.q, cfg.p
+    def __init__(self, subsets, cfg, coords_test=None, subset_base=0):
         self.n_part = np.ascontiguousarray([s["coords"].shape[0] for s in subsets], dtype=np.int32)
         self.S = len(subsets)
         self.coords = _f64(np.concatenate([np.asarray(s["coords"], float).ravel(order="F") for s in subsets]))
@@ -149,6 +144,23 @@ class Session:
         pr.coords, pr.y, pr.weights, pr.x = dptr(self.coords), dptr(self.y), dptr(self.weights), dptr(self.x)
         pr.n_test = self.n_test
         pr.coords_test = dptr(self.coords_test) if self.coords_test is not None else None
+        self.c = pr
+
+
+class Session:
+    """One shard of subsets resident on one GPU.
+
+    subsets: list of dicts with 'coords' (n_s,2), 'y' (n_s*q,), 'weights' (n_s*q,), 'x' (n_s*q, p).
+    """
+
+    def __init__(self, subsets, cfg, coords_test=None, subset_base=0, device=0, record_w=False, lookahead=None):
+        lib = _lib.load()
+        self.cfg = cfg
+        self.q, self.p = cfg.q, cfg.p
+        self._prob = PackedProblem(subsets, cfg, coords_test, subset_base)
+        self.n_part, self.S = self._prob.n_part, self._prob.S
+        self.n_test, self.coords_test = self._prob.n_test, self._prob.coords_test
+        pr = self._prob.c
         c, self._keep = cfg.to_c(device=device, record_w=record_w)
         self.record_w = record_w
         h = ctypes.c_void_p()

@@ -84,7 +84,22 @@ def _config(q, p, starting, tuning, priors, amcmc, cov_model, burn_in=None, seed
 class SpMvGLMFit(dict):
     """Result of spMvGLM: keys 'p.beta.theta.samples' (n.samples x P), 'p.w.samples'
     ((n q) x n.samples), 'acceptance' (n.batch x (p + n_theta + 1)), plus the inputs
-    spPredict needs."""
+    spPredict needs.
+
+    The fit holds its device session (every recorded chain state, for spPredict) until
+    ``close()`` -- or the end of a ``with`` block, or garbage collection.  Close fits you no
+    longer predict from when fitting many subsets in a loop: each holds its factors in HBM."""
+
+    def close(self):
+        ses = self.pop("_session", None)
+        if ses is not None:
+            ses.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
 
 
 def spMvGLM(formula, coords, weights, starting, tuning, priors, amcmc, cov_model="exponential",
@@ -115,7 +130,9 @@ def spMvGLM(formula, coords, weights, starting, tuning, priors, amcmc, cov_model
 def spPredict(sp_obj, pred_coords, pred_covars=None, start=1, end=None, thin=1):
     """p.w.predictive.samples ((q n_test) x kept) for kept iterations start..end (1-based,
     inclusive; every thin-th), kriged from the chain states spMvGLM recorded (no refit)."""
-    ses = sp_obj["_session"]
+    ses = sp_obj.get("_session")
+    if ses is None:
+        raise ValueError("error: the spMvGLM fit was closed; spPredict needs its recorded chain states")
     n_samples = sp_obj["_n_samples"]
     end = n_samples if end is None else int(end)
     start = int(start)

@@ -250,7 +250,7 @@ def _c_sweep():
 
 
 def fit_subset(coords, y, wt, X, cfg, subset=0, coords_test=None, record_w=False,
-               quantiles=True, max_iter=None, sweep="py"):
+               quantiles=True, max_iter=None, sweep="py", site_index=None):
     """One subset: spMvGLM amcmc fit with fused spPredict on kept iterations.
 
     coords (n,2); y, wt (N=n*q) location-major; X (N,p) block-diagonal design.
@@ -259,7 +259,9 @@ def fit_subset(coords, y, wt, X, cfg, subset=0, coords_test=None, record_w=False
     q*n_test) predictive draws, and (if quantiles) 'param_q' (200,P), 'w_q'
     (200, q*n_test).  max_iter truncates the chain (bounded CPU timing).  sweep="c" runs step 5
     (the latent-w sweep) in oracle/csrc/sweep.c -- the same operations in the same order -- for
-    the CPU baseline's timing.
+    the CPU baseline's timing.  site_index (optional, [n_test] ints): the global index of each
+    test site, so a sub-sample of a large kriging set (configs[4]: 1M sites) draws the same
+    Philox streams as the device does for those sites (default 0..n_test-1).
     """
     q, p = cfg.q, cfg.p
     n = coords.shape[0]
@@ -319,6 +321,8 @@ def fit_subset(coords, y, wt, X, cfg, subset=0, coords_test=None, record_w=False
         n_test = coords_test.shape[0]
         Dt = distance_matrix(coords_test, coords)
         P_cache = [None] * q       # (phi,nu) -> (P_h, s_h)
+        site_ix = (np.arange(n_test, dtype=np.int64) if site_index is None
+                   else np.asarray(site_index, dtype=np.int64).reshape(n_test))
     else:
         n_test = 0
 
@@ -474,7 +478,7 @@ def fit_subset(coords, y, wt, X, cfg, subset=0, coords_test=None, record_w=False
                 _, Ph, sh = P_cache[h]
                 mean[:, h] = Ph @ G[:, h]
                 sd[:, h] = np.sqrt(np.maximum(1.0 - sh, 0.0))
-            idx = np.arange(n_test * q)
+            idx = (site_ix[:, None] * q + np.arange(q)[None, :]).reshape(-1)
             zt = philox.predict_normal(key, idx, key_s).reshape(n_test, q)
             draw = (mean + sd * zt) @ A.T                                # A(mean_h + sd_h z_h)
             w_pred[s - kept0] = draw.reshape(-1)

@@ -330,3 +330,36 @@ def test_sppredict_reuses_the_fit_without_refitting(mk, q, cov):
     # start + 2 .. 10, every 2nd, first 5 sites: rows (site, outcome) location-major
     sub = ref["w_pred_samples"][0][:5 * q, 2:10 - start + 1:2]
     assert np.array_equal(part, sub)
+
+
+def test_sppredict_at_the_reference_amcmc_length(mk):
+    """MK.R:83-87 as written: amcmc n.batch = 100 x batch.length = 50 (5,000 samples, every one of
+    them recorded by spMvGLM for spPredict), then spPredict(start = burn.in = 3,751, end = 5,000):
+    1,250 kept draws per site, equal to a session that fused the kriging into those iterations.
+    The fit's quantile grid of the 5,000 recorded samples is not needed, so no 2,048-sample cap
+    applies to the recording (the quantile sort takes up to 16,384)."""
+    n, n_test = 40, 6
+    d = mk.synthetic.generate(n, q=1, n_test=n_test, seed=88)
+    formula = [(d["y"], d["x"])]
+    starting = {"beta": np.zeros(2), "phi": 3 / 0.5, "A": np.ones(1), "w": 0.0}
+    tuning = {"beta": np.full(2, 0.05), "phi": 1.0, "A": 0.1, "w": 0.5}
+    priors = {"phi.Unif": (3 / 0.75, 3 / 0.25), "K.IW": (1, 0.1 * np.eye(1))}
+    amcmc = {"n.batch": 100, "batch.length": 50, "accept.rate": 0.43}
+    start = int(0.75 * 5000) + 1
+    with mk.spMvGLM(formula, d["coords"], np.ones((n, 1)), starting, tuning, priors, amcmc, seed=4) as fit:
+        assert fit["p.beta.theta.samples"].shape == (5000, 4)
+        pred = mk.spPredict(fit, d["coords_test"], start=start)["p.w.predictive.samples"]
+    assert pred.shape == (n_test, 5000 - start + 1)
+    with pytest.raises(ValueError):
+        mk.spPredict(fit, d["coords_test"], start=start)     # closed: the chain states are gone
+    from importlib import import_module
+    sb = import_module(mk.__name__ + ".spbayes")
+    cfg = sb._config(1, 2, starting, tuning, priors, amcmc, "exponential", burn_in=start, seed=4)
+    _, _, _, y, X, wt = sb._stack(formula, np.ones((n, 1)))
+    with mk.Session([dict(coords=d["coords"], y=y, weights=wt, x=X)], cfg, coords_test=d["coords_test"]) as ses:
+        ses.run(cfg.n_samples)
+        ref = ses.outputs(samples=True, w_pred_samples=True)
+    assert np.array_equal(fit["p.beta.theta.samples"], ref["samples"][0])
+    assert np.array_equal(pred, ref["w_pred_samples"][0])
+    # the 1,250-sample quantile grid of the reference workflow (MK.R:88-89)
+    assert np.array_equal(ref["w_predict"][0], r_quantile7(pred.T, PROBS200, axis=0))
