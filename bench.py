@@ -58,6 +58,8 @@ def parse():
                     help="strong (default): the one K-subset job split over the ranks; weak: K subsets per rank "
                          "(node job N*K)")
     ap.add_argument("--streams", type=int, default=0, help="HIP streams per GPU for subset groups (0: library default)")
+    ap.add_argument("--no-e2e", action="store_true",
+                    help="skip the measured end-to-end leg (N=1: the whole configs[2] script, ~2 minutes)")
     return ap.parse_args()
 
 
@@ -134,6 +136,32 @@ def _pmc_traffic():
             return json.load(f)["hbm_bytes_per_launch"]
     except (OSError, KeyError, ValueError):
         return None
+
+
+def end_to_end(mk, d, K):
+    """The whole reference script on this GPU (metakriging.reference_flow -> mk_meta_fit):
+    partition (R's stream) -> glm -> 5,000 amcmc iterations of every subset with spPredict on the
+    1,251 kept ones -> 200-level grids -> combine -> MK.R:136-165, wall clock per phase.  The
+    reference's own timer (MK.R:106-111) covers the foreach only: set-up + chains + quantiles."""
+    import time
+    marks = []
+    t0 = time.perf_counter()
+
+    def progress(it, n):      # spBayes's n.report = 10 batches (MK.R:84)
+        if it % 500 == 0:
+            marks.append((it, time.perf_counter() - t0))
+            print(f"e2e: {it}/{n} iterations, {marks[-1][1]:.1f}s", file=sys.stderr, flush=True)
+        return False
+
+    ph, result, result2, summ, cfg = mk.metakriging.reference_flow(d, K, 1, n_batch=100, batch_length=50,
+                                                                   seed=20250114, devices=(0,), progress=progress)
+    return {"phases": ph,
+            "reference_timer_s": ph["setup_s"] + ph["chains_s"] + ph["quantiles_combine_s"],
+            "chains_subset_iters_per_s": K * cfg.n_samples / ph["chains_s"],
+            "workload": f"configs[2] end to end on 1 GPU: n={len(d['coords'])}, K={K}, exponential, q=1, "
+                        f"n_test={len(d['coords_test'])}, 100 x 50 amcmc iterations, burn.in 3,750 "
+                        f"({cfg.kept} kept with spPredict), sequential-mean combine, 1,000-draw summary",
+            "param_median": summ["param_quant"][0].tolist()}
 
 
 def main():
@@ -218,6 +246,9 @@ def main():
     ses.run(n_post)
     kern = {name: {"ms": ses.kernel_stats(i)["ms"] - before[name]["ms"]} for name, i in kinds}
     ses.close()
+    e2e = None
+    if world == 1 and not a.no_e2e:
+        e2e = end_to_end(mk, d, K)
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
@@ -268,9 +299,28 @@ def main():
         "kernels_ms_per_step_note": f"untimed post-window pass of {n_post} iterations, every kernel kind evented",
         "end_to_end_estimate_s": elapsed / a.steps * 5000,
     }
+    if e2e is not None:
+        out["end_to_end_s"] = e2e["phases"]["end_to_end_s"]
+        out["end_to_end"] = e2e
     if cpu is not None:
         out["cpu_baseline"] = cpu
         out["gpu_over_cpu"] = value / cpu["value"]
+        # the port is one process per core (no shared state): its rate scales with cores.  Projections,
+        # labelled as such -- the job's CPU share on the box is cpu["cores"] cores
+        per_gpu_cores = max(1, cpu["host_nproc"] // 8)
+        out["cpu_projection"] = {
+            "note": "linear in cores (independent subsets, one process per core); not measured beyond the job's "
+                    f"{cpu['cores']}-core share",
+            "per_gpu_share_cores": per_gpu_cores,
+            "per_gpu_share_value": cpu["value"] * per_gpu_cores / cpu["cores"],
+            "gpu_over_per_gpu_share": value / (cpu["value"] * per_gpu_cores / cpu["cores"]),
+            "node_cores": cpu["host_nproc"],
+            "node_value": cpu["value"] * cpu["host_nproc"] / cpu["cores"],
+        }
+        if e2e is not None:
+            # the CPU port's wall clock for the same 250 x 5,000 subset-iterations (chains only)
+            out["cpu_projection"]["e2e_chains_s_at_node_cores"] = K * 5000 / out["cpu_projection"]["node_value"]
+            out["cpu_projection"]["e2e_chains_s_at_job_share"] = K * 5000 / cpu["value"]
     print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

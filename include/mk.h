@@ -128,6 +128,13 @@ int mk_session_outputs(mk_session* s, mk_outputs* out);
  * spPredict's start / end).  The draws are those a session with burn_in = first would make. */
 int mk_session_set_test_sites(mk_session* s, int32_t n_test, const double* coords_test);
 int mk_session_set_kept_window(mk_session* s, int32_t first, int32_t last);
+/* Tiled sessions (predict_tile > 0), after all iterations: the 200-level w.predict grids of the test
+ * sites of tile [t0, t0 + Tc) (Tc = min(predict_tile, n_test - t0), t0 a multiple of predict_tile),
+ * every subset: [n_subsets] x (200 x q*Tc) column-major, into out -- host memory, or HBM of the
+ * session's device when device_out != 0 (e.g. an RCCL send buffer).  Replays that tile's kriging
+ * only (spPredict, MK.R:87-89), so a host can combine tile by tile: at configs[4] the per-subset
+ * grids of all 1M sites never coexist. */
+int mk_session_tile_grids(mk_session* s, int32_t t0, double* out, int32_t device_out);
 /* Per-kernel timing (HIP events on the launching streams): launches, total ms and
  * algorithmic flops per kernel kind (0 Cholesky panel update, 128-tiles; 1 diagonal tile;
  * 2 panel trsm; 3 latent sweep; 4 R^-1 diagonal tiles; 5 whole iterations; 6 inverse levels;

@@ -670,9 +670,10 @@ static bool la_auto(const mk_session* s) { return (long)s->S * s->q <= 224; }
 // sweep (q W panels per block, q x 64 MH steps) is the iteration's longest chain and the
 // cooperative kernel wins: q = 3, 7 subsets 1,050 -> 1,601, 13 subsets 1,553 -> 1,956 subset-iters/s
 // (25 subsets: equal).
-// The q >= 2 gain is not taken by default: in one round-end style run of the GPU suite a q = 3
-// lookahead replay stalled with the plainly launched cooperative kernel (not reproduced; the
-// one-workgroup kernel has no inter-workgroup waits).  MK_SWEEP=2 opts in.
+// The cooperative kernel's q >= 2 gain is not taken by default: runs of the GPU suite with it
+// stalled in session create / destroy.  q >= 2 small shards use the split-launch
+// sweep instead (no inter-workgroup waits; q = 3: 7 subsets 1,050 -> 1,213, 13 subsets 1,553 ->
+// 1,657 subset-iters/s, r03b); MK_SWEEP=2 opts in to the cooperative kernel.
 static bool use_sweep_mg(const mk_session* s) { return s->sweep_mg && (!s->la || s->sweep_mg_forced); }
 
 static void launch_sweep(mk_session* s, Group& g, int it) {
@@ -1353,7 +1354,10 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
     // the iteration's longest chain), else the cooperative kernel on small sequential shards
     s->sweep_split = mode == 3 || (mode == 0 && q >= 2 && S <= 16);
     s->sweep_mg = !s->sweep_split && fits && (mode == 2 || (mode == 0 && (long)S * 4 <= n_cu));
-    s->sweep_mg_forced = s->sweep_mg && mode == 2;
+    // under the lookahead schedule the sweep runs on the CU-masked main stream, beside the candidates'
+    // chain: MK_SWEEP=2 is honoured there only when its grid fits the CUs that mask leaves
+    const int mask_cu = tile_env("MK_LA_MASK", 32);
+    s->sweep_mg_forced = s->sweep_mg && mode == 2 && grid <= (long)per_cu * std::max(0, n_cu - mask_cu);
     if (s->sweep_split) {
       HIPCHK(hipFuncSetAttribute(sweep_split_kernel(q, true), hipFuncAttributeMaxDynamicSharedMemorySize,
                                  q * (64 * 64 + 2 * 64) * 8));
@@ -1663,6 +1667,21 @@ int session_tile_grids(mk_session* s, int t0, double* d_out, mk_outputs* o) {
   return predict_tile(s, t0, d_out, o);
 }
 }  // namespace mk
+
+extern "C" int mk_session_tile_grids(mk_session* s, int32_t t0, double* out, int32_t device_out) {
+  if (!s || !out) return set_err(MK_E_ARG, "null session/output");
+  if (!s->tiled) return set_err(MK_E_ARG, "tile grids need a session created with predict_tile > 0");
+  if (device_out) return session_tile_grids(s, t0, out, nullptr);
+  const long Tc = std::min(s->pred_tile, s->n_test_all - t0);
+  HIPCHK(hipSetDevice(s->device));
+  DevBufs scratch;
+  double* dq = scratch.get<double>((size_t)s->S * s->q * std::max(Tc, 1L) * MK_N_LEVELS);
+  if (!dq) return set_err(MK_E_NOMEM, "tile grid scratch");
+  const int rc = session_tile_grids(s, t0, dq, nullptr);
+  if (rc) return rc;
+  HIPCHK(hipMemcpy(out, dq, (size_t)s->S * s->q * Tc * MK_N_LEVELS * 8, hipMemcpyDeviceToHost));
+  return 0;
+}
 
 extern "C" int mk_session_outputs(mk_session* s, mk_outputs* o) {
   if (!s || !o) return set_err(MK_E_ARG, "null session/outputs");

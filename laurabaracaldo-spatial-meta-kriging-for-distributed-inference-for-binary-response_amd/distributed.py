@@ -163,6 +163,23 @@ def combine_partial_sums(partial, K, dist, device=None, gpu=0, combine_fn=None):
     return total / K
 
 
+def combine_tiles(tile_grids, n_test, tile, q, K, dist, method="mean", device=None, gpu=0, combine_fn=None):
+    """result2 of MK.R:129-133 -- or its Weiszfeld median -- at configs[4] scale, one test-site tile
+    at a time: tile_grids(t0) returns this rank's subsets' (n_local, 200, q*Tc) grids of sites
+    [t0, t0 + Tc) (Session.tile_grids: that tile's kriging replay only), and each tile goes through
+    the column-sharded exchange + combine (combine_sharded), so the combine is the sequential one
+    -- bit-identical to one GPU -- or the per-column median, and a rank holds K x 200 x q*tile/world
+    exchanged doubles, not K x 200 x q*n_test (400 GB at 1M sites).  Every rank calls it with the
+    same tiling (an empty shard passes (0, 200, q*Tc) grids)."""
+    out = np.zeros((200, q * n_test))
+    for t0 in range(0, n_test, tile):
+        tc = min(tile, n_test - t0)
+        local = np.asarray(tile_grids(t0), dtype=np.float64).reshape(-1, 200, q * tc)
+        out[:, t0 * q:(t0 + tc) * q] = combine_sharded(local, K, dist, method=method, device=device, gpu=gpu,
+                                                       combine_fn=combine_fn)
+    return out
+
+
 def meta_fit_distributed(y, x, weight, coords, q, index_part, coords_test, cfg, dist, device=0, method="mean"):
     """Fit this rank's shard of subsets on its GPU, then the one exchange: the column-sharded
     combine (MK.R:119-133; method="median" for the Weiszfeld extension).

@@ -140,3 +140,52 @@ def posterior_summary(result, result2, x_test, q=None, samplesize=1000, seed=202
     index: a 1-based index vector drawn by the caller (R's own stream)."""
     return _post_summary(result, result2, x_test, samplesize=samplesize, seed=seed, device=device, rng=rng,
                          index=index, link=link)
+
+
+def reference_flow(d, K, q, cov_model="exponential", n_batch=100, batch_length=50, seed=20250114, devices=(0,),
+                   method="mean", predict_tile=0, partition_method="R", samplesize=1000, progress=None):
+    """The reference script end to end in one process over the GPUs in `devices` (mk_meta_fit: the
+    subsets sharded over them in-library, the combine device to device):
+
+      partition                 MK.R:15-41    mk_partition_r (R's own index sets after set.seed)
+      glm start values          MK.R:53-55    device IRLS on the full data, once
+      foreach %dopar% worker    MK.R:100-114  every subset's spMvGLM + spPredict + 200-level grids
+      combine                   MK.R:119-133  sequential mean (or Weiszfeld median), per test-site
+                                              tile when predict_tile > 0 (configs[4])
+      resample, p(y=1), quant.  MK.R:136-165  posterior_summary
+
+    d: synthetic.generate output.  progress(iterations, n_samples) is called between amcmc batches
+    (return True to stop).  Returns (phases, result, result2, summary, cfg) -- phases in seconds of
+    wall clock: set-up (partition, glm, subset slicing), the chains (to the last batch boundary),
+    quantiles + combine, post-processing, and the whole."""
+    import time
+    from .node import meta_fit_node
+    t = {}
+    n = len(d["coords"])
+    t0 = time.perf_counter()
+    n_part, index_part = partition(n, K, seed=seed, method=partition_method)                 # MK.R:15-41
+    beta0, bt = start_values(d["y"], d["x"], 1.0, q, device=int(devices[0]))                 # MK.R:53-55
+    p = d["x"].shape[1]
+    cfg = SamplerConfig(q, p, beta0, bt, cov_model=cov_model, n_batch=n_batch, batch_length=batch_length, seed=seed,
+                        predict_tile=predict_tile)
+    subs = [subset_data(d["y"], d["x"], 1.0, d["coords"], q, index_part[i]) for i in range(K)]
+    t["setup_s"] = time.perf_counter() - t0
+    t1 = time.perf_counter()
+    stamp = {}
+
+    def _progress(it, n_samples):
+        if it >= n_samples:
+            stamp["chains"] = time.perf_counter()
+        return bool(progress(it, n_samples)) if progress is not None else False
+
+    fit = meta_fit_node(subs, cfg, coords_test=d["coords_test"], devices=devices, method=method, per_subset=False,
+                        progress=_progress)                                                  # MK.R:100-133
+    t3 = time.perf_counter()
+    t["chains_s"] = stamp.get("chains", t3) - t1
+    t["quantiles_combine_s"] = t3 - stamp.get("chains", t3)
+    t2 = time.perf_counter()
+    summ = posterior_summary(fit["result"], fit["result2"], d["x_test"], samplesize=samplesize, seed=seed,
+                             device=int(devices[0]))                                         # MK.R:136-165
+    t["post_s"] = time.perf_counter() - t2
+    t["end_to_end_s"] = time.perf_counter() - t0
+    return t, fit["result"], fit["result2"], summ, cfg

@@ -181,6 +181,15 @@ class Session:
         self.coords_test = _f64(ct.ravel(order="F"))
         check(self._lib.mk_session_set_test_sites(self._h, self.n_test, dptr(self.coords_test)))
 
+    def tile_grids(self, t0):
+        """Tiled session (predict_tile > 0), after the run: (S, 200, q*Tc) w.predict grids of test
+        sites [t0, t0 + Tc) -- one tile's kriging replay only (configs[4]'s per-tile combine)."""
+        T = self.cfg.predict_tile
+        Tc = min(T, self.n_test - int(t0))
+        out = np.zeros((self.S, self.q * Tc, _lib.N_LEVELS))
+        check(self._lib.mk_session_tile_grids(self._h, int(t0), out.ctypes.data_as(ctypes.c_void_p), 0))
+        return np.ascontiguousarray(np.transpose(out, (0, 2, 1)))
+
     def set_kept_window(self, first, last):
         """Replay only iterations first..last (1-based; spPredict's start / end) in the next outputs()."""
         check(self._lib.mk_session_set_kept_window(self._h, int(first), int(last)))

@@ -57,6 +57,9 @@ def main():
     ap.add_argument("--seed", type=int, default=20250114)
     ap.add_argument("--partition", default="R", choices=["R", "permutation"],
                     help="R: the subsets R draws after set.seed(seed) (mk_partition_r)")
+    ap.add_argument("--devices", default=None,
+                    help="one process, libmk's multi-device driver (mk_meta_fit) over these HIP devices, e.g. "
+                         "0,1,2,3,4,5,6,7 (a device may repeat: several shards on one GPU, device-copy exchange)")
     a = ap.parse_args()
     c = dict(CONFIGS[a.config])
     for k_arg, k_cfg in [("n", "n"), ("subsets", "K"), ("n_test", "n_test"), ("n_batch", "n_batch"),
@@ -64,6 +67,8 @@ def main():
         v = getattr(a, k_arg)
         if v is not None:
             c[k_cfg] = v
+    if a.devices is not None:
+        return node_main(a, c)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -95,23 +100,30 @@ def main():
     big = cfg.predict_tile > 0 and cfg.predict_tile < c["n_test"]
     C = q * c["n_test"]
     P = cfg.P
+    ses = None
     if subs:
-        with mk.Session(subs, cfg, coords_test=d["coords_test"], subset_base=lo, device=local) as ses:   # MK.R:108
-            for b in range(cfg.n_batch):          # progress every n.report = 10 batches (MK.R:84)
-                ses.run(cfg.batch_length)
-                if rank == 0 and (b + 1) % 10 == 0:
-                    print(f"batch {b + 1}/{cfg.n_batch}  {time.perf_counter() - t2:.1f}s", file=sys.stderr, flush=True)
-            t3 = time.perf_counter()
-            # 1M sites: per-subset parameter grids, w.predict only as this shard's partial sum
-            out = ses.outputs(quantiles=True, w_predict=not big, w_predict_sum=big)
+        ses = mk.Session(subs, cfg, coords_test=d["coords_test"], subset_base=lo, device=local)   # MK.R:108
+        for b in range(cfg.n_batch):          # progress every n.report = 10 batches (MK.R:84)
+            ses.run(cfg.batch_length)
+            if rank == 0 and (b + 1) % 10 == 0:
+                print(f"batch {b + 1}/{cfg.n_batch}  {time.perf_counter() - t2:.1f}s", file=sys.stderr, flush=True)
+        t3 = time.perf_counter()
+        # 1M sites (tiled kriging): the parameter grids now; w.predict tile by tile in the combine
+        out = ses.outputs(quantiles=True, w_predict=not big)
     else:                                         # K < world: this rank has no subsets, it joins the exchange
         t3 = time.perf_counter()
-        out = {"parameters": [], "w_predict": [], "w_predict_sum": np.zeros((200, C))}
+        out = {"parameters": [], "w_predict": []}
     t["fit_s"] = t3 - t2
     t["predict_quantiles_s"] = time.perf_counter() - t3
 
     t4 = time.perf_counter()
     par = np.stack(out["parameters"]) if out["parameters"] else np.zeros((0, 200, P))
+    tile = cfg.predict_tile
+
+    def tile_grids(t0):                           # this shard's grids of one test-site tile (kriging replay)
+        tc = min(tile, c["n_test"] - t0)
+        return ses.tile_grids(t0) if ses is not None else np.zeros((0, 200, q * tc))
+
     if world > 1:
         import torch
         dev = torch.device("cuda", local)
@@ -120,17 +132,23 @@ def main():
             wp = np.stack(out["w_predict"]) if out["w_predict"] else np.zeros((0, 200, C))
             result2 = dmod.combine_sharded(wp, K, dist, method=a.combine, device=dev, gpu=local)
         else:
-            # tiled kriging (cfg5): every rank holds only its shard's partial sum of w.predict;
-            # result2 = (S_0 + S_1 + ...) / K with the rank terms added in rank order
-            if a.combine != "mean":
-                raise SystemExit("error: --combine median needs the per-subset grids (not available with predict_tile)")
-            result2 = dmod.combine_partial_sums(out["w_predict_sum"], K, dist, device=dev, gpu=local)
+            # tiled kriging (cfg5): per test-site tile, the column-sharded exchange + combine of that
+            # tile's grids (sequential mean, or the Weiszfeld median per column)
+            result2 = dmod.combine_tiles(tile_grids, c["n_test"], tile, q, K, dist, method=a.combine, device=dev,
+                                         gpu=local)
     elif not big:
         obj = [{"parameters": out["parameters"][i], "w.predict": out["w_predict"][i]} for i in range(len(subs))]
         result, result2 = mk.combine_results(obj, device=local, method=a.combine)             # MK.R:123-133
-    else:   # tiled kriging (cfg5), one process: the partial sum over all K subsets is the whole sum
-        result = mk.combine(out["parameters"], device=local)
-        result2 = out["w_predict_sum"] / K
+    else:   # tiled kriging (cfg5), one process: every tile's K grids combined as they are replayed
+        result = mk.combine_results([{"parameters": g} for g in out["parameters"]], device=local,
+                                    method=a.combine)[0]
+        result2 = np.zeros((200, C))
+        for t0 in range(0, c["n_test"], tile):
+            g = tile_grids(t0)
+            result2[:, t0 * q:t0 * q + g.shape[2]] = mk.combine_results([{"parameters": x} for x in g], device=local,
+                                                                        method=a.combine)[0]
+    if ses is not None:
+        ses.close()
     t["combine_s"] = time.perf_counter() - t4
 
     t5 = time.perf_counter()
@@ -152,6 +170,37 @@ def main():
         print(json.dumps(rec), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def node_main(a, c):
+    """The script in one process over a device list (mk_meta_fit): shards, combine (mean or median,
+    per test-site tile at configs[4]) and post-processing without torch or a second process."""
+    mk = importlib.import_module(PKG)
+    devices = [int(x) for x in a.devices.split(",")]
+    t0 = time.perf_counter()
+    q, n, K = c["q"], c["n"], c["K"]
+    d = mk.synthetic.generate(n, q=q, n_test=c["n_test"], cov_model=1 if c["cov"] == "matern" else 0, seed=a.seed)
+    data_s = time.perf_counter() - t0
+
+    def progress(it, n_samples):
+        if it % (10 * c["batch_length"]) == 0:    # n.report = 10 batches (MK.R:84)
+            print(f"iterations {it}/{n_samples}  {time.perf_counter() - t0:.1f}s", file=sys.stderr, flush=True)
+        return False
+
+    ph, result, result2, summ, cfg = mk.metakriging.reference_flow(
+        d, K, q, cov_model=c["cov"], n_batch=c["n_batch"], batch_length=c["batch_length"], seed=a.seed,
+        devices=devices, method=a.combine, predict_tile=c.get("predict_tile", 0), partition_method=a.partition,
+        progress=progress)
+    ph["data_s"] = data_s
+    rec = dict(config=a.config, workload=c, devices=devices, combine=a.combine, phases=ph,
+               subset_iters_per_s=K * cfg.n_samples / ph["chains_s"])
+    truth = np.concatenate([d["beta_true"], [1.0] if q == 1 else [], [6.0] if q == 1 else []])
+    rec["param_median"] = summ["param_quant"][0].tolist()
+    rec["param_95ci"] = [summ["param_quant"][1].tolist(), summ["param_quant"][2].tolist()]
+    wq = summ["w_quant"]
+    rec["w_test_coverage_95"] = float(np.mean((d["w_test_true"] >= wq[1]) & (d["w_test_true"] <= wq[2])))
+    rec["truth_beta_phi"] = truth.tolist()
+    print(json.dumps(rec), flush=True)
 
 
 if __name__ == "__main__":

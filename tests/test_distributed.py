@@ -198,3 +198,55 @@ def test_partial_sums_and_empty_shards(K, C, world):
         assert np.array_equal(full, ref)
         np.testing.assert_allclose(full, one_gpu, rtol=1e-13, atol=1e-13)   # re-association only
         assert np.array_equal(small, small_ref)
+
+
+def _tile_worker(rank, world, port, K, n_test, tile, method, out_q):
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    from oracle.post import weiszfeld_median
+    from oracle.spmvglm import combine_mean
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    dmod = importlib.import_module(PKG + ".distributed")
+    lo, hi = dmod.shard_range(K, world, rank)
+    calls = []
+
+    def tile_grids(t0):             # this rank's subsets' grids of sites [t0, t0 + Tc)
+        calls.append(t0)
+        tc = min(tile, n_test - t0)
+        return np.stack([_grid_wide(k, n_test)[:, t0:t0 + tc] for k in range(lo, hi)]) if hi > lo \
+            else np.zeros((0, 200, tc))
+
+    fn = combine_mean if method == "mean" else (lambda g: weiszfeld_median(np.stack(g))[0])
+    full = dmod.combine_tiles(tile_grids, n_test, tile, 1, K, dist, method=method, combine_fn=fn)
+    out_q.put((rank, full, calls))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("K,n_test,tile,world,method", [(5, 11, 4, 2, "median"), (7, 9, 9, 2, "mean"),
+                                                        (1, 6, 4, 2, "median")])
+def test_tiled_combine_matches_whole_grid_combine(K, n_test, tile, world, method):
+    """configs[4]'s combine tile by tile: per test-site tile a column-sharded
+    exchange + combine of the subsets' grids of that tile; the assembled result equals the oracle's
+    combine of the whole grids (mean: bit for bit; Weiszfeld median (oracle/post.py): per column)."""
+    import torch.multiprocessing as mp
+    from oracle.post import weiszfeld_median
+    from oracle.spmvglm import combine_mean
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_tile_worker, args=(r, world, port, K, n_test, tile, method, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    grids = [_grid_wide(k, n_test) for k in range(K)]
+    ref = combine_mean(grids) if method == "mean" else weiszfeld_median(np.stack(grids))[0]
+    for rank, full, calls in res:
+        assert calls == list(range(0, n_test, tile))
+        if method == "mean":
+            assert np.array_equal(full, ref)
+        else:
+            np.testing.assert_allclose(full, ref, rtol=1e-14, atol=1e-14)

@@ -92,3 +92,19 @@ def test_node_progress_and_interrupt(mk):
         mk.meta_fit_node(subs, cfg, coords_test=ct, devices=[0], progress=lambda it, n: it >= 4)
     assert e.value.code == -5
     assert mk.load().mk_session_count() == 0
+
+
+def test_session_tile_grids_equal_the_whole_grids(mk):
+    """mk_session_tile_grids: one tile's kriging replay gives exactly the columns of the tiled
+    session's whole w.predict grids (the per-tile combine of configs[4] reads these)."""
+    subs, ct = _problem(mk, [90, 80], n_test=10, seed=12)
+    cfg = _cfg(mk, predict_tile=4)
+    with mk.Session(subs, cfg, coords_test=ct) as ses:
+        ses.run(cfg.n_samples)
+        whole = ses.outputs()["w_predict"]
+        for t0 in (0, 4, 8):
+            g = ses.tile_grids(t0)
+            tc = min(4, 10 - t0)
+            assert g.shape == (2, 200, tc)
+            for s in range(2):
+                assert np.array_equal(g[s], whole[s][:, t0:t0 + tc])

@@ -334,8 +334,8 @@ def test_sppredict_reuses_the_fit_without_refitting(mk, q, cov):
 
 def test_sppredict_at_the_reference_amcmc_length(mk):
     """MK.R:83-87 as written: amcmc n.batch = 100 x batch.length = 50 (5,000 samples, every one of
-    them recorded by spMvGLM for spPredict), then spPredict(start = burn.in = 3,751, end = 5,000):
-    1,250 kept draws per site, equal to a session that fused the kriging into those iterations.
+    them recorded by spMvGLM for spPredict), then spPredict(start = burn.in = 3,750, end = 5,000):
+    1,251 kept draws per site, equal to a session that fused the kriging into those iterations.
     The fit's quantile grid of the 5,000 recorded samples is not needed, so no 2,048-sample cap
     applies to the recording (the quantile sort takes up to 16,384)."""
     n, n_test = 40, 6
@@ -345,7 +345,7 @@ def test_sppredict_at_the_reference_amcmc_length(mk):
     tuning = {"beta": np.full(2, 0.05), "phi": 1.0, "A": 0.1, "w": 0.5}
     priors = {"phi.Unif": (3 / 0.75, 3 / 0.25), "K.IW": (1, 0.1 * np.eye(1))}
     amcmc = {"n.batch": 100, "batch.length": 50, "accept.rate": 0.43}
-    start = int(0.75 * 5000) + 1
+    start = int(0.75 * 5000)                 # MK.R:85-87: burn.in = 0.75 n.samples, start = burn.in
     with mk.spMvGLM(formula, d["coords"], np.ones((n, 1)), starting, tuning, priors, amcmc, seed=4) as fit:
         assert fit["p.beta.theta.samples"].shape == (5000, 4)
         pred = mk.spPredict(fit, d["coords_test"], start=start)["p.w.predictive.samples"]

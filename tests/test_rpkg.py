@@ -21,15 +21,19 @@ def _struct_fields(header, name):
 def test_every_config_and_problem_field_is_set_by_the_glue():
     h, c = _read("include", "mk.h"), _read("mkgpu", "src", "mk_r.c")
     for f in _struct_fields(h, "mk_config"):
-        assert re.search(r"\bc\.%s\s*=" % f, c), f"mk_r_fit leaves mk_config.{f} unset"
+        assert re.search(r"\bc->%s\s*=" % f, c), f"read_config leaves mk_config.{f} unset"
     for f in _struct_fields(h, "mk_problem"):
-        assert re.search(r"\bpr\.%s\s*=" % f, c), f"mk_r_fit leaves mk_problem.{f} unset"
+        assert re.search(r"\bpr->%s\s*=" % f, c), f"read_problem leaves mk_problem.{f} unset"
+    for f in _struct_fields(h, "mk_combined"):
+        if f != "exchange":    # an output
+            assert re.search(r"\bcb\.%s\s*=" % f, c), f"mk_r_fit leaves mk_combined.{f} unset"
 
 
 def test_call_registrations_match_c_signatures_and_r_calls():
     c, r = _read("mkgpu", "src", "mk_r.c"), _read("mkgpu", "R", "mkgpu.R")
     reg = dict((n, int(k)) for n, k in re.findall(r'\{"(\w+)", \(DL_FUNC\)&\w+, (\d+)\}', c))
-    assert set(reg) == {"mk_r_fit", "mk_r_combine", "mk_r_summary", "mk_r_glm"}
+    assert set(reg) == {"mk_r_fit", "mk_r_spmvglm", "mk_r_sppredict", "mk_r_combine", "mk_r_summary", "mk_r_glm",
+                        "mk_r_hw_queues"}
     for name, nargs in reg.items():
         sig = re.search(r"SEXP %s\((.*?)\) \{" % name, c, re.S).group(1)
         assert sig.count("SEXP") == nargs, name
@@ -72,3 +76,26 @@ def test_glue_calls_only_declared_entry_points():
             items += 1
         i += 1
     assert items == n_cfg, (items, n_cfg)
+
+
+def test_r_wrappers_mirror_the_reference_calls():
+    """mk_spMvGLM / mk_spPredict take spBayes's argument names as MK.R:80-87 passes them, the
+    fit runs batch by batch with the interrupt check, coordinates are coerced with as.matrix,
+    and mk_meta_fit hands its device list to the multi-device entry point."""
+    r, c = _read("mkgpu", "R", "mkgpu.R"), _read("mkgpu", "src", "mk_r.c")
+    sig = re.search(r"mk_spMvGLM <- function\((.*?)\) \{", r, re.S).group(1)
+    for arg in ("formula", "coords", "weights", "starting", "tuning", "priors", "amcmc", "cov.model", "n.report"):
+        assert re.search(r"\b%s\b" % re.escape(arg), sig), arg
+    sig = re.search(r"mk_spPredict <- function\((.*?)\) \{", r, re.S).group(1)
+    for arg in ("sp.obj", "pred.coords", "pred.covars", "start", "end"):
+        assert re.search(r"\b%s\b" % re.escape(arg), sig), arg
+    for field in ("p.beta.theta.samples", "p.w.samples", "p.w.predictive.samples"):
+        assert field in r
+    assert "devices = 0L" in r and "as.integer(devices)" in r
+    assert "R_ToplevelExec(check_interrupt" in c and "R_CheckUserInterrupt()" in c
+    assert "mk_meta_fit(&pr, &c, INTEGER(devices)" in c
+    assert c.count("mk_session_run(") == 1 and "for (int it = 0; it < n_samples; it += c.batch_length)" in c
+    assert r.count(".mk_coords(") >= 4          # coords, coords.test, pred.coords coerced
+    exports = re.search(r"export\((.*?)\)", _read("mkgpu", "NAMESPACE"), re.S).group(1)
+    for fn in ("mk_meta_fit", "mk_spMvGLM", "mk_spPredict", "mk_combine", "mk_posterior_summary"):
+        assert fn in exports
