@@ -21,6 +21,9 @@
 #include <dlfcn.h>
 #include <rccl/rccl.h>
 #include <algorithm>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -86,24 +89,71 @@ const Rccl& rccl() {
     if (e_ != ncclSuccess) return fail(MK_E_HIP, std::string(#x " -> ") + rccl().error_string(e_)); \
   } while (0)
 
-// Runs f(r) for r in [0, n) on n threads and returns the first failure with its message (the
-// library's error text is thread-local: it is carried back to the calling thread).
-template <typename F>
-int parallel(int n, F&& f) {
-  std::vector<int> rc(n, 0);
-  std::vector<std::string> msg(n);
-  std::vector<std::thread> th;
-  th.reserve(n);
-  for (int r = 0; r < n; ++r)
-    th.emplace_back([&, r] {
-      rc[r] = f(r);
-      if (rc[r]) msg[r] = mk_last_error();
-    });
-  for (auto& t : th) t.join();
-  for (int r = 0; r < n; ++r)
-    if (rc[r]) return fail(rc[r], "device block " + std::to_string(r) + ": " + msg[r]);
-  return 0;
-}
+// One persistent host thread per device block for the whole call (HIP's per-thread state stays
+// warm: a fresh thread per amcmc batch measured 2-4x slower chains on small shards, whose
+// iterations are bound by the host's launch rate).  run(f) executes f(r) on worker r for every r
+// and returns the first failure with its message (the library's error text is thread-local: it
+// is carried back to the calling thread).
+class Pool {
+ public:
+  explicit Pool(int n) : n_(n), rc_(n, 0), msg_(n) {
+    for (int r = 0; r < n; ++r) th_.emplace_back([this, r] { loop(r); });
+  }
+  ~Pool() {
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      stop_ = true;
+      ++gen_;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  int run(const std::function<int(int)>& f) {
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      job_ = &f;
+      pending_ = n_;
+      ++gen_;
+    }
+    cv_.notify_all();
+    std::unique_lock<std::mutex> lk(m_);
+    done_.wait(lk, [&] { return pending_ == 0; });
+    for (int r = 0; r < n_; ++r)
+      if (rc_[r]) return fail(rc_[r], "device block " + std::to_string(r) + ": " + msg_[r]);
+    return 0;
+  }
+
+ private:
+  void loop(int r) {
+    long seen = 0;
+    for (;;) {
+      const std::function<int(int)>* job;
+      {
+        std::unique_lock<std::mutex> lk(m_);
+        cv_.wait(lk, [&] { return gen_ != seen; });
+        seen = gen_;
+        if (stop_) return;
+        job = job_;
+      }
+      const int rc = (*job)(r);
+      std::string msg = rc ? mk_last_error() : "";
+      std::lock_guard<std::mutex> lk(m_);
+      rc_[r] = rc;
+      msg_[r] = std::move(msg);
+      if (--pending_ == 0) done_.notify_one();
+    }
+  }
+  int n_;
+  std::vector<int> rc_;
+  std::vector<std::string> msg_;
+  std::vector<std::thread> th_;
+  std::mutex m_;
+  std::condition_variable cv_, done_;
+  const std::function<int(int)>* job_ = nullptr;
+  long gen_ = 0;
+  int pending_ = 0;
+  bool stop_ = false;
+};
 
 // Device buffer that grows on demand (freed on its device).
 struct DBuf {
@@ -149,6 +199,7 @@ struct Block {
 };
 
 struct Node {
+  std::unique_ptr<Pool> pool;   // first member: its threads are joined after the blocks are freed
   int G = 0, K = 0;
   std::vector<std::unique_ptr<Block>> b;
   bool use_rccl = false;
@@ -172,7 +223,7 @@ int exchange_combine(Node& nd, long C, const mk_combined* comb, double* h_comb, 
   auto ncol = [&](int j) { return std::min(C, (long)(j + 1) * per) - col0(j); };
   const bool median = comb && comb->method == MK_COMBINE_MEDIAN;
   // pack: column block j of every subset of block r
-  int rc = parallel(G, [&](int r) -> int {
+  int rc = nd.pool->run([&](int r) -> int {
     Block& x = *nd.b[r];
     MHIP(hipSetDevice(x.dev));
     int e;
@@ -228,7 +279,7 @@ int exchange_combine(Node& nd, long C, const mk_combined* comb, double* h_comb, 
     }
   }
   // combine on the owner of each column block, in global subset order; columns to the host
-  return parallel(G, [&](int j) -> int {
+  return nd.pool->run([&](int j) -> int {
     Block& x = *nd.b[j];
     MHIP(hipSetDevice(x.dev));
     const long a = col0(j), cj = ncol(j);
@@ -281,6 +332,7 @@ extern "C" int mk_meta_fit(const mk_problem* pr, const mk_config* c, const int32
   Node nd;
   nd.G = G;
   nd.K = K;
+  nd.pool = std::make_unique<Pool>(G);
   bool distinct = true;
   for (int r = 0; r < G; ++r)
     for (int j = 0; j < r; ++j) distinct = distinct && devices[r] != devices[j];
@@ -299,7 +351,7 @@ extern "C" int mk_meta_fit(const mk_problem* pr, const mk_config* c, const int32
     x->grids.dev = x->send.dev = x->recv.dev = x->comb.dev = x->sum.dev = x->iters.dev = x->dev;
     nd.b.push_back(std::move(x));
   }
-  int rc = parallel(G, [&](int r) -> int {
+  int rc = nd.pool->run([&](int r) -> int {
     Block& x = *nd.b[r];
     MHIP(hipSetDevice(x.dev));
     MHIP(hipStreamCreateWithFlags(&x.st, hipStreamNonBlocking));
@@ -327,7 +379,7 @@ extern "C" int mk_meta_fit(const mk_problem* pr, const mk_config* c, const int32
 
   // ---- the chains, one amcmc batch at a time on every device; progress between batches
   for (int it = 0; it < n_samples; it += c->batch_length) {
-    rc = parallel(G, [&](int r) -> int {
+    rc = nd.pool->run([&](int r) -> int {
       Block& x = *nd.b[r];
       return x.ses ? mk_session_run(x.ses, c->batch_length) : 0;
     });
@@ -359,7 +411,7 @@ extern "C" int mk_meta_fit(const mk_problem* pr, const mk_config* c, const int32
     if (out->acceptance) o.acceptance = out->acceptance + (size_t)x.lo * c->n_batch * (p + n_theta + 1);
     return o;
   };
-  rc = parallel(G, [&](int r) -> int {
+  rc = nd.pool->run([&](int r) -> int {
     Block& x = *nd.b[r];
     if (!x.ses) return 0;
     mk_outputs o = shard_out(x);
@@ -372,7 +424,7 @@ extern "C" int mk_meta_fit(const mk_problem* pr, const mk_config* c, const int32
   // ---- parameter grids (MK.R:89) -> out->parameters, combine -> comb->result (MK.R:127)
   const bool want_par = (out && out->parameters) || (comb && comb->result);
   if (want_par) {
-    rc = parallel(G, [&](int r) -> int {
+    rc = nd.pool->run([&](int r) -> int {
       Block& x = *nd.b[r];
       if (!x.ses) return 0;
       int e = x.grids.ensure((size_t)x.S * P * L);
@@ -393,7 +445,7 @@ extern "C" int mk_meta_fit(const mk_problem* pr, const mk_config* c, const int32
     double* h_comb = comb ? comb->result2 : nullptr;
     const bool want_w = h_w || h_sum || h_comb || (tiled && out && out->w_pred_samples);
     if (want_w && !tiled) {
-      rc = parallel(G, [&](int r) -> int {
+      rc = nd.pool->run([&](int r) -> int {
         Block& x = *nd.b[r];
         if (!x.ses) return 0;
         int e = x.grids.ensure((size_t)x.S * C * L);
@@ -407,7 +459,7 @@ extern "C" int mk_meta_fit(const mk_problem* pr, const mk_config* c, const int32
       const int T = info0.pred_tile;
       for (int t0 = 0; t0 < n_test; t0 += T) {
         const long Ct = (long)q * std::min(T, n_test - t0);
-        rc = parallel(G, [&](int r) -> int {
+        rc = nd.pool->run([&](int r) -> int {
           Block& x = *nd.b[r];
           if (!x.ses) return 0;
           mk_outputs o = shard_out(x);
