@@ -207,6 +207,7 @@ struct mk_session {
   // split-launch sweep (k_sweep_tiles / k_sweep_block, no inter-workgroup waits): partial dots
   // [S][nt][q][64], the block's coefficients [S][q][64] and any-moved flags [S]
   bool sweep_split = false;
+  bool sweep_step = false;        // one launch per block (k_sweep_step); else two (MK_SWEEP=4)
   double* sp_part = nullptr;
   double* sp_dacc = nullptr;
   int* sp_any = nullptr;
@@ -588,7 +589,7 @@ static void launch_cholesky(mk_session* s, Group& g, int h0, int hc, const int* 
 // W = L^-1 of the listed pairs: diagonal tiles, then recursive doubling.
 static void launch_trinv(mk_session* s, Group& g, int max_entries, const int* list, const int* count) {
   const int nt = s->nt;
-  hipLaunchKernelGGL(k_inv_copydiag, dim3(max_entries * nt), dim3(256), 0, g.stream, g.ms, list, count);
+  hipLaunchKernelGGL(k_inv_copydiag, dim3(max_entries * nt * 8), dim3(256), 0, g.stream, g.ms, list, count);
   for (int sz = 1; sz < nt; sz *= 2) {
     const int npairs = (nt + 2 * sz - 1) / (2 * sz);
     // the grid is sized for every pair, but only the accepted candidates' factors are in the
@@ -685,10 +686,22 @@ static void launch_sweep(mk_session* s, Group& g, int it) {
     Model md = g.md;
     MatSet ms = g.ms;
     int iter = it;
-    double* part = s->sp_part + (long)g.s0 * nt * q * 64;
+    double* part = s->sp_part + (long)g.s0 * (s->sweep_step ? 2 : 1) * nt * q * 64;
     double* dacc = s->sp_dacc + (long)g.s0 * q * 64;
     int* any = s->sp_any + g.s0;
     const size_t lds = (size_t)q * (64 * 64 + 2 * 64) * sizeof(double);
+    if (s->sweep_step) {
+      const size_t lds_s = lds + 4 * MK_NB * sizeof(double);
+      for (int B = 0; B <= nblk; ++B) {
+        void* ta[] = {&md, &ms, &iter, &B, &part};
+        const hipError_t e = hipLaunchKernel(sweep_step_kernel(q), dim3(g.S * nt), dim3(256), ta, lds_s, g.stream);
+        if (e != hipSuccess) {
+          if (s->launch_err == hipSuccess) s->launch_err = e;
+          return;
+        }
+      }
+      return;
+    }
     for (int B = 0; B <= nblk; ++B) {
       void* ta[] = {&md, &ms, &iter, &B, &part, &dacc, &any};
       hipError_t e = hipLaunchKernel(sweep_split_kernel(q, false), dim3(g.S * nt), dim3(256), ta, 0, g.stream);
@@ -1324,6 +1337,8 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
   HIPCHK(hipMemsetAsync(md.z, 0, (size_t)S * q * n_pad * 8, s->stream));
   HIPCHK(hipMemsetAsync(md.Z, 0, (size_t)S * q * q * n_pad * 8, s->stream));
   HIPCHK(hipMemsetAsync(ms.W, 0, (size_t)S * q * n_pad * n_pad * 8, s->stream));
+  // upper triangles of the Winv tiles stay zero (k_chol_diag writes the lower triangles only)
+  HIPCHK(hipMemsetAsync(ms.Winv, 0, (size_t)S * q * 2 * nt * MK_NB * MK_NB * 8, s->stream));
   {
     std::vector<double> probs(MK_N_LEVELS);
     // seq(0.005, 1, 0.005): from + (0:n)*by, pmin(x, to)  (MK.R:88)
@@ -1352,7 +1367,8 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
     // 0 (default): split launches for multi-outcome small shards (q >= 2, <= 16 subsets: the
     // one-workgroup sweep's q x 64 MH steps and q W panels per block on one CU per subset are
     // the iteration's longest chain), else the cooperative kernel on small sequential shards
-    s->sweep_split = mode == 3 || (mode == 0 && q >= 2 && S <= 16);
+    s->sweep_split = mode == 3 || mode == 4 || (mode == 0 && q >= 2 && S <= 16);
+    s->sweep_step = s->sweep_split && mode != 4;
     s->sweep_mg = !s->sweep_split && fits && (mode == 2 || (mode == 0 && (long)S * 4 <= n_cu));
     // under the lookahead schedule the sweep runs on the CU-masked main stream, beside the candidates'
     // chain: MK_SWEEP=2 is honoured there only when its grid fits the CUs that mask leaves
@@ -1361,7 +1377,9 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
     if (s->sweep_split) {
       HIPCHK(hipFuncSetAttribute(sweep_split_kernel(q, true), hipFuncAttributeMaxDynamicSharedMemorySize,
                                  q * (64 * 64 + 2 * 64) * 8));
-      if ((rc = s->alloc(&s->sp_part, (size_t)S * nt * q * 64)) || (rc = s->alloc(&s->sp_dacc, (size_t)S * q * 64)) ||
+      HIPCHK(hipFuncSetAttribute(sweep_step_kernel(q), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 q * (64 * 64 + 2 * 64) * 8 + 4 * MK_NB * 8));
+      if ((rc = s->alloc(&s->sp_part, (size_t)S * 2 * nt * q * 64)) || (rc = s->alloc(&s->sp_dacc, (size_t)S * q * 64)) ||
           (rc = s->alloc(&s->sp_any, (size_t)S)))
         return rc;
     }
@@ -2159,7 +2177,8 @@ extern "C" int mk_cholesky_batched(const double* A, int32_t S, int32_t n, double
   std::vector<int> hn(S, n);
   if (hipMemcpy(d_ns, hn.data(), S * 4, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(dA, A, (size_t)S * n * n * 8, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemset(ms.cur, 0, S * 4) != hipSuccess || hipMemset(md.info, 0, S * 4) != hipSuccess)
+      hipMemset(ms.cur, 0, S * 4) != hipSuccess || hipMemset(md.info, 0, S * 4) != hipSuccess ||
+      hipMemset(ms.Winv, 0, (size_t)S * 2 * nt * MK_NB * MK_NB * 8) != hipSuccess)
     return fail(set_err(MK_E_HIP, "cholesky upload"));
   if (hipFuncSetAttribute((const void*)k_chol_diag, hipFuncAttributeMaxDynamicSharedMemorySize,
                           MK_DIAG_LDS_BYTES) != hipSuccess || !set_gemm_lds())

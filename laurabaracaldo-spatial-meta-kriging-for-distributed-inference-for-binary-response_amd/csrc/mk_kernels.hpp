@@ -56,6 +56,16 @@ template <int Q>
 __global__ void k_sweep_tiles(Model md, MatSet ms, int iter, int B, double* part, const double* dacc_g, const int* any_g);
 template <int Q>
 __global__ void k_sweep_block(Model md, MatSet ms, int B, const double* part, double* dacc_g, int* any_g);
+template <int Q>
+__global__ void k_sweep_step(Model md, MatSet ms, int iter, int B, double* part);
+inline const void* sweep_step_kernel(int q) {
+  switch (q) {
+    case 1: return (const void*)k_sweep_step<1>;
+    case 2: return (const void*)k_sweep_step<2>;
+    case 3: return (const void*)k_sweep_step<3>;
+    default: return (const void*)k_sweep_step<4>;
+  }
+}
 // the split-launch sweep's two kernels for q outcomes
 inline const void* sweep_split_kernel(int q, bool block) {
   switch (q) {

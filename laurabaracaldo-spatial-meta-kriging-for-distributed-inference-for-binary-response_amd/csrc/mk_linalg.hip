@@ -624,18 +624,23 @@ __global__ __launch_bounds__(256) void k_chol_diag(MatSet ms, const int* __restr
     }
   }
   MK_TSTAMP(41);
+  // L and Winv_k out: 16-byte row pairs (rows r, r+1 of column c), values by selects (no divergent
+  // branches); pairs entirely above the diagonal are not stored -- the Winv slots are zeroed once
+  // when the session is created and never written there, and M's upper triangle is never read.
+  // The one upper element of a pair that straddles the diagonal gets a zero in both.
   double* W = winv_slot(ms, sh, slot, k);
-  for (int e = tid; e < MK_NB * MK_NB; e += 256) {
+#pragma unroll 4
+  for (int e0 = 0; e0 < MK_NB * MK_NB; e0 += 512) {
+    const int e = e0 + 2 * tid;
     const int r = e & 127, c = e >> 7;
-    if (r > c) {
-      Mt[r + (long)c * ld] = T[r + c * TLD];
-      W[r + c * MK_NB] = T[c + r * TLD];
-    } else if (r == c) {
-      Mt[r + (long)c * ld] = dg[r];
-      W[r + c * MK_NB] = xd[r];
-    } else {
-      W[r + c * MK_NB] = 0.0;
-    }
+    if (r + 1 < c) continue;
+    d2 lv, wv;
+    lv.x = (r > c) ? T[r + c * TLD] : ((r == c) ? dg[r] : 0.0);
+    lv.y = (r + 1 > c) ? T[r + 1 + c * TLD] : dg[r + 1];
+    wv.x = (r > c) ? T[c + r * TLD] : ((r == c) ? xd[r] : 0.0);
+    wv.y = (r + 1 > c) ? T[c + (r + 1) * TLD] : xd[r + 1];
+    *reinterpret_cast<d2*>(Mt + r + (long)c * ld) = lv;
+    *reinterpret_cast<d2*>(W + r + c * MK_NB) = wv;
   }
   MK_TSTAMP(42);
 }
@@ -643,28 +648,27 @@ __global__ __launch_bounds__(256) void k_chol_diag(MatSet ms, const int* __restr
 // ---------------------------------------------------------------- inverse (W = L^-1, persistent)
 __device__ inline double* wmat(const MatSet& ms, int sh) { return ms.W + (long)sh * mat_elems(ms); }
 
+// Eight workgroups per 128-tile, each copying one eighth of it (16 rows' worth: 2,048
+// doubles) with every load in flight at once: the copy is latency-bound (one tile per workgroup
+// took 100-150 us per launch at small shards, on the main stream's critical path).
+#define MK_CD_SPLIT 8
 __global__ __launch_bounds__(256) void k_inv_copydiag(MatSet ms, const int* __restrict__ list, const int* __restrict__ count) {
-  const int e = blockIdx.x / ms.nt, k = blockIdx.x % ms.nt;
+  const int part = blockIdx.x % MK_CD_SPLIT, rest = blockIdx.x / MK_CD_SPLIT;
+  const int e = rest / ms.nt, k = rest % ms.nt;
   if (e >= *count) return;
   const int sh = list[e];
   const double* Wd = winv_slot(ms, sh, ms.cur[sh], k);
   const long ld = ms.ld;
   double* Wt = wmat(ms, sh) + k * MK_NB + (long)k * MK_NB * ld;
-  // 16-byte row pairs, 16 loads in flight per thread (one dependent round trip per element made
-  // this copy 100-150 us per launch, on the main stream's critical path at small shards)
-#pragma unroll 1
-  for (int e0 = 0; e0 < MK_NB * MK_NB; e0 += 256 * 2 * 16) {
-    d2 v[16];
+  constexpr int PER = MK_NB * MK_NB / MK_CD_SPLIT;   // doubles per workgroup: 16 columns
+  const int e0 = part * PER;
+  d2 v[PER / 512];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int e = e0 + 2 * (threadIdx.x + 256 * j);
-      v[j] = *reinterpret_cast<const d2*>(Wd + e);
-    }
+  for (int j = 0; j < PER / 512; ++j) v[j] = *reinterpret_cast<const d2*>(Wd + e0 + 2 * (threadIdx.x + 256 * j));
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int e = e0 + 2 * (threadIdx.x + 256 * j);
-      *reinterpret_cast<d2*>(Wt + (e & 127) + (long)(e >> 7) * ld) = v[j];
-    }
+  for (int j = 0; j < PER / 512; ++j) {
+    const int e2 = e0 + 2 * (threadIdx.x + 256 * j);
+    *reinterpret_cast<d2*>(Wt + (e2 & 127) + (long)(e2 >> 7) * ld) = v[j];
   }
 }
 

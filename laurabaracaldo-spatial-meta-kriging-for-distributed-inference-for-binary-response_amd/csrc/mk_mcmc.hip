@@ -886,6 +886,134 @@ __global__ __launch_bounds__(256) void k_sweep_block(Model md, MatSet ms, int B,
   }
 }
 
+// Split-launch sweep, one launch per block: launch B is k_sweep_tiles(B) with k_sweep_block(B-1)
+// folded in as a prologue that every tile workgroup of the subset runs redundantly -- the same
+// partials summed in the same order, the same Q_BB and draws, so every copy makes the same
+// decisions and computes the same delta' (the owner tile, tf, records the accept flags).  Half the
+// launches of the two-kernel form.  The partials are double-buffered by block parity (launch B
+// reads block B-1's while it writes block B's).  part: [S][2][nt][q][64].
+template <int Q>
+__global__ __launch_bounds__(256) void k_sweep_step(Model md, MatSet ms, int iter, int B, double* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  constexpr int q = Q;
+  double* Qb = smem;                              // [q][SW_B*SW_B]
+  double* gb = Qb + q * SW_B * SW_B;              // [q][SW_B]
+  double* dacc = gb + q * SW_B;                   // [q][SW_B]
+  double* red = dacc + q * SW_B;                  // [4][MK_NB]
+  __shared__ double Ai[MK_QMAX * MK_QMAX];
+  __shared__ int any_acc;
+  const int nt = ms.nt;
+  const int s = blockIdx.x / nt, t = blockIdx.x % nt;
+  const int ns = md.n_s[s];
+  const int tl = (ns - 1) / MK_NB;
+  if (t > tl) return;
+  const int n_blk = (ns + SW_B - 1) / SW_B;
+  if (B > n_blk) return;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const long ld = ms.ld;
+  const int r0 = MK_NB * t + 2 * lane;
+  const long pstride = (long)nt * q * SW_B;       // one parity buffer of a subset
+  double* ps = part + (long)s * 2 * pstride;
+  if (tid < q * q) Ai[tid] = md.Ainv[(long)s * q * q + tid];
+  if (B == 0) sweep_precompute(md, s, iter, MK_NB * t * q, min(MK_NB * (t + 1), ns) * q, tid, 256);
+  d2 zr[Q];
+#pragma unroll
+  for (int h = 0; h < Q; ++h) zr[h] = *reinterpret_cast<const d2*>(md.z + ((long)s * q + h) * md.n_pad + r0);
+  bool zdirty = false;
+  if (B > 0) {
+    const int bp = (B - 1) * SW_B, nbp = min(SW_B, ns - bp), tfp = bp / MK_NB;
+    if (t >= tfp) {
+      // ---- prologue: block B-1's MH steps (k_sweep_block), redundantly in every tile workgroup
+      const int off = bp % MK_NB;
+      for (int h = 0; h < q; ++h) {
+        const double* QBt = ms.QB + (((long)s * q + h) * nt + tfp) * MK_NB * MK_NB;
+        for (int e = tid; e < SW_B * SW_B; e += 256) {
+          const int r = e & (SW_B - 1), c = e / SW_B;
+          Qb[h * SW_B * SW_B + e] = QBt[(off + r) + (off + c) * MK_NB];
+        }
+      }
+      const double* pb = ps + ((B - 1) & 1) * pstride;
+      for (int e = tid; e < q * SW_B; e += 256) {
+        const int h = e / SW_B, i = e % SW_B;
+        const double* pp = pb + (long)h * SW_B + i;
+        double g = pp[(long)tfp * q * SW_B];
+        for (int u = tfp + 1; u <= tl; ++u) g = g + pp[(long)u * q * SW_B];
+        gb[e] = g;
+      }
+      __syncthreads();
+      if (wv == 0) {
+        const int anyl = sweep_block_mh_q<Q, false>(md, s, bp, nbp, gb, Qb, Ai, dacc, t == tfp);
+        if (lane == 0) any_acc = anyl;
+      }
+      __syncthreads();
+      // ---- z rows of tile t (rows >= bp) += W[:, B-1] delta'_{B-1}
+      if (any_acc) {
+        zdirty = true;
+        for (int h = 0; h < q; ++h) {
+          const double* Wt = ms.W + ((long)s * q + h) * (ld * ld) + (long)bp * ld + r0;
+          d2 wreg[16];
+#pragma unroll
+          for (int j = 0; j < 16; ++j) wreg[j] = *reinterpret_cast<const d2*>(Wt + (long)(wv + 4 * j) * ld);
+          d2 sw = {0.0, 0.0};
+#pragma unroll
+          for (int j = 0; j < 16; ++j) {
+            const int i = wv + 4 * j;
+            const double c = (i < nbp) ? dacc[h * SW_B + i] : 0.0;
+            sw.x = fma(wreg[j].x, c, sw.x);
+            sw.y = fma(wreg[j].y, c, sw.y);
+          }
+          red[wv * MK_NB + 2 * lane] = sw.x;
+          red[wv * MK_NB + 2 * lane + 1] = sw.y;
+          __syncthreads();
+          const double vx =
+              ((red[2 * lane] + red[MK_NB + 2 * lane]) + red[2 * MK_NB + 2 * lane]) + red[3 * MK_NB + 2 * lane];
+          const double vy = ((red[2 * lane + 1] + red[MK_NB + 2 * lane + 1]) + red[2 * MK_NB + 2 * lane + 1]) +
+                            red[3 * MK_NB + 2 * lane + 1];
+          __syncthreads();
+#pragma unroll
+          for (int hh = 0; hh < Q; ++hh) {
+            if (hh != h) continue;
+            if (r0 >= bp && r0 < ns) zr[hh].x += vx;
+            if (r0 + 1 >= bp && r0 + 1 < ns) zr[hh].y += vy;
+          }
+        }
+      }
+    }
+  }
+  if (B < n_blk) {
+    // ---- partial dots of tile t for block B's columns (tiles >= the block's first tile)
+    const int b0 = B * SW_B;
+    if (t >= b0 / MK_NB) {
+      double* pb = ps + (B & 1) * pstride + (long)t * q * SW_B;
+      for (int h = 0; h < q; ++h) {
+        const double* Wt = ms.W + ((long)s * q + h) * (ld * ld) + (long)b0 * ld + r0;
+        d2 wreg[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) wreg[j] = *reinterpret_cast<const d2*>(Wt + (long)(wv + 4 * j) * ld);
+        d2 zz = zr[0];
+#pragma unroll
+        for (int hh = 1; hh < Q; ++hh)
+          if (hh == h) zz = zr[hh];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const double a0 = (r0 >= b0 && r0 < ns) ? wreg[j].x * zz.x : 0.0;
+          const double a1 = (r0 + 1 >= b0 && r0 + 1 < ns) ? wreg[j].y * zz.y : 0.0;
+          const double p = wave_sum_dpp(a0 + a1);
+          if (lane == 0) pb[h * SW_B + wv + 4 * j] = p;
+        }
+      }
+    }
+  }
+  if (zdirty && wv == 0) {
+#pragma unroll
+    for (int h = 0; h < Q; ++h) *reinterpret_cast<d2*>(md.z + ((long)s * q + h) * md.n_pad + r0) = zr[h];
+  }
+  if (B == n_blk) {   // the subset's last block is done: apply this tile's accepted moves
+    __syncthreads();
+    sweep_apply(md, s, MK_NB * t, min(MK_NB * (t + 1), ns), Ai, tid, 256);
+  }
+}
+
 template __global__ void k_sweep<1>(Model, MatSet, int);
 template __global__ void k_sweep<2>(Model, MatSet, int);
 template __global__ void k_sweep<3>(Model, MatSet, int);
@@ -897,6 +1025,11 @@ template __global__ void k_sweep_mg<4>(Model, MatSet, int, double*, int*, int*, 
 #define MK_INST_SPLIT(Q)                                                                                   \
   template __global__ void k_sweep_tiles<Q>(Model, MatSet, int, int, double*, const double*, const int*); \
   template __global__ void k_sweep_block<Q>(Model, MatSet, int, const double*, double*, int*);
+#define MK_INST_STEP(Q) template __global__ void k_sweep_step<Q>(Model, MatSet, int, int, double*);
+MK_INST_STEP(1)
+MK_INST_STEP(2)
+MK_INST_STEP(3)
+MK_INST_STEP(4)
 MK_INST_SPLIT(1)
 MK_INST_SPLIT(2)
 MK_INST_SPLIT(3)

@@ -21,6 +21,7 @@ int main(int argc, char** argv) {
   const long me = (long)ld * ld;
   hipMalloc(&ms.L, (size_t)S * 2 * me * 8);
   hipMalloc(&ms.Winv, (size_t)S * 2 * nt * MK_NB * MK_NB * 8);
+  hipMemset(ms.Winv, 0, (size_t)S * 2 * nt * MK_NB * MK_NB * 8);
   hipMalloc(&ms.cur, S * 4);
   hipMemset(ms.cur, 0, S * 4);
   int* ns; double *ldp, *qc; int* info;
