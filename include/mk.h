@@ -128,6 +128,11 @@ int mk_session_outputs(mk_session* s, mk_outputs* out);
  * spPredict's start / end).  The draws are those a session with burn_in = first would make. */
 int mk_session_set_test_sites(mk_session* s, int32_t n_test, const double* coords_test);
 int mk_session_set_kept_window(mk_session* s, int32_t first, int32_t last);
+/* After all iterations: the shard's 200-level grids, [n_subsets] x (200 x C) column-major -- which 0:
+ * obj[[i]]$parameters (C = P), which 1: obj[[i]]$w.predict (C = q*n_test; fused sessions, tiled ones
+ * use mk_session_tile_grids) -- into out: host memory, or HBM of the session's device when
+ * device_out != 0 (e.g. the send buffer of a device-resident combine; no host round trip). */
+int mk_session_grids(mk_session* s, int32_t which, double* out, int32_t device_out);
 /* Tiled sessions (predict_tile > 0), after all iterations: the 200-level w.predict grids of the test
  * sites of tile [t0, t0 + Tc) (Tc = min(predict_tile, n_test - t0), t0 a multiple of predict_tile),
  * every subset: [n_subsets] x (200 x q*Tc) column-major, into out -- host memory, or HBM of the

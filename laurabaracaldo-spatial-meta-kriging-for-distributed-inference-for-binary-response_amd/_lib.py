@@ -83,6 +83,7 @@ EXPORTS = {
     "mk_session_lookahead": (ctypes.c_int32, [ctypes.c_void_p]),
     "mk_session_outputs": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Outputs)]),
     "mk_session_set_test_sites": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(ctypes.c_double)]),
+    "mk_session_grids": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32]),
     "mk_session_tile_grids": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32]),
     "mk_session_set_kept_window": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32]),
     "mk_session_profile": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32]),

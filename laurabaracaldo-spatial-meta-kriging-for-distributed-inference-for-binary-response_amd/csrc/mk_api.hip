@@ -1686,6 +1686,22 @@ int session_tile_grids(mk_session* s, int t0, double* d_out, mk_outputs* o) {
 }
 }  // namespace mk
 
+extern "C" int mk_session_grids(mk_session* s, int32_t which, double* out, int32_t device_out) {
+  if (!s || !out) return set_err(MK_E_ARG, "null session/output");
+  if (which != 0 && which != 1) return set_err(MK_E_ARG, "which must be 0 (parameters) or 1 (w.predict)");
+  if (which == 1 && s->tiled) return set_err(MK_E_ARG, "tiled sessions give w.predict grids per tile (mk_session_tile_grids)");
+  if (which == 1 && s->md.n_test < 1) return set_err(MK_E_ARG, "the session has no test sites");
+  const long C = which == 0 ? (long)s->P : (long)s->q * s->md.n_test;
+  HIPCHK(hipSetDevice(s->device));
+  DevBufs scratch;
+  double* d = out;
+  if (!device_out && !(d = scratch.get<double>((size_t)s->S * C * MK_N_LEVELS))) return set_err(MK_E_NOMEM, "grid scratch");
+  const int rc = which == 0 ? session_param_grids(s, d) : session_wpred_grids(s, d);
+  if (rc) return rc;
+  if (!device_out) HIPCHK(hipMemcpy(out, d, (size_t)s->S * C * MK_N_LEVELS * 8, hipMemcpyDeviceToHost));
+  return 0;
+}
+
 extern "C" int mk_session_tile_grids(mk_session* s, int32_t t0, double* out, int32_t device_out) {
   if (!s || !out) return set_err(MK_E_ARG, "null session/output");
   if (!s->tiled) return set_err(MK_E_ARG, "tile grids need a session created with predict_tile > 0");

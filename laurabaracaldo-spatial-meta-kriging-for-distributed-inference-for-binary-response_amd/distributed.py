@@ -93,7 +93,9 @@ def _device_combine(grids, method, gpu):
 def combine_sharded(local, K, dist, method="mean", device=None, gpu=0, combine_fn=None):
     """Column-sharded combine of K subset grids held by contiguous subset blocks of the ranks.
 
-    local: (n_local, L, C) grids of this rank's subsets (shard_range order).  One all-to-all
+    local: (n_local, L, C) grids of this rank's subsets (shard_range order) -- a NumPy array, or a
+    torch tensor already in HBM (e.g. Session.grids_device's (n_local, C, L) buffer transposed:
+    then nothing of the exchange touches the host until the combined grid).  One all-to-all
     exchange gives rank r every subset's grid for its column block; it combines them in global
     subset order -- "mean" is MK.R:123-133 in the reference's summation order (so the result is
     bit-identical to one GPU), "sum" the same without the 1/K, "median" the Weiszfeld extension
@@ -106,17 +108,21 @@ def combine_sharded(local, K, dist, method="mean", device=None, gpu=0, combine_f
     combine_fn(list of L x c grids) -> L x c overrides the combine (CPU tests)."""
     import torch
     world, rank = dist.get_world_size(), dist.get_rank()
-    local = np.asarray(local, dtype=np.float64)
-    L, C = local.shape[1], local.shape[2]
+    dev = torch.device("cpu") if device is None else torch.device(device)
+    on_gpu = dev.type == "cuda"
+    if isinstance(local, torch.Tensor):
+        # device-resident grids (Session.grids_device): the send buffer is packed in HBM
+        local_t = local.to(dev)
+    else:
+        local_t = torch.from_numpy(np.ascontiguousarray(np.asarray(local, dtype=np.float64)))
+    L, C = int(local_t.shape[1]), int(local_t.shape[2])
     per_k = shard_capacity(K, world)
     blocks = col_blocks(C, world)
     cmax = max(1, max(b - a for a, b in blocks))
-    dev = torch.device("cpu") if device is None else torch.device(device)
-    on_gpu = dev.type == "cuda"
-    send = torch.zeros((world, per_k, L, cmax), dtype=torch.float64)
+    send = torch.zeros((world, per_k, L, cmax), dtype=torch.float64, device=local_t.device)
     for r, (a, b) in enumerate(blocks):
-        if b > a and local.shape[0]:
-            send[r, :local.shape[0], :, :b - a] = torch.from_numpy(np.ascontiguousarray(local[:, :, a:b]))
+        if b > a and local_t.shape[0]:
+            send[r, :local_t.shape[0], :, :b - a] = local_t[:, :, a:b]
     send = send.to(dev)
     recv = torch.empty_like(send)
     _exchange(send, recv, dist)

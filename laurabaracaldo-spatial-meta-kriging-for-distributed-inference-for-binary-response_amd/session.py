@@ -181,6 +181,12 @@ class Session:
         self.coords_test = _f64(ct.ravel(order="F"))
         check(self._lib.mk_session_set_test_sites(self._h, self.n_test, dptr(self.coords_test)))
 
+    def grids_device(self, which, out_ptr):
+        """Write the shard's (S, C, 200) grids -- which 0 parameters, 1 w.predict -- into device memory
+        at out_ptr (HBM of the session's device, e.g. a torch CUDA tensor's data_ptr()): the
+        device-resident combine's input, no host round trip."""
+        check(self._lib.mk_session_grids(self._h, int(which), ctypes.c_void_p(int(out_ptr)), 1))
+
     def tile_grids(self, t0):
         """Tiled session (predict_tile > 0), after the run: (S, 200, q*Tc) w.predict grids of test
         sites [t0, t0 + Tc) -- one tile's kriging replay only (configs[4]'s per-tile combine)."""

@@ -109,7 +109,8 @@ def main():
                 print(f"batch {b + 1}/{cfg.n_batch}  {time.perf_counter() - t2:.1f}s", file=sys.stderr, flush=True)
         t3 = time.perf_counter()
         # 1M sites (tiled kriging): the parameter grids now; w.predict tile by tile in the combine
-        out = ses.outputs(quantiles=True, w_predict=not big)
+        # one process: the grids to the host for the combine; N > 1: they stay in HBM (shard_grids below)
+        out = ses.outputs(quantiles=True, w_predict=not big) if world == 1 else {"parameters": [], "w_predict": []}
     else:                                         # K < world: this rank has no subsets, it joins the exchange
         t3 = time.perf_counter()
         out = {"parameters": [], "w_predict": []}
@@ -127,10 +128,16 @@ def main():
     if world > 1:
         import torch
         dev = torch.device("cuda", local)
-        result = dmod.combine_sharded(par, K, dist, method=a.combine, device=dev, gpu=local)   # MK.R:123-127
+
+        def shard_grids(which, ncol):   # this shard's (S, 200, ncol) grids, written by libmk into HBM
+            g = torch.empty((len(subs), ncol, 200), dtype=torch.float64, device=dev)
+            if ses is not None:
+                ses.grids_device(which, g.data_ptr())
+            return g.transpose(1, 2)
+
+        result = dmod.combine_sharded(shard_grids(0, P), K, dist, method=a.combine, device=dev, gpu=local)   # MK.R:123-127
         if not big:
-            wp = np.stack(out["w_predict"]) if out["w_predict"] else np.zeros((0, 200, C))
-            result2 = dmod.combine_sharded(wp, K, dist, method=a.combine, device=dev, gpu=local)
+            result2 = dmod.combine_sharded(shard_grids(1, C), K, dist, method=a.combine, device=dev, gpu=local)
         else:
             # tiled kriging (cfg5): per test-site tile, the column-sharded exchange + combine of that
             # tile's grids (sequential mean, or the Weiszfeld median per column)
