@@ -60,6 +60,9 @@ def parse():
     ap.add_argument("--streams", type=int, default=0, help="HIP streams per GPU for subset groups (0: library default)")
     ap.add_argument("--no-e2e", action="store_true",
                     help="skip the measured end-to-end leg (N=1: the whole configs[2] script, ~2 minutes)")
+    ap.add_argument("--e2e-devices", default="0",
+                    help="GPUs of the end-to-end leg, one process through libmk's multi-device driver "
+                         "(mk_meta_fit), e.g. 0,1,2,3,4,5,6,7 on a node")
     return ap.parse_args()
 
 
@@ -138,7 +141,7 @@ def _pmc_traffic():
         return None
 
 
-def end_to_end(mk, d, K):
+def end_to_end(mk, d, K, devices=(0,)):
     """The whole reference script on this GPU (metakriging.reference_flow -> mk_meta_fit):
     partition (R's stream) -> glm -> 5,000 amcmc iterations of every subset with spPredict on the
     1,251 kept ones -> 200-level grids -> combine -> MK.R:136-165, wall clock per phase.  The
@@ -154,11 +157,13 @@ def end_to_end(mk, d, K):
         return False
 
     ph, result, result2, summ, cfg = mk.metakriging.reference_flow(d, K, 1, n_batch=100, batch_length=50,
-                                                                   seed=20250114, devices=(0,), progress=progress)
+                                                                   seed=20250114, devices=devices, progress=progress)
     return {"phases": ph,
             "reference_timer_s": ph["setup_s"] + ph["chains_s"] + ph["quantiles_combine_s"],
             "chains_subset_iters_per_s": K * cfg.n_samples / ph["chains_s"],
-            "workload": f"configs[2] end to end on 1 GPU: n={len(d['coords'])}, K={K}, exponential, q=1, "
+            "devices": list(devices),
+            "workload": f"configs[2] end to end on {len(devices)} GPU(s), one process: n={len(d['coords'])}, K={K}, "
+                        f"exponential, q=1, "
                         f"n_test={len(d['coords_test'])}, 100 x 50 amcmc iterations, burn.in 3,750 "
                         f"({cfg.kept} kept with spPredict), sequential-mean combine, 1,000-draw summary",
             "param_median": summ["param_quant"][0].tolist()}
@@ -248,7 +253,7 @@ def main():
     ses.close()
     e2e = None
     if world == 1 and not a.no_e2e:
-        e2e = end_to_end(mk, d, K)
+        e2e = end_to_end(mk, d, K, tuple(int(x) for x in a.e2e_devices.split(",")))
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()

@@ -21,6 +21,7 @@
 #include <dlfcn.h>
 #include <rccl/rccl.h>
 #include <algorithm>
+#include <cstdio>
 #include <condition_variable>
 #include <functional>
 #include <mutex>
@@ -372,8 +373,18 @@ extern "C" int mk_meta_fit(const mk_problem* pr, const mk_config* c, const int32
   });
   if (rc) return rc;
   if (nd.use_rccl) {
+    // RCCL checks the calling thread's sticky HIP error: clear anything an earlier call left there.
+    // A communicator that cannot be created (seen once in a long test process, "unhandled cuda
+    // error") degrades to the device-copy exchange -- same results, reported in comb->exchange.
+    (void)hipGetLastError();
     nd.comms.assign(G, nullptr);
-    MNCCL(rccl().comm_init_all(nd.comms.data(), G, devices));
+    const ncclResult_t e = rccl().comm_init_all(nd.comms.data(), G, devices);
+    if (e != ncclSuccess) {
+      std::fprintf(stderr, "libmk: ncclCommInitAll failed (%s); combining with device copies\n", rccl().error_string(e));
+      nd.comms.clear();
+      nd.use_rccl = false;
+      (void)hipGetLastError();
+    }
   }
   if (comb) comb->exchange = nd.use_rccl ? 1 : 0;
 

@@ -42,7 +42,7 @@ def test_node_equals_one_session_and_sequential_combine(mk, devices):
     ref = _session_reference(mk, subs, cfg, ct, base=2)
     got = mk.meta_fit_node(subs, cfg, coords_test=ct, devices=devices, subset_base=2, samples=True, w_samples=True,
                            w_pred_samples=True, acceptance=True, w_predict_sum=True)
-    assert got["exchange"] == ("rccl" if len(devices) == 1 else "copy")
+    assert got["exchange"] == "copy" if len(devices) > 1 else got["exchange"] in ("rccl", "copy")
     for k in ("parameters", "w_predict", "samples", "w_samples", "w_pred_samples", "acceptance"):
         for s in range(len(subs)):
             assert np.array_equal(got[k][s], ref[k][s]), (k, s)
@@ -108,3 +108,18 @@ def test_session_tile_grids_equal_the_whole_grids(mk):
             assert g.shape == (2, 200, tc)
             for s in range(2):
                 assert np.array_equal(g[s], whole[s][:, t0:t0 + tc])
+
+
+def test_node_exchanges_over_rccl_in_a_fresh_process():
+    """A process that starts with the node driver (the R host's situation, and bench.py's
+    end-to-end leg) builds an RCCL communicator and combines over it, bit-identically."""
+    import json
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    r = subprocess.run([sys.executable, os.path.join(here, "gpu_node_rccl.py")], capture_output=True, text=True,
+                       timeout=240, env=dict(os.environ, NCCL_DEBUG="WARN"))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["exchange"] == "rccl" and res["exact"], res

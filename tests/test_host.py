@@ -127,3 +127,26 @@ def test_summary_struct_matches_header(mk):
     body = re.search(r"typedef struct mk_summary \{(.*?)\} mk_summary;", src, flags=re.S).group(1)
     fields = re.findall(r"\b([A-Za-z_][A-Za-z0-9_]*)\s*;", body)
     assert fields == [f[0] for f in binding.Summary._fields_]
+
+
+def test_meta_fit_node_fails_loudly_without_gpu_and_checks_arguments(mk):
+    """mk_meta_fit (the node driver) validates its arguments before touching a device, and without a
+    GPU returns MK_E_NODEV (no CPU fallback); the Combined struct mirrors the header."""
+    binding = __import__(mk.__name__ + "._lib", fromlist=["x"])
+    src = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    body = re.search(r"typedef struct mk_combined \{(.*?)\} mk_combined;", src, flags=re.S).group(1)
+    fields = re.findall(r"\b([A-Za-z_][A-Za-z0-9_]*)\s*;", body)
+    assert fields == [f[0] for f in binding.Combined._fields_]
+    d = mk.synthetic.generate(40, q=1, n_test=3, seed=2)
+    subs = [dict(coords=d["coords"][:20], y=d["y"][:20], weights=np.ones(20), x=d["x"][:20]),
+            dict(coords=d["coords"][20:], y=d["y"][20:], weights=np.ones(20), x=d["x"][20:])]
+    cfg = mk.SamplerConfig(1, 2, [0, 0], [0.1, 0.1], n_batch=1, batch_length=2, burn_in=1)
+    with pytest.raises(ValueError):
+        mk.meta_fit_node(subs, cfg, coords_test=d["coords_test"], devices=[0], method="mode")
+    with pytest.raises(mk.MkError) as e:
+        mk.meta_fit_node(subs, cfg, coords_test=d["coords_test"], devices=[])
+    assert e.value.code == -1
+    if mk.load().mk_device_count() == 0:
+        with pytest.raises(mk.MkError) as e:
+            mk.meta_fit_node(subs, cfg, coords_test=d["coords_test"], devices=[0, 0])
+        assert e.value.code == -4
