@@ -1363,13 +1363,16 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
     const long grid = xcd_grid(S, nt);
     const int mode = tile_env("MK_SWEEP", 0);
     const bool fits = coop && grid <= (long)per_cu * n_cu && nt <= 32;
-    // MK_SWEEP: 1 one workgroup per subset, 2 cooperative multi-workgroup, 3 split launches;
-    // 0 (default): split launches for multi-outcome small shards (q >= 2, <= 16 subsets: the
-    // one-workgroup sweep's q x 64 MH steps and q W panels per block on one CU per subset are
-    // the iteration's longest chain), else the cooperative kernel on small sequential shards
+    // MK_SWEEP: 1 one workgroup per subset, 2 cooperative multi-workgroup, 3 split launches (one per
+    // block), 4 split launches (two per block); 0 (default): split launches for multi-outcome small
+    // shards (q >= 2, <= 16 subsets: the one-workgroup sweep's q x 64 MH steps and q W panels per
+    // block on one CU per subset are the iteration's longest chain), else one workgroup per subset.
+    // No default path launches a kernel whose workgroups wait on each other: the cooperative kernel
+    // (opt-in) was followed by intermittent stalls of the GPU suite -- once more in
+    // round 3, on the sequential schedule where it had been the default for <= 64 subsets.
     s->sweep_split = mode == 3 || mode == 4 || (mode == 0 && q >= 2 && S <= 16);
     s->sweep_step = s->sweep_split && mode != 4;
-    s->sweep_mg = !s->sweep_split && fits && (mode == 2 || (mode == 0 && (long)S * 4 <= n_cu));
+    s->sweep_mg = !s->sweep_split && fits && mode == 2;
     // under the lookahead schedule the sweep runs on the CU-masked main stream, beside the candidates'
     // chain: MK_SWEEP=2 is honoured there only when its grid fits the CUs that mask leaves
     const int mask_cu = tile_env("MK_LA_MASK", 32);
