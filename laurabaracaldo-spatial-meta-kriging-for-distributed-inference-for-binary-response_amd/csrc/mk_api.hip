@@ -208,6 +208,7 @@ struct mk_session {
   // [S][nt][q][64], the block's coefficients [S][q][64] and any-moved flags [S]
   bool sweep_split = false;
   bool sweep_step = false;        // one launch per block (k_sweep_step); else two (MK_SWEEP=4)
+  bool sweep_rows = false;        // one-workgroup sweep with rows owned by waves (k_sweep_rows, MK_SWEEP=5)
   double* sp_part = nullptr;
   double* sp_dacc = nullptr;
   int* sp_any = nullptr;
@@ -747,7 +748,10 @@ static void launch_sweep(mk_session* s, Group& g, int it) {
   MatSet ms = g.ms;
   int iter = it;
   void* args[] = {&md, &ms, &iter};
-  const hipError_t e = hipLaunchKernel(sweep_kernel(q, false), dim3(g.S), dim3(MK_SW_T), args, sw_lds, g.stream);
+  const hipError_t e =
+      s->sweep_rows ? hipLaunchKernel(sweep_rows_kernel(q), dim3(g.S), dim3(512), args,
+                                      sw_lds + (size_t)s->nt * q * 64 * sizeof(double), g.stream)
+                    : hipLaunchKernel(sweep_kernel(q, false), dim3(g.S), dim3(MK_SW_T), args, sw_lds, g.stream);
   if (e != hipSuccess && s->launch_err == hipSuccess) s->launch_err = e;
 }
 
@@ -1373,6 +1377,10 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
     s->sweep_split = mode == 3 || mode == 4 || (mode == 0 && q >= 2 && S <= 16);
     s->sweep_step = s->sweep_split && mode != 4;
     s->sweep_mg = !s->sweep_split && fits && mode == 2;
+    s->sweep_rows = mode == 5 && q <= 3 && nt <= 32;
+    if (s->sweep_rows)
+      HIPCHK(hipFuncSetAttribute(sweep_rows_kernel(q), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 q * (64 * 64 + 2 * 64) * 8 + nt * q * 64 * 8));
     // under the lookahead schedule the sweep runs on the CU-masked main stream, beside the candidates'
     // chain: MK_SWEEP=2 is honoured there only when its grid fits the CUs that mask leaves
     const int mask_cu = tile_env("MK_LA_MASK", 32);

@@ -57,6 +57,11 @@ __global__ void k_sweep_tiles(Model md, MatSet ms, int iter, int B, double* part
 template <int Q>
 __global__ void k_sweep_block(Model md, MatSet ms, int B, const double* part, double* dacc_g, int* any_g);
 template <int Q>
+__global__ void k_sweep_rows(Model md, MatSet ms, int iter);
+inline const void* sweep_rows_kernel(int q) {
+  return q == 1 ? (const void*)k_sweep_rows<1> : (q == 2 ? (const void*)k_sweep_rows<2> : (const void*)k_sweep_rows<3>);
+}
+template <int Q>
 __global__ void k_sweep_step(Model md, MatSet ms, int iter, int B, double* part);
 inline const void* sweep_step_kernel(int q) {
   switch (q) {

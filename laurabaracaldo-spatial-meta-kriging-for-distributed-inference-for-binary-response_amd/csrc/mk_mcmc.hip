@@ -552,6 +552,144 @@ __global__ __launch_bounds__(SW_T) void k_sweep(Model md, MatSet ms, int iter) {
   sweep_apply(md, s, 0, ns, Ai, tid, SW_T);
 }
 
+// One workgroup per subset, rows owned by waves (k_sweep's arithmetic, laid out for latency):
+// wave w of 8 owns the rows of tiles w, w + 8, w + 16, w + 24 (lane l: rows 128 t + 2 l, + 1) and
+// keeps their z in registers for the whole sweep, so a block's z update (panel B-1) and its dots (panel B) are one
+// pass over the wave's own rows -- no z round trip through memory and no per-column pass over
+// every tile: per block each wave issues its tile's loads of both panels in 16-column batches.
+// Same bits as k_sweep: the update is per row in the same column-residue FMA order (row pairs are
+// even-aligned in both, and a pair is never split by p0), the dots are the same per-tile DPP
+// reductions summed in tile order.  q <= 3 (LDS: Q_BB + the per-tile partials).
+#define SR_T 512                                  // k_sweep_rows: 8 waves, 2 per SIMD (256 VGPRs)
+#define SR_W (SR_T / 64)
+template <int Q>
+__global__ __launch_bounds__(SR_T) void k_sweep_rows(Model md, MatSet ms, int iter) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  constexpr int q = Q;
+  const int nt = ms.nt;
+  double* Qb = smem;                              // [q][SW_B*SW_B] column-major
+  double* gb = Qb + q * SW_B * SW_B;              // [q][SW_B]
+  double* dacc = gb + q * SW_B;                   // [q][SW_B]
+  double* part = dacc + q * SW_B;                 // [nt][q][SW_B] per-tile partial dots
+  __shared__ int any_acc;
+  __shared__ double Ai[MK_QMAX * MK_QMAX];
+  const int s = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int ns = md.n_s[s];
+  const long ld = ms.ld;
+  const int tl = (ns - 1) / MK_NB;
+  double* z = md.z + (long)s * q * md.n_pad;
+  if (tid < q * q) Ai[tid] = md.Ainv[(long)s * q * q + tid];
+  sweep_precompute(md, s, iter, 0, ns * q, tid, SR_T);
+  constexpr int NS = 4;                           // tile slots per wave: tiles wv, wv + 8, wv + 16, wv + 24
+  d2 zr[NS][Q];
+#pragma unroll
+  for (int k = 0; k < NS; ++k) {
+    const int r0 = MK_NB * (wv + SR_W * k) + 2 * lane;
+#pragma unroll
+    for (int h = 0; h < Q; ++h)
+      zr[k][h] = (wv + SR_W * k <= tl) ? *reinterpret_cast<const d2*>(z + (long)h * md.n_pad + r0) : d2{0.0, 0.0};
+  }
+  if (tid == 0) any_acc = 0;
+  __syncthreads();
+  int p0 = 0, pnb = 0;
+  for (int b0 = 0; b0 < ns + SW_B; b0 += SW_B) {
+    const int nb = min(SW_B, ns - b0);
+    const bool upd = pnb > 0 && any_acc;
+    const int tile = b0 / MK_NB;
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+      const int t = wv + SR_W * k;
+      if (t > tl) continue;
+      const int r0 = MK_NB * t + 2 * lane;
+      // ---- (a) own rows >= p0: z += W[:, prev block] delta'_prev (k_sweep's column-residue order)
+      if (upd && MK_NB * t + MK_NB > p0) {
+#pragma unroll
+        for (int h = 0; h < Q; ++h) {
+          const double* Wp = ms.W + ((long)s * q + h) * (ld * ld) + (long)p0 * ld + r0;
+          const double* da = dacc + h * SW_B;
+          d2 v4[4] = {{0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}};
+          for (int k0 = 0; k0 < pnb; k0 += 16) {
+            d2 wv2[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) wv2[u] = *reinterpret_cast<const d2*>(Wp + (long)min(k0 + u, pnb - 1) * ld);
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+              const double c = (k0 + u < pnb) ? da[k0 + u] : 0.0;
+              v4[u & 3].x = fma(wv2[u].x, c, v4[u & 3].x);
+              v4[u & 3].y = fma(wv2[u].y, c, v4[u & 3].y);
+            }
+          }
+          const double vx = ((v4[0].x + v4[1].x) + v4[2].x) + v4[3].x;
+          const double vy = ((v4[0].y + v4[1].y) + v4[2].y) + v4[3].y;
+          if (r0 >= p0 && r0 < ns) zr[k][h].x += vx;
+          if (r0 >= p0 && r0 + 1 < ns) zr[k][h].y += vy;
+        }
+      }
+      // ---- (b) own tile's partial dots of the block's columns (tiles >= the block's first tile)
+      if (nb > 0 && t >= tile) {
+#pragma unroll
+        for (int h = 0; h < Q; ++h) {
+          const double* Wb = ms.W + ((long)s * q + h) * (ld * ld) + (long)b0 * ld + r0;
+          for (int i0 = 0; i0 < nb; i0 += 16) {
+            d2 wv2[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) wv2[u] = *reinterpret_cast<const d2*>(Wb + (long)min(i0 + u, nb - 1) * ld);
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+              const double a0 = (r0 >= b0 && r0 < ns) ? wv2[u].x * zr[k][h].x : 0.0;
+              const double a1 = (r0 + 1 >= b0 && r0 + 1 < ns) ? wv2[u].y * zr[k][h].y : 0.0;
+              const double pp = wave_sum_dpp(a0 + a1);
+              if (lane == 0 && i0 + u < nb) part[((long)t * q + h) * SW_B + i0 + u] = pp;
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (nb <= 0) break;
+    if (tid == 0) any_acc = 0;
+    // ---- dots summed in tile order; Q_BB into LDS
+    for (int e = tid; e < q * SW_B; e += SR_T) {
+      const int h = e / SW_B, i = e % SW_B;
+      double g = part[((long)tile * q + h) * SW_B + i];
+      for (int t = tile + 1; t <= tl; ++t) g = g + part[((long)t * q + h) * SW_B + i];
+      gb[e] = (i < nb) ? g : 0.0;
+    }
+    const int off = b0 % MK_NB;
+    for (int h = 0; h < q; ++h) {
+      const double* QBt = ms.QB + (((long)s * q + h) * ms.nt + tile) * MK_NB * MK_NB;
+      for (int e = tid; e < SW_B * SW_B; e += SR_T) {
+        const int r = e & (SW_B - 1), c = e / SW_B;
+        const double v = QBt[(off + r) + (off + c) * MK_NB];
+        Qb[h * SW_B * SW_B + e] = (r < nb && c < nb) ? v : 0.0;
+      }
+    }
+    __syncthreads();
+    // ---- the block's sequential Metropolis steps (wave 0)
+    if (wv == 0) {
+      const int anyl = sweep_block_mh_q<Q, false>(md, s, b0, nb, gb, Qb, Ai, dacc, true);
+      if (lane == 0) any_acc = anyl;
+    }
+    __syncthreads();
+    p0 = b0;
+    pnb = nb;
+  }
+  // ---- write back own z rows; apply accepted moves
+#pragma unroll
+  for (int k = 0; k < NS; ++k) {
+    const int t = wv + SR_W * k;
+    if (t > tl) continue;
+    const int r0 = MK_NB * t + 2 * lane;
+#pragma unroll
+    for (int h = 0; h < Q; ++h) *reinterpret_cast<d2*>(z + (long)h * md.n_pad + r0) = zr[k][h];
+  }
+  __syncthreads();
+  sweep_apply(md, s, 0, ns, Ai, tid, SR_T);
+}
+template __global__ void k_sweep_rows<1>(Model, MatSet, int);
+template __global__ void k_sweep_rows<2>(Model, MatSet, int);
+template __global__ void k_sweep_rows<3>(Model, MatSet, int);
+
 // Multi-workgroup sweep (small shards).  Grid: xcd_grid(S, nt) workgroups of 256 threads,
 // cooperative (all co-resident); workgroup (s, t) owns rows [128t, 128t + 128) of subset s
 // (its z rows in registers, replicated in the four waves; its sites' proposals and final

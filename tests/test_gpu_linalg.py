@@ -115,7 +115,8 @@ def test_sub_tile_gemm_split_cholesky_and_multi_wg_sweep_are_bit_identical(tmp_p
     split two-stream Cholesky schedule (bulk update by panels < k-1 on a CU-masked stream, the
     rank-128 correction on the critical stream; the accumulator passes through fp64 memory) and
     the split-launch sweeps (MK_SWEEP=3: k_sweep_step, one launch per block; 4: k_sweep_tiles /
-    k_sweep_block, two), under both launch schedules,
+    k_sweep_block, two) and the row-owning one-workgroup sweep (5: k_sweep_rows), under both launch
+    schedules,
     and the kriging GEMM with P^T generated in LDS (MK_PRED_GEN=1, exponential model) against
     the default stored-P^T path (k_pred_PT writes the same exp(-phi d) values to HBM first).
     Also the split schedule's depth (MK_CHOL_DEPTH: the bulk update d critical steps ahead, the
@@ -140,6 +141,8 @@ def test_sub_tile_gemm_split_cholesky_and_multi_wg_sweep_are_bit_identical(tmp_p
                ("64", "1", "1", "0", "1", "1", "4", "1"),
                ("128", "3", "0", "0", "0", "2", "1", "1"),
                ("64", "4", "0", "0", "0", "2", "1", "1"),
+               ("128", "5", "1", "0", "0", "2", "1", "1"),
+               ("128", "5", "0", "0", "0", "2", "1", "0"),
                ("64", "3", "1", "0", "0", "2", "1", "0"),
                ("128", "1", "0", "0", "0", "2", "1", "0"))
     for cfg in configs:
