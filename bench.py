@@ -143,6 +143,18 @@ def _pmc_traffic():
         return None
 
 
+def hbm_subphases(kern, n_post, n_s):
+    """GB/s of the covariance assembly and the latent sweep over the post-window pass (per-kernel
+    HIP events), on algorithmic bytes, as a fraction of the HBM peak."""
+    out = {}
+    for name, per_subset in (("cov_candidate", lambda n: 4.0 * (n + 1) ** 2), ("w_sweep", lambda n: 4.0 * n * n)):
+        ms = kern[name]["ms"]
+        if ms > 0:
+            gbs = sum(per_subset(n) for n in n_s) * n_post / (ms * 1e-3) / 1e9
+            out[name] = {"GB/s": gbs, "frac_of_hbm_peak": gbs / HBM_PEAK_GBS}
+    return out
+
+
 def end_to_end(mk, d, K, devices=(0,)):
     """The whole reference script on this GPU (metakriging.reference_flow -> mk_meta_fit):
     partition (R's stream) -> glm -> 5,000 amcmc iterations of every subset with spPredict on the
@@ -252,7 +264,7 @@ def main():
     summed_ms = sts[0]["ms"] + sts[1]["ms"]
     # per-kernel breakdown: a separate untimed pass of n_post (kept) iterations, every kind evented
     kinds = [("chol_update", 0), ("chol_update_sub", 7), ("chol_diag", 1), ("chol_trsm", 2), ("w_sweep", 3),
-             ("qblocks", 4), ("inverse", 6)]
+             ("qblocks", 4), ("inverse", 6), ("cov_candidate", 10)]
     before = {name: ses.kernel_stats(i) for name, i in kinds}
     ses.profile(True)
     ses.run(n_post)
@@ -310,6 +322,10 @@ def main():
                                      if la else "update launches run alone on the stream (sequential schedule)")},
         "kernels_ms_per_step": {k: v["ms"] / n_post for k, v in kern.items()},
         "kernels_ms_per_step_note": f"untimed post-window pass of {n_post} iterations, every kernel kind evented",
+        # the HBM-bound sub-phases in GB/s, on algorithmic bytes per subset-iteration --
+        # the candidate's lower triangle written once (4 (n_s+1)^2 B), W read once by the sweep (4 n_s^2 B)
+        "hbm_subphases": hbm_subphases(kern, n_post, [len(s_["coords"]) for s_ in subs]),
+        "chain_iters_per_s": a.steps / elapsed,
         "end_to_end_estimate_s": elapsed / a.steps * 5000,
     }
     if e2e is not None:

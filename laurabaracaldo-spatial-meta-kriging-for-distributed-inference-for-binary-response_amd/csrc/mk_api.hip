@@ -61,15 +61,16 @@ extern "C" int mk_device_memory(int32_t device, int64_t* free_bytes, int64_t* to
 
 namespace {
 
-constexpr int NKSTAT = 10;
+constexpr int NKSTAT = 11;
 // KS_CHOL_UPDATE: the 128-tile panel-update launches (k_chol_update<128>); KS_CHOL_UPDATE_SUB:
 // the 64- / 32-sub-tile ones (small grids).  Together: the roofline kernel k_chol_update.
 // KS_UPDATE_BUSY: both, with the time of launches that overlap (the split schedule's bulk and
 // critical streams) counted once -- the union of their event intervals.
 // KS_PRED_VAR: the kriging GEMM k_pred_var; its flops assume every pair is refreshed (an upper
 // bound: only the pairs whose factor changed are in the list -- bench_kriging counts exactly).
+// KS_COV: the candidates' covariance assembly (k_cov_candidate, with k_matern_table for Matern).
 enum { KS_CHOL_UPDATE = 0, KS_CHOL_DIAG, KS_CHOL_TRSM, KS_SWEEP, KS_LAUUM, KS_ITER, KS_INV, KS_CHOL_UPDATE_SUB,
-       KS_UPDATE_BUSY, KS_PRED_VAR };
+       KS_UPDATE_BUSY, KS_PRED_VAR, KS_COV };
 
 struct Stat {
   long launches = 0;
@@ -767,7 +768,7 @@ static void iteration_pre_sweep(mk_session* s, Group& g, int it) {
   const int nkinds = s->matern ? 2 : 1;
   // the q outcomes' (phi_h, nu_h) steps are independent given u: one batched pass per kind
   for (int which = 0; which < nkinds; ++which) {
-    launch_candidates(md, g.ms, st, S * q, 0, q, which, it);
+    timed(s, st, KS_COV, 0.0, [&] { launch_candidates(md, g.ms, st, S * q, 0, q, which, it); });
     launch_cholesky(s, g, 0, q);
     hipLaunchKernelGGL(k_theta_mh, dim3((S * q + 63) / 64), dim3(64), 0, st, md, g.ms, 0, q, which, it);
   }
@@ -811,7 +812,7 @@ static int la_head(mk_session* s) {
 static void enqueue_candidates(mk_session* s, Group& g, int it, hipEvent_t after, int k_hi) {
   const int S = g.S, q = s->q, nt = s->nt;
   hipStreamWaitEvent(s->la_c, after, 0);
-  launch_candidates(g.md, g.ms, s->la_c, S * q, 0, q, 0 | MK_CAND_NOBORDER, it);
+  timed(s, s->la_c, KS_COV, 0.0, [&] { launch_candidates(g.md, g.ms, s->la_c, S * q, 0, q, 0 | MK_CAND_NOBORDER, it); });
   launch_cholesky(s, g, 0, q, nullptr, nullptr, s->la_c, s->la_ev.data(), 0, k_hi);
   s->la_next = it;
   s->la_enq = k_hi;
@@ -849,7 +850,7 @@ static void run_iteration_la(mk_session* s, int it) {
     // (k_nu_border into zc).  The next phi candidates follow on the same stream (they need nu_t).
     hipEventRecord(ev_d, M);
     hipStreamWaitEvent(s->la_c, ev_d, 0);
-    launch_candidates(md, g.ms, s->la_c, S * q, 0, q, 1, it);
+    timed(s, s->la_c, KS_COV, 0.0, [&] { launch_candidates(md, g.ms, s->la_c, S * q, 0, q, 1, it); });
     launch_cholesky(s, g, 0, q, nullptr, nullptr, s->la_c);
     hipLaunchKernelGGL(k_theta_mh, dim3((S * q + 63) / 64), dim3(64), 0, s->la_c, md, g.ms, 0, q, 1, it);
     hipLaunchKernelGGL(k_nu_border, dim3(S * q * ((s->n_pad + 255) / 256)), dim3(256), 0, s->la_c, md, g.ms);
