@@ -65,6 +65,9 @@ def parse():
     ap.add_argument("--e2e-devices", default="0",
                     help="GPUs of the end-to-end leg, one process through libmk's multi-device driver "
                          "(mk_meta_fit), e.g. 0,1,2,3,4,5,6,7 on a node")
+    ap.add_argument("--e2e-only", action="store_true",
+                    help="internal: run only the end-to-end leg on --e2e-devices and print its JSON (rank 0 of a "
+                         "multi-GPU bench starts this as a child process)")
     return ap.parse_args()
 
 
@@ -183,8 +186,29 @@ def end_to_end(mk, d, K, devices=(0,)):
             "param_median": summ["param_quant"][0].tolist()}
 
 
+def node_end_to_end(a, world):
+    """N > 1 (strong scaling): the same whole configs[2] script over the node's N GPUs through
+    mk_meta_fit (libmk's threads, RCCL combine) -- a fresh child process, started (not exec'd)
+    by rank 0 once every rank has closed its session; the other ranks wait on a CPU barrier."""
+    import subprocess
+    cmd = [sys.executable, os.path.abspath(__file__), "--e2e-only", "--n", str(a.n), "--subsets", str(a.subsets),
+           "--n-test", str(a.n_test), "--e2e-devices", ",".join(str(i) for i in range(world))]
+    try:
+        r = subprocess.run(cmd, stdout=subprocess.PIPE, text=True, timeout=1500)   # stderr: progress lines
+        if r.returncode != 0:
+            return {"error": f"exit {r.returncode}", "stdout_tail": r.stdout[-500:]}
+        return json.loads(r.stdout.strip().splitlines()[-1])
+    except Exception as e:          # the bench line is printed regardless
+        return {"error": repr(e)[:500]}
+
+
 def main():
     a = parse()
+    if a.e2e_only:
+        mk = importlib.import_module(PKG)
+        d = mk.synthetic.generate(a.n, q=1, n_test=a.n_test, seed=20250114)
+        print(json.dumps(end_to_end(mk, d, a.subsets, tuple(int(x) for x in a.e2e_devices.split(",")))), flush=True)
+        return
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -203,6 +227,7 @@ def main():
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", rank=rank, world_size=world)
+        cpu_group = dist.new_group(backend="gloo")   # waits that must not hold a GPU kernel
 
     mk = importlib.import_module(PKG)
     weak = a.scaling == "weak"
@@ -273,6 +298,10 @@ def main():
     e2e = None
     if world == 1 and not a.no_e2e:
         e2e = end_to_end(mk, d, K, tuple(int(x) for x in a.e2e_devices.split(",")))
+    elif world > 1 and not a.no_e2e and not weak:
+        if rank == 0:
+            e2e = node_end_to_end(a, world)
+        dist.barrier(group=cpu_group)
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
@@ -329,7 +358,8 @@ def main():
         "end_to_end_estimate_s": elapsed / a.steps * 5000,
     }
     if e2e is not None:
-        out["end_to_end_s"] = e2e["phases"]["end_to_end_s"]
+        if "phases" in e2e:
+            out["end_to_end_s"] = e2e["phases"]["end_to_end_s"]
         out["end_to_end"] = e2e
     if cpu is not None:
         out["cpu_baseline"] = cpu
