@@ -1376,7 +1376,7 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
     // (opt-in) was followed by intermittent stalls of the GPU suite -- once more in
     // round 3, on the sequential schedule where it had been the default for <= 64 subsets.
     s->sweep_split = mode == 3 || mode == 4 || (mode == 0 && q >= 2 && S <= 16);
-    s->sweep_step = s->sweep_split && mode != 4;
+    s->sweep_step = s->sweep_split && mode != 4 && nt <= 32;   // k_sweep_step sums <= 32 tile partials
     s->sweep_mg = !s->sweep_split && fits && mode == 2;
     s->sweep_rows = mode == 5 && q <= 3 && nt <= 32;
     if (s->sweep_rows)

@@ -943,7 +943,30 @@ __global__ __launch_bounds__(256) void k_trmv_Z(Model md, MatSet ms) {
     }
     __syncthreads();
     const int jend = min(MK_ZCH, jmax - j0);   // <= 0: nothing left for this row
+    // 64 column loads in flight per row (one HBM round trip per 64 columns, not per 8; the bytes in
+    // flight bound a single CU's bandwidth, and the bottom row block reads 2,000 columns); the
+    // products are added in ascending column order as before (same bits)
     int jj = 0;
+    for (; jj + 64 <= jend; jj += 64) {
+      double wv[64];
+#pragma unroll
+      for (int v = 0; v < 64; ++v) wv[v] = Wm[(long)(j0 + jj + v) * ld];
+#pragma unroll
+      for (int v = 0; v < 64; ++v)
+#pragma unroll
+        for (int c = 0; c < MK_QMAX; ++c)
+          if (c < q) acc[c] += wv[v] * us[c][jj + v];
+    }
+    for (; jj + 32 <= jend; jj += 32) {
+      double wv[32];
+#pragma unroll
+      for (int v = 0; v < 32; ++v) wv[v] = Wm[(long)(j0 + jj + v) * ld];
+#pragma unroll
+      for (int v = 0; v < 32; ++v)
+#pragma unroll
+        for (int c = 0; c < MK_QMAX; ++c)
+          if (c < q) acc[c] += wv[v] * us[c][jj + v];
+    }
     for (; jj + 8 <= jend; jj += 8) {
       double wv[8];
 #pragma unroll

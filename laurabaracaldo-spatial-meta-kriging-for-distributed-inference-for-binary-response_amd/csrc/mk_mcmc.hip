@@ -53,6 +53,10 @@ __device__ inline double iw_logprior(const double* A, const double* Ai, int q, d
 }
 
 // ---------------------------------------------------------------- 1. beta_j (flat prior)
+// One workgroup per subset walks its n_s q sites once per beta_j: the loads of MK_BATCH strided
+// iterations are issued together before their terms are added (in the same order as a plain
+// strided loop: the same bits), so the loop pays the HBM latency once per batch, not per site.
+#define MK_BATCH 8
 __global__ __launch_bounds__(256) void k_beta(Model md, int iter) {
   __shared__ double red[8];
   const int s = blockIdx.x, tid = threadIdx.x;
@@ -67,9 +71,27 @@ __global__ __launch_bounds__(256) void k_beta(Model md, int iter) {
     const double delta = exp(md.tune[(long)s * md.n_mh_max + j]) * z;
     const double* xj = md.X + ((long)s * md.p + j) * md.Np;
     double loc = 0.0;
-    for (int k = tid; k < Ns; k += 256) {
-      const double e0 = eta[k];
-      loc += loglik_term(y[k], wt[k], e0 + delta * xj[k], md.link) - loglik_term(y[k], wt[k], e0, md.link);
+    for (int k0 = tid; k0 < Ns; k0 += 256 * MK_BATCH) {
+      double yv[MK_BATCH], wv[MK_BATCH], ev[MK_BATCH], xv[MK_BATCH];
+#pragma unroll
+      for (int u = 0; u < MK_BATCH; ++u) {
+        const int k = min(k0 + 256 * u, Ns - 1);   // clamped: in bounds, unused past Ns
+        yv[u] = y[k];
+        wv[u] = wt[k];
+        ev[u] = eta[k];
+        xv[u] = xj[k];
+      }
+      // the batch's terms are independent (no branch between them: their exp / log1p chains
+      // interleave); past-the-end entries add an exact +0.0 (loc is never -0.0), same bits
+      double tv[MK_BATCH];
+#pragma unroll
+      for (int u = 0; u < MK_BATCH; ++u) {
+        const double t =
+            loglik_term(yv[u], wv[u], ev[u] + delta * xv[u], md.link) - loglik_term(yv[u], wv[u], ev[u], md.link);
+        tv[u] = (k0 + 256 * u < Ns) ? t : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < MK_BATCH; ++u) loc += tv[u];
     }
     const double tot = block_sum<256>(loc, red);
     if (lu <= tot) {
@@ -95,14 +117,25 @@ __global__ __launch_bounds__(256) void k_Aphase(Model md, int iter) {
   const Key key = subset_key(md, s);
   double* z = md.z + (long)s * q * md.n_pad;
   const double* Z = md.Z + (long)s * q * q * md.n_pad;
-  // ---- T (symmetric in c,d)
+  // ---- T (symmetric in c,d); batched loads as in k_beta (same order, same bits)
   for (int h = 0; h < q; ++h)
     for (int c = 0; c < q; ++c)
       for (int d = c; d < q; ++d) {
         const double* zc = (q == 1) ? z : Z + ((long)h * q + c) * md.n_pad;
         const double* zd = (q == 1) ? z : Z + ((long)h * q + d) * md.n_pad;
         double loc = 0.0;
-        for (int i = tid; i < ns; i += 256) loc += zc[i] * zd[i];
+        for (int i0 = tid; i0 < ns; i0 += 256 * MK_BATCH) {
+          double a[MK_BATCH], b[MK_BATCH];
+#pragma unroll
+          for (int u = 0; u < MK_BATCH; ++u) {
+            const int i = min(i0 + 256 * u, ns - 1);
+            a[u] = zc[i];
+            b[u] = zd[i];
+          }
+#pragma unroll
+          for (int u = 0; u < MK_BATCH; ++u)
+            if (i0 + 256 * u < ns) loc += a[u] * b[u];
+        }
         const double tot = block_sum<256>(loc, red);
         if (tid == 0) { T[(h * q + c) * q + d] = tot; T[(h * q + d) * q + c] = tot; }
       }
@@ -182,7 +215,15 @@ __global__ __launch_bounds__(256) void k_Aphase(Model md, int iter) {
   // ---- current quadratic forms |z_h|^2 = u_h' R_h^-1 u_h for the phi / nu proposals
   for (int h = 0; h < q; ++h) {
     double loc = 0.0;
-    for (int i = tid; i < ns; i += 256) loc += z[(long)h * md.n_pad + i] * z[(long)h * md.n_pad + i];
+    const double* zh = z + (long)h * md.n_pad;
+    for (int i0 = tid; i0 < ns; i0 += 256 * MK_BATCH) {
+      double a[MK_BATCH];
+#pragma unroll
+      for (int u = 0; u < MK_BATCH; ++u) a[u] = zh[min(i0 + 256 * u, ns - 1)];
+#pragma unroll
+      for (int u = 0; u < MK_BATCH; ++u)
+        if (i0 + 256 * u < ns) loc += a[u] * a[u];
+    }
     const double tot = block_sum<256>(loc, red);
     if (tid == 0) md.quad[(long)s * q + h] = tot;
   }
@@ -1061,24 +1102,31 @@ __global__ __launch_bounds__(256) void k_sweep_step(Model md, MatSet ms, int ite
   if (B > 0) {
     const int bp = (B - 1) * SW_B, nbp = min(SW_B, ns - bp), tfp = bp / MK_NB;
     if (t >= tfp) {
-      // ---- prologue: block B-1's MH steps (k_sweep_block), redundantly in every tile workgroup
-      const int off = bp % MK_NB;
-      for (int h = 0; h < q; ++h) {
-        const double* QBt = ms.QB + (((long)s * q + h) * nt + tfp) * MK_NB * MK_NB;
-        for (int e = tid; e < SW_B * SW_B; e += 256) {
-          const int r = e & (SW_B - 1), c = e / SW_B;
-          Qb[h * SW_B * SW_B + e] = QBt[(off + r) + (off + c) * MK_NB];
-        }
-      }
+      // ---- prologue: block B-1's MH steps (k_sweep_block), redundantly in every tile workgroup.
+      // Q_BB by LDS-DMA (in flight while the partials load), the partials of tiles tfp .. tl all
+      // loaded before they are summed in tile order (same values, same order: same bits)
+      qbb_dma(md, ms, s, bp, Qb);
       const double* pb = ps + ((B - 1) & 1) * pstride;
       for (int e = tid; e < q * SW_B; e += 256) {
         const int h = e / SW_B, i = e % SW_B;
         const double* pp = pb + (long)h * SW_B + i;
-        double g = pp[(long)tfp * q * SW_B];
-        for (int u = tfp + 1; u <= tl; ++u) g = g + pp[(long)u * q * SW_B];
+        double pv[MK_NT_MAX_MG];
+#pragma unroll
+        for (int u = 0; u < MK_NT_MAX_MG; ++u) pv[u] = pp[(long)min(tfp + u, tl) * q * SW_B];
+        double g = pv[0];
+#pragma unroll
+        for (int u = 1; u < MK_NT_MAX_MG; ++u)
+          if (tfp + u <= tl) g = g + pv[u];
         gb[e] = g;
       }
+      __builtin_amdgcn_s_waitcnt(0);   // this wave's Q_BB DMA has landed
       __syncthreads();
+      // the update's first W panel streams in under the MH steps; each later panel under the
+      // previous one's arithmetic (same values, same arithmetic: same bits)
+      const double* Wu = ms.W + (long)s * q * (ld * ld) + (long)bp * ld + r0;
+      d2 wa[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) wa[j] = *reinterpret_cast<const d2*>(Wu + (long)(wv + 4 * j) * ld);
       if (wv == 0) {
         const int anyl = sweep_block_mh_q<Q, false>(md, s, bp, nbp, gb, Qb, Ai, dacc, t == tfp);
         if (lane == 0) any_acc = anyl;
@@ -1087,18 +1135,25 @@ __global__ __launch_bounds__(256) void k_sweep_step(Model md, MatSet ms, int ite
       // ---- z rows of tile t (rows >= bp) += W[:, B-1] delta'_{B-1}
       if (any_acc) {
         zdirty = true;
-        for (int h = 0; h < q; ++h) {
-          const double* Wt = ms.W + ((long)s * q + h) * (ld * ld) + (long)bp * ld + r0;
-          d2 wreg[16];
 #pragma unroll
-          for (int j = 0; j < 16; ++j) wreg[j] = *reinterpret_cast<const d2*>(Wt + (long)(wv + 4 * j) * ld);
+        for (int h = 0; h < Q; ++h) {
+          d2 wb[16];
+          if (h + 1 < Q) {
+#pragma unroll
+            for (int j = 0; j < 16; ++j)
+              wb[j] = *reinterpret_cast<const d2*>(Wu + (long)(h + 1) * (ld * ld) + (long)(wv + 4 * j) * ld);
+          }
           d2 sw = {0.0, 0.0};
 #pragma unroll
           for (int j = 0; j < 16; ++j) {
             const int i = wv + 4 * j;
             const double c = (i < nbp) ? dacc[h * SW_B + i] : 0.0;
-            sw.x = fma(wreg[j].x, c, sw.x);
-            sw.y = fma(wreg[j].y, c, sw.y);
+            sw.x = fma(wa[j].x, c, sw.x);
+            sw.y = fma(wa[j].y, c, sw.y);
+          }
+          if (h + 1 < Q) {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) wa[j] = wb[j];
           }
           red[wv * MK_NB + 2 * lane] = sw.x;
           red[wv * MK_NB + 2 * lane + 1] = sw.y;
@@ -1123,21 +1178,29 @@ __global__ __launch_bounds__(256) void k_sweep_step(Model md, MatSet ms, int ite
     const int b0 = B * SW_B;
     if (t >= b0 / MK_NB) {
       double* pb = ps + (B & 1) * pstride + (long)t * q * SW_B;
-      for (int h = 0; h < q; ++h) {
-        const double* Wt = ms.W + ((long)s * q + h) * (ld * ld) + (long)b0 * ld + r0;
-        d2 wreg[16];
+      const double* Wd = ms.W + (long)s * q * (ld * ld) + (long)b0 * ld + r0;
+      d2 wa[16];
 #pragma unroll
-        for (int j = 0; j < 16; ++j) wreg[j] = *reinterpret_cast<const d2*>(Wt + (long)(wv + 4 * j) * ld);
-        d2 zz = zr[0];
+      for (int j = 0; j < 16; ++j) wa[j] = *reinterpret_cast<const d2*>(Wd + (long)(wv + 4 * j) * ld);
 #pragma unroll
-        for (int hh = 1; hh < Q; ++hh)
-          if (hh == h) zz = zr[hh];
+      for (int h = 0; h < Q; ++h) {
+        d2 wb[16];
+        if (h + 1 < Q) {
+#pragma unroll
+          for (int j = 0; j < 16; ++j)
+            wb[j] = *reinterpret_cast<const d2*>(Wd + (long)(h + 1) * (ld * ld) + (long)(wv + 4 * j) * ld);
+        }
+        const d2 zz = zr[h];
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
-          const double a0 = (r0 >= b0 && r0 < ns) ? wreg[j].x * zz.x : 0.0;
-          const double a1 = (r0 + 1 >= b0 && r0 + 1 < ns) ? wreg[j].y * zz.y : 0.0;
+          const double a0 = (r0 >= b0 && r0 < ns) ? wa[j].x * zz.x : 0.0;
+          const double a1 = (r0 + 1 >= b0 && r0 + 1 < ns) ? wa[j].y * zz.y : 0.0;
           const double p = wave_sum_dpp(a0 + a1);
           if (lane == 0) pb[h * SW_B + wv + 4 * j] = p;
+        }
+        if (h + 1 < Q) {
+#pragma unroll
+          for (int j = 0; j < 16; ++j) wa[j] = wb[j];
         }
       }
     }
