@@ -361,9 +361,11 @@ template __global__ void k_chol_trsm<32>(MatSet, int, int, int, int, int, int, c
 #define SLD 17
 #ifdef MK_DIAG_TIMING   // development probe only (tools/diag_probe.hip): shader-clock stamps per phase
 __device__ long long* mk_diag_ts;
-#define MK_TSTAMP(i) do { if (threadIdx.x == 0) mk_diag_ts[blockIdx.x * 64 + (i)] = clock64(); } while (0)
+#define MK_TSTAMP(i) do { if (threadIdx.x == 0) mk_diag_ts[blockIdx.x * 128 + (i)] = clock64(); } while (0)
+#define MK_TSTAMPW(i, t) do { if (threadIdx.x == (t)) mk_diag_ts[blockIdx.x * 128 + (i)] = clock64(); } while (0)
 #else
 #define MK_TSTAMP(i) do { } while (0)
+#define MK_TSTAMPW(i, t) do { } while (0)
 #endif     // wave-private 16 x 16 staging, padded likewise
 
 __device__ inline double rlane(double v, int lane) {
@@ -432,6 +434,94 @@ __device__ inline double xget(const double* T, int r, int c) {
 // Lane l holds row (l & 15); lanes 16..63 mirror lanes 0..15 (same instructions, results
 // unused).  Column values are broadcast by 64-bit DPP row_newbcast (no SGPR round trips);
 // upper-triangle entries are updated unconditionally and never read.
+// acc += (lane n's value of src within this lane's 16-lane DPP row) * mul: one v_fmac_f64 with a
+// 64-bit row_newbcast DPP source (the compiler keeps v_mov_b64_dpp + v_fma_f64 apart, plus a copy
+// for the old value: three instructions per element).  The asm is volatile, so the calls keep
+// their program order; a DPP read needs two wait states after a VALU write of its source, which
+// the callers give with NOP = true on the first call after such a write (the compiler does not
+// see inside the asm).  SELF: the source is acc itself (one register, no copy the compiler could
+// place right before the read).
+#define MK_FMAC_BC(N)                                                                                   \
+  do {                                                                                                  \
+    if (SELF) {                                                                                         \
+      if (NOP) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %0, %1 row_newbcast:" #N " row_mask:0xf bank_mask:0xf" \
+                            : "+v"(acc) : "v"(mul));                                                      \
+      else asm volatile("v_fmac_f64_dpp %0, %0, %1 row_newbcast:" #N " row_mask:0xf bank_mask:0xf"        \
+                        : "+v"(acc) : "v"(mul));                                                          \
+    } else {                                                                                            \
+      if (NOP) asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:" #N " row_mask:0xf bank_mask:0xf" \
+                            : "+v"(acc) : "v"(src), "v"(mul));                                            \
+      else asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:" #N " row_mask:0xf bank_mask:0xf"        \
+                        : "+v"(acc) : "v"(src), "v"(mul));                                                \
+    }                                                                                                   \
+  } while (0)
+template <bool NOP, bool SELF>
+__device__ __forceinline__ void fmac_bc16(double& acc, double src, double mul, int n) {
+  switch (n) {
+    case 0: MK_FMAC_BC(0); break;   case 1: MK_FMAC_BC(1); break;   case 2: MK_FMAC_BC(2); break;
+    case 3: MK_FMAC_BC(3); break;   case 4: MK_FMAC_BC(4); break;   case 5: MK_FMAC_BC(5); break;
+    case 6: MK_FMAC_BC(6); break;   case 7: MK_FMAC_BC(7); break;   case 8: MK_FMAC_BC(8); break;
+    case 9: MK_FMAC_BC(9); break;   case 10: MK_FMAC_BC(10); break; case 11: MK_FMAC_BC(11); break;
+    case 12: MK_FMAC_BC(12); break; case 13: MK_FMAC_BC(13); break; case 14: MK_FMAC_BC(14); break;
+    default: MK_FMAC_BC(15); break;
+  }
+}
+#undef MK_FMAC_BC
+
+#ifndef MK_DIAG_V1
+
+// The pivot is issue-bound (one row per lane, lanes 16..63 mirroring: ~1,500 wave instructions,
+// ~10k cycles per block), so every broadcast-multiply-add is one fused DPP instruction
+// (fmac_bc16) -- the same fma, operands and order as before, so the same bits.  Branch-free:
+// the bordered row is a select and its pivot is stored after the loop.
+__device__ inline void factor_pivot(double* T, double* dg, double* xd, int b, int rb, double* quad_out, bool& bad) {
+  const int l = threadIdx.x & 63;
+  // lr opaque to the compiler, so the ~50 lane masks (lr == j, lr > m, ...) are formed where they
+  // are used instead of being hoisted out of the pivot-step loop and spilled to VGPR lanes
+  int lr = l & 15;
+  asm volatile("" : "+v"(lr));
+  double row[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) row[c] = T[(b + lr) + (b + c) * TLD];
+  double myinv = 0.0;   // 1 / L(lr, lr)
+  double qv = 0.0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const double a = bcast16(row[j], j);
+    const bool border = (b + j == rb);
+    double d, inv;
+    rsqrt_sqrt(a, &d, &inv);
+    bad |= !border && !(a > 0.0);
+    qv = border ? -a : qv;
+    d = border ? 1.0 : d;
+    inv = border ? 1.0 : inv;
+    myinv = (lr == j) ? inv : myinv;
+    row[j] = (lr == j) ? d : row[j] * inv;
+    const double nrj = -row[j];
+#pragma unroll
+    for (int c = j + 1; c < 16; ++c) {
+      // row[j] was written just above (first call waits); the later calls read it again
+      if (c == j + 1) fmac_bc16<true, false>(row[c], row[j], nrj, c);
+      else fmac_bc16<false, false>(row[c], row[j], nrj, c);
+    }
+  }
+  if (l == 0 && rb >= b && rb < b + 16) *quad_out = qv;
+  // inverse of the pivot block, row lr of Dinv in xr: with the row-scaled factor
+  // Ls(l, m) = L(l, m) / L(l, l),  X(l, c) = [l == c] / L(l, l) - sum_{c <= m < l} Ls(l, m) X(m, c)
+  double xr[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) xr[c] = (c == lr) ? myinv : 0.0;
+#pragma unroll
+  for (int m = 0; m < 15; ++m) {
+    const double ncf = (lr > m) ? -(row[m] * myinv) : -0.0;
+#pragma unroll
+    for (int c = 0; c <= m; ++c) {
+      // xr[c] was last written by call c of step m-1: m calls (+ the wait) apart
+      if (c == 0) fmac_bc16<true, true>(xr[c], xr[c], ncf, m);
+      else fmac_bc16<false, true>(xr[c], xr[c], ncf, m);
+    }
+  }
+#else
 __device__ inline void factor_pivot(double* T, double* dg, double* xd, int b, int rb, double* quad_out, bool& bad) {
   const int l = threadIdx.x & 63, lr = l & 15;
   double row[16];
@@ -455,8 +545,6 @@ __device__ inline void factor_pivot(double* T, double* dg, double* xd, int b, in
 #pragma unroll
     for (int c = j + 1; c < 16; ++c) row[c] = fma(-row[j], bcast16(row[j], c), row[c]);
   }
-  // inverse of the pivot block, row lr of Dinv in xr: with the row-scaled factor
-  // Ls(l, m) = L(l, m) / L(l, l),  X(l, c) = [l == c] / L(l, l) - sum_{c <= m < l} Ls(l, m) X(m, c)
   double xr[16];
 #pragma unroll
   for (int c = 0; c < 16; ++c) xr[c] = (c == lr) ? myinv : 0.0;
@@ -466,6 +554,7 @@ __device__ inline void factor_pivot(double* T, double* dg, double* xd, int b, in
 #pragma unroll
     for (int c = 0; c <= m; ++c) xr[c] = fma(-cf, bcast16(xr[c], m), xr[c]);
   }
+#endif
   if (l < 16) {
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
@@ -480,6 +569,43 @@ __device__ inline void factor_pivot(double* T, double* dg, double* xd, int b, in
   }
 }
 
+// N F3 blocks at once: their operand reads issued together and their MFMA chains interleaved
+// (independent accumulators; a single block is latency-bound on its four dependent MFMAs); each
+// block sees the same MFMA sequence as trailing_block.
+template <int N>
+__device__ inline void trailing_multi(double* T, int pc, const int* RR, const int* CC) {
+  const int l = threadIdx.x & 63, bc = 16 * pc;
+  d4 a[N];
+  double x[N][4], y[N][4];
+#pragma unroll
+  for (int q = 0; q < N; ++q) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) a[q][r] = T[(16 * RR[q] + (l >> 4) + 4 * r) + (16 * CC[q] + (l & 15)) * TLD];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = 4 * u + (l >> 4);
+      x[q][u] = -T[(16 * RR[q] + (l & 15)) + (bc + k) * TLD];
+      y[q][u] = T[(16 * CC[q] + (l & 15)) + (bc + k) * TLD];
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int q = 0; q < N; ++q) a[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(x[q][u], y[q][u], a[q], 0, 0, 0);
+#pragma unroll
+  for (int q = 0; q < N; ++q)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) T[(16 * RR[q] + (l >> 4) + 4 * r) + (16 * CC[q] + (l & 15)) * TLD] = a[q][r];
+}
+
+// Trailing block index u (0 = (p, p)) of step p-1 -> (row, column) block offsets from p.
+__device__ inline void trail_rc(int u, int* R, int* C) {
+  int r = 0;
+  while ((r + 1) * (r + 2) / 2 <= u) ++r;
+  *R = r;
+  *C = u - r * (r + 1) / 2;
+}
+
 // F3 block (RR, CC) of the trailing update after pivot column block pc: T_RC -= P_R P_C^T.
 __device__ inline void trailing_block(double* T, int pc, int RR, int CC) {
   const int l = threadIdx.x & 63, bc = 16 * pc;
@@ -490,6 +616,50 @@ __device__ inline void trailing_block(double* T, int pc, int RR, int CC) {
                [&](int k, int j) { return T[(16 * CC + j) + (bc + k) * TLD]; });
 #pragma unroll
   for (int r = 0; r < 4; ++r) T[(16 * RR + (l >> 4) + 4 * r) + (16 * CC + (l & 15)) * TLD] = acc[r];
+}
+
+// L (its diagonal from dg) into Mt and X = Winv_k into W, as 16-byte row pairs (rows r, r+1 of
+// column c), all 256 threads, eight pairs per thread in flight (every LDS read of a batch issued
+// before its stores: the loop was latency-bound at ~450 cycles per pair otherwise).  Pairs entirely
+// above the diagonal are not stored -- the Winv slots are zeroed once when the session is created
+// and never written there, and M's upper triangle is never read -- and the one upper element of a
+// pair that straddles the diagonal gets a zero in both.
+__device__ inline void store_tile_lw(const double* T, const double* dg, const double* xd, double* Mt, long ld,
+                                     double* W) {
+  constexpr int B = 8;
+  const int tid = threadIdx.x;
+#pragma unroll 1
+  for (int e0 = 0; e0 < MK_NB * (MK_NB / 2); e0 += 256 * B) {
+    // every read of the batch unconditional and issued before any use (the memory clobber keeps
+    // the compiler from sinking them into per-select branches, one LDS round trip each)
+    d2 lr2[B], wr2[B], dd[B], xx[B];
+#pragma unroll
+    for (int u = 0; u < B; ++u) {
+      const int e = e0 + tid + 256 * u;
+      const int c = e >> 6, r = 2 * (e & 63);
+      lr2[u].x = T[r + c * TLD];
+      lr2[u].y = T[r + 1 + c * TLD];
+      wr2[u].x = T[c + r * TLD];
+      wr2[u].y = T[c + (r + 1) * TLD];
+      dd[u] = *reinterpret_cast<const d2*>(dg + r);
+      xx[u] = *reinterpret_cast<const d2*>(xd + r);
+    }
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int u = 0; u < B; ++u) {
+      const int e = e0 + tid + 256 * u;
+      const int c = e >> 6, r = 2 * (e & 63);
+      d2 lv, wv;
+      lv.x = (r > c) ? lr2[u].x : ((r == c) ? dd[u].x : 0.0);
+      lv.y = (r + 1 > c) ? lr2[u].y : dd[u].y;
+      wv.x = (r > c) ? wr2[u].x : ((r == c) ? xx[u].x : 0.0);
+      wv.y = (r + 1 > c) ? wr2[u].y : xx[u].y;
+      if (r + 1 >= c) {
+        *reinterpret_cast<d2*>(Mt + r + (long)c * ld) = lv;
+        *reinterpret_cast<d2*>(W + r + c * MK_NB) = wv;
+      }
+    }
+  }
 }
 
 // Blocked by 16, two barriers per pivot step p, the inverse X = L^-1 computed by block rows
@@ -509,37 +679,50 @@ __device__ void factor_invert_tile(double* T, double* dg, double* xd, double* Sb
     const int nb = 8 - p;                       // trailing blocks of step p-1: rows/cols p..7
     const int ntrail = (p > 0) ? nb * (nb + 1) / 2 : 0;
     if (wv == 0) {
-      if (p > 0) {
-        trailing_block(T, p - 1, p, p);
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-      }
+      // (block (p, p)'s update by step p-1 was done by this wave at the end of step p-1)
+      MK_TSTAMPW(44 + 4 * p, 0);
       factor_pivot(T, dg, xd, 16 * p, rb, quad_out, bad);
+      MK_TSTAMPW(45 + 4 * p, 0);
     } else {
-      // tasks: S_pc (c < p, longest first), then trailing blocks t = 1 .. ntrail-1
-      for (int t = wv - 1; t < p + ntrail - 1; t += 3) {
-        if (t < p) {
-          const int Cb = t;
-          d4 acc = {0.0, 0.0, 0.0, 0.0};
-          acc = mfma16(acc, 16 * (p - Cb), [&](int r, int m) { return T[(16 * p + r) + (16 * Cb + m) * TLD]; },
-                       [&](int m, int c) { return xget(T, 16 * Cb + m, 16 * Cb + c); });
-          double* S = Sb + Cb * 16 * SLD;
+      // tasks t (dealt round-robin over the three waves): S_pc for t < p (c = t, longest first),
+      // then trailing blocks u = t - p + 1 = 1 .. ntrail-1, two per pass
+      const int ntask = p + ntrail - 1;
+      int t = wv - 1;
+      for (; t < p; t += 3) {
+        const int Cb = t;
+        d4 acc = {0.0, 0.0, 0.0, 0.0};
+        acc = mfma16(acc, 16 * (p - Cb), [&](int r, int m) { return T[(16 * p + r) + (16 * Cb + m) * TLD]; },
+                     [&](int m, int c) { return xget(T, 16 * Cb + m, 16 * Cb + c); });
+        double* S = Sb + Cb * 16 * SLD;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) S[((l >> 4) + 4 * r) + (l & 15) * SLD] = acc[r];
-        } else {
-          const int u = t - p + 1;              // trailing block index (0 = (p, p), done by wave 0)
-          int R = 0;
-          while ((R + 1) * (R + 2) / 2 <= u) ++R;
-          const int C = u - R * (R + 1) / 2;
-          trailing_block(T, p - 1, p + R, p + C);
-        }
+        for (int r = 0; r < 4; ++r) S[((l >> 4) + 4 * r) + (l & 15) * SLD] = acc[r];
       }
+      // up to four trailing blocks per pass
+      while (t < ntask) {
+        const int nq = min(4, (ntask - t + 2) / 3);
+        int RR[4], CC[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          trail_rc(min(t + 3 * q, ntask - 1) - p + 1, &RR[q], &CC[q]);
+          RR[q] += p;
+          CC[q] += p;
+        }
+        if (nq == 4) trailing_multi<4>(T, p - 1, RR, CC);
+        else if (nq == 3) trailing_multi<3>(T, p - 1, RR, CC);
+        else if (nq == 2) trailing_multi<2>(T, p - 1, RR, CC);
+        else trailing_multi<1>(T, p - 1, RR, CC);
+        t += 3 * nq;
+      }
+      MK_TSTAMPW(46 + 4 * p, 64);
     }
     __syncthreads();
     MK_TSTAMP(1 + 3 * p);
-    // ---- phase 2: F2 panel blocks R = p+1..7, inverse blocks X_pc, c = 0..p-1
+    // ---- phase 2: F2 panel blocks R = p+1..7, inverse blocks X_pc, c = 0..p-1 (tasks t < 7).
+    // Wave 0 takes panel block p+1 and then the next pivot block's trailing update T_{p+1,p+1} -=
+    // P_{p+1} P_{p+1}^T right away (the next pivot's only input from this step), so its phase 1
+    // starts with the pivot; waves 1-3 take the other tasks.
     const int b = 16 * p;
-    for (int t = wv; t < 7; t += 4) {
+    auto task = [&](int t) {
       if (t < 7 - p) {
         const int R = p + 1 + t;
         d4 acc = {0.0, 0.0, 0.0, 0.0};
@@ -559,6 +742,16 @@ __device__ void factor_invert_tile(double* T, double* dg, double* xd, double* Sb
           T[cc + rr * TLD] = out[r];
         }
       }
+    };
+    if (wv == 0) {
+      task(0);
+      if (p < 7) {
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        trailing_block(T, p, p + 1, p + 1);
+      }
+    } else {
+      for (int t = wv; t < 7; t += 3) task(t);
     }
     __syncthreads();
     MK_TSTAMP(2 + 3 * p);
@@ -577,7 +770,6 @@ __global__ __launch_bounds__(256) void k_chol_diag(MatSet ms, const int* __restr
   double* dg = T + MK_NB * TLD;        // [128]
   double* xd = dg + MK_NB;             // [128]
   double* Sb = xd + MK_NB;             // [7][16 * SLD]
-  __shared__ int badf;
   int s, h;
   if (!pick_pair(slist, scount, blockIdx.x, h0, hc, &s, &h)) return;
   MK_TSTAMP(0);
@@ -589,30 +781,32 @@ __global__ __launch_bounds__(256) void k_chol_diag(MatSet ms, const int* __restr
   const int base = k * MK_NB;
   const int ns = n_s[s];
   double* Mt = M + base + (long)base * ld;
-  // Unconditional 16-byte loads, 8 in flight per thread, then the upper triangle is zeroed in
-  // LDS (a masked load per element compiled to one dependent round trip each: 64 per thread).
-  for (int e0 = 0; e0 < MK_NB * MK_NB; e0 += 256 * 2 * 8) {
-    d2 v[8];
+  // Unconditional 16-byte loads, all 32 per thread in flight at once (one memory round trip
+  // instead of four), then the upper triangle is zeroed in LDS (a masked load per element
+  // compiled to one dependent round trip each: 64 per thread).
+  {
+    constexpr int NL = MK_NB * MK_NB / (256 * 2);
+    d2 v[NL];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int e = e0 + 2 * (tid + 256 * j);
+    for (int j = 0; j < NL; ++j) {
+      const int e = 2 * (tid + 256 * j);
       v[j] = *reinterpret_cast<const d2*>(Mt + (e & 127) + (long)(e >> 7) * ld);
     }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int e = e0 + 2 * (tid + 256 * j);
+    for (int j = 0; j < NL; ++j) {
+      const int e = 2 * (tid + 256 * j);
       const int r = e & 127, c = e >> 7;
       T[r + c * TLD] = (r >= c) ? v[j].x : 0.0;
       T[r + 1 + c * TLD] = (r + 1 >= c) ? v[j].y : 0.0;
     }
   }
-  if (tid == 0) badf = 0;
   __syncthreads();
   MK_TSTAMP(40);
   bool bad = false;
-  factor_invert_tile(T, dg, xd, Sb, ns - base, quad_c + sh, &bad);
-  if (bad) badf = 1;
-  __syncthreads();
+  double* W = winv_slot(ms, sh, slot, k);
+  factor_invert_tile(T, dg, xd, Sb, ns - base, quad_c + sh, &bad);   // ends with a barrier
+  // wave 0: log-det partial and the factorisation flag (the pivot ran on wave 0; its test is on the
+  // broadcast pivot, so every lane's flag is the same), then it joins the stores
   if (tid < 64) {
     double v = 0.0;
     for (int r = tid; r < MK_NB; r += 64) v += (base + r < ns) ? 2.0 * log(dg[r]) : 0.0;
@@ -620,28 +814,11 @@ __global__ __launch_bounds__(256) void k_chol_diag(MatSet ms, const int* __restr
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     if (tid == 0) {
       ld_part[(long)sh * ms.nt + k] = v;
-      if (badf) info[sh] = 1;
+      if (bad) info[sh] = 1;
     }
   }
   MK_TSTAMP(41);
-  // L and Winv_k out: 16-byte row pairs (rows r, r+1 of column c), values by selects (no divergent
-  // branches); pairs entirely above the diagonal are not stored -- the Winv slots are zeroed once
-  // when the session is created and never written there, and M's upper triangle is never read.
-  // The one upper element of a pair that straddles the diagonal gets a zero in both.
-  double* W = winv_slot(ms, sh, slot, k);
-#pragma unroll 4
-  for (int e0 = 0; e0 < MK_NB * MK_NB; e0 += 512) {
-    const int e = e0 + 2 * tid;
-    const int r = e & 127, c = e >> 7;
-    if (r + 1 < c) continue;
-    d2 lv, wv;
-    lv.x = (r > c) ? T[r + c * TLD] : ((r == c) ? dg[r] : 0.0);
-    lv.y = (r + 1 > c) ? T[r + 1 + c * TLD] : dg[r + 1];
-    wv.x = (r > c) ? T[c + r * TLD] : ((r == c) ? xd[r] : 0.0);
-    wv.y = (r + 1 > c) ? T[c + (r + 1) * TLD] : xd[r + 1];
-    *reinterpret_cast<d2*>(Mt + r + (long)c * ld) = lv;
-    *reinterpret_cast<d2*>(W + r + c * MK_NB) = wv;
-  }
+  store_tile_lw(T, dg, xd, Mt, ld, W);
   MK_TSTAMP(42);
 }
 

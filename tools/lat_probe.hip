@@ -1,0 +1,194 @@
+// Development probe: single-wave dependent-chain latencies on gfx950 (cycles per instruction) for
+// the fp64 ops of the diagonal-tile pivot, then the pivot variants of mk_linalg.hip timed alone.
+// Build: hipcc -w --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -DMK_DIAG_TIMING tools/lat_probe.hip -o tools/lat_probe
+#include <cstdio>
+#include <vector>
+#include "../laurabaracaldo-spatial-meta-kriging-for-distributed-inference-for-binary-response_amd/csrc/mk_linalg.hip"
+using namespace mk;
+
+#define CHAIN 64
+__global__ void k_lat(double* out, long long* cyc, double x0, double y) {
+  double x = x0 + threadIdx.x * 1e-9;
+  long long t0, t1;
+  // 0: dependent v_fma_f64
+  t0 = clock64();
+#pragma unroll
+  for (int i = 0; i < CHAIN; ++i) { x = fma(x, y, 1e-3); asm volatile("" : "+v"(x)); }
+  t1 = clock64();
+  if (threadIdx.x == 0) cyc[0] = t1 - t0;
+  // 1: dependent v_mul_f64
+  t0 = clock64();
+#pragma unroll
+  for (int i = 0; i < CHAIN; ++i) { x = x * y; asm volatile("" : "+v"(x)); }
+  t1 = clock64();
+  if (threadIdx.x == 0) cyc[1] = t1 - t0;
+  // 2: dependent v_rsq_f64
+  t0 = clock64();
+#pragma unroll
+  for (int i = 0; i < CHAIN; ++i) { x = __builtin_amdgcn_rsq(x); asm volatile("" : "+v"(x)); }
+  t1 = clock64();
+  if (threadIdx.x == 0) cyc[2] = t1 - t0;
+  // 3: dependent v_mov_b64_dpp row_newbcast (bound_ctrl)
+  t0 = clock64();
+#pragma unroll
+  for (int i = 0; i < CHAIN; ++i) { x = __builtin_amdgcn_mov_dpp(x, 0x151, 0xf, 0xf, true); asm volatile("" : "+v"(x)); }
+  t1 = clock64();
+  if (threadIdx.x == 0) cyc[3] = t1 - t0;
+  // 4: dependent fused dpp fmac
+  t0 = clock64();
+#pragma unroll
+  for (int i = 0; i < CHAIN; ++i) { fmac_bc16<true, true>(x, x, y, 3); asm volatile("" : "+v"(x)); }
+  t1 = clock64();
+  if (threadIdx.x == 0) cyc[4] = t1 - t0;
+  // 5: independent fmas (8 chains interleaved): throughput
+  double v[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) v[k] = x + k;
+  t0 = clock64();
+#pragma unroll
+  for (int i = 0; i < CHAIN / 8; ++i)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { v[k] = fma(v[k], y, 1e-3); asm volatile("" : "+v"(v[k])); }
+  t1 = clock64();
+  if (threadIdx.x == 0) cyc[5] = t1 - t0;
+  // 6: independent fused dpp fmacs (8 chains)
+  t0 = clock64();
+#pragma unroll
+  for (int i = 0; i < CHAIN / 8; ++i)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { fmac_bc16<false, false>(v[k], x, y, k); asm volatile("" : "+v"(v[k])); }
+  t1 = clock64();
+  if (threadIdx.x == 0) cyc[6] = t1 - t0;
+  // 7: dependent v_rcp_f64
+  t0 = clock64();
+#pragma unroll
+  for (int i = 0; i < CHAIN; ++i) { x = __builtin_amdgcn_rcp(x); asm volatile("" : "+v"(x)); }
+  t1 = clock64();
+  if (threadIdx.x == 0) cyc[7] = t1 - t0;
+  // 8: dependent v_cndmask pair (select on a lane compare)
+  const bool m = (threadIdx.x & 15) == 3;
+  t0 = clock64();
+#pragma unroll
+  for (int i = 0; i < CHAIN; ++i) { x = m ? y : x; asm volatile("" : "+v"(x)); }
+  t1 = clock64();
+  if (threadIdx.x == 0) cyc[8] = t1 - t0;
+  // 9: the asm barrier alone (baseline)
+  t0 = clock64();
+#pragma unroll
+  for (int i = 0; i < CHAIN; ++i) asm volatile("" : "+v"(x));
+  t1 = clock64();
+  if (threadIdx.x == 0) cyc[9] = t1 - t0;
+  // 10: dependent 32-bit int add
+  int iv = threadIdx.x;
+  t0 = clock64();
+#pragma unroll
+  for (int i = 0; i < CHAIN; ++i) { iv = iv * 3 + 1; asm volatile("" : "+v"(iv)); }
+  t1 = clock64();
+  if (threadIdx.x == 0) cyc[10] = t1 - t0;
+  x += iv;
+  // 11: dependent f64 MFMA 16x16x4 (one accumulator); 12: four independent accumulators
+  typedef double d4v __attribute__((ext_vector_type(4)));
+  d4v m0 = {x, 0, 0, 0}, m1 = m0, m2 = m0, m3 = m0;
+  const double fa = y, fb = 1e-3;
+  t0 = clock64();
+#pragma unroll
+  for (int i = 0; i < 16; ++i) { m0 = __builtin_amdgcn_mfma_f64_16x16x4f64(fa, fb, m0, 0, 0, 0); asm volatile("" : "+a"(m0)); }
+  t1 = clock64();
+  if (threadIdx.x == 0) cyc[11] = (t1 - t0) * 4;   // per CHAIN=64 normalisation: 16 instrs
+  t0 = clock64();
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    m0 = __builtin_amdgcn_mfma_f64_16x16x4f64(fa, fb, m0, 0, 0, 0);
+    m1 = __builtin_amdgcn_mfma_f64_16x16x4f64(fa, fb, m1, 0, 0, 0);
+    m2 = __builtin_amdgcn_mfma_f64_16x16x4f64(fa, fb, m2, 0, 0, 0);
+    m3 = __builtin_amdgcn_mfma_f64_16x16x4f64(fa, fb, m3, 0, 0, 0);
+    asm volatile("" : "+a"(m0), "+a"(m1), "+a"(m2), "+a"(m3));
+  }
+  t1 = clock64();
+  if (threadIdx.x == 0) cyc[12] = t1 - t0;          // 64 instrs
+  x += m0[0] + m1[1] + m2[2] + m3[3];
+  // 13: LDS ds_read_b64 throughput on the diagonal kernel's column-major stride-129 pattern
+  // (16 independent reads, lane l: row (l & 15), column (l >> 4) + 4u); 14: the same at stride 128+16
+  __shared__ double lds[129 * 80];
+  for (int e = threadIdx.x; e < 129 * 80; e += 64) lds[e] = e;
+  __syncthreads();
+  double acc = 0;
+  t0 = clock64();
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    double v = lds[(threadIdx.x & 15) + ((threadIdx.x >> 4) + 4 * u) * 129];
+    asm volatile("" : "+v"(v));
+    acc += v;
+  }
+  t1 = clock64();
+  if (threadIdx.x == 0) cyc[13] = (t1 - t0) * 4;
+  t0 = clock64();
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    double v = lds[(threadIdx.x & 15) + ((threadIdx.x >> 4) + 4 * u) * 136];
+    asm volatile("" : "+v"(v));
+    acc += v;
+  }
+  t1 = clock64();
+  if (threadIdx.x == 0) cyc[14] = (t1 - t0) * 4;
+  x += acc;
+  double s = x;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s += v[k];
+  out[threadIdx.x] = s;
+}
+
+// the pivot alone: one wave, block 0 of a 128x128 SPD tile in LDS, 8 repetitions on fresh copies
+__global__ void k_pivot(const double* A, double* out, long long* cyc) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  double* T = sm;
+  double* dg = T + MK_NB * TLD;
+  double* xd = dg + MK_NB;
+  double q = 0.0;
+  bool bad = false;
+  long long tot = 0;
+  for (int rep = 0; rep < 8; ++rep) {
+    for (int e = threadIdx.x; e < 16 * 16; e += 64) T[(e & 15) + (e >> 4) * TLD] = A[e] + rep * 1e-3 * ((e & 15) == (e >> 4));
+    __syncthreads();
+    const long long t0 = clock64();
+    factor_pivot(T, dg, xd, 0, 1 << 20, &q, bad);
+    __builtin_amdgcn_s_waitcnt(0);
+    const long long t1 = clock64();
+    tot += t1 - t0;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) cyc[0] = tot / 8;
+  for (int e = threadIdx.x; e < 16 * 16; e += 64) out[e] = T[(e & 15) + (e >> 4) * TLD];
+  if (threadIdx.x < 16) { out[256 + threadIdx.x] = dg[threadIdx.x]; out[272 + threadIdx.x] = xd[threadIdx.x]; }
+  if (bad) out[300] = 1.0;
+}
+
+int main() {
+  double* out; long long* cyc;
+  hipMalloc(&out, 4096 * 8); hipMalloc(&cyc, 64 * 8);
+  hipLaunchKernelGGL(k_lat, dim3(1), dim3(64), 0, 0, out, cyc, 1.5, 0.999);
+  hipLaunchKernelGGL(k_lat, dim3(1), dim3(64), 0, 0, out, cyc, 1.5, 0.999);
+  std::vector<long long> c(16);
+  hipMemcpy(c.data(), cyc, 16 * 8, hipMemcpyDeviceToHost);
+  const char* nm[] = {"fma dep", "mul dep", "rsq dep", "mov_dpp dep", "fmac_dpp dep", "fma indep x8",
+                      "fmac_dpp indep x8", "rcp dep", "cndmask dep", "asm barrier", "int mad dep", "mfma f64 dep", "mfma f64 x4",
+                      "ds_read stride129", "ds_read stride136"};
+  for (int i = 0; i < 15; ++i) printf("%-18s %6.1f cycles/instr\n", nm[i], (double)c[i] / CHAIN);
+  std::vector<double> A(256);
+  for (int r = 0; r < 16; ++r)
+    for (int cc = 0; cc < 16; ++cc) A[r + 16 * cc] = (r == cc) ? 20.0 : 0.01 * ((r * 7 + cc * 3) % 11) - 0.05 + 0.0;
+  for (int r = 0; r < 16; ++r)
+    for (int cc = 0; cc < r; ++cc) A[cc + 16 * r] = A[r + 16 * cc];
+  double* dA; hipMalloc(&dA, 256 * 8);
+  hipMemcpy(dA, A.data(), 256 * 8, hipMemcpyHostToDevice);
+  hipFuncSetAttribute((const void*)k_pivot, hipFuncAttributeMaxDynamicSharedMemorySize, MK_DIAG_LDS_BYTES);
+  for (int it = 0; it < 2; ++it)
+    hipLaunchKernelGGL(k_pivot, dim3(1), dim3(64), MK_DIAG_LDS_BYTES, 0, dA, out, cyc);
+  hipDeviceSynchronize();
+  long long pc; hipMemcpy(&pc, cyc, 8, hipMemcpyDeviceToHost);
+  std::vector<double> o(512);
+  hipMemcpy(o.data(), out, 512 * 8, hipMemcpyDeviceToHost);
+  double cs = 0; for (int i = 0; i < 288; ++i) cs += o[i] * (1 + (i % 7));
+  printf("pivot alone: %lld cycles (checksum %.17g)\n", pc, cs);
+  return 0;
+}

@@ -1,0 +1,5 @@
+#!/bin/bash
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/r03p
+mkdir -p $O
+timeout -k 10 60 ./tools/lat_probe > $O/lat3.log 2>&1 || exit 1
