@@ -569,41 +569,114 @@ __device__ inline void factor_pivot(double* T, double* dg, double* xd, int b, in
   }
 }
 
-// N F3 blocks at once: their operand reads issued together and their MFMA chains interleaved
-// (independent accumulators; a single block is latency-bound on its four dependent MFMAs); each
-// block sees the same MFMA sequence as trailing_block.
-template <int N>
-__device__ inline void trailing_multi(double* T, int pc, const int* RR, const int* CC) {
-  const int l = threadIdx.x & 63, bc = 16 * pc;
-  d4 a[N];
-  double x[N][4], y[N][4];
-#pragma unroll
-  for (int q = 0; q < N; ++q) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) a[q][r] = T[(16 * RR[q] + (l >> 4) + 4 * r) + (16 * CC[q] + (l & 15)) * TLD];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int k = 4 * u + (l >> 4);
-      x[q][u] = -T[(16 * RR[q] + (l & 15)) + (bc + k) * TLD];
-      y[q][u] = T[(16 * CC[q] + (l & 15)) + (bc + k) * TLD];
-    }
-  }
-#pragma unroll
-  for (int u = 0; u < 4; ++u)
-#pragma unroll
-    for (int q = 0; q < N; ++q) a[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(x[q][u], y[q][u], a[q], 0, 0, 0);
-#pragma unroll
-  for (int q = 0; q < N; ++q)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) T[(16 * RR[q] + (l >> 4) + 4 * r) + (16 * CC[q] + (l & 15)) * TLD] = a[q][r];
-}
-
 // Trailing block index u (0 = (p, p)) of step p-1 -> (row, column) block offsets from p.
 __device__ inline void trail_rc(int u, int* R, int* C) {
   int r = 0;
   while ((r + 1) * (r + 2) / 2 <= u) ++r;
   *R = r;
   *C = u - r * (r + 1) / 2;
+}
+
+// Phase-1 work of waves 1-3, software-pipelined: the three waves share the CU's LDS, and with their
+// reads issued just before the MFMAs that consume them the tasks ran ~3x slower than one wave alone
+// (LDS contention exposed on every group).  Each group's reads are now issued before the previous
+// group's MFMAs (64 cycles each on the SIMD's matrix pipe), which hide them.  Same operands, same
+// MFMA order per block: same bits.
+// f64 MFMA modifier (the blgp operand of the f64 forms): negate the A operand, neg:[1,0,0] -- a
+// negated fragment then needs no VALU pass between its LDS read and the MFMA.
+#define MK_MFMA_NEG_A 1
+struct TrailGrp {
+  d4 a[4];
+  double x[4][4], y[4][4];
+  int R[4], C[4];
+  int n;
+};
+
+// Group of up to four trailing blocks of step p-1 from this wave's tasks t, t+3, ... < ntask (task t
+// = block u = t - p + 1); issues its LDS reads.
+__device__ __forceinline__ void trail_load(const double* T, int p, int t, int ntask, TrailGrp& g) {
+  const int l = threadIdx.x & 63, bc = 16 * (p - 1);
+  g.n = t < ntask ? min(4, (ntask - t + 2) / 3) : 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (q < g.n) {
+      int R, C;
+      trail_rc(t + 3 * q - p + 1, &R, &C);
+      R += p;
+      C += p;
+      g.R[q] = R;
+      g.C[q] = C;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) g.a[q][r] = T[(16 * R + (l >> 4) + 4 * r) + (16 * C + (l & 15)) * TLD];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int k = 4 * u + (l >> 4);
+        g.x[q][u] = T[(16 * R + (l & 15)) + (bc + k) * TLD];   // negated by the MFMA (neg A)
+        g.y[q][u] = T[(16 * C + (l & 15)) + (bc + k) * TLD];
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ void trail_mma_store(double* T, TrailGrp& g) {
+  const int l = threadIdx.x & 63;
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (q < g.n) g.a[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(g.x[q][u], g.y[q][u], g.a[q], 0, 0, MK_MFMA_NEG_A);
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if (q < g.n) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) T[(16 * g.R[q] + (l >> 4) + 4 * r) + (16 * g.C[q] + (l & 15)) * TLD] = g.a[q][r];
+    }
+}
+
+// This wave's trailing blocks (tasks t, t+3, ... < ntask), groups of four, double-buffered.
+__device__ __forceinline__ void trail_tasks(double* T, int p, int t, int ntask) {
+  TrailGrp g0, g1;
+  trail_load(T, p, t, ntask, g0);
+  t += 3 * g0.n;
+  while (g0.n) {
+    trail_load(T, p, t, ntask, g1);
+    t += 3 * g1.n;
+    trail_mma_store(T, g0);
+    if (!g1.n) break;
+    trail_load(T, p, t, ntask, g0);
+    t += 3 * g0.n;
+    trail_mma_store(T, g1);
+  }
+}
+
+// S_pc = sum_{K=c}^{p-1} L_pK X_Kc into Sb, one 16-deep chunk per K, each chunk's reads issued before
+// the previous chunk's MFMAs.  (mfma16's operands and order: same bits.)
+__device__ __forceinline__ void s_task(const double* T, double* Sb, int p, int c) {
+  const int l = threadIdx.x & 63;
+  double a0[4], b0[4], a1[4], b1[4];
+  // X_Kc: only the diagonal block (K = c) needs xget's mask; below it every entry is r > c
+  auto ld = [&](int K, double* a, double* b) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int m = 4 * u + (l >> 4);
+      a[u] = T[(16 * p + (l & 15)) + (16 * K + m) * TLD];
+      b[u] = (K == c) ? xget(T, 16 * K + m, 16 * c + (l & 15)) : T[(16 * c + (l & 15)) + (16 * K + m) * TLD];
+    }
+  };
+  d4 acc = {0.0, 0.0, 0.0, 0.0};
+  ld(c, a0, b0);
+  for (int K = c; K < p; K += 2) {
+    if (K + 1 < p) ld(K + 1, a1, b1);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a0[u], b0[u], acc, 0, 0, 0);
+    if (K + 1 >= p) break;
+    if (K + 2 < p) ld(K + 2, a0, b0);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a1[u], b1[u], acc, 0, 0, 0);
+  }
+  double* S = Sb + c * 16 * SLD;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) S[((l >> 4) + 4 * r) + (l & 15) * SLD] = acc[r];
 }
 
 // F3 block (RR, CC) of the trailing update after pivot column block pc: T_RC -= P_R P_C^T.
@@ -672,7 +745,9 @@ __device__ inline void store_tile_lw(const double* T, const double* dg, const do
 // (X[r][c] at T[c + r*TLD]); diag(L) in dg, diag(X) in xd; S stagings in Sb (7 x 16 x SLD).
 __device__ void factor_invert_tile(double* T, double* dg, double* xd, double* Sb, int rb, double* quad_out,
                                    bool* bad_out) {
-  const int tid = threadIdx.x, l = tid & 63, wv = tid >> 6;
+  // wv through readfirstlane: the task indices derived from it are wave-uniform scalars (in VGPRs the
+  // compiler treated them as divergent: exec-masked MFMAs and full MFMA-drain waits around each one)
+  const int tid = threadIdx.x, l = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   bool bad = false;
   for (int p = 0; p < 8; ++p) {
     // ---- phase 1
@@ -681,39 +756,22 @@ __device__ void factor_invert_tile(double* T, double* dg, double* xd, double* Sb
     if (wv == 0) {
       // (block (p, p)'s update by step p-1 was done by this wave at the end of step p-1)
       MK_TSTAMPW(44 + 4 * p, 0);
+#ifndef MK_DIAG_PROBE_NOPIVOT
       factor_pivot(T, dg, xd, 16 * p, rb, quad_out, bad);
+#endif
       MK_TSTAMPW(45 + 4 * p, 0);
     } else {
       // tasks t (dealt round-robin over the three waves): S_pc for t < p (c = t, longest first),
-      // then trailing blocks u = t - p + 1 = 1 .. ntrail-1, two per pass
+      // then trailing blocks u = t - p + 1 = 1 .. ntrail-1
       const int ntask = p + ntrail - 1;
+      MK_TSTAMPW(96 + p, 64);
       int t = wv - 1;
-      for (; t < p; t += 3) {
-        const int Cb = t;
-        d4 acc = {0.0, 0.0, 0.0, 0.0};
-        acc = mfma16(acc, 16 * (p - Cb), [&](int r, int m) { return T[(16 * p + r) + (16 * Cb + m) * TLD]; },
-                     [&](int m, int c) { return xget(T, 16 * Cb + m, 16 * Cb + c); });
-        double* S = Sb + Cb * 16 * SLD;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) S[((l >> 4) + 4 * r) + (l & 15) * SLD] = acc[r];
-      }
-      // up to four trailing blocks per pass
-      while (t < ntask) {
-        const int nq = min(4, (ntask - t + 2) / 3);
-        int RR[4], CC[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          trail_rc(min(t + 3 * q, ntask - 1) - p + 1, &RR[q], &CC[q]);
-          RR[q] += p;
-          CC[q] += p;
-        }
-        if (nq == 4) trailing_multi<4>(T, p - 1, RR, CC);
-        else if (nq == 3) trailing_multi<3>(T, p - 1, RR, CC);
-        else if (nq == 2) trailing_multi<2>(T, p - 1, RR, CC);
-        else trailing_multi<1>(T, p - 1, RR, CC);
-        t += 3 * nq;
-      }
+      for (; t < p; t += 3) s_task(T, Sb, p, t);
+      MK_TSTAMPW(47 + 4 * p, 64);
+      trail_tasks(T, p, t, ntask);
       MK_TSTAMPW(46 + 4 * p, 64);
+      MK_TSTAMPW(80 + p, 128);
+      MK_TSTAMPW(88 + p, 192);
     }
     __syncthreads();
     MK_TSTAMP(1 + 3 * p);

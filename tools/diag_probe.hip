@@ -80,9 +80,9 @@ int main(int argc, char** argv) {
     printf("k=%d best %.1f us  (cycles since start, avg over %d WGs)\n", k, best * 1e3, S);
     printf("  load %.0f\n", avg[40]);
     for (int p = 0; p < 8; ++p)
-      printf("  p%d phase1 %.0f phase2 %.0f | w0 pivot %.0f-%.0f | w1 tasks-end %.0f\n", p, avg[1 + 3 * p],
-             avg[2 + 3 * p], avg[44 + 4 * p], avg[45 + 4 * p], avg[46 + 4 * p]);
-  
+      printf("  p%d ph1 %.0f ph2 %.0f | w0 pivot %.0f-%.0f | w1 start %.0f S-end %.0f end %.0f | w2 end %.0f | w3 end %.0f\n",
+             p, avg[1 + 3 * p], avg[2 + 3 * p], avg[44 + 4 * p], avg[45 + 4 * p], avg[96 + p], avg[47 + 4 * p],
+             avg[46 + 4 * p], avg[80 + p], avg[88 + p]);
     printf("  logdet %.0f store %.0f\n", avg[41], avg[42]);
   }
   return 0;

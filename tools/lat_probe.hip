@@ -163,6 +163,97 @@ __global__ void k_pivot(const double* A, double* out, long long* cyc) {
   if (bad) out[300] = 1.0;
 }
 
+// phase-1 task pieces alone on one wave (T = the diagonal kernel's LDS image, random SPD-ish data)
+__global__ void k_tasks(double* out, long long* cyc) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  double* T = sm;
+  double* Sb = T + MK_NB * TLD + 2 * MK_NB;
+  for (int e = threadIdx.x; e < MK_NB * TLD; e += 64) T[e] = 1e-3 * (e % 97);
+  __syncthreads();
+  long long t0 = clock64();
+  for (int rep = 0; rep < 8; ++rep) { trail_tasks(T, 1, 0, 28); __builtin_amdgcn_s_waitcnt(0); }   // p = 1: 10 blocks
+  long long t1 = clock64();
+  if (threadIdx.x == 0) cyc[0] = (t1 - t0) / 8;
+  t0 = clock64();
+  for (int rep = 0; rep < 8; ++rep) { trailing_block(T, 0, 3, 2); __builtin_amdgcn_s_waitcnt(0); }
+  t1 = clock64();
+  if (threadIdx.x == 0) cyc[1] = (t1 - t0) / 8;
+  // S task of length 7 (p = 7, c = 0)
+  const int l = threadIdx.x & 63;
+  t0 = clock64();
+  for (int rep = 0; rep < 8; ++rep) {
+    s_task(T, Sb, 7, 0);
+    __builtin_amdgcn_s_waitcnt(0);
+  }
+  t1 = clock64();
+  if (threadIdx.x == 0) cyc[2] = (t1 - t0) / 8;
+  out[threadIdx.x] = T[threadIdx.x * 7] + Sb[threadIdx.x];
+}
+
+// MFMA f64 issue rate with W waves of one workgroup issuing at once (per-SIMD unit or shared?)
+__global__ void k_mfma_waves(double* out, long long* cyc, int active) {
+  typedef double d4v __attribute__((ext_vector_type(4)));
+  const int w = threadIdx.x >> 6;
+  d4v m0 = {1.0 * threadIdx.x, 0, 0, 0}, m1 = m0, m2 = m0, m3 = m0;
+  const double fa = 0.999, fb = 1e-3;
+  __syncthreads();
+  long long t0 = clock64();
+  if (w < active) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      m0 = __builtin_amdgcn_mfma_f64_16x16x4f64(fa, fb, m0, 0, 0, 0);
+      m1 = __builtin_amdgcn_mfma_f64_16x16x4f64(fa, fb, m1, 0, 0, 0);
+      m2 = __builtin_amdgcn_mfma_f64_16x16x4f64(fa, fb, m2, 0, 0, 0);
+      m3 = __builtin_amdgcn_mfma_f64_16x16x4f64(fa, fb, m3, 0, 0, 0);
+      asm volatile("" : "+a"(m0), "+a"(m1), "+a"(m2), "+a"(m3));
+    }
+  }
+  long long t1 = clock64();
+  if ((threadIdx.x & 63) == 0) cyc[w] = t1 - t0;
+  out[threadIdx.x] = m0[0] + m1[1] + m2[2] + m3[3];
+}
+
+// LDS ds_read_b64 throughput with W waves reading at once (the diagonal kernel's fragment pattern:
+// lane l reads row (l & 15), column (l >> 4) + 4u of a column-major stride-129 image), 16 reads in
+// flight per batch, 8 batches
+__global__ void k_lds_waves(double* out, long long* cyc, int active, int stride) {
+  __shared__ double lds[129 * 128];
+  for (int e = threadIdx.x; e < 129 * 128; e += 256) lds[e] = e;
+  __syncthreads();
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  double acc = 0;
+  long long t0 = clock64();
+  if (w < active) {
+    for (int b = 0; b < 8; ++b) {
+      double v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = lds[(l & 15) + 16 * (b & 3) + ((l >> 4) + 4 * u) * stride];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) acc += v[u];
+      asm volatile("" : "+v"(acc));
+    }
+  }
+  long long t1 = clock64();
+  if (l == 0) cyc[w] = t1 - t0;
+  out[threadIdx.x] = acc;
+}
+
+// the diagonal kernel's step-1 trailing tasks on 1 or 3 concurrent waves (waves 1..active)
+__global__ void k_trail_waves(double* out, long long* cyc, int active) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  double* T = sm;
+  for (int e = threadIdx.x; e < MK_NB * TLD; e += 256) T[e] = 1e-3 * (e % 97);
+  __syncthreads();
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  long long t0 = clock64();
+  if (wv >= 1 && wv <= active) trail_tasks(T, 1, wv - 1 + 3, 28);
+  __builtin_amdgcn_s_waitcnt(0);
+  long long t1 = clock64();
+  if ((threadIdx.x & 63) == 0) cyc[wv] = t1 - t0;
+  __syncthreads();
+  out[threadIdx.x] = T[threadIdx.x * 3];
+}
+
 int main() {
   double* out; long long* cyc;
   hipMalloc(&out, 4096 * 8); hipMalloc(&cyc, 64 * 8);
@@ -190,5 +281,36 @@ int main() {
   hipMemcpy(o.data(), out, 512 * 8, hipMemcpyDeviceToHost);
   double cs = 0; for (int i = 0; i < 288; ++i) cs += o[i] * (1 + (i % 7));
   printf("pivot alone: %lld cycles (checksum %.17g)\n", pc, cs);
+  hipFuncSetAttribute((const void*)k_tasks, hipFuncAttributeMaxDynamicSharedMemorySize, MK_DIAG_LDS_BYTES);
+  for (int it = 0; it < 2; ++it) hipLaunchKernelGGL(k_tasks, dim3(1), dim3(64), MK_DIAG_LDS_BYTES, 0, out, cyc);
+  hipDeviceSynchronize();
+  long long tc[3]; hipMemcpy(tc, cyc, 24, hipMemcpyDeviceToHost);
+  for (int act = 1; act <= 4; ++act) {
+    hipLaunchKernelGGL(k_mfma_waves, dim3(1), dim3(256), 0, 0, out, cyc, act);
+    hipLaunchKernelGGL(k_mfma_waves, dim3(1), dim3(256), 0, 0, out, cyc, act);
+    hipDeviceSynchronize();
+    long long cw[4]; hipMemcpy(cw, cyc, 32, hipMemcpyDeviceToHost);
+    printf("mfma f64, %d waves issuing: cycles per MFMA per wave %.1f %.1f %.1f %.1f\n", act, cw[0] / 64.0, cw[1] / 64.0,
+           cw[2] / 64.0, cw[3] / 64.0);
+  }
+  for (int st : {129, 144}) {
+    for (int act = 1; act <= 4; ++act) {
+      hipLaunchKernelGGL(k_lds_waves, dim3(1), dim3(256), 0, 0, out, cyc, act, st);
+      hipLaunchKernelGGL(k_lds_waves, dim3(1), dim3(256), 0, 0, out, cyc, act, st);
+      hipDeviceSynchronize();
+      long long cw[4]; hipMemcpy(cw, cyc, 32, hipMemcpyDeviceToHost);
+      printf("ds_read_b64 stride %d, %d waves: cycles per read per wave %.1f %.1f %.1f %.1f\n", st, act, cw[0] / 128.0,
+             cw[1] / 128.0, cw[2] / 128.0, cw[3] / 128.0);
+    }
+  }
+  hipFuncSetAttribute((const void*)k_trail_waves, hipFuncAttributeMaxDynamicSharedMemorySize, MK_DIAG_LDS_BYTES);
+  for (int act = 1; act <= 3; act += 2) {
+    hipLaunchKernelGGL(k_trail_waves, dim3(1), dim3(256), MK_DIAG_LDS_BYTES, 0, out, cyc, act);
+    hipLaunchKernelGGL(k_trail_waves, dim3(1), dim3(256), MK_DIAG_LDS_BYTES, 0, out, cyc, act);
+    hipDeviceSynchronize();
+    long long cw[4]; hipMemcpy(cw, cyc, 32, hipMemcpyDeviceToHost);
+    printf("trail_tasks p=1 (9 blocks per wave), %d waves: cycles %lld %lld %lld\n", act, cw[1], cw[2], cw[3]);
+  }
+  printf("trail_tasks p=1 (10 blocks): %lld cycles, trailing_block: %lld cycles, S task (7 chunks): %lld cycles\n", tc[0], tc[1], tc[2]);
   return 0;
 }
