@@ -12,6 +12,15 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _no_rccl_in_the_test_process(monkeypatch):
+    """The in-process node tests exchange by device copies (MK_EXCHANGE=copy): RCCL is exercised
+    in fresh processes only (test_node_exchanges_over_rccl_in_a_fresh_process, and the torch-first
+    test in test_gpu_post.py), so no RCCL state lives on in the pytest process that runs the rest
+    of the suite (intermittent stalls were seen only after in-process RCCL use)."""
+    monkeypatch.setenv("MK_EXCHANGE", "copy")
+
+
 def _problem(mk, sizes, q=1, n_test=9, seed=3, cov=0):
     d = mk.synthetic.generate(sum(sizes), q=q, n_test=n_test, seed=seed, cov_model=cov)
     subs, off = [], 0
@@ -118,8 +127,10 @@ def test_node_exchanges_over_rccl_in_a_fresh_process():
     import subprocess
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
+    env = {k: v for k, v in os.environ.items() if k != "MK_EXCHANGE"}
+    env["NCCL_DEBUG"] = "WARN"
     r = subprocess.run([sys.executable, os.path.join(here, "gpu_node_rccl.py")], capture_output=True, text=True,
-                       timeout=240, env=dict(os.environ, NCCL_DEBUG="WARN"))
+                       timeout=240, env=env)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     res = json.loads(r.stdout.strip().splitlines()[-1])
     assert res["exchange"] == "rccl" and res["exact"], res
