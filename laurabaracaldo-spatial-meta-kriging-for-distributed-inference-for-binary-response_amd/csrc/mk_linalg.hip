@@ -430,10 +430,6 @@ __device__ inline double xget(const double* T, int r, int c) {
   return (r >= c) ? v : 0.0;
 }
 
-// Pivot block p: factor the 16x16 block in registers of one wave and invert it (F1).
-// Lane l holds row (l & 15); lanes 16..63 mirror lanes 0..15 (same instructions, results
-// unused).  Column values are broadcast by 64-bit DPP row_newbcast (no SGPR round trips);
-// upper-triangle entries are updated unconditionally and never read.
 // acc += (lane n's value of src within this lane's 16-lane DPP row) * mul: one v_fmac_f64 with a
 // 64-bit row_newbcast DPP source (the compiler keeps v_mov_b64_dpp + v_fma_f64 apart, plus a copy
 // for the old value: three instructions per element).  The asm is volatile, so the calls keep
@@ -468,12 +464,15 @@ __device__ __forceinline__ void fmac_bc16(double& acc, double src, double mul, i
 }
 #undef MK_FMAC_BC
 
-#ifndef MK_DIAG_V1
 
-// The pivot is issue-bound (one row per lane, lanes 16..63 mirroring: ~1,500 wave instructions,
-// ~10k cycles per block), so every broadcast-multiply-add is one fused DPP instruction
-// (fmac_bc16) -- the same fma, operands and order as before, so the same bits.  Branch-free:
-// the bordered row is a select and its pivot is stored after the loop.
+// Pivot block p: factor the 16x16 block in registers of one wave and invert it (F1).  Lane l holds
+// row (l & 15); in the factor lanes 16..63 mirror lanes 0..15 (same instructions, results unused),
+// in the inverse each 16-lane row group owns a quarter of the columns.  Column values are broadcast
+// by 64-bit DPP row_newbcast.  The pivot is issue-bound (~1,500 wave instructions, ~10k cycles per
+// block before round 3's rework; 5.2k now, tools/lat_probe.hip), so every broadcast-multiply-add is
+// one fused DPP instruction (fmac_bc16) -- the same fma, operands and order, so the same bits.
+// Branch-free: the bordered row is a select and its pivot is stored after the loop; upper-triangle
+// entries are updated unconditionally and never read.
 __device__ inline void factor_pivot(double* T, double* dg, double* xd, int b, int rb, double* quad_out, bool& bad) {
   const int l = threadIdx.x & 63;
   // lr opaque to the compiler, so the ~50 lane masks (lr == j, lr > m, ...) are formed where they
@@ -508,64 +507,40 @@ __device__ inline void factor_pivot(double* T, double* dg, double* xd, int b, in
   if (l == 0 && rb >= b && rb < b + 16) *quad_out = qv;
   // inverse of the pivot block, row lr of Dinv in xr: with the row-scaled factor
   // Ls(l, m) = L(l, m) / L(l, l),  X(l, c) = [l == c] / L(l, l) - sum_{c <= m < l} Ls(l, m) X(m, c)
-  double xr[16];
+  // The four 16-lane row groups split the inverse's columns: group g = l >> 4 keeps X(lr, c) for
+  // c = 4i + g in xr[i] (every broadcast it needs, X(m, c) at lane m, lives in its own row), so a
+  // step issues ceil((m+1)/4) fused fmacs instead of m+1.  Columns past m in some groups take a zero
+  // multiplier (adds an exact zero).  Each element sees the same fmas as one row per lane: same bits.
+  const int g = l >> 4;
+  double xr[4];
 #pragma unroll
-  for (int c = 0; c < 16; ++c) xr[c] = (c == lr) ? myinv : 0.0;
+  for (int i = 0; i < 4; ++i) xr[i] = (4 * i + g == lr) ? myinv : 0.0;
 #pragma unroll
   for (int m = 0; m < 15; ++m) {
     const double ncf = (lr > m) ? -(row[m] * myinv) : -0.0;
 #pragma unroll
-    for (int c = 0; c <= m; ++c) {
-      // xr[c] was last written by call c of step m-1: m calls (+ the wait) apart
-      if (c == 0) fmac_bc16<true, true>(xr[c], xr[c], ncf, m);
-      else fmac_bc16<false, true>(xr[c], xr[c], ncf, m);
-    }
-  }
-#else
-__device__ inline void factor_pivot(double* T, double* dg, double* xd, int b, int rb, double* quad_out, bool& bad) {
-  const int l = threadIdx.x & 63, lr = l & 15;
-  double row[16];
-#pragma unroll
-  for (int c = 0; c < 16; ++c) row[c] = T[(b + lr) + (b + c) * TLD];
-  double myinv = 0.0;   // 1 / L(lr, lr)
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const double a = bcast16(row[j], j);
-    double d, inv;
-    if (b + j == rb) {
-      d = 1.0;
-      inv = 1.0;
-      if (l == 0) *quad_out = -a;
-    } else {
-      bad |= !(a > 0.0);
-      rsqrt_sqrt(a, &d, &inv);
-    }
-    if (lr == j) myinv = inv;
-    row[j] = (lr == j) ? d : row[j] * inv;
-#pragma unroll
-    for (int c = j + 1; c < 16; ++c) row[c] = fma(-row[j], bcast16(row[j], c), row[c]);
-  }
-  double xr[16];
-#pragma unroll
-  for (int c = 0; c < 16; ++c) xr[c] = (c == lr) ? myinv : 0.0;
-#pragma unroll
-  for (int m = 0; m < 15; ++m) {
-    const double cf = (lr > m) ? row[m] * myinv : 0.0;
-#pragma unroll
-    for (int c = 0; c <= m; ++c) xr[c] = fma(-cf, bcast16(xr[c], m), xr[c]);
-  }
-#endif
-  if (l < 16) {
-#pragma unroll
-    for (int c = 0; c < 16; ++c) {
-      if (c < l) {
-        T[(b + l) + (b + c) * TLD] = row[c];
-        T[(b + c) + (b + l) * TLD] = xr[c];     // Dinv strictly lower, transposed
+    for (int i = 0; i < 4; ++i) {
+      if (4 * i <= m) {
+        const double mi = (4 * i + g <= m) ? ncf : 0.0;
+        fmac_bc16<true, true>(xr[i], xr[i], mi, m);   // xr[i] was written one or a few calls earlier
       }
     }
+  }
+  // X out, all 64 lanes (row lr, columns 4i + g): strictly lower transposed, the diagonal in place
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = 4 * i + g;
+    if (c < lr) T[(b + c) + (b + lr) * TLD] = xr[i];
+    if (c == lr) {
+      xd[b + lr] = xr[i];
+      T[(b + lr) + (b + lr) * TLD] = xr[i];   // X diagonal in place (the L diagonal lives in dg)
+    }
+  }
+  if (l < 16) {
+#pragma unroll
+    for (int c = 0; c < 16; ++c)
+      if (c < l) T[(b + l) + (b + c) * TLD] = row[c];
     dg[b + l] = row[l];
-    xd[b + l] = xr[l];
-    T[(b + l) + (b + l) * TLD] = xr[l];   // X diagonal in place (the L diagonal lives in dg)
   }
 }
 
@@ -756,9 +731,7 @@ __device__ void factor_invert_tile(double* T, double* dg, double* xd, double* Sb
     if (wv == 0) {
       // (block (p, p)'s update by step p-1 was done by this wave at the end of step p-1)
       MK_TSTAMPW(44 + 4 * p, 0);
-#ifndef MK_DIAG_PROBE_NOPIVOT
       factor_pivot(T, dg, xd, 16 * p, rb, quad_out, bad);
-#endif
       MK_TSTAMPW(45 + 4 * p, 0);
     } else {
       // tasks t (dealt round-robin over the three waves): S_pc for t < p (c = t, longest first),

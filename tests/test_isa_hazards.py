@@ -20,5 +20,5 @@ def test_fused_dpp_fmacs_have_their_wait_states(tmp_path):
     subprocess.check_call([hipcc, "-w", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
                            "--cuda-device-only", "-S", os.path.join(CSRC, "mk_linalg.hip"), "-o", str(out)])
     n, bad = dpp_hazards.check(out.read_text())
-    assert n >= 240, n          # 120 factor + 120 inverse updates per pivot block
+    assert n >= 150, n          # 120 factor updates + 36 inverse updates (four row groups) per pivot block
     assert not bad, bad[:3]
