@@ -1,0 +1,9 @@
+#!/bin/bash
+# Diagonal tile on its pair's XCD (the tile kernels' xcd_map): probe, windows at 32 and 250 subsets.
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/r03z
+mkdir -p $O
+timeout -k 10 60 ./tools/diag_probe 32 > $O/dp_32.log 2>&1 || exit 1
+timeout -k 10 150 python bench.py --no-cpu-baseline --no-e2e --n 64000 --subsets 32 --steps 40 --warmup 4 > $O/b32.json 2> $O/b32.err || exit 1
+timeout -k 10 200 python bench.py --no-cpu-baseline --no-e2e > $O/b250.json 2> $O/b250.err || exit 1
+timeout -k 10 150 python bench.py --no-cpu-baseline --no-e2e --n 64000 --subsets 32 --steps 40 --warmup 4 > $O/b32b.json 2> $O/b32b.err || exit 1
