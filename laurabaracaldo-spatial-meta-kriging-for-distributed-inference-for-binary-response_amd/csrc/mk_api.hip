@@ -17,6 +17,7 @@
 #include <cstdlib>
 #include <utility>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 #include "../../include/mk.h"
@@ -166,6 +167,66 @@ MatSet matset_view(const MatSet& m, int s0) {
 }  // namespace
 
 static std::atomic<int> g_live_sessions{0};
+
+// ------------------------------------------------------------------ stream pool
+// HIP streams outlive the sessions that use them: a session takes its streams from a per-process
+// pool keyed by device and kind (plain, high priority, CU-masked with a given mask) and hands them
+// back drained when it is destroyed.  A process that runs many sessions (the GPU test suite
+// creates a few hundred) then creates its queues once instead of creating and destroying HIP
+// queues -- CU-masked and priority ones included -- per session, the common factor of the
+// intermittent stalls DESIGN.md 4.2 records (in session create / destroy).
+enum { SK_PLAIN = 0, SK_PRIO = 1, SK_CUMASK = 2 };
+struct PoolKey {
+  int device = -1, kind = SK_PLAIN, prio = 0;
+  std::vector<uint32_t> mask;
+  bool operator==(const PoolKey& o) const {
+    return device == o.device && kind == o.kind && prio == o.prio && mask == o.mask;
+  }
+};
+typedef std::vector<std::pair<PoolKey, hipStream_t>> StreamList;
+static std::mutex g_pool_mu;
+static StreamList g_pool;   // idle streams
+
+// A stream of this kind on the current device (hipSetDevice(device) done by the caller), recorded
+// in `owned` for the session's destructor.
+static hipError_t pool_stream(StreamList& owned, hipStream_t* st, int device, int kind, int prio = 0,
+                              const std::vector<uint32_t>& mask = {}) {
+  PoolKey k;
+  k.device = device;
+  k.kind = kind;
+  k.prio = prio;
+  k.mask = mask;
+  {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    for (size_t i = 0; i < g_pool.size(); ++i)
+      if (g_pool[i].first == k) {
+        *st = g_pool[i].second;
+        g_pool.erase(g_pool.begin() + (long)i);
+        owned.push_back({k, *st});
+        return hipSuccess;
+      }
+  }
+  hipError_t e;
+  if (kind == SK_CUMASK) {
+    // cuMaskSize = the device's CU count (as before the pool); the array is padded to that many
+    // words so the runtime never reads past it, whichever unit it counts in (the words past the
+    // CU count are ignored)
+    const uint32_t size = (uint32_t)(mask.size() * 32);
+    std::vector<uint32_t> padded(size, 0xffffffffu);
+    for (size_t i = 0; i < mask.size(); ++i) padded[i] = mask[i];
+    e = hipExtStreamCreateWithCUMask(st, size, padded.data());
+  } else {
+    e = kind == SK_PRIO ? hipStreamCreateWithPriority(st, hipStreamNonBlocking, prio)
+                        : hipStreamCreateWithFlags(st, hipStreamNonBlocking);
+  }
+  if (e == hipSuccess) owned.push_back({k, *st});
+  return e;
+}
+static void pool_return(StreamList& owned) {
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  for (auto& o : owned) g_pool.push_back(o);
+  owned.clear();
+}
 // Hardware queues of this process's HIP runtime (mk_set_hw_queues; -1: GPU_MAX_HW_QUEUES as set in
 // the environment, HIP's default 4 when unset).
 static std::atomic<int> g_hw_queues{-1};
@@ -184,6 +245,7 @@ struct mk_session {
   mk_session() { g_live_sessions.fetch_add(1); }
   int device = 0;
   hipStream_t stream = nullptr;   // set-up, outputs and the one-group paths
+  StreamList owned;               // every stream of the session (pool_stream), back to the pool at the end
   Model md{};
   MatSet ms{};
   int S = 0, q = 1, p = 0, n_pad = 0, nt = 0, P = 0;
@@ -269,14 +331,7 @@ struct mk_session {
   ~mk_session() {
     g_live_sessions.fetch_sub(1);
     if (device >= 0) hipSetDevice(device);
-    std::vector<hipStream_t> streams;
-    for (auto& g : groups) {
-      if (g.stream && g.stream != stream) streams.push_back(g.stream);
-      if (g.bulk) streams.push_back(g.bulk);
-    }
-    for (hipStream_t st : {la_c, la_m, la_k, stream})
-      if (st) streams.push_back(st);
-    for (hipStream_t st : streams) hipStreamSynchronize(st);
+    for (auto& o : owned) hipStreamSynchronize(o.second);
     for (auto& t : pending) { hipEventDestroy(t.a); hipEventDestroy(t.b); }
     for (auto& g : groups) {
       if (g.done) hipEventDestroy(g.done);
@@ -284,7 +339,7 @@ struct mk_session {
     }
     if (swept) hipEventDestroy(swept);
     for (hipEvent_t e : la_ev) hipEventDestroy(e);
-    for (hipStream_t st : streams) hipStreamDestroy(st);
+    pool_return(owned);   // drained above; their waits on the destroyed events are satisfied
     for (void* p_ : allocs) hipFree(p_);
     (void)hipGetLastError();   // teardown errors are not the next call's
   }
@@ -980,7 +1035,7 @@ static int setup_groups(mk_session* s, int n_groups) {
     g.d_pcount = counts + 2 * gi + 1;
     if (G == 1) {
       g.stream = s->stream;
-    } else if (hipStreamCreateWithFlags(&g.stream, hipStreamNonBlocking) != hipSuccess) {
+    } else if (pool_stream(s->owned, &g.stream, s->device, SK_PLAIN) != hipSuccess) {
       return set_err(MK_E_HIP, "group stream");
     }
     s->groups.push_back(g);
@@ -1004,7 +1059,7 @@ static int setup_groups(mk_session* s, int n_groups) {
     std::vector<uint32_t> mask((n_cu + 31) / 32, 0xffffffffu);
     for (int b = 0; b < reserve && b < n_cu; ++b) mask[b / 32] &= ~(1u << (b % 32));
     Group& g = s->groups[0];
-    if (hipExtStreamCreateWithCUMask(&g.bulk, (uint32_t)n_cu, mask.data()) != hipSuccess)
+    if (pool_stream(s->owned, &g.bulk, s->device, SK_CUMASK, 0, mask) != hipSuccess)
       return set_err(MK_E_HIP, "bulk stream");
     g.ev.assign(3 * s->nt + 1, nullptr);
     for (auto& e : g.ev)
@@ -1113,7 +1168,7 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
   std::unique_ptr<mk_session> hold(new mk_session());
   mk_session* s = hold.get();
   s->device = c->device;
-  if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) return set_err(MK_E_HIP, "stream");
+  if (pool_stream(s->owned, &s->stream, s->device, SK_PLAIN) != hipSuccess) return set_err(MK_E_HIP, "stream");
 
   const int S = pr->n_subsets, q = pr->q, p = pr->p;
   s->S = S; s->q = q; s->p = p;
@@ -1433,9 +1488,9 @@ extern "C" int mk_session_run(mk_session* s, int32_t n_iter) {
     static const int prio_env = tile_env("MK_LA_PRIO", 1);
     int lo = 0, hi = 0;
     if (prio_env && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess) {
-      if (hipStreamCreateWithPriority(&s->la_c, hipStreamNonBlocking, hi) != hipSuccess)
+      if (pool_stream(s->owned, &s->la_c, s->device, SK_PRIO, hi) != hipSuccess)
         return set_err(MK_E_HIP, "lookahead stream");
-    } else if (hipStreamCreateWithFlags(&s->la_c, hipStreamNonBlocking) != hipSuccess) {
+    } else if (pool_stream(s->owned, &s->la_c, s->device, SK_PLAIN) != hipSuccess) {
       return set_err(MK_E_HIP, "lookahead stream");
     }
     // Two more streams when the process has the hardware queues for them (HIP maps streams onto
@@ -1450,7 +1505,7 @@ extern "C" int mk_session_run(mk_session* s, int32_t n_iter) {
     const bool queues = hw_queues() >= 8;
     static const int krig_env = tile_env("MK_LA_KRIG", -1);
     if ((krig_env == 1 || (krig_env < 0 && queues)) && s->md.n_test > 0 && !s->tiled &&
-        hipStreamCreateWithFlags(&s->la_k, hipStreamNonBlocking) != hipSuccess)
+        pool_stream(s->owned, &s->la_k, s->device, SK_PLAIN) != hipSuccess)
       return set_err(MK_E_HIP, "lookahead kriging stream");
     static const int mask_env = tile_env("MK_LA_MASK", -1);
     const int mask_cu = mask_env >= 0 ? mask_env : (queues ? 32 : 0);
@@ -1458,7 +1513,7 @@ extern "C" int mk_session_run(mk_session* s, int32_t n_iter) {
     if (mask_cu > 0 && hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, s->device) == hipSuccess) {
       std::vector<uint32_t> mask((n_cu + 31) / 32, 0xffffffffu);
       for (int b = 0; b < mask_cu && b < n_cu; ++b) mask[b / 32] &= ~(1u << (b % 32));
-      if (hipExtStreamCreateWithCUMask(&s->la_m, (uint32_t)n_cu, mask.data()) != hipSuccess)
+      if (pool_stream(s->owned, &s->la_m, s->device, SK_CUMASK, 0, mask) != hipSuccess)
         return set_err(MK_E_HIP, "lookahead main stream");
     }
   }
@@ -2181,7 +2236,7 @@ extern "C" int mk_cholesky_batched(const double* A, int32_t S, int32_t n, double
   mk_session* s = new mk_session();
   s->device = device;
   auto fail = [&](int code) { delete s; return code; };
-  if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) return fail(set_err(MK_E_HIP, "stream"));
+  if (pool_stream(s->owned, &s->stream, device, SK_PLAIN) != hipSuccess) return fail(set_err(MK_E_HIP, "stream"));
   const int n_pad = round_up(n + 1, MK_NB), nt = n_pad / MK_NB;
   s->S = S; s->q = 1; s->n_pad = n_pad; s->nt = nt;
   s->n_part.assign(S, n);
