@@ -227,6 +227,20 @@ static void pool_return(StreamList& owned) {
   for (auto& o : owned) g_pool.push_back(o);
   owned.clear();
 }
+namespace mk {
+hipError_t stream_acquire(int device, hipStream_t* st) {
+  StreamList one;
+  return pool_stream(one, st, device, SK_PLAIN);
+}
+void stream_release(int device, hipStream_t st) {
+  StreamList one;
+  PoolKey k;
+  k.device = device;
+  k.kind = SK_PLAIN;
+  one.push_back({k, st});
+  pool_return(one);
+}
+}  // namespace mk
 // Hardware queues of this process's HIP runtime (mk_set_hw_queues; -1: GPU_MAX_HW_QUEUES as set in
 // the environment, HIP's default 4 when unset).
 static std::atomic<int> g_hw_queues{-1};

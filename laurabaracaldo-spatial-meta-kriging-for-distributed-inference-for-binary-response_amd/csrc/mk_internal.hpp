@@ -15,4 +15,8 @@ int session_info(const mk_session* s, ShardInfo* info);
 int session_param_grids(mk_session* s, double* d_out);                   // [S][P][200]
 int session_wpred_grids(mk_session* s, double* d_out);                   // fused: [S][q n_test][200]
 int session_tile_grids(mk_session* s, int t0, double* d_out, mk_outputs* o);   // tiled: [S][q Tc][200]
+// A plain non-blocking stream of the current device from libmk's stream pool, and its return
+// (drained by the caller): the node driver's per-block streams live as long as the sessions' do.
+hipError_t stream_acquire(int device, hipStream_t* st);
+void stream_release(int device, hipStream_t st);
 }  // namespace mk

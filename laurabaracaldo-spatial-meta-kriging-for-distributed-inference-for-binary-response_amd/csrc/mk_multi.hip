@@ -195,7 +195,7 @@ struct Block {
     if (st) (void)hipStreamSynchronize(st);
     if (ses) mk_session_destroy(ses);
     if (packed) (void)hipEventDestroy(packed);
-    if (st) (void)hipStreamDestroy(st);
+    if (st) stream_release(dev, st);   // drained above
   }
 };
 
@@ -355,7 +355,7 @@ extern "C" int mk_meta_fit(const mk_problem* pr, const mk_config* c, const int32
   int rc = nd.pool->run([&](int r) -> int {
     Block& x = *nd.b[r];
     MHIP(hipSetDevice(x.dev));
-    MHIP(hipStreamCreateWithFlags(&x.st, hipStreamNonBlocking));
+    MHIP(stream_acquire(x.dev, &x.st));
     MHIP(hipEventCreateWithFlags(&x.packed, hipEventDisableTiming));
     if (x.S == 0) return 0;
     mk_problem sp = *pr;
