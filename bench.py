@@ -51,7 +51,12 @@ def parse():
     ap.add_argument("--subsets", type=int, default=250)
     ap.add_argument("--n-test", type=int, default=1000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-iters", type=int, default=40)
+    ap.add_argument("--no-legs", action="store_true",
+                    help="skip the extra legs (N=1): the 32-subset shard window and the configs[4] kriging sample")
+    ap.add_argument("--shard-subsets", type=int, default=32,
+                    help="subsets of the shard leg (the per-GPU share of configs[2] on 8 GPUs)")
+    ap.add_argument("--krig-subsets", type=int, default=32, help="subsets of the configs[4] kriging leg")
+    ap.add_argument("--krig-sites", type=int, default=1_000_000, help="test sites of the configs[4] kriging leg")
     ap.add_argument("--no-kernel-events", action="store_true",
                     help="diagnostic: no per-kernel HIP events in the timed region (roofline fields then null)")
     ap.add_argument("--scaling", choices=("weak", "strong"), default="strong",
@@ -73,28 +78,33 @@ def parse():
 
 # ------------------------------------------------------------------ CPU baseline (oracle, rank 0, N=1)
 def _cpu_worker(args):
-    n_s, iters, seed, idx = args
+    sub, coords_test, cfg_kw, subset, state, end = args
     os.environ["OPENBLAS_NUM_THREADS"] = "1"
     sys.path.insert(0, ROOT)
     from oracle import spmvglm as om
-    syn = importlib.import_module(PKG + ".synthetic")
-    d = syn.generate(n_s, q=1, n_test=1000, seed=seed + idx)
-    cfg = om.Config(1, 2, beta_starting=[0.9, -0.9], beta_tuning=[0.01, 0.01], n_batch=100, batch_length=50,
-                    burn_in=2, seed=seed)
-    r = om.fit_subset(d["coords"], d["y"], np.ones(n_s), d["x"], cfg, subset=idx, coords_test=d["coords_test"],
-                      max_iter=iters, quantiles=False, sweep="c")
-    return r["loop_seconds"]       # the MCMC iterations only (set-up excluded, as on the GPU side)
+    cfg = om.Config(1, 2, **cfg_kw)
+    r = om.fit_subset(sub["coords"], sub["y"], sub["weights"], sub["x"], cfg, subset=subset, coords_test=coords_test,
+                      max_iter=end, quantiles=False, sweep="c", start=state)
+    # the MCMC iterations only (set-up and the resume's re-factorisation excluded, as on the GPU side)
+    return r["loop_seconds"], r["phase_seconds"], r["samples"][state["iteration"]:end]
 
 
-def cpu_baseline(n_s, iters, workers):
+def cpu_baseline(subs, coords_test, cfg_kw, states, end, workers):
+    """The oracle over the device's own timed window: subset i (i < workers, global index i, the same
+    Philox streams) resumes from the device's chain state at the window's first iteration
+    (mk_session_chain_state: adapted proposal scales, the current batch's accept counts) and runs the
+    same iterations -- the same burn-in : kept split, kriging on the kept ones -- one process and one
+    BLAS thread per core.  Returns the rate, the per-phase seconds per subset-iteration and the
+    window's samples (to compare with the device's)."""
     import multiprocessing as mp
     ctx = mp.get_context("spawn")
     saved = {k: os.environ.get(k) for k in ("OPENBLAS_NUM_THREADS", "OMP_NUM_THREADS")}
     os.environ["OPENBLAS_NUM_THREADS"] = os.environ["OMP_NUM_THREADS"] = "1"   # inherited by the spawned workers
+    jobs = [(subs[i], coords_test, cfg_kw, i, states[i], end) for i in range(workers)]
     t0 = time.perf_counter()
     try:
         with ctx.Pool(workers) as pool:
-            per = pool.map(_cpu_worker, [(n_s, iters, 7, i) for i in range(workers)])
+            res = pool.map(_cpu_worker, jobs)
     finally:
         for k, v in saved.items():
             if v is None:
@@ -102,13 +112,63 @@ def cpu_baseline(n_s, iters, workers):
             else:
                 os.environ[k] = v
     wall = time.perf_counter() - t0
-    # rate over the slowest worker's iteration loop (set-up and interpreter start-up excluded)
-    rate = workers * iters / max(per)
+    steps = end - states[0]["iteration"]
+    loops = [r[0] for r in res]
+    rate = workers * steps / max(loops)      # over the slowest worker's iteration loop
+    phases = {k: sum(r[1][k] for r in res) / (workers * steps) for k in res[0][1]}
     return dict(value=rate, unit="subset-iters/s", cores=workers, kind="port",
-                sample=f"{workers} subsets x {iters} kept iterations (n_s={n_s}, 1000 kriging sites) of the same "
-                       f"workload, oracle/spmvglm.py: LAPACK dpotrf/dpotri (OpenBLAS), NumPy vector work and the "
-                       f"latent sweep in C (oracle/csrc/sweep.c), one process and one BLAS thread per core; "
-                       f"wall {wall:.1f}s incl. start-up")
+                phase_s_per_subset_iter=phases,
+                sample=f"{workers} of the device's subsets (global indices 0..{workers - 1}, n_s="
+                       f"{len(subs[0]['coords'])}, {np.asarray(coords_test).shape[0]} kriging sites) over the device's "
+                       f"own timed window, iterations {states[0]['iteration'] + 1}-{end}, resumed from the device's "
+                       f"chain state there (adapted scales); oracle/spmvglm.py: LAPACK dpotrf/dpotri (OpenBLAS), "
+                       f"NumPy vector work and the latent sweep in C (oracle/csrc/sweep.c), one process and one BLAS "
+                       f"thread per core; wall {wall:.1f}s incl. start-up"), [r[2] for r in res]
+
+
+def physical_cores():
+    """Physical cores of the host: distinct SMT sibling sets in sysfs (None if unreadable)."""
+    import glob
+    sets = set()
+    for p_ in glob.glob("/sys/devices/system/cpu/cpu[0-9]*/topology/thread_siblings_list"):
+        try:
+            with open(p_) as f:
+                sets.add(f.read().strip())
+        except OSError:
+            pass
+    return len(sets) or None
+
+
+def shard_leg(mk, d, idx, S, beta0, bt, adapt_batches, warmup, steps):
+    """The per-GPU share of configs[2] on 8 GPUs (S = 32 of its 250 subsets, global indices 0..S-1)
+    over the same kind of window as the headline: adapt, warm up, then `steps` iterations timed with
+    the same 3:1 burn-in : kept split.  The rate an 8-GPU strong-scaling run's ranks each see."""
+    A = max(0, adapt_batches) * 50
+    W = max(1, warmup) + A
+    n_burn = int(round(0.75 * steps))
+    cfg = mk.SamplerConfig(1, 2, beta0, bt, n_batch=(W + steps + 49) // 50, batch_length=50,
+                           burn_in=W + n_burn + 1, seed=20250114)
+    subs = [mk.subset_data(d["y"], d["x"], 1.0, d["coords"], 1, idx[i]) for i in range(S)]
+    with mk.Session(subs, cfg, coords_test=d["coords_test"]) as ses:
+        ses.run(W)
+        ses.profile(True, kinds=[mk.session.KS_CHOL_UPDATE, mk.session.KS_CHOL_UPDATE_SUB])
+        t0 = time.perf_counter()
+        ses.run(steps)
+        el = time.perf_counter() - t0
+        st = ses.kernel_stats(mk.session.KS_UPDATE_BUSY)
+        la = ses.lookahead
+    tf = st["flops"] / (st["ms"] * 1e-3) / 1e12 if st["ms"] > 0 else 0.0
+    return {"value": S * steps / el, "unit": "subset-iters/s", "ms_per_step": el / steps * 1e3,
+            "workload": f"{S} of configs[2]'s subsets (the per-GPU share of K=250 on 8 GPUs), n_s=2000, exponential, "
+                        f"q=1, n_test=1000, window {n_burn} burn-in + {steps - n_burn} kept iterations at "
+                        f"{W + 1}-{W + steps} (after {A} adaptation + {W - A} warmup iterations)",
+            "schedule": "lookahead" if la else "sequential",
+            # an 8-GPU strong-scaling run: every rank holds <= S (31-32) of the 250 subsets at this chain rate
+            "projected_8gpu_value": 250 * steps / el,
+            "roofline": {"kernel": "k_chol_update (union of its launch intervals)", "achieved": tf,
+                         "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": tf / FP64_PEAK_TFLOPS,
+                         "note": "update launches share the chip with the main stream (lookahead schedule): "
+                                 "the fraction understates the kernel's own rate"}}
 
 
 def host_cores():
@@ -179,6 +239,7 @@ def end_to_end(mk, d, K, devices=(0,)):
             "reference_timer_s": ph["setup_s"] + ph["chains_s"] + ph["quantiles_combine_s"],
             "chains_subset_iters_per_s": K * cfg.n_samples / ph["chains_s"],
             "devices": list(devices),
+            "exchange": ph.get("exchange"),
             "workload": f"configs[2] end to end on {len(devices)} GPU(s), one process: n={len(d['coords'])}, K={K}, "
                         f"exponential, q=1, "
                         f"n_test={len(d['coords_test'])}, 100 x 50 amcmc iterations, burn.in 3,750 "
@@ -213,13 +274,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     K, n, n_test = a.subsets, a.n, a.n_test
-
-    cpu = None
-    if rank == 0 and world == 1 and not a.no_cpu_baseline and a.cpu_iters > 0:
-        host = host_cores()
-        cpu = cpu_baseline(n // K, a.cpu_iters, host["usable"])   # before any GPU initialisation (spawn pool)
-        cpu.update(host_nproc=host["nproc"], host_affinity=host["affinity"], cpu_model=host["model"],
-                   cores_note=host["note"])
+    want_cpu = rank == 0 and world == 1 and not a.no_cpu_baseline
+    host = host_cores() if want_cpu else None
 
     dist = None
     if world > 1:
@@ -259,6 +315,9 @@ def main():
     ses = mk.Session(subs, cfg, coords_test=d["coords_test"], subset_base=base, device=local if world > 1 else 0)
     la = ses.lookahead
     ses.run(W)                                    # warmup
+    # the CPU baseline resumes the first chains from here: the state at the window's first iteration
+    n_cpu = min(host["usable"], hi - lo) if want_cpu else 0
+    cpu_states = [ses.chain_state(i) for i in range(n_cpu)]
     # timed window: HIP events bracket only the roofline kernel (k_chol_update) on its stream
     upd_kinds = [mk.session.KS_CHOL_UPDATE, mk.session.KS_CHOL_UPDATE_SUB]   # k_chol_update<128> + <64>/<32>
     ses.profile(not a.no_kernel_events, kinds=upd_kinds)
@@ -294,7 +353,15 @@ def main():
     ses.profile(True)
     ses.run(n_post)
     kern = {name: {"ms": ses.kernel_stats(i)["ms"] - before[name]["ms"]} for name, i in kinds}
+    dev_window = ses.outputs(quantiles=False, samples=True)["samples"][:n_cpu] if n_cpu else []
     ses.close()
+    legs = {}
+    if world == 1 and not a.no_legs:
+        legs["shard32"] = shard_leg(mk, d, idx, min(a.shard_subsets, K), beta0, bt, a.adapt_batches, a.warmup, a.steps)
+        import bench_kriging
+        kr_sites = np.random.default_rng(20250115).uniform(size=(a.krig_sites, 2))   # configs[4]: 1M held-out sites
+        kr_subs = [mk.subset_data(d["y"], d["x"], 1.0, d["coords"], 1, idx[i]) for i in range(min(a.krig_subsets, K))]
+        legs["kriging_cfg5"] = bench_kriging.kriging_leg(mk, kr_subs, kr_sites, beta0, bt)
     e2e = None
     if world == 1 and not a.no_e2e:
         e2e = end_to_end(mk, d, K, tuple(int(x) for x in a.e2e_devices.split(",")))
@@ -306,6 +373,15 @@ def main():
         if dist is not None:
             dist.destroy_process_group()
         return
+    cpu = None
+    if n_cpu:
+        cfg_kw = dict(beta_starting=beta0, beta_tuning=bt, n_batch=cfg.n_batch, batch_length=50, burn_in=burn_in,
+                      seed=20250114)
+        cpu, cpu_window = cpu_baseline(subs, d["coords_test"], cfg_kw, cpu_states, W + a.steps, n_cpu)
+        dev = np.stack([smp[W:W + a.steps] for smp in dev_window])
+        cpu["window_max_abs_dev_vs_device"] = float(np.max(np.abs(np.stack(cpu_window) - dev)))
+        cpu.update(host_nproc=host["nproc"], host_affinity=host["affinity"], cpu_model=host["model"],
+                   cores_note=host["note"], host_physical_cores=physical_cores())
     K_job = K * world if weak else K
     value = K_job * a.steps / elapsed
     avg_ms = summed_ms / max(1, st["launches"])   # per-launch duration (what rocprofv3 reports)
@@ -357,6 +433,8 @@ def main():
         "chain_iters_per_s": a.steps / elapsed,
         "end_to_end_estimate_s": elapsed / a.steps * 5000,
     }
+    if legs:
+        out["legs"] = legs
     if e2e is not None:
         if "phases" in e2e:
             out["end_to_end_s"] = e2e["phases"]["end_to_end_s"]
@@ -364,17 +442,19 @@ def main():
     if cpu is not None:
         out["cpu_baseline"] = cpu
         out["gpu_over_cpu"] = value / cpu["value"]
-        # the port is one process per core (no shared state): its rate scales with cores.  Projections,
-        # labelled as such -- the job's CPU share on the box is cpu["cores"] cores
-        per_gpu_cores = max(1, cpu["host_nproc"] // 8)
+        # the port is one process per core (no shared state): its rate scales with PHYSICAL cores (SMT
+        # siblings share a core's FP64 units).  Projections, labelled as such -- the job's CPU share on
+        # the box is cpu["cores"] cores
+        phys = cpu.get("host_physical_cores") or cpu["host_nproc"]
+        per_gpu_cores = max(1, phys // 8)
         out["cpu_projection"] = {
-            "note": "linear in cores (independent subsets, one process per core); not measured beyond the job's "
-                    f"{cpu['cores']}-core share",
+            "note": "linear in physical cores (independent subsets, one process per core); not measured beyond "
+                    f"the job's {cpu['cores']}-core share",
             "per_gpu_share_cores": per_gpu_cores,
             "per_gpu_share_value": cpu["value"] * per_gpu_cores / cpu["cores"],
             "gpu_over_per_gpu_share": value / (cpu["value"] * per_gpu_cores / cpu["cores"]),
-            "node_cores": cpu["host_nproc"],
-            "node_value": cpu["value"] * cpu["host_nproc"] / cpu["cores"],
+            "node_cores": phys,
+            "node_value": cpu["value"] * phys / cpu["cores"],
         }
         if e2e is not None:
             # the CPU port's wall clock for the same 250 x 5,000 subset-iterations (chains only)

@@ -33,6 +33,62 @@ PKG = "laurabaracaldo-spatial-meta-kriging-for-distributed-inference-for-binary-
 FP64_PEAK_TFLOPS = 78.6
 
 
+def kriging_leg(mk, subs, coords_test, beta0, bt, kept=6, burn=14, tile=65536, kernel_events=True, subset_base=0):
+    """Tiled spPredict of `coords_test` from the subsets `subs` (n_s each): burn + kept iterations with
+    the kept states recorded, then the replay over test-site tiles, timed.  Returns the result dict
+    (draws/s, k_pred_var roofline, the configs[4] extrapolation).  bench.py runs it on the per-GPU
+    share of configs[2]'s own subsets with 1M sites (the driver-measured configs[4] rate)."""
+    S = len(subs)
+    ns = int(max(len(s_["coords"]) for s_ in subs))
+    n_test = int(np.asarray(coords_test).shape[0])
+    n_samples = burn + kept
+    cfg = mk.SamplerConfig(1, 2, beta0, bt, n_batch=1, batch_length=n_samples, burn_in=burn + 1, seed=20250114,
+                           predict_tile=tile)
+    with mk.Session(subs, cfg, coords_test=coords_test, subset_base=subset_base) as ses:
+        t0 = time.perf_counter()
+        ses.run(n_samples)
+        t1 = time.perf_counter()
+        if kernel_events:   # HIP events around every k_pred_var launch (the kriging GEMM)
+            ses.profile(True, kinds=[mk.session.KS_PRED_VAR])
+        out = ses.outputs(quantiles=False, samples=True, w_predict_sum=True)
+        t2 = time.perf_counter()
+        pv = ses.kernel_stats(mk.session.KS_PRED_VAR)
+    kept_phi = np.stack([smp[burn:, 3] for smp in out["samples"]])          # phi column of p.beta.theta.samples
+    runs = int(sum(1 + np.count_nonzero(np.diff(r)) for r in kept_phi))
+    pred_s = t2 - t1
+    flops = runs * (ns * ns * n_test + 2.0 * ns ** 3 / 3.0 * ((n_test + tile - 1) // tile)) \
+        + 2.0 * ns * S * n_test * kept
+    draws = S * n_test * kept
+    # extrapolation: cfg5 = 250 subsets x 1M sites x 1251 kept; runs scale with the kept acceptance of phi
+    run_frac = runs / (S * kept)
+    cfg5_flops = 250 * 1251 * run_frac * ns * ns * 1_000_000
+    rate_tf = flops / pred_s / 1e12
+    res = {
+        "metric": "kriging draws/s (tiled spPredict, configs[4] scale)",
+        "value": draws / pred_s, "unit": "draws/s", "n_gpus": 1, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": f"configs[4] sample: {S} subsets of {ns}, {n_test} test sites, {kept} kept samples, "
+                               f"tile {tile}", "subsets": S, "n_test": n_test, "kept": kept, "tile": tile},
+        "fit_seconds": t1 - t0, "predict_seconds": pred_s, "phi_runs": runs,
+        "roofline": {"bound": "mfma", "achieved": rate_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": rate_tf / FP64_PEAK_TFLOPS},
+        "cfg5_extrapolation": {"flops": cfg5_flops, "seconds_1gpu": cfg5_flops / (rate_tf * 1e12),
+                               "seconds_8gpu": cfg5_flops / (rate_tf * 1e12) / 8,
+                               "assumes": f"phi runs per kept sample {run_frac:.3f} as measured here"},
+        "w_predict_sum_finite": bool(np.isfinite(out["w_predict_sum"]).all()),
+    }
+    if kernel_events and pv["ms"] > 0:
+        gemm_flops = runs * ns * ns * n_test   # X = W P^T, W lower-triangular, per (subset, phi run)
+        tf = gemm_flops / (pv["ms"] * 1e-3) / 1e12
+        gen = os.environ.get("MK_PRED_GEN", "0") not in ("", "0")
+        res["k_pred_var"] = {"launches": pv["launches"], "ms": pv["ms"], "avg_launch_ms": pv["ms"] / pv["launches"],
+                             "algorithmic_flops": gemm_flops, "achieved": tf, "unit": "TFLOP/s",
+                             "frac": tf / FP64_PEAK_TFLOPS, "p_t": "generated in LDS" if gen else "stored",
+                             "algorithmic_bytes": runs * (ns * ns / 2 + (1 if gen else 2) * ns * n_test) * 8.0,
+                             "bytes_note": "per (subset, phi run): W (lower) read once, X written once"
+                                           + ("" if gen else ", P^T read once")}
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--subsets", type=int, default=32)   # the per-GPU share of K = 250 on 8 GPUs
@@ -47,53 +103,10 @@ def main():
     S, ns = a.subsets, a.n_sub
     d = mk.synthetic.generate(S * ns, q=1, n_test=a.n_test, seed=20250114)
     beta0, bt = mk.start_values(d["y"], d["x"], 1.0, 1)
-    n_samples = a.burn + a.kept
-    cfg = mk.SamplerConfig(1, 2, beta0, bt, n_batch=1, batch_length=n_samples, burn_in=a.burn + 1, seed=20250114,
-                           predict_tile=a.tile)
     subs = [dict(coords=d["coords"][i * ns:(i + 1) * ns], y=d["y"][i * ns:(i + 1) * ns], weights=np.ones(ns),
                  x=d["x"][i * ns:(i + 1) * ns]) for i in range(S)]
-    with mk.Session(subs, cfg, coords_test=d["coords_test"]) as ses:
-        t0 = time.perf_counter()
-        ses.run(n_samples)
-        t1 = time.perf_counter()
-        if a.kernel_events:   # HIP events around every k_pred_var launch (the kriging GEMM)
-            ses.profile(True, kinds=[mk.session.KS_PRED_VAR])
-        out = ses.outputs(quantiles=False, samples=True, w_predict_sum=True)
-        t2 = time.perf_counter()
-        pv = ses.kernel_stats(mk.session.KS_PRED_VAR)
-    kept_phi = np.stack([smp[a.burn:, 3] for smp in out["samples"]])          # phi column of p.beta.theta.samples
-    runs = int(sum(1 + np.count_nonzero(np.diff(r)) for r in kept_phi))
-    pred_s = t2 - t1
-    flops = runs * (ns * ns * a.n_test + 2.0 * ns ** 3 / 3.0 * ((a.n_test + a.tile - 1) // a.tile)) \
-        + 2.0 * ns * S * a.n_test * a.kept
-    draws = S * a.n_test * a.kept
-    # extrapolation: cfg5 = 250 subsets x 1M sites x 1251 kept; runs scale with the kept acceptance of phi
-    run_frac = runs / (S * a.kept)
-    cfg5_flops = 250 * 1251 * run_frac * ns * ns * 1_000_000
-    rate_tf = flops / pred_s / 1e12
-    res = {
-        "metric": "kriging draws/s (tiled spPredict, configs[4] scale)",
-        "value": draws / pred_s, "unit": "draws/s", "n_gpus": 1, "dtype": "f64", "data": "synthetic",
-        "config": {"workload": f"configs[4] sample: {S} subsets of {ns}, {a.n_test} test sites, {a.kept} kept samples, "
-                               f"tile {a.tile}", "subsets": S, "n_test": a.n_test, "kept": a.kept, "tile": a.tile},
-        "fit_seconds": t1 - t0, "predict_seconds": pred_s, "phi_runs": runs,
-        "roofline": {"bound": "mfma", "achieved": rate_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": rate_tf / FP64_PEAK_TFLOPS},
-        "cfg5_extrapolation": {"flops": cfg5_flops, "seconds_1gpu": cfg5_flops / (rate_tf * 1e12),
-                               "seconds_8gpu": cfg5_flops / (rate_tf * 1e12) / 8,
-                               "assumes": f"phi runs per kept sample {run_frac:.3f} as measured here"},
-        "w_predict_sum_finite": bool(np.isfinite(out["w_predict_sum"]).all()),
-    }
-    if a.kernel_events and pv["ms"] > 0:
-        gemm_flops = runs * ns * ns * a.n_test   # X = W P^T, W lower-triangular, per (subset, phi run)
-        tf = gemm_flops / (pv["ms"] * 1e-3) / 1e12
-        gen = os.environ.get("MK_PRED_GEN", "0") not in ("", "0")
-        res["k_pred_var"] = {"launches": pv["launches"], "ms": pv["ms"], "avg_launch_ms": pv["ms"] / pv["launches"],
-                             "algorithmic_flops": gemm_flops, "achieved": tf, "unit": "TFLOP/s",
-                             "frac": tf / FP64_PEAK_TFLOPS, "p_t": "generated in LDS" if gen else "stored",
-                             "algorithmic_bytes": runs * (ns * ns / 2 + (1 if gen else 2) * ns * a.n_test) * 8.0,
-                             "bytes_note": "per (subset, phi run): W (lower) read once, X written once"
-                                           + ("" if gen else ", P^T read once")}
+    res = kriging_leg(mk, subs, d["coords_test"], beta0, bt, kept=a.kept, burn=a.burn, tile=a.tile,
+                      kernel_events=bool(a.kernel_events))
     print(json.dumps(res), flush=True)
 
 

@@ -110,6 +110,13 @@ int mk_session_create(const mk_problem* prob, const mk_config* cfg, mk_session**
 int mk_session_run(mk_session* s, int32_t n_iter);
 /* Iterations done so far. */
 int32_t mk_session_iteration(const mk_session* s);
+/* One subset's chain state after the iterations done so far, in spMvGLM's MH parameter order:
+ * beta [p]; theta [n_theta] (A lower-tri col-major with log diagonal | logit phi | logit nu);
+ * w [n_s q] location-major; tune [p + n_theta + n_s q] log proposal sds; accept [same] accept counts
+ * of the current amcmc batch.  Any pointer may be NULL.  (Resuming the chain on another host: the CPU
+ * baseline of bench.py times the oracle over the window the device timed.) */
+int mk_session_chain_state(mk_session* s, int32_t subset, double* beta, double* theta, double* w, double* tune,
+                           double* accept);
 /* Launch schedule (results are the same chain either way): mode 1 = lookahead
  * (the next iteration's phi candidates are factored while this iteration's inverse and latent
  * sweep run; Matern: the nu step follows the phi decision; n_streams <= 1), 0 = sequential, -1 = default (lookahead where
@@ -274,6 +281,23 @@ int mk_cholesky_batched(const double* A, int32_t S, int32_t n, double* L_out, do
  * DESIGN.md 4.2).  A host that knows HIP started before its own setting took effect (e.g. torch
  * first) passes the real count; n < 0 restores the default: GPU_MAX_HW_QUEUES from the environment. */
 int mk_set_hw_queues(int32_t n);
+
+/* Whether this process's HIP runtime has already started (the process holds /dev/kfd open), without
+ * starting it: a host that sets GPU_MAX_HW_QUEUES first checks whether the setting can still take
+ * effect (the R package's .onLoad; libmk itself has not touched HIP when this is called). */
+int mk_hip_initialized(void);
+
+/* Drains and destroys libmk's idle pooled HIP streams (CU-masked and priority queues included) while
+ * the runtime is alive; streams of sessions still open are destroyed with them.  libmk registers it
+ * with atexit after its first stream; hosts call it from their own exit hooks too (Python atexit,
+ * R .onUnload).  Idempotent; libmk stays usable afterwards (new streams are no longer pooled). */
+void mk_shutdown(void);
+
+/* Stall watchdog: when seconds > 0 every launch is followed by a progress-word store into pinned host
+ * memory, and a C-ABI call still running after `seconds` prints (stderr, and MK_WATCHDOG_LOG=<path>
+ * if set) every stream with work outstanding and the kernel it is on.  0 = off (default; the
+ * environment variable MK_WATCHDOG=<seconds> sets it at load). */
+int mk_set_watchdog(int32_t seconds);
 
 const char* mk_last_error(void);
 int mk_device_count(void);

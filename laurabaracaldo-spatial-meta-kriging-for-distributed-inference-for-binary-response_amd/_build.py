@@ -6,7 +6,7 @@ import sys
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_PATH = os.path.join(PKG_DIR, "libmk.so")
-SOURCES = ["mk_linalg.hip", "mk_mcmc.hip", "mk_init.hip", "mk_post.hip", "mk_api.hip", "mk_multi.hip", "mk_rsample.cpp"]
+SOURCES = ["mk_linalg.hip", "mk_mcmc.hip", "mk_init.hip", "mk_post.hip", "mk_api.hip", "mk_multi.hip", "mk_watch.hip", "mk_rsample.cpp"]
 HEADERS = ["mk_common.hpp", "mk_types.hpp", "mk_gemm.hpp", "mk_corr.hpp", "mk_kernels.hpp", "mk_internal.hpp"]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wno-unused-value",
          "-Wno-unused-result"]

@@ -79,6 +79,7 @@ EXPORTS = {
     "mk_session_create": (ctypes.c_int, [ctypes.POINTER(Problem), ctypes.POINTER(Config), ctypes.POINTER(ctypes.c_void_p)]),
     "mk_session_run": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32]),
     "mk_session_iteration": (ctypes.c_int32, [ctypes.c_void_p]),
+    "mk_session_chain_state": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, _dp, _dp, _dp, _dp, _dp]),
     "mk_session_set_lookahead": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32]),
     "mk_session_lookahead": (ctypes.c_int32, [ctypes.c_void_p]),
     "mk_session_outputs": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Outputs)]),
@@ -118,6 +119,9 @@ EXPORTS = {
     "mk_r_sample": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _ip]),
     "mk_r_sample_replace": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _ip]),
     "mk_set_hw_queues": (ctypes.c_int, [ctypes.c_int32]),
+    "mk_hip_initialized": (ctypes.c_int, []),
+    "mk_shutdown": (None, []),
+    "mk_set_watchdog": (ctypes.c_int, [ctypes.c_int32]),
     "mk_last_error": (ctypes.c_char_p, []),
     "mk_device_count": (ctypes.c_int, []),
     "mk_device_memory": (ctypes.c_int, [ctypes.c_int32, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
@@ -128,14 +132,19 @@ HW_QUEUES = None     # hardware queues of this process's HIP runtime, as passed 
 
 
 def _hip_started():
-    """True when this process's HIP runtime is already initialised (torch first): a
-    GPU_MAX_HW_QUEUES set now would no longer be read."""
-    import sys
-    torch = sys.modules.get("torch")
+    """True when this process's HIP runtime is already initialised (torch first, or any other
+    library): a GPU_MAX_HW_QUEUES set now would no longer be read.  The process then holds /dev/kfd
+    open (mk_hip_initialized checks the same without starting HIP)."""
     try:
-        return bool(torch is not None and torch.cuda.is_initialized())
-    except Exception:
-        return False
+        for fd in os.listdir("/proc/self/fd"):
+            try:
+                if os.readlink("/proc/self/fd/" + fd) == "/dev/kfd":
+                    return True
+            except OSError:
+                pass
+    except OSError:
+        pass
+    return False
 
 
 def load():
@@ -163,6 +172,11 @@ def load():
         fn.restype = res
         fn.argtypes = args
     lib.mk_set_hw_queues(HW_QUEUES)
+    # libmk's pooled streams (CU-masked / priority queues) are destroyed while the HIP runtime is
+    # alive: Python's atexit runs before the C library's exit handlers (libmk registers mk_shutdown
+    # there too; it is idempotent)
+    import atexit
+    atexit.register(lib.mk_shutdown)
     _LIB = lib
     return lib
 

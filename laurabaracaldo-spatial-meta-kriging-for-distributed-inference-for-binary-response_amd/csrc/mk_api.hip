@@ -9,6 +9,8 @@
 // is a pointer view into the shard's arrays (every array is [subset][...]); the chains do
 // not depend on the grouping (RNG streams are keyed by global subset index).
 #include <hip/hip_runtime.h>
+#include <dirent.h>
+#include <unistd.h>
 #include <atomic>
 #include <chrono>
 #include <cmath>
@@ -40,9 +42,36 @@ static int set_err(int code, const std::string& msg) {
     if (e_ != hipSuccess) return set_err(MK_E_HIP, std::string(#x " -> ") + hipGetErrorString(e_)); \
   } while (0)
 
+// Entry of a C-ABI call that works on `dev`: registered with the stall watchdog, the caller's
+// current device restored on every return path (an R or torch host keeps its own device).
+#define MK_ENTRY_DEVICE(dev) \
+  ApiCall mk_call_(__func__); \
+  DeviceGuard mk_dg_;         \
+  HIPCHK(hipSetDevice(dev))
+
 extern "C" const char* mk_last_error(void) { return g_err.c_str(); }
 namespace mk {
 int host_error(int code, const char* msg) { return set_err(code, msg); }   // for host-only sources
+}
+
+extern "C" int mk_hip_initialized(void) {
+  DIR* d = opendir("/proc/self/fd");
+  if (!d) return 0;
+  int found = 0;
+  char path[64], target[256];
+  while (dirent* e = readdir(d)) {
+    if (e->d_name[0] == '.') continue;
+    std::snprintf(path, sizeof path, "/proc/self/fd/%s", e->d_name);
+    const ssize_t n = readlink(path, target, sizeof target - 1);
+    if (n <= 0) continue;
+    target[n] = 0;
+    if (std::strcmp(target, "/dev/kfd") == 0) {
+      found = 1;
+      break;
+    }
+  }
+  closedir(d);
+  return found;
 }
 
 extern "C" int mk_device_count(void) {
@@ -52,7 +81,7 @@ extern "C" int mk_device_count(void) {
 }
 
 extern "C" int mk_device_memory(int32_t device, int64_t* free_bytes, int64_t* total_bytes) {
-  HIPCHK(hipSetDevice(device));
+  MK_ENTRY_DEVICE(device);
   size_t f = 0, t = 0;
   HIPCHK(hipMemGetInfo(&f, &t));
   if (free_bytes) *free_bytes = (int64_t)f;
@@ -185,7 +214,38 @@ struct PoolKey {
 };
 typedef std::vector<std::pair<PoolKey, hipStream_t>> StreamList;
 static std::mutex g_pool_mu;
-static StreamList g_pool;   // idle streams
+static StreamList g_pool;        // idle streams
+static bool g_pool_closed = false;   // mk_shutdown ran: returned streams are destroyed, not pooled
+
+// Drain and destroy one stream on its device (the calling thread's device is restored).
+static void stream_destroy(const PoolKey& k, hipStream_t st) {
+  DeviceGuard dg;
+  if (hipSetDevice(k.device) == hipSuccess) {
+    (void)hipStreamSynchronize(st);
+    wd_forget(st);
+    (void)hipStreamDestroy(st);
+  }
+  (void)hipGetLastError();
+}
+
+// Every idle pooled stream is destroyed while the HIP runtime is still alive.  Before this, the
+// pool's CU-masked and priority queues stayed alive into the runtime's own static teardown, which
+// crashed in __cxa_finalize after a profiler had finalised (rocprofv3, profiles/r03/final3/prof32.log:
+// the 32-subset shard's lookahead schedule is the path that creates CU-masked queues).  Registered
+// with atexit at the first stream the pool creates -- after HIP initialised, so it runs before HIP's
+// own exit handlers -- and called by the hosts' exit hooks (Python atexit, the R package's
+// .onUnload / exit finalizer).  Idempotent; sessions still alive keep their streams, which are then
+// destroyed when the session is.
+extern "C" void mk_shutdown(void) {
+  StreamList idle;
+  {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    g_pool_closed = true;
+    idle.swap(g_pool);
+  }
+  for (auto& o : idle) stream_destroy(o.first, o.second);
+}
+static void shutdown_at_exit() { mk_shutdown(); }
 
 // A stream of this kind on the current device (hipSetDevice(device) done by the caller), recorded
 // in `owned` for the session's destructor.
@@ -219,13 +279,21 @@ static hipError_t pool_stream(StreamList& owned, hipStream_t* st, int device, in
     e = kind == SK_PRIO ? hipStreamCreateWithPriority(st, hipStreamNonBlocking, prio)
                         : hipStreamCreateWithFlags(st, hipStreamNonBlocking);
   }
-  if (e == hipSuccess) owned.push_back({k, *st});
+  if (e == hipSuccess) {
+    owned.push_back({k, *st});
+    static std::once_flag at_exit;
+    std::call_once(at_exit, [] { std::atexit(shutdown_at_exit); });
+  }
   return e;
 }
 static void pool_return(StreamList& owned) {
-  std::lock_guard<std::mutex> lk(g_pool_mu);
-  for (auto& o : owned) g_pool.push_back(o);
+  StreamList gone;
+  {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    for (auto& o : owned) (g_pool_closed ? gone : g_pool).push_back(o);
+  }
   owned.clear();
+  for (auto& o : gone) stream_destroy(o.first, o.second);
 }
 namespace mk {
 hipError_t stream_acquire(int device, hipStream_t* st) {
@@ -446,7 +514,7 @@ static int launch_quantiles(unsigned grid, hipStream_t st, const double* data, l
     return set_err(MK_E_ARG, "quantile summaries take 1 .. " + std::to_string(MK_QUANT_MAX) + " kept samples");
   size_t n2 = 1;
   while (n2 < (size_t)n_rows) n2 <<= 1;
-  hipLaunchKernelGGL(k_quantiles, dim3(grid), dim3(256), n2 * 8, st, data, subset_stride, row_stride, n_rows, n_cols,
+  MK_LAUNCH(k_quantiles, dim3(grid), dim3(256), n2 * 8, st, data, subset_stride, row_stride, n_rows, n_cols,
                      probs, n_probs, out);
   HIPCHK(hipGetLastError());
   return 0;
@@ -475,8 +543,8 @@ static int tile_size(long wg128) {
 static void launch_candidates(const Model& md, const MatSet& ms, hipStream_t st, int n_entries, int h0, int hc,
                               int which, int iter, const int* slist = nullptr, const int* scount = nullptr) {
   if (md.cov_model == MK_COV_MATERN && md.chtab)
-    hipLaunchKernelGGL(k_matern_table, dim3(n_entries), dim3(256), 0, st, md, h0, hc, which, iter, slist, scount);
-  hipLaunchKernelGGL(cov_candidate_kernel(md.cov_model), dim3(xcd_grid_h(n_entries, ms.nt * (ms.nt + 1) / 2)),
+    MK_LAUNCH(k_matern_table, dim3(n_entries), dim3(256), 0, st, md, h0, hc, which, iter, slist, scount);
+  MK_LAUNCH(cov_candidate_kernel(md.cov_model), dim3(xcd_grid_h(n_entries, ms.nt * (ms.nt + 1) / 2)),
                      dim3(256), 0, st, md, ms, h0, hc, which, iter, slist, scount);
 }
 
@@ -491,17 +559,17 @@ static void chol_update(mk_session* s, Group& g, hipStream_t st, int h0, int hc,
   const int tm = tile_size((long)E * nti);
   if (tm == 32) {
     timed(s, st, KS_CHOL_UPDATE_SUB, flops, [&] {
-      hipLaunchKernelGGL(k_chol_update<32>, dim3(xcd_grid_h(E, nti * 16)), dim3(256), LDS_32, st, g.ms, g.S, h0, hc, k, ia,
+      MK_LAUNCH(k_chol_update<32>, dim3(xcd_grid_h(E, nti * 16)), dim3(256), LDS_32, st, g.ms, g.S, h0, hc, k, ia,
                          ib, j0, j1, slist, scount);
     });
   } else if (tm == 64) {
     timed(s, st, KS_CHOL_UPDATE_SUB, flops, [&] {
-      hipLaunchKernelGGL(k_chol_update<64>, dim3(xcd_grid_h(E, nti * 4)), dim3(256), LDS_64, st, g.ms, g.S, h0, hc, k, ia,
+      MK_LAUNCH(k_chol_update<64>, dim3(xcd_grid_h(E, nti * 4)), dim3(256), LDS_64, st, g.ms, g.S, h0, hc, k, ia,
                          ib, j0, j1, slist, scount);
     });
   } else {
     timed(s, st, KS_CHOL_UPDATE, flops, [&] {
-      hipLaunchKernelGGL(k_chol_update<128>, dim3(xcd_grid_h(E, nti)), dim3(256), LDS_128, st, g.ms, g.S, h0, hc, k, ia,
+      MK_LAUNCH(k_chol_update<128>, dim3(xcd_grid_h(E, nti)), dim3(256), LDS_128, st, g.ms, g.S, h0, hc, k, ia,
                          ib, j0, j1, slist, scount);
     });
   }
@@ -513,20 +581,20 @@ static void chol_trsm(mk_session* s, Group& g, hipStream_t st, int h0, int hc, i
   const int tm = tile_size((long)E * nti);
   timed(s, st, KS_CHOL_TRSM, flops, [&] {
     if (tm == 32)
-      hipLaunchKernelGGL(k_chol_trsm<32>, dim3(xcd_grid_h(E, nti * 4)), dim3(256), LDS_32x128, st, g.ms, g.S, h0, hc, k,
+      MK_LAUNCH(k_chol_trsm<32>, dim3(xcd_grid_h(E, nti * 4)), dim3(256), LDS_32x128, st, g.ms, g.S, h0, hc, k,
                          ia, ib, slist, scount);
     else if (tm == 64)
-      hipLaunchKernelGGL(k_chol_trsm<64>, dim3(xcd_grid_h(E, nti * 2)), dim3(256), LDS_64x128, st, g.ms, g.S, h0, hc, k,
+      MK_LAUNCH(k_chol_trsm<64>, dim3(xcd_grid_h(E, nti * 2)), dim3(256), LDS_64x128, st, g.ms, g.S, h0, hc, k,
                          ia, ib, slist, scount);
     else
-      hipLaunchKernelGGL(k_chol_trsm<128>, dim3(xcd_grid_h(E, nti)), dim3(256), LDS_128, st, g.ms, g.S, h0, hc, k, ia, ib,
+      MK_LAUNCH(k_chol_trsm<128>, dim3(xcd_grid_h(E, nti)), dim3(256), LDS_128, st, g.ms, g.S, h0, hc, k, ia, ib,
                          slist, scount);
   });
 }
 static void chol_diag(mk_session* s, Group& g, hipStream_t st, int h0, int hc, int k, const int* slist,
                       const int* scount) {
   timed(s, st, KS_CHOL_DIAG, 0.0, [&] {
-    hipLaunchKernelGGL(k_chol_diag, dim3(g.S * hc), dim3(256), (size_t)MK_DIAG_LDS_BYTES, st, g.ms, g.md.n_s, h0, hc, k,
+    MK_LAUNCH(k_chol_diag, dim3(g.S * hc), dim3(256), (size_t)MK_DIAG_LDS_BYTES, st, g.ms, g.md.n_s, h0, hc, k,
                        g.md.ld_part, g.md.quad_c, g.md.info, slist, scount);
   });
 }
@@ -660,7 +728,7 @@ static void launch_cholesky(mk_session* s, Group& g, int h0, int hc, const int* 
 // W = L^-1 of the listed pairs: diagonal tiles, then recursive doubling.
 static void launch_trinv(mk_session* s, Group& g, int max_entries, const int* list, const int* count) {
   const int nt = s->nt;
-  hipLaunchKernelGGL(k_inv_copydiag, dim3(max_entries * nt * 8), dim3(256), 0, g.stream, g.ms, list, count);
+  MK_LAUNCH(k_inv_copydiag, dim3(max_entries * nt * MK_CD_SPLIT), dim3(256), 0, g.stream, g.ms, list, count);
   for (int sz = 1; sz < nt; sz *= 2) {
     const int npairs = (nt + 2 * sz - 1) / (2 * sz);
     // the grid is sized for every pair, but only the accepted candidates' factors are in the
@@ -670,13 +738,13 @@ static void launch_trinv(mk_session* s, Group& g, int max_entries, const int* li
     for (int phase = 0; phase < 2; ++phase)
       timed(s, g.stream, KS_INV, 0.0, [&] {
         if (tm == 32)
-          hipLaunchKernelGGL(k_inv_level<32>, dim3(xcd_grid_h(max_entries, npairs * sz * sz * 16)), dim3(256), LDS_32,
+          MK_LAUNCH(k_inv_level<32>, dim3(xcd_grid_h(max_entries, npairs * sz * sz * 16)), dim3(256), LDS_32,
                              g.stream, g.ms, list, count, sz, phase);
         else if (tm == 64)
-          hipLaunchKernelGGL(k_inv_level<64>, dim3(xcd_grid_h(max_entries, npairs * sz * sz * 4)), dim3(256), LDS_64,
+          MK_LAUNCH(k_inv_level<64>, dim3(xcd_grid_h(max_entries, npairs * sz * sz * 4)), dim3(256), LDS_64,
                              g.stream, g.ms, list, count, sz, phase);
         else
-          hipLaunchKernelGGL(k_inv_level<128>, dim3(xcd_grid_h(max_entries, npairs * sz * sz)), dim3(256), LDS_128,
+          MK_LAUNCH(k_inv_level<128>, dim3(xcd_grid_h(max_entries, npairs * sz * sz)), dim3(256), LDS_128,
                              g.stream, g.ms, list, count, sz, phase);
       });
   }
@@ -687,10 +755,10 @@ static void launch_inverse(mk_session* s, Group& g, bool from_zc = false) {
   const int nt = s->nt, max_entries = g.S * s->q;
   launch_trinv(s, g, max_entries, g.d_list, g.d_count);
   timed(s, g.stream, KS_LAUUM, 0.0, [&] {
-    hipLaunchKernelGGL(k_qblocks, dim3(xcd_grid_h(max_entries, nt * 2)), dim3(256), LDS_64, g.stream, g.ms, g.md.n_s,
+    MK_LAUNCH(k_qblocks, dim3(xcd_grid_h(max_entries, nt * 2)), dim3(256), LDS_64, g.stream, g.ms, g.md.n_s,
                        g.d_list, g.d_count);
   });
-  hipLaunchKernelGGL(k_take_border, dim3(max_entries * ((s->n_pad + 255) / 256)), dim3(256), 0, g.stream, g.md, g.ms,
+  MK_LAUNCH(k_take_border, dim3(max_entries * ((s->n_pad + 255) / 256)), dim3(256), 0, g.stream, g.md, g.ms,
                      g.d_list, g.d_count, from_zc ? (const double*)g.md.zc : nullptr);
 }
 
@@ -710,18 +778,18 @@ static void launch_pred_refresh(mk_session* s, Group& g, hipStream_t st = nullpt
   if (!st) st = g.stream;
   const int nt = s->nt, max_entries = g.S * s->q;
   if (md.cov_model == MK_COV_MATERN && md.chtab_p)
-    hipLaunchKernelGGL(k_matern_table_list, dim3(max_entries), dim3(256), 0, st, md, g.d_plist, g.d_pcount);
+    MK_LAUNCH(k_matern_table_list, dim3(max_entries), dim3(256), 0, st, md, g.d_plist, g.d_pcount);
   if (md.cov_model == MK_COV_MATERN)
-    hipLaunchKernelGGL(k_pred_PT_matern, dim3(max_entries * (md.n_pad / MK_PT_RB)), dim3(256), 0, st, md, g.d_plist,
+    MK_LAUNCH(k_pred_PT_matern, dim3(max_entries * (md.n_pad / MK_PT_RB)), dim3(256), 0, st, md, g.d_plist,
                        g.d_pcount);
   else if (!s->pred_gen)
-    hipLaunchKernelGGL(pred_PT_kernel(md.cov_model), dim3(max_entries * md.n_pad), dim3(256), 0, st, md, g.d_plist,
+    MK_LAUNCH(pred_PT_kernel(md.cov_model), dim3(max_entries * md.n_pad), dim3(256), 0, st, md, g.d_plist,
                        g.d_pcount);
   timed(s, st, KS_PRED_VAR, pred_flops(s, g), [&] {
-    hipLaunchKernelGGL(s->pred_gen ? k_pred_var<true> : k_pred_var<false>, dim3(xcd_grid_h(max_entries, nt * md.ntt)),
+    MK_LAUNCH(s->pred_gen ? k_pred_var<true> : k_pred_var<false>, dim3(xcd_grid_h(max_entries, nt * md.ntt)),
                        dim3(256), LDS_128, st, md, g.ms, g.d_plist, g.d_pcount);
   });
-  hipLaunchKernelGGL(k_pred_var_reduce, dim3(max_entries * (md.n_test_pad / 256)), dim3(256), 0, st, md, nt,
+  MK_LAUNCH(k_pred_var_reduce, dim3(max_entries * (md.n_test_pad / 256)), dim3(256), 0, st, md, nt,
                      g.d_plist, g.d_pcount);
 }
 
@@ -766,6 +834,7 @@ static void launch_sweep(mk_session* s, Group& g, int it) {
       for (int B = 0; B <= nblk; ++B) {
         void* ta[] = {&md, &ms, &iter, &B, &part};
         const hipError_t e = hipLaunchKernel(sweep_step_kernel(q), dim3(g.S * nt), dim3(256), ta, lds_s, g.stream);
+        wd_trace(g.stream, "k_sweep_step");
         if (e != hipSuccess) {
           if (s->launch_err == hipSuccess) s->launch_err = e;
           return;
@@ -776,9 +845,11 @@ static void launch_sweep(mk_session* s, Group& g, int it) {
     for (int B = 0; B <= nblk; ++B) {
       void* ta[] = {&md, &ms, &iter, &B, &part, &dacc, &any};
       hipError_t e = hipLaunchKernel(sweep_split_kernel(q, false), dim3(g.S * nt), dim3(256), ta, 0, g.stream);
+      wd_trace(g.stream, "k_sweep_tiles");
       if (e == hipSuccess && B < nblk) {
         void* ba[] = {&md, &ms, &B, &part, &dacc, &any};
         e = hipLaunchKernel(sweep_split_kernel(q, true), dim3(g.S), dim3(256), ba, lds, g.stream);
+        wd_trace(g.stream, "k_sweep_block");
       }
       if (e != hipSuccess) {
         if (s->launch_err == hipSuccess) s->launch_err = e;
@@ -810,6 +881,7 @@ static void launch_sweep(mk_session* s, Group& g, int it) {
     else
       e = hipLaunchCooperativeKernel(sweep_kernel(q, true), dim3(xcd_grid(g.S, s->nt)), dim3(256), args,
                                      (unsigned)s->sweep_mg_lds, g.stream);
+    wd_trace(g.stream, "k_sweep_mg");
     if (e != hipSuccess && s->launch_err == hipSuccess) s->launch_err = e;
     return;
   }
@@ -822,6 +894,7 @@ static void launch_sweep(mk_session* s, Group& g, int it) {
       s->sweep_rows ? hipLaunchKernel(sweep_rows_kernel(q), dim3(g.S), dim3(512), args,
                                       sw_lds + (size_t)s->nt * q * 64 * sizeof(double), g.stream)
                     : hipLaunchKernel(sweep_kernel(q, false), dim3(g.S), dim3(MK_SW_T), args, sw_lds, g.stream);
+  wd_trace(g.stream, s->sweep_rows ? "k_sweep_rows" : "k_sweep");
   if (e != hipSuccess && s->launch_err == hipSuccess) s->launch_err = e;
 }
 
@@ -831,17 +904,17 @@ static void iteration_pre_sweep(mk_session* s, Group& g, int it) {
   const int S = g.S, q = s->q;
   const bool kept = it >= md.kept0;
   hipStream_t st = g.stream;
-  hipLaunchKernelGGL(k_beta, dim3(S), dim3(256), 0, st, md, it);
-  if (q > 1) hipLaunchKernelGGL(k_trmv_Z, dim3(S * q * ((s->n_pad + 255) / 256)), dim3(256), 0, st, md, g.ms);
-  hipLaunchKernelGGL(k_Aphase, dim3(S), dim3(256), 0, st, md, it);
+  MK_LAUNCH(k_beta, dim3(S), dim3(256), 0, st, md, it);
+  if (q > 1) MK_LAUNCH(k_trmv_Z, dim3(S * q * ((s->n_pad + 255) / 256)), dim3(256), 0, st, md, g.ms);
+  MK_LAUNCH(k_Aphase, dim3(S), dim3(256), 0, st, md, it);
   const int nkinds = s->matern ? 2 : 1;
   // the q outcomes' (phi_h, nu_h) steps are independent given u: one batched pass per kind
   for (int which = 0; which < nkinds; ++which) {
     timed(s, st, KS_COV, 0.0, [&] { launch_candidates(md, g.ms, st, S * q, 0, q, which, it); });
     launch_cholesky(s, g, 0, q);
-    hipLaunchKernelGGL(k_theta_mh, dim3((S * q + 63) / 64), dim3(64), 0, st, md, g.ms, 0, q, which, it);
+    MK_LAUNCH(k_theta_mh, dim3((S * q + 63) / 64), dim3(64), 0, st, md, g.ms, 0, q, which, it);
   }
-  hipLaunchKernelGGL(k_dirty_list, dim3(1), dim3(256), 0, st, md, (int)(it == md.kept0), g.d_list, g.d_count,
+  MK_LAUNCH(k_dirty_list, dim3(1), dim3(256), 0, st, md, (int)(it == md.kept0), g.d_list, g.d_count,
                      g.d_plist, g.d_pcount);
   launch_inverse(s, g);
   if (kept && !s->tiled) launch_pred_refresh(s, g);
@@ -852,14 +925,14 @@ static void iteration_post_sweep(mk_session* s, Group& g, int it) {
   const int S = g.S;
   const bool kept = it >= md.kept0;
   hipStream_t st = g.stream;
-  if (s->record_samples) hipLaunchKernelGGL(k_record, dim3((S + 63) / 64), dim3(64), 0, st, md, it);
-  if (s->record_w) hipLaunchKernelGGL(k_record_w, dim3((md.Np + 255) / 256, S), dim3(256), 0, st, md, it);
+  if (s->record_samples) MK_LAUNCH(k_record, dim3((S + 63) / 64), dim3(64), 0, st, md, it);
+  if (s->record_w) MK_LAUNCH(k_record_w, dim3((md.Np + 255) / 256, S), dim3(256), 0, st, md, it);
   if (kept && md.n_test > 0 && !s->tiled) {
     const int per = (md.n_test + 3) / 4;
-    hipLaunchKernelGGL(k_pred_draw, dim3(S * per), dim3(256), 0, st, md, it, it - md.kept0);
+    MK_LAUNCH(k_pred_draw, dim3(S * per), dim3(256), 0, st, md, it, it - md.kept0);
   }
-  if (kept && s->tiled) hipLaunchKernelGGL(k_record_kept, dim3(S), dim3(256), 0, st, md, it - md.kept0);
-  if ((it + 1) % md.batch_length == 0) hipLaunchKernelGGL(k_adapt, dim3(S), dim3(256), 0, st, md, it / md.batch_length);
+  if (kept && s->tiled) MK_LAUNCH(k_record_kept, dim3(S), dim3(256), 0, st, md, it - md.kept0);
+  if ((it + 1) % md.batch_length == 0) MK_LAUNCH(k_adapt, dim3(S), dim3(256), 0, st, md, it / md.batch_length);
 }
 
 // Lookahead schedule (exponential model, one group).  The phi proposal of iteration t+1 is known
@@ -903,15 +976,15 @@ static void run_iteration_la(mk_session* s, int it) {
     enqueue_candidates(s, g, it, ev_d, nt);
   }
   enqueue_candidates_rest(s, g);
-  hipLaunchKernelGGL(k_beta, dim3(S), dim3(256), 0, M, md, it);
-  if (q > 1) hipLaunchKernelGGL(k_trmv_Z, dim3(S * q * ((s->n_pad + 255) / 256)), dim3(256), 0, M, md, g.ms);
-  hipLaunchKernelGGL(k_Aphase, dim3(S), dim3(256), 0, M, md, it);
+  MK_LAUNCH(k_beta, dim3(S), dim3(256), 0, M, md, it);
+  if (q > 1) MK_LAUNCH(k_trmv_Z, dim3(S * q * ((s->n_pad + 255) / 256)), dim3(256), 0, M, md, g.ms);
+  MK_LAUNCH(k_Aphase, dim3(S), dim3(256), 0, M, md, it);
   for (int k = 0; k < nt; ++k) {   // z' = L'^-1 u, trailing the candidates' panels
     hipStreamWaitEvent(M, evP[k], 0);
-    hipLaunchKernelGGL(k_border_step, dim3(xcd_grid_h(S * q, std::max(1, nt - 1 - k))), dim3(256), 0, M, md, g.ms, k);
+    MK_LAUNCH(k_border_step, dim3(xcd_grid_h(S * q, std::max(1, nt - 1 - k))), dim3(256), 0, M, md, g.ms, k);
   }
-  hipLaunchKernelGGL(k_border_quad, dim3(S * q), dim3(256), 0, M, md);
-  hipLaunchKernelGGL(k_theta_mh, dim3((S * q + 63) / 64), dim3(64), 0, M, md, g.ms, 0, q, 0, it);
+  MK_LAUNCH(k_border_quad, dim3(S * q), dim3(256), 0, M, md);
+  MK_LAUNCH(k_theta_mh, dim3((S * q + 63) / 64), dim3(64), 0, M, md, g.ms, 0, q, 0, it);
   if (s->matern) {
     // the nu step: its candidate R(phi_t, nu') needs this phi decision, so it is factored now, as in
     // the sequential schedule (bordered row: u is known), on the idle high-priority candidate stream
@@ -921,8 +994,8 @@ static void run_iteration_la(mk_session* s, int it) {
     hipStreamWaitEvent(s->la_c, ev_d, 0);
     timed(s, s->la_c, KS_COV, 0.0, [&] { launch_candidates(md, g.ms, s->la_c, S * q, 0, q, 1, it); });
     launch_cholesky(s, g, 0, q, nullptr, nullptr, s->la_c);
-    hipLaunchKernelGGL(k_theta_mh, dim3((S * q + 63) / 64), dim3(64), 0, s->la_c, md, g.ms, 0, q, 1, it);
-    hipLaunchKernelGGL(k_nu_border, dim3(S * q * ((s->n_pad + 255) / 256)), dim3(256), 0, s->la_c, md, g.ms);
+    MK_LAUNCH(k_theta_mh, dim3((S * q + 63) / 64), dim3(64), 0, s->la_c, md, g.ms, 0, q, 1, it);
+    MK_LAUNCH(k_nu_border, dim3(S * q * ((s->n_pad + 255) / 256)), dim3(256), 0, s->la_c, md, g.ms);
     hipEventRecord(evP[nt + 4], s->la_c);
     hipStreamWaitEvent(M, evP[nt + 4], 0);
   }
@@ -931,7 +1004,7 @@ static void run_iteration_la(mk_session* s, int it) {
     hipEventRecord(ev_d, M);
     enqueue_candidates(s, g, it + 1, ev_d, la_head(s));
   }
-  hipLaunchKernelGGL(k_dirty_list, dim3(1), dim3(256), 0, M, md, (int)(it == md.kept0), g.d_list, g.d_count, g.d_plist,
+  MK_LAUNCH(k_dirty_list, dim3(1), dim3(256), 0, M, md, (int)(it == md.kept0), g.d_list, g.d_count, g.d_plist,
                      g.d_pcount);
   launch_inverse(s, g, true);
   const bool kept = it >= md.kept0;
@@ -1152,7 +1225,7 @@ extern "C" int mk_session_set_test_sites(mk_session* s, int32_t n_test, const do
   if (!s->tiled)
     return set_err(MK_E_ARG, "the session keeps no chain states: create it with predict_tile > 0 (and no test sites)");
   if (n_test < 1 || !coords_test) return set_err(MK_E_ARG, "n_test must be >= 1 with coordinates");
-  HIPCHK(hipSetDevice(s->device));
+  MK_ENTRY_DEVICE(s->device);
   HIPCHK(hipStreamSynchronize(s->stream));
   return kriging_buffers(s, n_test, coords_test);
 }
@@ -1176,7 +1249,7 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return set_err(MK_E_NODEV, "no HIP device");
   if (c->device < 0 || c->device >= ndev) return set_err(MK_E_ARG, "bad device ordinal");
-  HIPCHK(hipSetDevice(c->device));
+  MK_ENTRY_DEVICE(c->device);
   // the guard owns the session until it is handed out: every early return (allocation failure,
   // HIPCHK, argument error) frees the session and every device buffer allocated so far
   std::unique_ptr<mk_session> hold(new mk_session());
@@ -1474,11 +1547,11 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
 
   // ---------------- initial state: eta, u, factor every R_h at the starting values, W, z (whole shard)
   Group& a = s->all;
-  hipLaunchKernelGGL(k_init_state, dim3(S), dim3(256), 0, s->stream, md);
+  MK_LAUNCH(k_init_state, dim3(S), dim3(256), 0, s->stream, md);
   launch_candidates(md, ms, s->stream, S * q, 0, q, 2, 0);
   launch_cholesky(s, a, 0, q);
-  hipLaunchKernelGGL(k_theta_init, dim3((S * q + 63) / 64), dim3(64), 0, s->stream, md, ms, 0, q);
-  hipLaunchKernelGGL(k_dirty_list, dim3(1), dim3(256), 0, s->stream, md, 0, a.d_list, a.d_count, a.d_plist, a.d_pcount);
+  MK_LAUNCH(k_theta_init, dim3((S * q + 63) / 64), dim3(64), 0, s->stream, md, ms, 0, q);
+  MK_LAUNCH(k_dirty_list, dim3(1), dim3(256), 0, s->stream, md, 0, a.d_list, a.d_count, a.d_plist, a.d_pcount);
   launch_inverse(s, a);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(s->stream));
@@ -1493,7 +1566,7 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
 
 extern "C" int mk_session_run(mk_session* s, int32_t n_iter) {
   if (!s) return set_err(MK_E_ARG, "null session");
-  HIPCHK(hipSetDevice(s->device));
+  MK_ENTRY_DEVICE(s->device);
   if (n_iter < 0 || s->iter + n_iter > s->md.n_samples) return set_err(MK_E_ARG, "n_iter beyond n.samples");
   if (s->la && !s->la_c) {
     // the candidates' factorisation is the critical chain: its stream gets the device's highest
@@ -1574,6 +1647,27 @@ extern "C" int mk_session_run(mk_session* s, int32_t n_iter) {
 }
 
 extern "C" int32_t mk_session_iteration(const mk_session* s) { return s ? s->iter : -1; }
+
+// The chain state of one subset after the iterations run so far, in spMvGLM's MH order: beta (p),
+// theta (n_theta: A lower-tri col-major with log diagonal | logit phi | logit nu), w (n_s q,
+// location-major), tune (p + n_theta + n_s q log proposal sds) and accept (the same, accept counts
+// of the current amcmc batch).  Any pointer may be NULL.  A host can resume the chain elsewhere from
+// it -- bench.py's CPU baseline times the oracle over the very window the device timed.
+extern "C" int mk_session_chain_state(mk_session* s, int32_t subset, double* beta, double* theta, double* w,
+                                      double* tune, double* accept) {
+  if (!s) return set_err(MK_E_ARG, "null session");
+  if (subset < 0 || subset >= s->S) return set_err(MK_E_ARG, "subset out of range");
+  MK_ENTRY_DEVICE(s->device);
+  const Model& md = s->md;
+  const long i = subset, nq = (long)s->n_part[subset] * s->q, nmh = md.o_w + nq;
+  HIPCHK(hipStreamSynchronize(s->stream));
+  if (beta) HIPCHK(hipMemcpy(beta, md.beta + i * md.p, (size_t)md.p * 8, hipMemcpyDeviceToHost));
+  if (theta) HIPCHK(hipMemcpy(theta, md.theta + i * md.n_theta, (size_t)md.n_theta * 8, hipMemcpyDeviceToHost));
+  if (w) HIPCHK(hipMemcpy(w, md.w + i * md.Np, (size_t)nq * 8, hipMemcpyDeviceToHost));
+  if (tune) HIPCHK(hipMemcpy(tune, md.tune + i * md.n_mh_max, (size_t)nmh * 8, hipMemcpyDeviceToHost));
+  if (accept) HIPCHK(hipMemcpy(accept, md.acc + i * md.n_mh_max, (size_t)nmh * 8, hipMemcpyDeviceToHost));
+  return 0;
+}
 
 
 extern "C" int mk_session_set_lookahead(mk_session* s, int32_t mode) {
@@ -1662,18 +1756,18 @@ static int predict_tile(mk_session* s, int t0, double* dq, mk_outputs* o) {
     mt.z = md.kz + (long)k * S * q * md.n_pad;
     mt.A_full = md.kA + (long)k * S * q * q;
     const double* prev = j ? md.kth + (long)(k - 1) * S * md.n_theta : nullptr;
-    hipLaunchKernelGGL(k_kept_dirty, dim3(1), dim3(256), 0, st, mt, prev, s->d_slist, s->d_scount, g.d_plist,
+    MK_LAUNCH(k_kept_dirty, dim3(1), dim3(256), 0, st, mt, prev, s->d_slist, s->d_scount, g.d_plist,
                        g.d_pcount);
     for (int h = 0; h < q; ++h) {
       launch_candidates(mt, g.ms, st, S, h, 1, 2, 0, s->d_slist + h * S, s->d_scount + h);
       launch_cholesky(s, g, h, 1, s->d_slist + h * S, s->d_scount + h);
     }
-    hipLaunchKernelGGL(k_flip_pairs, dim3((S * q + 255) / 256), dim3(256), 0, st, g.ms, g.d_plist, g.d_pcount);
+    MK_LAUNCH(k_flip_pairs, dim3((S * q + 255) / 256), dim3(256), 0, st, g.ms, g.d_plist, g.d_pcount);
     launch_trinv(s, g, S * q, g.d_plist, g.d_pcount);
     g.md = mt;
     launch_pred_refresh(s, g);
     const int per = (Tc + 3) / 4;
-    hipLaunchKernelGGL(k_pred_draw, dim3(S * per), dim3(256), 0, st, mt, md.kept0 + k, j);
+    MK_LAUNCH(k_pred_draw, dim3(S * per), dim3(256), 0, st, mt, md.kept0 + k, j);
     HIPCHK(hipGetLastError());
   }
   if (dq) {
@@ -1708,7 +1802,7 @@ static int predict_tiled(mk_session* s, mk_outputs* o) {
       HIPCHK(hipMemcpy2DAsync(o->w_predict + (size_t)t0 * q * MK_N_LEVELS, (size_t)C * MK_N_LEVELS * 8, dq,
                               (size_t)Ct * MK_N_LEVELS * 8, (size_t)Ct * MK_N_LEVELS * 8, S, hipMemcpyDeviceToHost, st));
     if (o->w_predict_sum) {
-      hipLaunchKernelGGL(k_combine, dim3((unsigned)(((long)Ct * MK_N_LEVELS + 255) / 256)), dim3(256), 0, st, dq, S,
+      MK_LAUNCH(k_combine, dim3((unsigned)(((long)Ct * MK_N_LEVELS + 255) / 256)), dim3(256), 0, st, dq, S,
                          (long)Ct * MK_N_LEVELS, dsum, 0);
       HIPCHK(hipMemcpyAsync(o->w_predict_sum + (size_t)t0 * q * MK_N_LEVELS, dsum, (size_t)Ct * MK_N_LEVELS * 8,
                             hipMemcpyDeviceToHost, st));
@@ -1734,7 +1828,7 @@ int session_info(const mk_session* s, ShardInfo* in) {
 }
 // [S][P][200] parameter grids (obj[[i]]$parameters, MK.R:89) into d_out (HBM), on the session stream.
 int session_param_grids(mk_session* s, double* d_out) {
-  HIPCHK(hipSetDevice(s->device));
+  MK_ENTRY_DEVICE(s->device);
   Model& md = s->md;
   if (s->iter < md.n_samples) return set_err(MK_E_ARG, "quantile outputs need all n.samples iterations");
   const int rq = launch_quantiles(s->S * s->P, s->stream, md.samples + (long)md.kept0 * s->P, (long)md.n_samples * s->P,
@@ -1745,7 +1839,7 @@ int session_param_grids(mk_session* s, double* d_out) {
 }
 // [S][q n_test][200] w.predict grids of a fused session into d_out.
 int session_wpred_grids(mk_session* s, double* d_out) {
-  HIPCHK(hipSetDevice(s->device));
+  MK_ENTRY_DEVICE(s->device);
   Model& md = s->md;
   if (s->tiled) return set_err(MK_E_ARG, "tiled sessions produce their grids per tile");
   if (s->iter < md.n_samples) return set_err(MK_E_ARG, "quantile outputs need all n.samples iterations");
@@ -1759,7 +1853,7 @@ int session_wpred_grids(mk_session* s, double* d_out) {
 // Tiled session: the grids [S][q Tc][200] of test-site tile [t0, t0 + Tc) into d_out (and the
 // tile's draws into o->w_pred_samples when set).
 int session_tile_grids(mk_session* s, int t0, double* d_out, mk_outputs* o) {
-  HIPCHK(hipSetDevice(s->device));
+  MK_ENTRY_DEVICE(s->device);
   if (!s->tiled) return set_err(MK_E_ARG, "not a tiled session");
   if (s->iter < s->md.n_samples) return set_err(MK_E_ARG, "quantile outputs need all n.samples iterations");
   if (t0 < 0 || t0 >= s->n_test_all || t0 % s->pred_tile) return set_err(MK_E_ARG, "bad tile offset");
@@ -1773,7 +1867,7 @@ extern "C" int mk_session_grids(mk_session* s, int32_t which, double* out, int32
   if (which == 1 && s->tiled) return set_err(MK_E_ARG, "tiled sessions give w.predict grids per tile (mk_session_tile_grids)");
   if (which == 1 && s->md.n_test < 1) return set_err(MK_E_ARG, "the session has no test sites");
   const long C = which == 0 ? (long)s->P : (long)s->q * s->md.n_test;
-  HIPCHK(hipSetDevice(s->device));
+  MK_ENTRY_DEVICE(s->device);
   DevBufs scratch;
   double* d = out;
   if (!device_out && !(d = scratch.get<double>((size_t)s->S * C * MK_N_LEVELS))) return set_err(MK_E_NOMEM, "grid scratch");
@@ -1788,7 +1882,7 @@ extern "C" int mk_session_tile_grids(mk_session* s, int32_t t0, double* out, int
   if (!s->tiled) return set_err(MK_E_ARG, "tile grids need a session created with predict_tile > 0");
   if (device_out) return session_tile_grids(s, t0, out, nullptr);
   const long Tc = std::min(s->pred_tile, s->n_test_all - t0);
-  HIPCHK(hipSetDevice(s->device));
+  MK_ENTRY_DEVICE(s->device);
   DevBufs scratch;
   double* dq = scratch.get<double>((size_t)s->S * s->q * std::max(Tc, 1L) * MK_N_LEVELS);
   if (!dq) return set_err(MK_E_NOMEM, "tile grid scratch");
@@ -1800,7 +1894,7 @@ extern "C" int mk_session_tile_grids(mk_session* s, int32_t t0, double* out, int
 
 extern "C" int mk_session_outputs(mk_session* s, mk_outputs* o) {
   if (!s || !o) return set_err(MK_E_ARG, "null session/outputs");
-  HIPCHK(hipSetDevice(s->device));
+  MK_ENTRY_DEVICE(s->device);
   Model& md = s->md;
   const int S = s->S, P = s->P, q = s->q;
   const int n_test = md.n_test;
@@ -1834,7 +1928,7 @@ extern "C" int mk_session_outputs(mk_session* s, mk_outputs* o) {
     if (o->w_predict_sum) {   // this shard's term of the combine: sequential sum over its subsets
       double* dsum = scratch.get<double>((size_t)C * MK_N_LEVELS);
       if (!dsum) return set_err(MK_E_NOMEM, "combine scratch");
-      hipLaunchKernelGGL(k_combine, dim3((unsigned)(((long)C * MK_N_LEVELS + 255) / 256)), dim3(256), 0, s->stream, dq,
+      MK_LAUNCH(k_combine, dim3((unsigned)(((long)C * MK_N_LEVELS + 255) / 256)), dim3(256), 0, s->stream, dq,
                          S, (long)C * MK_N_LEVELS, dsum, 0);
       HIPCHK(hipMemcpyAsync(o->w_predict_sum, dsum, (size_t)C * MK_N_LEVELS * 8, hipMemcpyDeviceToHost, s->stream));
     }
@@ -1887,7 +1981,11 @@ extern "C" int mk_session_outputs(mk_session* s, mk_outputs* o) {
   return 0;
 }
 
-extern "C" void mk_session_destroy(mk_session* s) { delete s; }
+extern "C" void mk_session_destroy(mk_session* s) {
+  ApiCall call(__func__);
+  DeviceGuard dg;
+  delete s;
+}
 
 extern "C" int32_t mk_session_count(void) { return g_live_sessions.load(); }
 
@@ -1914,13 +2012,13 @@ std::vector<double> r_seq(double from, double to, double by) {
 // ------------------------------------------------------------------ combine
 static int combine_host(const double* grids, int32_t K, int64_t G, double* out, int mean, int32_t device) {
   if (!grids || !out || K < 1 || G < 1) return set_err(MK_E_ARG, "bad combine arguments");
-  HIPCHK(hipSetDevice(device));
+  MK_ENTRY_DEVICE(device);
   DevBufs b;
   double* dg = b.get<double>((size_t)K * G);
   double* dout = b.get<double>((size_t)G);
   if (!dg || !dout) return set_err(MK_E_NOMEM, "combine alloc");
   HIPCHK(hipMemcpy(dg, grids, (size_t)K * G * 8, hipMemcpyHostToDevice));
-  hipLaunchKernelGGL(k_combine, dim3((unsigned)((G + 255) / 256)), dim3(256), 0, 0, dg, K, (long)G, dout, mean);
+  MK_LAUNCH(k_combine, dim3((unsigned)((G + 255) / 256)), dim3(256), 0, 0, dg, K, (long)G, dout, mean);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpy(out, dout, (size_t)G * 8, hipMemcpyDeviceToHost));
   return 0;
@@ -1937,8 +2035,8 @@ extern "C" int mk_combine_sum(const double* grids, int32_t K, int64_t G, double*
 extern "C" int mk_combine_device(const double* d_grids, int32_t K, int64_t G, double* d_out, int32_t mean,
                                  int32_t device, void* stream) {
   if (!d_grids || !d_out || K < 1 || G < 1) return set_err(MK_E_ARG, "bad combine arguments");
-  HIPCHK(hipSetDevice(device));
-  hipLaunchKernelGGL(k_combine, dim3((unsigned)((G + 255) / 256)), dim3(256), 0, (hipStream_t)stream, d_grids, K, (long)G,
+  MK_ENTRY_DEVICE(device);
+  MK_LAUNCH(k_combine, dim3((unsigned)((G + 255) / 256)), dim3(256), 0, (hipStream_t)stream, d_grids, K, (long)G,
                      d_out, mean ? 1 : 0);
   HIPCHK(hipGetLastError());
   return 0;
@@ -1948,7 +2046,7 @@ extern "C" int mk_combine_median(const double* grids, int32_t K, int32_t L, int6
                                  double* out, int32_t* iters, int32_t device) {
   if (!grids || !out || K < 1 || L < 1 || L > 256 || C < 1 || max_iter < 1 || !(tol >= 0.0))
     return set_err(MK_E_ARG, "bad combine_median arguments (1 <= n_levels <= 256, max_iter >= 1, tol >= 0)");
-  HIPCHK(hipSetDevice(device));
+  MK_ENTRY_DEVICE(device);
   DevBufs b;
   const size_t G = (size_t)L * C;
   double* dg = b.get<double>((size_t)K * G);
@@ -1956,7 +2054,7 @@ extern "C" int mk_combine_median(const double* grids, int32_t K, int32_t L, int6
   int* dit = b.get<int>((size_t)C);
   if (!dg || !dout || !dit) return set_err(MK_E_NOMEM, "combine_median alloc");
   HIPCHK(hipMemcpy(dg, grids, (size_t)K * G * 8, hipMemcpyHostToDevice));
-  hipLaunchKernelGGL(k_weiszfeld, dim3((unsigned)((C + 3) / 4)), dim3(256), 0, 0, dg, K, L, (long)C, max_iter, tol, dout,
+  MK_LAUNCH(k_weiszfeld, dim3((unsigned)((C + 3) / 4)), dim3(256), 0, 0, dg, K, L, (long)C, max_iter, tol, dout,
                      dit);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpy(out, dout, G * 8, hipMemcpyDeviceToHost));
@@ -1969,8 +2067,8 @@ extern "C" int mk_combine_median_device(const double* d_grids, int32_t K, int32_
                                         double tol, double* d_out, int32_t* d_iters, int32_t device, void* stream) {
   if (!d_grids || !d_out || K < 1 || L < 1 || L > 256 || C < 1 || max_iter < 1 || !(tol >= 0.0))
     return set_err(MK_E_ARG, "bad combine_median arguments (1 <= n_levels <= 256, max_iter >= 1, tol >= 0)");
-  HIPCHK(hipSetDevice(device));
-  hipLaunchKernelGGL(k_weiszfeld, dim3((unsigned)((C + 3) / 4)), dim3(256), 0, (hipStream_t)stream, d_grids, K, L, (long)C,
+  MK_ENTRY_DEVICE(device);
+  MK_LAUNCH(k_weiszfeld, dim3((unsigned)((C + 3) / 4)), dim3(256), 0, (hipStream_t)stream, d_grids, K, L, (long)C,
                      max_iter, tol, d_out, d_iters);
   HIPCHK(hipGetLastError());
   return 0;
@@ -1983,7 +2081,7 @@ extern "C" int mk_posterior_summary_ex(const double* result, int32_t P, const do
     return set_err(MK_E_ARG, "bad posterior_summary arguments (P >= 1, 0 <= p <= P, 1 <= samplesize <= 16384)");
   if (C > 0 && (!result2 || (p > 0 && !x_test))) return set_err(MK_E_ARG, "result2 / x_test missing");
   if (link != MK_LINK_LOGIT && link != MK_LINK_PROBIT) return set_err(MK_E_ARG, "link must be logit or probit");
-  HIPCHK(hipSetDevice(device));
+  MK_ENTRY_DEVICE(device);
   const int L = MK_N_LEVELS;
   const std::vector<double> xg = r_seq(0.005, 1.0, 0.005);   // allquant levels (MK.R:88)
   const std::vector<double> xo = r_seq(0.005, 1.0, 0.001);   // Xout (MK.R:140)
@@ -2041,15 +2139,15 @@ extern "C" int mk_posterior_summary_ex(const double* result, int32_t P, const do
     }
     HIPCHK(hipMemcpy(d_idx, hidx.data(), (size_t)S * 4, hipMemcpyHostToDevice));
   } else {
-    hipLaunchKernelGGL(k_post_index, dim3((S + 255) / 256), dim3(256), 0, st, seed, S, NL, d_idx);
+    MK_LAUNCH(k_post_index, dim3((S + 255) / 256), dim3(256), 0, st, seed, S, NL, d_idx);
   }
-  hipLaunchKernelGGL(k_post_interp, dim3((unsigned)(((long)S * P + 255) / 256)), dim3(256), 0, st, d_res, L, (long)P,
+  MK_LAUNCH(k_post_interp, dim3((unsigned)(((long)S * P + 255) / 256)), dim3(256), 0, st, d_res, L, (long)P,
                      d_idx, S, d_lo, d_hi, d_mode, d_t, d_spar);
   if (C > 0) {
     const unsigned nb = (unsigned)(((long)S * C + 255) / 256);
-    hipLaunchKernelGGL(k_post_interp, dim3(nb), dim3(256), 0, st, d_res2, L, (long)C, d_idx, S, d_lo, d_hi, d_mode, d_t,
+    MK_LAUNCH(k_post_interp, dim3(nb), dim3(256), 0, st, d_res2, L, (long)C, d_idx, S, d_lo, d_hi, d_mode, d_t,
                        d_sw);
-    hipLaunchKernelGGL(k_post_prob, dim3(nb), dim3(256), 0, st, d_spar, S, d_xt, (long)C, p, d_sw, link, d_p);
+    MK_LAUNCH(k_post_prob, dim3(nb), dim3(256), 0, st, d_spar, S, d_xt, (long)C, p, d_sw, link, d_p);
   }
   HIPCHK(hipGetLastError());
   if (o->index) HIPCHK(hipMemcpy(o->index, d_idx, (size_t)S * 4, hipMemcpyDeviceToHost));
@@ -2114,7 +2212,7 @@ extern "C" int mk_glm_binomial_link(const double* y, const double* weights, cons
   if (!y || !weights || !x || !coef || n < 1 || p < 1 || p > 8 || maxit < 1)
     return set_err(MK_E_ARG, "bad glm arguments (n >= 1, 1 <= p <= 8, maxit >= 1)");
   if (link != MK_LINK_LOGIT && link != MK_LINK_PROBIT) return set_err(MK_E_ARG, "link must be logit or probit");
-  HIPCHK(hipSetDevice(device));
+  MK_ENTRY_DEVICE(device);
   std::vector<double> yp((size_t)n);
   for (int64_t i = 0; i < n; ++i) yp[i] = y[i] / weights[i];     // glm((y/weight) ~ x - 1, ...)  MK.R:53
   const int ntri = p * (p + 1) / 2, NP = 1 + ntri + p;
@@ -2133,7 +2231,7 @@ extern "C" int mk_glm_binomial_link(const double* y, const double* weights, cons
   double dev = 0.0;
   auto pass = [&](int mode) -> int {
     if (mode == 1) HIPCHK(hipMemcpy(d_c, c.data(), (size_t)p * 8, hipMemcpyHostToDevice));
-    hipLaunchKernelGGL(k_glm_pass, dim3(nblk), dim3(256), 0, 0, d_y, d_w, d_x, (long)n, p, d_c, mode, link, d_part);
+    MK_LAUNCH(k_glm_pass, dim3(nblk), dim3(256), 0, 0, d_y, d_w, d_x, (long)n, p, d_c, mode, link, d_part);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpy(part.data(), d_part, part.size() * 8, hipMemcpyDeviceToHost));
     std::vector<double> tot(NP, 0.0);
@@ -2189,7 +2287,7 @@ extern "C" int mk_correlation_batched(const double* coords, int32_t S, int32_t n
   for (int s = 0; s < S; ++s)
     if (!(phi[s] > 0.0) || (nu && cov_model == MK_COV_MATERN && !(nu[s] > 0.0)))
       return set_err(MK_E_ARG, "phi and nu must be > 0");
-  HIPCHK(hipSetDevice(device));
+  MK_ENTRY_DEVICE(device);
   // The sampler's own candidate kernel (k_cov_candidate, which = 2: the current theta) on a
   // one-outcome model per point set: theta = 0 with Unif(0, 2 phi) / Unif(0, 2 nu) supports gives
   // exactly phi and nu (logitInv(0, 0, b) = b - b/2).  The border row is u = 0.
@@ -2234,10 +2332,10 @@ extern "C" int mk_correlation_batched(const double* coords, int32_t S, int32_t n
     MatSet mv = ms;
     mv.L = dL + (size_t)s * 2 * n_pad * n_pad;
     mv.cur = dcur + s;
-    hipLaunchKernelGGL(cov_candidate_kernel(cov_model), dim3(xcd_grid_h(1, ntri_tiles)), dim3(256), 0, 0, md, mv, 0, 1,
+    MK_LAUNCH(cov_candidate_kernel(cov_model), dim3(xcd_grid_h(1, ntri_tiles)), dim3(256), 0, 0, md, mv, 0, 1,
                        2, 0, nullptr, nullptr);
   }
-  hipLaunchKernelGGL(k_extract_candidate, dim3(2048), dim3(256), 0, 0, ms, n, S, dr);
+  MK_LAUNCH(k_extract_candidate, dim3(2048), dim3(256), 0, 0, ms, n, S, dr);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpy(R_out, dr, (size_t)S * n * n * 8, hipMemcpyDeviceToHost));
   return 0;
@@ -2246,7 +2344,7 @@ extern "C" int mk_correlation_batched(const double* coords, int32_t S, int32_t n
 extern "C" int mk_cholesky_batched(const double* A, int32_t S, int32_t n, double* L_out, double* logdet_out,
                                    double* inv_out, int32_t device) {
   if (!A || S < 1 || n < 1) return set_err(MK_E_ARG, "bad cholesky arguments");
-  HIPCHK(hipSetDevice(device));
+  MK_ENTRY_DEVICE(device);
   mk_session* s = new mk_session();
   s->device = device;
   auto fail = [&](int code) { delete s; return code; };
@@ -2280,7 +2378,7 @@ extern "C" int mk_cholesky_batched(const double* A, int32_t S, int32_t n, double
   if (hipFuncSetAttribute((const void*)k_chol_diag, hipFuncAttributeMaxDynamicSharedMemorySize,
                           MK_DIAG_LDS_BYTES) != hipSuccess || !set_gemm_lds())
     return fail(set_err(MK_E_HIP, "lds attribute"));
-  hipLaunchKernelGGL(k_load_plain, dim3(2048), dim3(256), 0, s->stream, ms, dA, n, S);
+  MK_LAUNCH(k_load_plain, dim3(2048), dim3(256), 0, s->stream, ms, dA, n, S);
   launch_cholesky(s, a, 0, 1);
   std::vector<double> part((size_t)S * nt);
   std::vector<int> info(S);
@@ -2289,11 +2387,11 @@ extern "C" int mk_cholesky_batched(const double* A, int32_t S, int32_t n, double
     return fail(set_err(MK_E_HIP, "info download"));
   for (int i = 0; i < S; ++i)
     if (info[i]) return fail(set_err(MK_E_ARG, "matrix " + std::to_string(i) + " is not positive definite"));
-  hipLaunchKernelGGL(k_theta_init, dim3((S + 63) / 64), dim3(64), 0, s->stream, md, ms, 0, 1);
+  MK_LAUNCH(k_theta_init, dim3((S + 63) / 64), dim3(64), 0, s->stream, md, ms, 0, 1);
   double* dL = nullptr;
   if ((rc = s->alloc(&dL, (size_t)S * n * n))) return fail(rc);
   if (L_out) {
-    hipLaunchKernelGGL(k_extract_L, dim3(2048), dim3(256), 0, s->stream, ms, n, S, dL, 0);
+    MK_LAUNCH(k_extract_L, dim3(2048), dim3(256), 0, s->stream, ms, n, S, dL, 0);
     if (hipMemcpyAsync(L_out, dL, (size_t)S * n * n * 8, hipMemcpyDeviceToHost, s->stream) != hipSuccess)
       return fail(set_err(MK_E_HIP, "L download"));
   }
@@ -2307,12 +2405,12 @@ extern "C" int mk_cholesky_batched(const double* A, int32_t S, int32_t n, double
     }
   }
   if (inv_out) {
-    hipLaunchKernelGGL(k_dirty_list, dim3(1), dim3(256), 0, s->stream, md, 1, a.d_plist, a.d_pcount, a.d_list,
+    MK_LAUNCH(k_dirty_list, dim3(1), dim3(256), 0, s->stream, md, 1, a.d_plist, a.d_pcount, a.d_list,
                        a.d_count);
     const int ntiles = nt * (nt + 1) / 2;
     launch_trinv(s, a, S, a.d_list, a.d_count);
-    hipLaunchKernelGGL(k_lauum, dim3(S * ntiles), dim3(256), LDS_128, s->stream, ms, md.n_s, a.d_list, a.d_count);
-    hipLaunchKernelGGL(k_extract_L, dim3(2048), dim3(256), 0, s->stream, ms, n, S, dL, 1);
+    MK_LAUNCH(k_lauum, dim3(S * ntiles), dim3(256), LDS_128, s->stream, ms, md.n_s, a.d_list, a.d_count);
+    MK_LAUNCH(k_extract_L, dim3(2048), dim3(256), 0, s->stream, ms, n, S, dL, 1);
     if (hipMemcpyAsync(inv_out, dL, (size_t)S * n * n * 8, hipMemcpyDeviceToHost, s->stream) != hipSuccess)
       return fail(set_err(MK_E_HIP, "inverse download"));
   }

@@ -859,7 +859,7 @@ __device__ inline double* wmat(const MatSet& ms, int sh) { return ms.W + (long)s
 // Eight workgroups per 128-tile, each copying one eighth of it (16 rows' worth: 2,048
 // doubles) with every load in flight at once: the copy is latency-bound (one tile per workgroup
 // took 100-150 us per launch at small shards, on the main stream's critical path).
-#define MK_CD_SPLIT 8
+// MK_CD_SPLIT (mk_types.hpp): workgroups per tile, shared with the launch site's grid.
 __global__ __launch_bounds__(256) void k_inv_copydiag(MatSet ms, const int* __restrict__ list, const int* __restrict__ count) {
   const int part = blockIdx.x % MK_CD_SPLIT, rest = blockIdx.x / MK_CD_SPLIT;
   const int e = rest / ms.nt, k = rest % ms.nt;

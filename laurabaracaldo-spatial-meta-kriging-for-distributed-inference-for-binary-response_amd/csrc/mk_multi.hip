@@ -53,6 +53,8 @@ struct Rccl {
   std::string why;
   ncclResult_t (*comm_init_all)(ncclComm_t*, int, const int*) = nullptr;
   ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*comm_abort)(ncclComm_t) = nullptr;
+  const char* (*last_error)(ncclComm_t) = nullptr;   // optional: RCCL's last WARN text
   ncclResult_t (*group_start)() = nullptr;
   ncclResult_t (*group_end)() = nullptr;
   ncclResult_t (*send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
@@ -72,12 +74,14 @@ const Rccl& rccl() {
     }
     x.comm_init_all = (decltype(x.comm_init_all))dlsym(h, "ncclCommInitAll");
     x.comm_destroy = (decltype(x.comm_destroy))dlsym(h, "ncclCommDestroy");
+    x.comm_abort = (decltype(x.comm_abort))dlsym(h, "ncclCommAbort");
+    x.last_error = (decltype(x.last_error))dlsym(h, "ncclGetLastError");
     x.group_start = (decltype(x.group_start))dlsym(h, "ncclGroupStart");
     x.group_end = (decltype(x.group_end))dlsym(h, "ncclGroupEnd");
     x.send = (decltype(x.send))dlsym(h, "ncclSend");
     x.recv = (decltype(x.recv))dlsym(h, "ncclRecv");
     x.error_string = (decltype(x.error_string))dlsym(h, "ncclGetErrorString");
-    x.ok = x.comm_init_all && x.comm_destroy && x.group_start && x.group_end && x.send && x.recv && x.error_string;
+    x.ok = x.comm_init_all && x.comm_destroy && x.comm_abort && x.group_start && x.group_end && x.send && x.recv && x.error_string;
     if (!x.ok) x.why = "librccl lacks a symbol";
     return x;
   }();
@@ -199,17 +203,43 @@ struct Block {
   }
 };
 
+// Teardown order: every block's stream is drained before the communicators go (a send/recv still
+// queued on a stream must not outlive its communicator); after a failed exchange the communicators
+// are aborted instead of destroyed, since a recv whose matching send was never issued would never
+// complete and a drain would wait on it forever.  Then the blocks (sessions, buffers), then the
+// host threads.
 struct Node {
   std::unique_ptr<Pool> pool;   // first member: its threads are joined after the blocks are freed
   int G = 0, K = 0;
   std::vector<std::unique_ptr<Block>> b;
   bool use_rccl = false;
+  bool exchange_failed = false;
   std::vector<ncclComm_t> comms;
   ~Node() {
+    if (exchange_failed) {
+      for (ncclComm_t c : comms)
+        if (c) rccl().comm_abort(c);
+      comms.clear();
+    }
+    for (auto& x : b)
+      if (x && x->st) {
+        (void)hipSetDevice(x->dev);
+        (void)hipStreamSynchronize(x->st);
+      }
     for (ncclComm_t c : comms)
       if (c) rccl().comm_destroy(c);
+    comms.clear();
   }
 };
+
+std::string rccl_detail(ncclResult_t e) {
+  std::string m = rccl().error_string(e);
+  if (rccl().last_error) {
+    const char* d = rccl().last_error(nullptr);
+    if (d && *d) m += std::string(" [") + d + "]";
+  }
+  return m;
+}
 
 constexpr int L = MK_N_LEVELS;
 
@@ -258,8 +288,9 @@ int exchange_combine(Node& nd, long C, const mk_combined* comb, double* h_comb, 
         if (first == ncclSuccess) first = e1 != ncclSuccess ? e1 : e2;
       }
     const ncclResult_t eg = R.group_end();
-    if (first != ncclSuccess) return fail(MK_E_HIP, std::string("ncclSend/ncclRecv -> ") + R.error_string(first));
-    if (eg != ncclSuccess) return fail(MK_E_HIP, std::string("ncclGroupEnd -> ") + R.error_string(eg));
+    if (first != ncclSuccess || eg != ncclSuccess) nd.exchange_failed = true;
+    if (first != ncclSuccess) return fail(MK_E_HIP, std::string("ncclSend/ncclRecv -> ") + rccl_detail(first));
+    if (eg != ncclSuccess) return fail(MK_E_HIP, std::string("ncclGroupEnd -> ") + rccl_detail(eg));
   } else {
     for (int j = 0; j < G; ++j) {
       Block& xj = *nd.b[j];
@@ -291,16 +322,16 @@ int exchange_combine(Node& nd, long C, const mk_combined* comb, double* h_comb, 
         if (median) {
           const int it = comb->max_iter > 0 ? comb->max_iter : 100;
           const double tol = comb->tol >= 0.0 ? comb->tol : 1e-12;
-          hipLaunchKernelGGL(k_weiszfeld, dim3((unsigned)((per + 3) / 4)), dim3(256), 0, x.st, x.recv.p, K, L, per, it,
+          MK_LAUNCH(k_weiszfeld, dim3((unsigned)((per + 3) / 4)), dim3(256), 0, x.st, x.recv.p, K, L, per, it,
                              tol, x.comb.p, (int*)x.iters.p);
         } else {
-          hipLaunchKernelGGL(k_combine, dim3(nb), dim3(256), 0, x.st, x.recv.p, K, g, x.comb.p, 1);
+          MK_LAUNCH(k_combine, dim3(nb), dim3(256), 0, x.st, x.recv.p, K, g, x.comb.p, 1);
         }
         MHIP(hipGetLastError());
         MHIP(hipMemcpyAsync(h_comb + a * L, x.comb.p, (size_t)cj * L * 8, hipMemcpyDeviceToHost, x.st));
       }
       if (h_sum) {
-        hipLaunchKernelGGL(k_combine, dim3(nb), dim3(256), 0, x.st, x.recv.p, K, g, x.sum.p, 0);
+        MK_LAUNCH(k_combine, dim3(nb), dim3(256), 0, x.st, x.recv.p, K, g, x.sum.p, 0);
         MHIP(hipGetLastError());
         MHIP(hipMemcpyAsync(h_sum + a * L, x.sum.p, (size_t)cj * L * 8, hipMemcpyDeviceToHost, x.st));
       }
@@ -321,6 +352,8 @@ extern "C" int mk_meta_fit(const mk_problem* pr, const mk_config* c, const int32
   if (pr->q < 1 || pr->q > 4 || pr->p < 1 || !pr->n_part) return fail(MK_E_ARG, "bad q / p / n_part");
   if (comb && comb->method != MK_COMBINE_MEAN && comb->method != MK_COMBINE_MEDIAN)
     return fail(MK_E_ARG, "combine method must be MK_COMBINE_MEAN or MK_COMBINE_MEDIAN");
+  ApiCall call(__func__);
+  DeviceGuard dg;   // the caller's current device is restored on every return path
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(MK_E_NODEV, "no HIP device");
   for (int r = 0; r < G; ++r)
@@ -337,7 +370,7 @@ extern "C" int mk_meta_fit(const mk_problem* pr, const mk_config* c, const int32
   bool distinct = true;
   for (int r = 0; r < G; ++r)
     for (int j = 0; j < r; ++j) distinct = distinct && devices[r] != devices[j];
-  const char* xenv = std::getenv("MK_EXCHANGE");   // "copy": device copies even on distinct devices
+  const char* xenv = std::getenv("MK_EXCHANGE");   // "copy": device copies even on distinct devices (opt-in)
   nd.use_rccl = distinct && !(xenv && std::strcmp(xenv, "copy") == 0);
   if (nd.use_rccl && !rccl().ok) return fail(MK_E_HIP, rccl().why);
 
@@ -373,17 +406,20 @@ extern "C" int mk_meta_fit(const mk_problem* pr, const mk_config* c, const int32
   });
   if (rc) return rc;
   if (nd.use_rccl) {
-    // RCCL checks the calling thread's sticky HIP error: clear anything an earlier call left there.
-    // A communicator that cannot be created (seen once in a long test process, "unhandled cuda
-    // error") degrades to the device-copy exchange -- same results, reported in comb->exchange.
-    (void)hipGetLastError();
+    // A communicator that cannot be created is an error (MK_E_HIP), never a silent switch to the
+    // device-copy exchange (MK_EXCHANGE=copy asks for that explicitly).  The message carries RCCL's
+    // own last warning and any HIP error this thread held before the call (RCCL reports a pending
+    // one as "unhandled cuda error"; seen once in a long round-3 test process), so a repeat names
+    // the failing call.
+    const hipError_t pending = hipGetLastError();
     nd.comms.assign(G, nullptr);
     const ncclResult_t e = rccl().comm_init_all(nd.comms.data(), G, devices);
     if (e != ncclSuccess) {
-      std::fprintf(stderr, "libmk: ncclCommInitAll failed (%s); combining with device copies\n", rccl().error_string(e));
       nd.comms.clear();
-      nd.use_rccl = false;
-      (void)hipGetLastError();
+      const hipError_t after = hipGetLastError();
+      return fail(MK_E_HIP, std::string("ncclCommInitAll -> ") + rccl_detail(e) + "; HIP error pending before: " +
+                                hipGetErrorName(pending) + ", after: " + hipGetErrorName(after) +
+                                " (MK_EXCHANGE=copy selects the device-copy exchange)");
     }
   }
   if (comb) comb->exchange = nd.use_rccl ? 1 : 0;

@@ -22,6 +22,7 @@
 #include "mk_common.hpp"
 
 #define MK_QMAX 4
+#define MK_CD_SPLIT 8        // k_inv_copydiag: workgroups per 128-tile (kernel and launch grid)
 #define MK_QUANT_MAX 16384   // kept samples per quantile summary (k_quantiles sorts them in 128 KB of LDS)
 
 namespace mk {

@@ -173,6 +173,20 @@ class Session:
     def run(self, n_iter):
         check(self._lib.mk_session_run(self._h, int(n_iter)))
 
+    def chain_state(self, i):
+        """Subset i's chain state now (mk_session_chain_state): beta, theta (A tri with log diagonal |
+        logit phi | logit nu), w (n_s q), tune (log proposal sds) and accept (this batch's counts), in
+        spMvGLM's MH order -- enough to resume the chain on another host at iteration `self.iteration`."""
+        cfg = self.cfg
+        nq = int(self.n_part[i]) * cfg.q
+        nmh = cfg.p + cfg.n_theta + nq
+        st = dict(beta=np.zeros(cfg.p), theta=np.zeros(cfg.n_theta), w=np.zeros(nq), tune=np.zeros(nmh),
+                  accept=np.zeros(nmh))
+        check(self._lib.mk_session_chain_state(self._h, int(i), dptr(st["beta"]), dptr(st["theta"]), dptr(st["w"]),
+                                               dptr(st["tune"]), dptr(st["accept"])))
+        st["iteration"] = self.iteration
+        return st
+
     def set_test_sites(self, coords_test):
         """Kriging sites for the next outputs() of a session created with predict_tile > 0
         (its kept chain states were recorded during the run): spPredict without refitting."""

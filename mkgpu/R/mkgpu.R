@@ -203,10 +203,27 @@ mk_posterior_summary <- function(result, result2, x.test, samplesize = 1000, n.o
 }
 
 # libmk's lookahead schedule runs up to five HIP streams; HIP reads its hardware-queue count
-# (default 4, streams beyond it share queues) when it starts, which is after this hook -- unless
-# another package started HIP first; the count HIP runs with is passed to libmk either way.
+# (default 4, streams beyond it share queues) once, when it starts.  If HIP has not started yet
+# (libmk has not touched it; mk_hip_initialized checks /dev/kfd without starting it) the variable
+# is raised to 8 here and libmk reads it itself.  If another package started HIP first, the
+# setting comes too late: libmk is told the count HIP started with -- the variable as it was, or
+# HIP's default 4 -- and runs three streams instead of five rather than share queues.
 .onLoad <- function(libname, pkgname) {
   q <- suppressWarnings(as.integer(Sys.getenv("GPU_MAX_HW_QUEUES", "0")))
-  if (is.na(q) || q < 8L) Sys.setenv(GPU_MAX_HW_QUEUES = "8")
-  .Call("mk_r_hw_queues", if (is.na(q) || q < 8L) 8L else q)
+  if (is.na(q)) q <- 0L
+  if (.Call("mk_r_hip_started")) {
+    .Call("mk_r_hw_queues", if (q > 0L) q else 4L)
+  } else {
+    if (q < 8L) Sys.setenv(GPU_MAX_HW_QUEUES = "8")
+    .Call("mk_r_hw_queues", -1L)
+  }
+  # libmk's pooled streams are destroyed while the HIP runtime is still alive at R's exit
+  reg.finalizer(.mk_exit, function(e) .Call("mk_r_shutdown"), onexit = TRUE)
+}
+
+.mk_exit <- new.env()
+
+.onUnload <- function(libpath) {
+  .Call("mk_r_shutdown")
+  library.dynam.unload("mkgpu", libpath)
 }

@@ -287,9 +287,20 @@ SEXP mk_r_glm(SEXP y, SEXP weights, SEXP x, SEXP link, SEXP device) {
   return res;
 }
 
-/* The process's HIP hardware queues (GPU_MAX_HW_QUEUES when HIP started; .onLoad sets 8 first). */
+/* The process's HIP hardware queues: n > 0 the count HIP started with (another package started HIP
+ * before .onLoad ran), n < 0 libmk reads GPU_MAX_HW_QUEUES itself (HIP starts after .onLoad set it). */
 SEXP mk_r_hw_queues(SEXP n) {
   mk_set_hw_queues(asInteger(n));
+  return R_NilValue;
+}
+
+/* TRUE when this process's HIP runtime already runs (it holds /dev/kfd open), checked without
+ * starting it: .onLoad's GPU_MAX_HW_QUEUES can then no longer take effect. */
+SEXP mk_r_hip_started(void) { return ScalarLogical(mk_hip_initialized() != 0); }
+
+/* libmk's pooled HIP streams go while the runtime is alive (.onUnload, and R's exit finalizer). */
+SEXP mk_r_shutdown(void) {
+  mk_shutdown();
   return R_NilValue;
 }
 
@@ -301,6 +312,8 @@ static const R_CallMethodDef call_methods[] = {
     {"mk_r_summary", (DL_FUNC)&mk_r_summary, 6},
     {"mk_r_glm", (DL_FUNC)&mk_r_glm, 5},
     {"mk_r_hw_queues", (DL_FUNC)&mk_r_hw_queues, 1},
+    {"mk_r_hip_started", (DL_FUNC)&mk_r_hip_started, 0},
+    {"mk_r_shutdown", (DL_FUNC)&mk_r_shutdown, 0},
     {NULL, NULL, 0}};
 
 void R_init_mkgpu(DllInfo* dll) {

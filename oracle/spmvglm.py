@@ -250,7 +250,7 @@ def _c_sweep():
 
 
 def fit_subset(coords, y, wt, X, cfg, subset=0, coords_test=None, record_w=False,
-               quantiles=True, max_iter=None, sweep="py", site_index=None):
+               quantiles=True, max_iter=None, sweep="py", site_index=None, start=None):
     """One subset: spMvGLM amcmc fit with fused spPredict on kept iterations.
 
     coords (n,2); y, wt (N=n*q) location-major; X (N,p) block-diagonal design.
@@ -261,7 +261,13 @@ def fit_subset(coords, y, wt, X, cfg, subset=0, coords_test=None, record_w=False
     (the latent-w sweep) in oracle/csrc/sweep.c -- the same operations in the same order -- for
     the CPU baseline's timing.  site_index (optional, [n_test] ints): the global index of each
     test site, so a sub-sample of a large kriging set (configs[4]: 1M sites) draws the same
-    Philox streams as the device does for those sites (default 0..n_test-1).
+    Philox streams as the device does for those sites (default 0..n_test-1).  start (optional):
+    resume a chain -- a dict with 'iteration' (iterations already done) and the state after them in
+    MH order, 'beta', 'theta' (A tri with log diagonal | logit phi | logit nu), 'w', 'tune' (log
+    sds) and 'accept' (the current batch's counts), as the device's mk_session_chain_state returns
+    it; the loop then runs iterations start['iteration'] .. max_iter - 1 with the same Philox
+    counters (bench.py's CPU baseline times the device's window this way).  out['phase_seconds']
+    splits the loop's time by step.
     """
     q, p = cfg.q, cfg.p
     n = coords.shape[0]
@@ -290,6 +296,19 @@ def fit_subset(coords, y, wt, X, cfg, subset=0, coords_test=None, record_w=False
         np.log(np.sqrt(cfg.phi_tuning)),
         np.log(np.sqrt(cfg.nu_tuning)) if matern else np.zeros(0),
         np.full(N, np.log(np.sqrt(cfg.w_tuning)))])
+    accept0 = None
+    s_begin = 0
+    if start is not None:
+        s_begin = int(start["iteration"])
+        beta = np.array(start["beta"], dtype=np.float64)
+        th = np.asarray(start["theta"], dtype=np.float64)
+        A = tri_to_A(th[:ntri], q)
+        theta_phi = th[ntri:ntri + q].copy()
+        if matern:
+            theta_nu = th[ntri + q:ntri + 2 * q].copy()
+        w = np.array(start["w"], dtype=np.float64)
+        tune = np.array(start["tune"], dtype=np.float64)
+        accept0 = np.array(start["accept"], dtype=np.float64)
     eta = X @ beta + w
 
     D = distance_matrix(coords, coords)
@@ -332,11 +351,14 @@ def fit_subset(coords, y, wt, X, cfg, subset=0, coords_test=None, record_w=False
     acc_hist = np.zeros((cfg.n_batch, n_mh))
     kept0 = cfg.burn_in - 1           # 0-based first kept iteration (R start=burn.in)
     w_pred = np.zeros((max(0, n_iter - kept0), q * n_test)) if n_test else None
-    accept = np.zeros(n_mh)
+    accept = np.zeros(n_mh) if accept0 is None else accept0
 
     import time as _time
-    t_loop = _time.perf_counter()
-    for s in range(n_iter):
+    clock = _time.perf_counter
+    phase = dict(beta_A=0.0, factor=0.0, inverse=0.0, sweep=0.0, krige=0.0, other=0.0)
+    t_loop = clock()
+    for s in range(s_begin, n_iter):
+        t_ph = clock()
         b = s // cfg.batch_length
         # all proposal normals / accept draws for this iteration (one Philox call each)
         js = np.arange(n_mh)
@@ -386,6 +408,9 @@ def fit_subset(coords, y, wt, X, cfg, subset=0, coords_test=None, record_w=False
         G = np.einsum('hc,ihc->ih', M, Gc)
 
         # ---------------- 3. phi_h then nu_h: one Cholesky per proposal
+        t_c = clock()
+        phase["beta_A"] += t_c - t_ph
+        t_ph = t_c
         quad_h = np.einsum('ih,ih->h', U, G)
         dirty = [False] * q
         for kind in (("phi", "nu") if matern else ("phi",)):
@@ -415,12 +440,18 @@ def fit_subset(coords, y, wt, X, cfg, subset=0, coords_test=None, record_w=False
                     accept[j] += 1
         # ---------------- 4. refresh Q_h, g_h where R_h changed (and for every h at the
         #                     first kept iteration, where kriging needs fresh factors)
+        t_c = clock()
+        phase["factor"] += t_c - t_ph
+        t_ph = t_c
         for h in range(q):
             if dirty[h] or s == kept0:
                 Q[h] = cho_inverse(L[h])
                 G[:, h] = Q[h] @ U[:, h]
 
         # ---------------- 5. single-site w sweep (site-major, outcome-minor)
+        t_c = clock()
+        phase["inverse"] += t_c - t_ph
+        t_ph = t_c
         delta_w = np.exp(tune[o_w:o_w + N]) * zs[o_w:o_w + N]
         dll = loglik_terms(y, wt, eta + delta_w, cfg.link) - loglik_terms(y, wt, eta, cfg.link)
         lu = logus[o_w:o_w + N]
@@ -454,6 +485,9 @@ def fit_subset(coords, y, wt, X, cfg, subset=0, coords_test=None, record_w=False
                 accept[o_w + k] += 1
 
         # ---------------- 6. record
+        t_c = clock()
+        phase["sweep"] += t_c - t_ph
+        t_ph = t_c
         K = A @ A.T
         samples[s, :p] = beta
         samples[s, p:p + ntri] = lower_tri_vec(K)
@@ -464,6 +498,9 @@ def fit_subset(coords, y, wt, X, cfg, subset=0, coords_test=None, record_w=False
             w_samples[s] = w
 
         # ---------------- 7. fused spPredict on kept iterations
+        t_c = clock()
+        phase["other"] += t_c - t_ph
+        t_ph = t_c
         if n_test and s >= kept0:
             key_s = s
             mean = np.zeros((n_test, q))
@@ -484,15 +521,23 @@ def fit_subset(coords, y, wt, X, cfg, subset=0, coords_test=None, record_w=False
             w_pred[s - kept0] = draw.reshape(-1)
 
         # ---------------- 8. batch end: adapt log-sd toward accept_rate
+        t_c = clock()
+        phase["krige"] += t_c - t_ph
+        t_ph = t_c
         if (s + 1) % cfg.batch_length == 0:
             rate = accept / cfg.batch_length
             acc_hist[b] = rate
             step = min(0.01, 1.0 / np.sqrt(b)) if b > 0 else 0.01
             tune = np.where(rate > cfg.accept_rate, tune + step, tune - step)
             accept[:] = 0.0
+        phase["other"] += clock() - t_ph
 
     out = dict(samples=samples, accept=acc_hist, tuning=tune, w_pred=w_pred,
-               beta=beta, A=A, w=w, n_iter=n_iter, loop_seconds=_time.perf_counter() - t_loop)
+               beta=beta, A=A, w=w, n_iter=n_iter, loop_seconds=clock() - t_loop, phase_seconds=phase)
+    # the state after the last iteration, in the layout `start` takes (and mk_session_chain_state returns)
+    th_out = [A_to_tri(A), theta_phi] + ([theta_nu] if matern else [])
+    out["state"] = dict(iteration=n_iter, beta=beta.copy(), theta=np.concatenate(th_out), w=w.copy(),
+                        tune=tune.copy(), accept=accept.copy())
     if record_w:
         out["w_samples"] = w_samples
     if quantiles and n_iter >= cfg.n_samples:

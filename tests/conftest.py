@@ -1,3 +1,4 @@
+import faulthandler
 import importlib
 import os
 import sys
@@ -10,8 +11,40 @@ if ROOT not in sys.path:
 PKG = "laurabaracaldo-spatial-meta-kriging-for-distributed-inference-for-binary-response_amd"
 
 
+HANG_DUMP_S = 100     # below pytest's 120 s per-test limit (pytest.ini) and gpurun's 180 s silence kill
+_dump_file = None
+
+
 def pytest_configure(config):
+    global _dump_file
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libmk.so on cuda:0)")
+    # Stalls must name where they are: libmk's watchdog prints the kernel every
+    # stuck stream is on once a library call has waited 60 s (read when libmk loads), and a test
+    # still running after HANG_DUMP_S dumps every Python thread's stack from faulthandler's own C
+    # thread (no GIL needed).  Both also go to gpurun_out/, which survives a killed GPU call.
+    out = os.path.join(ROOT, "gpurun_out")
+    os.makedirs(out, exist_ok=True)
+    os.environ.setdefault("MK_WATCHDOG", "60")
+    os.environ.setdefault("MK_WATCHDOG_LOG", os.path.join(out, "watchdog.log"))
+    _dump_file = open(os.path.join(out, "hang_dump.log"), "a")
+
+
+def pytest_collection_modifyitems(config, items):
+    # pytest.ini's 120 s limit is for the GPU tests (below gpurun's silence kill); the CPU tests that
+    # run oracle chains get more room on a loaded host
+    for item in items:
+        if item.get_closest_marker("gpu") is None and item.get_closest_marker("timeout") is None:
+            item.add_marker(pytest.mark.timeout(900))
+
+
+@pytest.fixture(autouse=True)
+def _dump_stacks_if_hung(request):
+    if _dump_file is not None:
+        _dump_file.write(f"--- {request.node.nodeid}\n")
+        _dump_file.flush()
+        faulthandler.dump_traceback_later(HANG_DUMP_S, exit=False, file=_dump_file)
+    yield
+    faulthandler.cancel_dump_traceback_later()
 
 
 @pytest.fixture(scope="session")

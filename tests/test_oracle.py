@@ -228,3 +228,24 @@ def test_c_sweep_matches_python_sweep(q, cov):
     else:
         np.testing.assert_allclose(b["samples"], a["samples"], rtol=1e-12, atol=1e-12)
         np.testing.assert_allclose(b["w_samples"], a["w_samples"], rtol=1e-12, atol=1e-12)
+
+
+def test_resumed_chain_continues_the_same_chain():
+    """fit_subset(start=state) resumes a chain at iteration m with the same Philox counters (bench.py's
+    CPU baseline resumes the device's chain this way): m = 60 crosses a batch end (adaptation at 50),
+    so the resumed iterations 60..99 use adapted scales; they equal the uninterrupted chain's to
+    rounding (the resumed side re-factors from the state instead of carrying its factors)."""
+    d = syn.generate(120, q=1, n_test=30, seed=17)
+    cfg = om.Config(1, 2, beta_starting=[0.5, -0.5], beta_tuning=[0.05, 0.05], n_batch=2, batch_length=50,
+                    burn_in=80, seed=9)
+    full = om.fit_subset(d["coords"], d["y"], np.ones(120), d["x"], cfg, subset=3, coords_test=d["coords_test"],
+                         quantiles=False)
+    head = om.fit_subset(d["coords"], d["y"], np.ones(120), d["x"], cfg, subset=3, coords_test=d["coords_test"],
+                         quantiles=False, max_iter=60)
+    assert head["state"]["iteration"] == 60
+    tail = om.fit_subset(d["coords"], d["y"], np.ones(120), d["x"], cfg, subset=3, coords_test=d["coords_test"],
+                         quantiles=False, start=head["state"])
+    np.testing.assert_allclose(tail["samples"][60:], full["samples"][60:], rtol=0, atol=1e-9)
+    np.testing.assert_allclose(tail["w_pred"], full["w_pred"], rtol=0, atol=1e-9)
+    np.testing.assert_allclose(tail["state"]["w"], full["state"]["w"], rtol=0, atol=1e-9)
+    assert set(tail["phase_seconds"]) == {"beta_A", "factor", "inverse", "sweep", "krige", "other"}

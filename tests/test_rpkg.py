@@ -33,7 +33,7 @@ def test_call_registrations_match_c_signatures_and_r_calls():
     c, r = _read("mkgpu", "src", "mk_r.c"), _read("mkgpu", "R", "mkgpu.R")
     reg = dict((n, int(k)) for n, k in re.findall(r'\{"(\w+)", \(DL_FUNC\)&\w+, (\d+)\}', c))
     assert set(reg) == {"mk_r_fit", "mk_r_spmvglm", "mk_r_sppredict", "mk_r_combine", "mk_r_summary", "mk_r_glm",
-                        "mk_r_hw_queues"}
+                        "mk_r_hw_queues", "mk_r_hip_started", "mk_r_shutdown"}
     for name, nargs in reg.items():
         sig = re.search(r"SEXP %s\((.*?)\) \{" % name, c, re.S).group(1)
         assert sig.count("SEXP") == nargs, name
@@ -99,3 +99,21 @@ def test_r_wrappers_mirror_the_reference_calls():
     exports = re.search(r"export\((.*?)\)", _read("mkgpu", "NAMESPACE"), re.S).group(1)
     for fn in ("mk_meta_fit", "mk_spMvGLM", "mk_spPredict", "mk_combine", "mk_posterior_summary"):
         assert fn in exports
+
+
+def test_onload_passes_the_queue_count_hip_started_with():
+    """.onLoad raises GPU_MAX_HW_QUEUES only while HIP has not started (libmk then reads the variable
+    itself: mk_set_hw_queues(-1)); when another package started HIP first it reports the count HIP
+    started with (the variable as it was, else HIP's default 4), never a blanket 8.
+    The pooled streams are released at unload and at R's exit."""
+    r, c = _read("mkgpu", "R", "mkgpu.R"), _read("mkgpu", "src", "mk_r.c")
+    body = r[r.index(".onLoad <- function"):]
+    body = body[:body.index("\n}\n") + 3]
+    assert 'if (.Call("mk_r_hip_started"))' in body
+    started, fresh = body.split("} else {")
+    assert '.Call("mk_r_hw_queues", if (q > 0L) q else 4L)' in started
+    assert "Sys.setenv" not in started
+    assert 'Sys.setenv(GPU_MAX_HW_QUEUES = "8")' in fresh and '.Call("mk_r_hw_queues", -1L)' in fresh
+    assert 'reg.finalizer(.mk_exit, function(e) .Call("mk_r_shutdown"), onexit = TRUE)' in body
+    assert '.Call("mk_r_shutdown")' in r[r.index(".onUnload"):]
+    assert "mk_hip_initialized()" in c and "mk_shutdown();" in c

@@ -1,0 +1,135 @@
+"""Monte Carlo-error parity at configs[1] and configs[3] geometry against the oracle's fixtures
+(tests/golden/stat/cfg2_matern.npz, cfg4_lmc.npz, made by tests/golden/stat/make_meta_fixture.py).
+
+  cfg2_matern  Matern with nu free (U(0.1, 2)), q = 1, K = 3 subsets of n_s = 1,000 (configs[1]'s subset
+               size), 1,000 amcmc iterations (20 x 50), 251 kept, 200 kriging sites
+  cfg4_lmc     q = 3 LMC (3n x 3n cross-covariance blocks), exponential, K = 2 subsets of n_s = 500,
+               1,000 iterations, 251 kept, 200 kriging sites (600 w.predict columns)
+
+Both: R's partition after set.seed (MK.R:15-41), glm start values on the full data (MK.R:53-55),
+per-subset spMvGLM + spPredict + 200 quantiles (MK.R:46-96), combine MK.R:123-133.
+
+GPU: one session of 16 replicate meta-fits per case (replicate r = global subsets rK .. rK + K - 1, so
+replicate 0 runs the oracle's Philox streams and replicates 1..15 are independent chains):
+  * replicate 0 replays the oracle over all 1,000 iterations (adaptation across 20 batch ends, the
+    K and nu chains' drift included): samples, per-subset grids and the combined grids within 1e-6;
+  * the oracle's combined quantiles lie within Monte Carlo error of the device's independent
+    replicates: per parameter and level |z| <= 4 with z = (oracle - mean_r) / (sd_r sqrt(1 + 1/15));
+    over the w.predict (site, level) pairs at most 2 % with |z| > 3 and mean z^2 in [0.5, 2].
+CPU: the fixtures' own consistency (inputs regenerate, the combine is the sequential mean).
+The fixtures pin the device to the build's oracle, not to spBayes (absent).
+"""
+import importlib
+import os
+
+import numpy as np
+import pytest
+
+from oracle import spmvglm as om
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = "laurabaracaldo-spatial-meta-kriging-for-distributed-inference-for-binary-response_amd"
+CASES = ("cfg2_matern", "cfg4_lmc")
+LEVELS3 = (4, 99, 194)
+R_REP = 16
+
+
+def _load(case):
+    z = np.load(os.path.join(HERE, "golden", "stat", case + ".npz"))   # allow_pickle=False (default): data only
+    return {k: z[k] for k in z.files}
+
+
+def _subsets(g):
+    q = int(g["q"])
+    offs = np.concatenate([[0], np.cumsum(g["n_part"])])
+    out = []
+    for s in range(int(g["K"])):
+        idx = g["index"][offs[s]:offs[s + 1]].astype(np.int64) - 1
+        rows = (idx[:, None] * q + np.arange(q)[None, :]).reshape(-1)
+        out.append(dict(coords=g["coords"][idx], y=g["y"][rows], weights=np.ones(rows.size), x=g["x"][rows]))
+    return out
+
+
+# ------------------------------------------------------------------ CPU
+@pytest.mark.parametrize("case", CASES)
+def test_fixture_inputs_regenerate(case):
+    """The stored inputs are the SURVEY.md 8d generator's draw, R's partition and the glm.fit start
+    values (guards against generator or oracle drift)."""
+    from oracle import rrng, rstats
+    syn = importlib.import_module(PKG + ".synthetic")
+    g = _load(case)
+    n, q = int(g["n"]), int(g["q"])
+    d = syn.generate(n, q=q, n_test=int(g["n_test"]), cov_model=int(g["cov_model"]), seed=int(g["seed"]))
+    for k in ("coords", "y", "x", "coords_test", "x_test"):
+        assert np.array_equal(d[k], g[k]), k
+    # the exact GP draw goes through a BLAS Cholesky: its last bits follow the BLAS thread count
+    np.testing.assert_allclose(d["w_test_true"], g["w_test_true"], rtol=1e-9, atol=1e-12)
+    n_part, idx = rrng.partition(n, int(g["K"]), int(g["seed"]))
+    assert np.array_equal(n_part, g["n_part"])
+    assert np.array_equal(np.concatenate(idx), g["index"])
+    coef, _ = rstats.glm_binomial(g["y"], g["x"], np.ones(g["y"].size))
+    np.testing.assert_allclose(coef, g["beta_starting"], rtol=1e-12)
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_fixture_combine_is_the_sequential_mean(case):
+    g = _load(case)
+    assert np.array_equal(om.combine_mean(list(g["param_q"])), g["result"])
+    assert g["result2"].shape == (200, int(g["q"]) * int(g["n_test"]))
+    # the slope of every outcome is covered by its combined 95 % interval (truth recovery)
+    q = int(g["q"])
+    for a in range(q):
+        j = 2 * a + 1
+        assert g["result"][4, j] <= g["beta_true"][j] <= g["result"][194, j], (a, g["result"][[4, 194], j])
+
+
+# ------------------------------------------------------------------ GPU
+_cache = {}
+
+
+def _device_replicates(mk, case):
+    if case in _cache:
+        return _cache[case]
+    g = _load(case)
+    subs = _subsets(g)
+    K, q = int(g["K"]), int(g["q"])
+    cfg = mk.SamplerConfig(q, 2 * q, g["beta_starting"], g["beta_tuning"],
+                           cov_model="matern" if int(g["cov_model"]) == 1 else "exponential",
+                           n_batch=int(g["n_batch"]), batch_length=int(g["batch_length"]), seed=int(g["seed"]))
+    with mk.Session(subs * R_REP, cfg, coords_test=g["coords_test"]) as ses:
+        ses.run(cfg.n_samples)
+        out = ses.outputs(samples=True)
+    res = np.stack([mk.combine(out["parameters"][r * K:(r + 1) * K]) for r in range(R_REP)])
+    res2 = np.stack([mk.combine(out["w_predict"][r * K:(r + 1) * K]) for r in range(R_REP)])
+    _cache[case] = (g, out, res, res2)
+    return _cache[case]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", CASES)
+def test_replica0_replays_oracle(mk, case):
+    g, out, res, res2 = _device_replicates(mk, case)
+    for s in range(int(g["K"])):
+        np.testing.assert_allclose(out["samples"][s], g["samples"][s], rtol=0, atol=1e-6)
+        np.testing.assert_allclose(out["parameters"][s], g["param_q"][s], rtol=0, atol=1e-6)
+        np.testing.assert_allclose(out["w_predict"][s][list(LEVELS3)], g["w_q3"][s], rtol=0, atol=1e-6)
+    np.testing.assert_allclose(res[0], g["result"], rtol=0, atol=1e-6)
+    np.testing.assert_allclose(res2[0], g["result2"], rtol=0, atol=1e-6)
+
+
+def _z(oracle, reps):
+    m = reps.mean(axis=0)
+    sd = reps.std(axis=0, ddof=1) * np.sqrt(1.0 + 1.0 / reps.shape[0])
+    return (oracle - m) / np.where(sd > 0, sd, np.inf)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", CASES)
+def test_oracle_within_mc_error_of_device(mk, case):
+    g, _, res, res2 = _device_replicates(mk, case)
+    L = list(LEVELS3)
+    zp = _z(g["result"][L], res[1:, L])                 # 3 levels x P parameters
+    assert np.all(np.abs(zp) <= 4.0), zp
+    zw = _z(g["result2"][L], res2[1:, L])               # 3 levels x q n_test columns
+    assert np.mean(np.abs(zw) > 3.0) <= 0.02, np.mean(np.abs(zw) > 3.0)
+    assert 0.5 <= np.mean(zw ** 2) <= 2.0, np.mean(zw ** 2)
