@@ -354,6 +354,8 @@ struct mk_session {
   bool sweep_split = false;
   bool sweep_step = false;        // one launch per block (k_sweep_step); else two (MK_SWEEP=4)
   bool sweep_rows = false;        // one-workgroup sweep with rows owned by waves (k_sweep_rows, MK_SWEEP=5)
+  int sweep_site = 0;             // one-pass site sweep (k_sweep_site, default for q <= 2): row pairs per thread (0: off)
+  size_t sweep_site_lds = 0;
   double* sp_part = nullptr;
   double* sp_dacc = nullptr;
   int* sp_any = nullptr;
@@ -754,10 +756,12 @@ static void launch_trinv(mk_session* s, Group& g, int max_entries, const int* li
 static void launch_inverse(mk_session* s, Group& g, bool from_zc = false) {
   const int nt = s->nt, max_entries = g.S * s->q;
   launch_trinv(s, g, max_entries, g.d_list, g.d_count);
-  timed(s, g.stream, KS_LAUUM, 0.0, [&] {
-    MK_LAUNCH(k_qblocks, dim3(xcd_grid_h(max_entries, nt * 2)), dim3(256), LDS_64, g.stream, g.ms, g.md.n_s,
-                       g.d_list, g.d_count);
-  });
+  // the diagonal tiles of R^-1 feed the 64-site-block sweeps only; the site sweep reads W alone
+  if (!s->sweep_site)
+    timed(s, g.stream, KS_LAUUM, 0.0, [&] {
+      MK_LAUNCH(k_qblocks, dim3(xcd_grid_h(max_entries, nt * 2)), dim3(256), LDS_64, g.stream, g.ms, g.md.n_s,
+                g.d_list, g.d_count);
+    });
   MK_LAUNCH(k_take_border, dim3(max_entries * ((s->n_pad + 255) / 256)), dim3(256), 0, g.stream, g.md, g.ms,
                      g.d_list, g.d_count, from_zc ? (const double*)g.md.zc : nullptr);
 }
@@ -856,6 +860,17 @@ static void launch_sweep(mk_session* s, Group& g, int it) {
         return;
       }
     }
+    return;
+  }
+  if (s->sweep_site) {
+    Model md = g.md;
+    MatSet ms = g.ms;
+    int iter = it;
+    void* args[] = {&md, &ms, &iter};
+    const hipError_t e = hipLaunchKernel(sweep_site_kernel(q, s->sweep_site), dim3(g.S), dim3(MK_SW_T), args,
+                                         s->sweep_site_lds, g.stream);
+    wd_trace(g.stream, "k_sweep_site");
+    if (e != hipSuccess && s->launch_err == hipSuccess) s->launch_err = e;
     return;
   }
   if (use_sweep_mg(s)) {
@@ -1521,6 +1536,16 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
     s->sweep_step = s->sweep_split && mode != 4 && nt <= 32;   // k_sweep_step sums <= 32 tile partials
     s->sweep_mg = !s->sweep_split && fits && mode == 2;
     s->sweep_rows = mode == 5 && q <= 3 && nt <= 32;
+    // MK_SWEEP=6 or the default (0) for q <= 2 where the split-launch sweep is not chosen: the one-pass
+    // site sweep (k_sweep_site; W read once, no Q_BB tiles).  1-5 select the 64-site-block kernels.
+    if ((mode == 0 || mode == 6) && !s->sweep_split && q <= 2 && n_pad <= 2 * 2 * MK_SW_T &&
+        sweep_site_lds_bytes(nmax, q) <= 150 * 1024) {
+      s->sweep_site = n_pad <= 2 * MK_SW_T ? 1 : 2;
+      s->sweep_site_lds = sweep_site_lds_bytes(nmax, q);
+      s->sweep_mg = false;
+      HIPCHK(hipFuncSetAttribute(sweep_site_kernel(q, s->sweep_site), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)s->sweep_site_lds));
+    }
     if (s->sweep_rows)
       HIPCHK(hipFuncSetAttribute(sweep_rows_kernel(q), hipFuncAttributeMaxDynamicSharedMemorySize,
                                  q * (64 * 64 + 2 * 64) * 8 + nt * q * 64 * 8));

@@ -61,6 +61,15 @@ __global__ void k_sweep_rows(Model md, MatSet ms, int iter);
 inline const void* sweep_rows_kernel(int q) {
   return q == 1 ? (const void*)k_sweep_rows<1> : (q == 2 ? (const void*)k_sweep_rows<2> : (const void*)k_sweep_rows<3>);
 }
+template <int Q, int KR>
+__global__ void k_sweep_site(Model md, MatSet ms, int iter);
+// its dynamic LDS: the sites' proposal / likelihood difference / accept draw + the accept flags
+inline size_t sweep_site_lds_bytes(int ns_max, int q) { return (size_t)ns_max * q * 3 * 8 + (size_t)ns_max * 4; }
+// the one-pass site sweep for q <= 2 outcomes and n_pad <= 4096 (kr: row pairs per thread, 1 or 2)
+inline const void* sweep_site_kernel(int q, int kr) {
+  if (q == 1) return kr == 1 ? (const void*)k_sweep_site<1, 1> : (const void*)k_sweep_site<1, 2>;
+  return kr == 1 ? (const void*)k_sweep_site<2, 1> : (const void*)k_sweep_site<2, 2>;
+}
 template <int Q>
 __global__ void k_sweep_step(Model md, MatSet ms, int iter, int B, double* part);
 inline const void* sweep_step_kernel(int q) {

@@ -1236,6 +1236,232 @@ MK_INST_SPLIT(2)
 MK_INST_SPLIT(3)
 MK_INST_SPLIT(4)
 
+// ---------------------------------------------------------------- 5b. one-pass site sweep (default, q <= 2)
+// The single-site w updates of spMvGLM (MK.R:80-84) with every column of W_h = L_h^-1 read from HBM
+// exactly once per sweep.  One 1024-thread workgroup per subset; thread t owns the row pairs
+// 2t + 2048k (k < KR) of every z_h and keeps them in registers for the whole sweep; the W columns
+// stream through a register ring D sites ahead of use.  Site i, outcomes a = 0 .. q-1 in order:
+//   every wave: p_h = sum over its rows of W_h[r,i] z_h[r] and s_h = sum of W_h[r,i]^2 (rows
+//     i <= r < n_s; one DPP tree each) into LDS slot [i & 1][value][wave], then one s_barrier --
+//     LDS writes drained (lgkmcnt) but no wait on the W loads in flight;
+//   every wave: g_h = the 16 wave partials summed by a 16-lane DPP row tree (the same order in
+//     every wave, so the same bits) and Q_ii,h = (R_h^-1)_ii the same way from s_h; the site's q MH
+//     steps, computed redundantly by every wave with identical decisions (accept iff
+//     log U <= dll - (d c + 0.5 d^2 dd), c = sum_h A^-1_ha g_h, dd = sum_h (A^-1_ha)^2 Q_ii,h), the
+//     carry to the site's next outcome g_h += coef_h Q_ii,h, and on acceptance
+//     z_h += coef_h W_h[:,i] from the registers that held the column (coef_h = d A^-1_ha).
+// Against the 64-site-block kernels (k_sweep and its multi-workgroup forms): one W pass instead of
+// two, no Q_BB tiles (k_qblocks is not launched for sessions on this kernel), one barrier per site.
+// The arithmetic is the same chain; the dot products' summation order differs (rounding only).
+// The loop body holds no memory-dependent control flow, so the W ring's loads stay in flight
+// across steps (the compiler's wait counts are exact): the column loads are buffer loads whose
+// skipped row pairs (the zero upper triangle, the border and padding rows) take an out-of-range
+// offset and return zero without touching memory; the sites' proposals, likelihood differences
+// and accept draws (sweep_precompute) and the accept flags live in LDS.
+#define SS_T 1024
+#define SS_W (SS_T / 64)
+#define SS_OOB 0x7ffffff0u   // buffer offset beyond every W matrix: the load returns zero
+// Sums of the 16-lane rows of a wave, in every lane of the row (quad xor 1, quad xor 2, half-row
+// mirror, row mirror: the first four steps of wave_sum_dpp).
+__device__ inline double row_sum_dpp(double x) {
+  x += dpp_f64<0xB1>(x);
+  x += dpp_f64<0x4E>(x);
+  x += dpp_f64<0x141>(x);
+  x += dpp_f64<0x140>(x);
+  return x;
+}
+__device__ inline double rfl_f64(double v) {   // a wave-uniform VGPR value as a scalar
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readfirstlane((int)(b & 0xffffffffll));
+  const int hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+// A compiler-only fence: keeps LDS accesses on their side of s_barrier without the hardware
+// waits of a release fence (which would drain the W loads in flight).
+#define SS_CFENCE() asm volatile("" ::: "memory")
+
+// Dynamic LDS (sweep_site_lds_bytes): site data [3][n_s q] (proposal, likelihood difference, log
+// accept draw) + accept flags [n_s] (bit a: outcome a).
+
+template <int Q, int KR>
+__global__ __launch_bounds__(SS_T) void k_sweep_site(Model md, MatSet ms, int iter) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  constexpr int q = Q, D = 16 / (Q * Q * KR), NV = 2 * Q;   // ring depth: q = 1 16 / KR, q = 2 4 / KR (VGPRs)
+  static_assert(NV <= 4, "the row-sum exchange carries at most four values");
+  __shared__ double part[2][NV][SS_W];
+  __shared__ double Ai_s[MK_QMAX * MK_QMAX];
+  const int s = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int ns = md.n_s[s];
+  const int nq = ns * q;
+  const long ld = ms.ld;
+  double* sd_dl = smem;
+  double* sd_dll = smem + nq;
+  double* sd_lgu = smem + 2 * nq;
+  int* sflag = reinterpret_cast<int*>(smem + 3 * nq);
+  double* z = md.z + (long)s * q * md.n_pad;
+  if (tid < q * q) Ai_s[tid] = md.Ainv[(long)s * q * q + tid];
+  {   // the sites' data into LDS (sweep_precompute's values; the proposals also to sw_delta for sweep_apply)
+    const Key key = subset_key(md, s);
+    const double* y = md.y + (long)s * md.Np;
+    const double* wt = md.wt + (long)s * md.Np;
+    const double* eta = md.eta + (long)s * md.Np;
+    const double* tune = md.tune + (long)s * md.n_mh_max + md.o_w;
+    double* gdl = md.sw_delta + (long)s * md.Np;
+    for (int k = tid; k < nq; k += SS_T) {
+      const int j = md.o_w + k;
+      const double d = exp(tune[k]) * proposal_normal(key, j, iter);
+      sd_dl[k] = d;
+      gdl[k] = d;
+      sd_dll[k] = loglik_term(y[k], wt[k], eta[k] + d, md.link) - loglik_term(y[k], wt[k], eta[k], md.link);
+      sd_lgu[k] = accept_log_uniform(key, j, iter);
+    }
+    for (int k = tid; k < ns; k += SS_T) sflag[k] = 0;
+  }
+  __syncthreads();
+  double ai[Q * Q];
+#pragma unroll
+  for (int e = 0; e < Q * Q; ++e) ai[e] = Ai_s[e];
+  d2 zr[KR][Q];
+#pragma unroll
+  for (int k = 0; k < KR; ++k) {
+    const int r0 = 2 * tid + 2 * SS_T * k;
+#pragma unroll
+    for (int h = 0; h < Q; ++h)
+      zr[k][h] = (r0 < md.n_pad) ? *reinterpret_cast<const d2*>(z + (long)h * md.n_pad + r0) : d2{0.0, 0.0};
+  }
+  __amdgpu_buffer_rsrc_t rs[Q];
+#pragma unroll
+  for (int h = 0; h < Q; ++h)
+    rs[h] = __builtin_amdgcn_make_buffer_rsrc((void*)(ms.W + ((long)s * q + h) * (ld * ld)), (short)0,
+                                              (int)(ld * ld * 8), 0x00020000);
+  // column c of every W_h for this thread's rows; pairs wholly outside rows c <= r < n_s (the upper
+  // triangle, the border and padding rows) are not fetched and read as zero.  The rest of the mask
+  // is applied where the column is used (a select right after the load would wait for it).
+  auto load_col = [&](int c, d2 (&w)[KR][Q]) {
+#pragma unroll
+    for (int k = 0; k < KR; ++k) {
+      const int r0 = 2 * tid + 2 * SS_T * k;
+      const bool any = c < ns && r0 + 1 >= c && r0 < ns;
+      const unsigned off = any ? (unsigned)(((long)c * ld + r0) * 8) : SS_OOB;
+#pragma unroll
+      for (int h = 0; h < Q; ++h)
+        w[k][h] = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(rs[h], (int)off, 0, 0));
+    }
+  };
+  d2 wr[D][KR][Q];
+#pragma unroll
+  for (int u = 0; u < D; ++u) load_col(u, wr[u]);
+  for (int i0 = 0; i0 < ns; i0 += D) {
+#pragma unroll
+    for (int u = 0; u < D; ++u) {
+      // Straight-line body (no early exit): every path issues the same loads, so the compiler's
+      // wait counts stay exact across the steps and the loop's back edge.  Steps past the last site
+      // (i >= n_s, in the last round) see an all-zero column and reject.
+      const int i = i0 + u;
+      const bool live = i < ns;
+      const int ic = live ? i : ns - 1;
+      // the site's data (uniform LDS reads, issued ahead of the reductions)
+      double dl_[Q], dll_[Q], lg_[Q];
+#pragma unroll
+      for (int a = 0; a < Q; ++a) {
+        dl_[a] = sd_dl[ic * q + a];
+        dll_[a] = sd_dll[ic * q + a];
+        lg_[a] = live ? sd_lgu[ic * q + a] : __builtin_huge_val();
+      }
+      // ---- column i masked to rows i <= r < n_s; the wave's partial dots and squared norms
+      d2 wc[KR][Q];
+#pragma unroll
+      for (int k = 0; k < KR; ++k) {
+        const int r0 = 2 * tid + 2 * SS_T * k;
+#pragma unroll
+        for (int h = 0; h < Q; ++h) {
+          wc[k][h].x = (r0 >= i) ? wr[u][k][h].x : 0.0;
+          wc[k][h].y = (r0 + 1 >= i && r0 + 1 < ns) ? wr[u][k][h].y : 0.0;
+        }
+      }
+      double v[NV];
+#pragma unroll
+      for (int h = 0; h < Q; ++h) {
+        double pd = 0.0, sq = 0.0;
+#pragma unroll
+        for (int k = 0; k < KR; ++k) {
+          pd += wc[k][h].x * zr[k][h].x + wc[k][h].y * zr[k][h].y;
+          sq += wc[k][h].x * wc[k][h].x + wc[k][h].y * wc[k][h].y;
+        }
+        v[h] = pd;
+        v[Q + h] = sq;
+      }
+#pragma unroll
+      for (int e = 0; e < NV; ++e) v[e] = wave_sum_dpp(v[e]);
+      SS_CFENCE();
+      if (lane == 0) {
+#pragma unroll
+        for (int e = 0; e < NV; ++e) part[i & 1][e][wv] = v[e];
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      SS_CFENCE();
+      // ---- every wave: the workgroup sums (row e of 16 lanes: value e over the 16 waves)
+      const int e_l = lane >> 4;
+      const double pv = part[i & 1][e_l < NV ? e_l : 0][lane & 15];
+      const double rsum = row_sum_dpp(e_l < NV ? pv : 0.0);
+      double g[Q], qd[Q];
+#pragma unroll
+      for (int h = 0; h < Q; ++h) {
+        g[h] = rlane_u(rsum, 16 * h);
+        qd[h] = rlane_u(rsum, 16 * (Q + h));
+      }
+      // ---- the site's MH steps (outcomes in order) and the z update
+      int fl = 0;
+#pragma unroll
+      for (int a = 0; a < Q; ++a) {
+        const double d = rfl_f64(dl_[a]);
+        double c = ai[a * q] * g[0];
+#pragma unroll
+        for (int h = 1; h < Q; ++h) c += ai[h + a * q] * g[h];
+        double dd = 0.0;
+#pragma unroll
+        for (int h = 0; h < Q; ++h) dd += (ai[h + a * q] * ai[h + a * q]) * qd[h];
+        const double ratio = rfl_f64(dll_[a]) - (d * c + 0.5 * d * d * dd);
+        if (rfl_f64(lg_[a]) <= ratio) {   // uniform
+#pragma unroll
+          for (int h = 0; h < Q; ++h) {
+            const double coef = d * ai[h + a * q];
+            g[h] += coef * qd[h];
+#pragma unroll
+            for (int k = 0; k < KR; ++k) {
+              zr[k][h].x = fma(coef, wc[k][h].x, zr[k][h].x);
+              zr[k][h].y = fma(coef, wc[k][h].y, zr[k][h].y);
+            }
+          }
+          fl |= 1 << a;
+        }
+      }
+      if (tid == 0 && live) sflag[i] = fl;
+      load_col(i + D, wr[u]);   // the ring slot's next column
+    }
+  }
+  // ---- write back own z rows; the accept flags to sw_acc; apply accepted moves
+#pragma unroll
+  for (int k = 0; k < KR; ++k) {
+    const int r0 = 2 * tid + 2 * SS_T * k;
+    if (r0 < md.n_pad) {
+#pragma unroll
+      for (int h = 0; h < Q; ++h) *reinterpret_cast<d2*>(z + (long)h * md.n_pad + r0) = zr[k][h];
+    }
+  }
+  __syncthreads();
+  int* sacc = md.sw_acc + (long)s * md.Np;
+  for (int k = tid; k < nq; k += SS_T) sacc[k] = (sflag[k / q] >> (k % q)) & 1;
+  __syncthreads();
+  sweep_apply(md, s, 0, ns, Ai_s, tid, SS_T);
+}
+template __global__ void k_sweep_site<1, 1>(Model, MatSet, int);
+template __global__ void k_sweep_site<1, 2>(Model, MatSet, int);
+template __global__ void k_sweep_site<2, 1>(Model, MatSet, int);
+template __global__ void k_sweep_site<2, 2>(Model, MatSet, int);
+
 // ---------------------------------------------------------------- 6. record / adapt
 __global__ __launch_bounds__(64) void k_record(Model md, int iter) {
   const int s = blockIdx.x * 64 + threadIdx.x;

@@ -62,14 +62,38 @@ struct Rccl {
   const char* (*error_string)(ncclResult_t) = nullptr;
 };
 
+// RCCL must run on the HIP runtime libmk runs on.  A process can hold two: a host that loads torch
+// after libmk (torch's CPU ops, e.g. the synthetic generator) maps torch's bundled libamdhip64 and
+// librccl beside the system's, and a dlopen("librccl.so.1") by soname then returns torch's RCCL,
+// bound to the second runtime -- which reported "no ROCm-capable device is detected" from
+// ncclCommInitAll (the round-3 "unhandled cuda error", reproduced in round 4 by the GPU suite).  So
+// the library is opened by path from the directory of the libamdhip64 libmk is bound to (dladdr).
+std::string hip_runtime_dir() {
+  Dl_info info{};
+  if (dladdr((const void*)&hipGetDeviceCount, &info) && info.dli_fname) {
+    std::string f = info.dli_fname;
+    const size_t slash = f.rfind('/');
+    if (slash != std::string::npos) return f.substr(0, slash);
+  }
+  return "";
+}
+
 const Rccl& rccl() {
   static const Rccl r = [] {
     Rccl x;
-    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
-    if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL);
+    const std::string dir = hip_runtime_dir();
+    void* h = nullptr;
+    std::string tried;
+    for (const char* name : {"librccl.so.1", "librccl.so"}) {
+      if (h || dir.empty()) break;
+      const std::string path = dir + "/" + name;
+      tried += path + " ";
+      h = dlopen(path.c_str(), RTLD_NOW | RTLD_LOCAL);
+    }
+    if (!h && dir.empty()) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);   // no path known: by soname
     if (!h) {
       const char* e = dlerror();
-      x.why = std::string("librccl not loadable: ") + (e ? e : "?");
+      x.why = std::string("librccl not loadable beside libmk's HIP runtime (") + tried + "): " + (e ? e : "?");
       return x;
     }
     x.comm_init_all = (decltype(x.comm_init_all))dlsym(h, "ncclCommInitAll");

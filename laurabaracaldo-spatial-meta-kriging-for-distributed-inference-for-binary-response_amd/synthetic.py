@@ -56,25 +56,33 @@ def _exact_field(coords, A, phi, nu, cov_model, rng):
 def _rff_field(coords, A, phi, nu, cov_model, rng, M=4096, chunk=8192):
     """Random Fourier features: exponential -> omega = phi*z/sqrt(u), u~chi2_1 (Cauchy-type);
     Matern -> multivariate-t(2 nu) frequencies scaled by phi.  M = 4096 features (SURVEY.md 8d);
-    the n x M cosines (2e9 at configs[2]) run as multithreaded torch CPU ops in row chunks."""
-    import torch
+    the n x M cosines (2e9 at configs[2]) in row chunks with NumPy.  (Not torch: a host that loads
+    torch after libmk maps torch's bundled HIP runtime beside libmk's -- two HIP runtimes in one
+    process)"""
+    import os
+    from concurrent.futures import ThreadPoolExecutor
     n = coords.shape[0]
     q = A.shape[0]
     W = np.zeros((n, q))
-    for h in range(q):
-        z = rng.standard_normal((M, 2))
-        dof = 1.0 if cov_model == 0 else 2.0 * nu
-        u = rng.chisquare(dof, size=M) / dof
-        omega = phi * z / np.sqrt(u)[:, None]
-        b = rng.uniform(0, 2 * np.pi, size=M)
-        c = rng.standard_normal(M)
-        om_t = torch.from_numpy(np.ascontiguousarray(omega.T))
-        b_t, c_t = torch.from_numpy(b), torch.from_numpy(c)
-        for s in range(0, n, chunk):
-            proj = torch.from_numpy(np.ascontiguousarray(coords[s:s + chunk])) @ om_t
-            proj += b_t
-            torch.cos_(proj)
-            W[s:s + chunk, h] = np.sqrt(2.0 / M) * (proj @ c_t).numpy()
+    n_thr = max(1, min(16, os.cpu_count() or 1, (n + chunk - 1) // chunk))
+
+    def rows(s, om_t, b, c, h):     # NumPy releases the GIL in matmul / cos: chunks run in parallel
+        m = min(chunk, n - s)
+        p_ = coords[s:s + m] @ om_t
+        p_ += b
+        np.cos(p_, out=p_)
+        W[s:s + m, h] = np.sqrt(2.0 / M) * (p_ @ c)
+
+    with ThreadPoolExecutor(n_thr) as ex:
+        for h in range(q):
+            z = rng.standard_normal((M, 2))
+            dof = 1.0 if cov_model == 0 else 2.0 * nu
+            u = rng.chisquare(dof, size=M) / dof
+            omega = phi * z / np.sqrt(u)[:, None]
+            b = rng.uniform(0, 2 * np.pi, size=M)
+            c = rng.standard_normal(M)
+            om_t = np.ascontiguousarray(omega.T)
+            list(ex.map(lambda s: rows(s, om_t, b, c, h), range(0, n, chunk)))
     return W @ A.T
 
 

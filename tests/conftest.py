@@ -51,10 +51,3 @@ def _dump_stacks_if_hung(request):
 def mk():
     return importlib.import_module(PKG)
 
-
-def gpu_available():
-    try:
-        import torch
-        return torch.cuda.is_available()
-    except Exception:
-        return False
