@@ -19,6 +19,7 @@ def test_fused_dpp_fmacs_have_their_wait_states(tmp_path):
     out = tmp_path / "linalg.s"
     subprocess.check_call([hipcc, "-w", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
                            "--cuda-device-only", "-S", os.path.join(CSRC, "mk_linalg.hip"), "-o", str(out)])
-    n, bad = dpp_hazards.check(out.read_text())
+    n, n_dpp, bad = dpp_hazards.check(out.read_text())
     assert n >= 150, n          # 120 factor updates + 36 inverse updates (four row groups) per pivot block
+    assert n_dpp > n            # the compiler's own DPP moves (wave reductions) are checked too
     assert not bad, bad[:3]
