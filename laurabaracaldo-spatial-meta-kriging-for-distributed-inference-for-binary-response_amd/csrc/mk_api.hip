@@ -125,6 +125,7 @@ struct Group {
   int* d_pcount = nullptr;
   hipEvent_t done = nullptr;         // fork-join sweep: this group's pre-sweep work is queued
   hipStream_t bulk = nullptr;        // split Cholesky (launch_cholesky): CU-masked bulk-update stream
+  hipStream_t near = nullptr;        // chain split (MK_CHOL_CHAIN): off-diagonal correction + trsm stream
   std::vector<hipEvent_t> ev;        // 2 nt + 1 events reused every factorisation
 };
 
@@ -670,6 +671,58 @@ static void launch_cholesky(mk_session* s, Group& g, int h0, int hc, const int* 
     hipEventRecord(g.ev[2 * nt], A);             // the candidates are on A
     hipStreamWaitEvent(B, g.ev[2 * nt], 0);
   }
+  if (g.near) {
+    // Chain split: only the diagonal tiles' dependency chain stays on the critical stream, as
+    // launches of one tile per matrix (S q workgroups: they fit the CUs the other streams' masks
+    // leave), the rest of each column's correction and trsm runs one column behind on `near`:
+    //   A (critical): [eU(k)] U(k; tile k; panels k-d..k-1), D(k) -> eD(k), [eUo(k)] T(k; tile k+1) -> eTn(k)
+    //   N (near):     [eU(k), eTn(k-1)] U(k; tiles > k; panels k-d..k-1) -> eUo(k),
+    //                 [eD(k)] T(k; tiles > k+1), [eTn(k)] -> eTr(k) = panel k final (evP(k))
+    //   B (bulk):     [eTr(k)] U(k+d+1; panels < k+1) -> eU(k+d+1)
+    // The critical chain per column is a one-tile correction, the diagonal factor and a one-tile
+    // trsm; the wide launches overlap it.  Every tile sees the same panels in the same order and
+    // chunking as in the other schedules (same bits).
+    hipStream_t N = g.near;
+    hipEvent_t* eD = g.ev.data() + 2 * nt + 1;
+    hipEvent_t* eTn = eD + nt;
+    hipEvent_t* eUo = eTn + nt;
+    hipEvent_t* eTr = eUo + nt;
+    if (k_lo == 0) hipStreamWaitEvent(N, g.ev[2 * nt], 0);   // the candidates are on A
+    for (int k = k_lo; k < k_hi; ++k) {
+      const int j0 = std::max(0, k - d);
+      if (k >= 1 && k + 1 < nt) {   // near: the off-diagonal tiles' correction of column k
+        if (k > d) hipStreamWaitEvent(N, eU[k], 0);
+        hipStreamWaitEvent(N, eTn[k - 1], 0);
+        chol_update(s, g, N, h0, hc, k, k + 1, nt, j0, k, nullptr, nullptr, panel_flops(s, g, hc, k, k + 1, nt, false, j0, k));
+        hipEventRecord(eUo[k], N);
+      }
+      if (k > d) hipStreamWaitEvent(A, eU[k], 0);
+      if (k >= 1)
+        chol_update(s, g, A, h0, hc, k, k, k + 1, j0, k, nullptr, nullptr, panel_flops(s, g, hc, k, k, k + 1, false, j0, k));
+      chol_diag(s, g, A, h0, hc, k, nullptr, nullptr);
+      if (k == nt - 1) {
+        if (evP) hipEventRecord(evP[k], A);
+        break;
+      }
+      hipEventRecord(eD[k], A);
+      if (k >= 1) hipStreamWaitEvent(A, eUo[k], 0);
+      chol_trsm(s, g, A, h0, hc, k, k + 1, k + 2, nullptr, nullptr, panel_flops(s, g, hc, k, k + 1, k + 2, true));
+      hipEventRecord(eTn[k], A);
+      hipStreamWaitEvent(N, eD[k], 0);
+      if (k + 2 < nt)
+        chol_trsm(s, g, N, h0, hc, k, k + 2, nt, nullptr, nullptr, panel_flops(s, g, hc, k, k + 2, nt, true));
+      hipStreamWaitEvent(N, eTn[k], 0);
+      hipEventRecord(eTr[k], N);
+      if (evP) hipEventRecord(evP[k], N);
+      if (k + d + 1 < nt) {
+        const int c = k + d + 1;
+        hipStreamWaitEvent(B, eTr[k], 0);
+        chol_update(s, g, B, h0, hc, c, c, nt, 0, c - d, nullptr, nullptr, panel_flops(s, g, hc, c, c, nt, false, 0, c - d));
+        hipEventRecord(eU[c], B);
+      }
+    }
+    return;
+  }
   static const int fine_env = tile_env("MK_CHOL_FINE", 0);
   if (fine_env) {
     // Fine split: the critical stream keeps only the diagonal tile's correction, the diagonal
@@ -1163,7 +1216,19 @@ static int setup_groups(mk_session* s, int n_groups) {
     Group& g = s->groups[0];
     if (pool_stream(s->owned, &g.bulk, s->device, SK_CUMASK, 0, mask) != hipSuccess)
       return set_err(MK_E_HIP, "bulk stream");
-    g.ev.assign(3 * s->nt + 1, nullptr);
+    // MK_CHOL_CHAIN=1: the chain split's near stream (1: high priority, all CUs; 2: the bulk mask)
+    static const int chain_env = tile_env("MK_CHOL_CHAIN", 0);
+    if (chain_env == 1) {
+      int lo = 0, hi = 0;
+      if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
+          pool_stream(s->owned, &g.near, s->device, SK_PRIO, hi) != hipSuccess)
+        return set_err(MK_E_HIP, "near stream");
+    } else if (chain_env == 2) {
+      if (pool_stream(s->owned, &g.near, s->device, SK_CUMASK, 0, mask) != hipSuccess)
+        return set_err(MK_E_HIP, "near stream");
+      // a second stream with the same mask: the pool hands out distinct streams per session
+    }
+    g.ev.assign(6 * s->nt + 2, nullptr);
     for (auto& e : g.ev)
       if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return set_err(MK_E_HIP, "cholesky event");
   }

@@ -187,3 +187,31 @@ def test_site_sweep_runs_the_block_sweeps_chain(tmp_path):
             res[sweep] = {k: z[k] for k in z.files}
         for k in res["1"]:
             np.testing.assert_allclose(res["6"][k], res["1"][k], rtol=0, atol=1e-9, err_msg=f"{k} la={la}")
+
+
+def test_chain_split_cholesky_is_bit_identical(tmp_path):
+    """The chain split (MK_CHOL_CHAIN: the diagonal tiles' correction, factor and next-tile trsm on the
+    critical stream, the other tiles' correction and trsm on a near stream one column behind, the
+    early panels on the bulk stream) gives the sequential factorisation's bits: every tile sees the
+    same panels in the same order and chunking.  Both near-stream kinds (1: high priority; 2: the bulk
+    stream's CU mask), both launch schedules, depths 1-3."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    runs = {}
+    for name, env in (("ref1", dict(MK_CHOL_SPLIT="0")), ("ref0", dict(MK_CHOL_SPLIT="0", MK_LOOKAHEAD="0")),
+                      ("c1", dict(MK_CHOL_SPLIT="1", MK_CHOL_CHAIN="1")),
+                      ("c2", dict(MK_CHOL_SPLIT="1", MK_CHOL_CHAIN="2", MK_CHOL_DEPTH="3")),
+                      ("c1d1", dict(MK_CHOL_SPLIT="1", MK_CHOL_CHAIN="1", MK_CHOL_DEPTH="1", MK_LOOKAHEAD="0")),
+                      ("c2s", dict(MK_CHOL_SPLIT="1", MK_CHOL_CHAIN="2", MK_LOOKAHEAD="0"))):
+        path = str(tmp_path / f"{name}.npz")
+        r = subprocess.run([sys.executable, os.path.join(here, "gpu_tile_run.py"), path], capture_output=True,
+                           text=True, timeout=240, env=dict(os.environ, MK_SWEEP="1", MK_TILE="128", **env))
+        assert r.returncode == 0, r.stderr[-4000:]
+        z = np.load(path)
+        runs[name] = {k: z[k] for k in z.files}
+    for name in ("c1", "c2", "c1d1", "c2s"):   # the two schedules agree to rounding: each against its own
+        got, ref = runs[name], runs["ref0" if name in ("c1d1", "c2s") else "ref1"]
+        for k in ref:
+            assert np.array_equal(got[k], ref[k]), (name, k)
