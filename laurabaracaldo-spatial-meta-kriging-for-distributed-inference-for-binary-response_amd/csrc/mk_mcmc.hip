@@ -1287,7 +1287,7 @@ typedef unsigned int u4v __attribute__((ext_vector_type(4)));
 template <int Q, int KR>
 __global__ __launch_bounds__(SS_T) void k_sweep_site(Model md, MatSet ms, int iter) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  constexpr int q = Q, D = 16 / (Q * Q * KR), NV = 2 * Q;   // ring depth: q = 1 16 / KR, q = 2 4 / KR (VGPRs)
+  constexpr int q = Q, H = (8 / (Q * Q * KR)) > 0 ? 8 / (Q * Q * KR) : 1, NV = 2 * Q;   // ring: 2H columns (VGPRs)
   static_assert(NV <= 4, "the row-sum exchange carries at most four values");
   __shared__ double part[2][NV][SS_W];
   __shared__ double Ai_s[MK_QMAX * MK_QMAX];
@@ -1349,98 +1349,108 @@ __global__ __launch_bounds__(SS_T) void k_sweep_site(Model md, MatSet ms, int it
         w[k][h] = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(rs[h], (int)off, 0, 0));
     }
   };
-  d2 wr[D][KR][Q];
+  // The ring in two halves of H columns, used and refilled in turn: while the sites of one half
+  // run, the other half's columns are in flight (issued H sites earlier).  A loop iteration holds
+  // both halves, so at its back edge only the half issued H sites ago is outstanding -- the wait
+  // the compiler places at the loop head (it does not track loads across the back edge) finds
+  // them arrived instead of stalling on a column issued one site earlier.
+  auto step = [&](const int i, d2 (&w)[KR][Q]) {
+    // Straight-line body (no early exit): every path issues the same loads, so the compiler's
+    // wait counts stay exact across the steps and the loop's back edge.  Steps past the last site
+    // (i >= n_s, in the last round) see an all-zero column and reject.
+    const bool live = i < ns;
+    const int ic = live ? i : ns - 1;
+    // the site's data (uniform LDS reads, issued ahead of the reductions)
+    double dl_[Q], dll_[Q], lg_[Q];
 #pragma unroll
-  for (int u = 0; u < D; ++u) load_col(u, wr[u]);
-  for (int i0 = 0; i0 < ns; i0 += D) {
+    for (int a = 0; a < Q; ++a) {
+      dl_[a] = sd_dl[ic * q + a];
+      dll_[a] = sd_dll[ic * q + a];
+      lg_[a] = live ? sd_lgu[ic * q + a] : __builtin_huge_val();
+    }
+    // ---- column i masked to rows i <= r < n_s; the wave's partial dots and squared norms
+    d2 wc[KR][Q];
 #pragma unroll
-    for (int u = 0; u < D; ++u) {
-      // Straight-line body (no early exit): every path issues the same loads, so the compiler's
-      // wait counts stay exact across the steps and the loop's back edge.  Steps past the last site
-      // (i >= n_s, in the last round) see an all-zero column and reject.
-      const int i = i0 + u;
-      const bool live = i < ns;
-      const int ic = live ? i : ns - 1;
-      // the site's data (uniform LDS reads, issued ahead of the reductions)
-      double dl_[Q], dll_[Q], lg_[Q];
+    for (int k = 0; k < KR; ++k) {
+      const int r0 = 2 * tid + 2 * SS_T * k;
 #pragma unroll
-      for (int a = 0; a < Q; ++a) {
-        dl_[a] = sd_dl[ic * q + a];
-        dll_[a] = sd_dll[ic * q + a];
-        lg_[a] = live ? sd_lgu[ic * q + a] : __builtin_huge_val();
+      for (int h = 0; h < Q; ++h) {
+        wc[k][h].x = (r0 >= i) ? w[k][h].x : 0.0;
+        wc[k][h].y = (r0 + 1 >= i && r0 + 1 < ns) ? w[k][h].y : 0.0;
       }
-      // ---- column i masked to rows i <= r < n_s; the wave's partial dots and squared norms
-      d2 wc[KR][Q];
+    }
+    double v[NV];
+#pragma unroll
+    for (int h = 0; h < Q; ++h) {
+      double pd = 0.0, sq = 0.0;
 #pragma unroll
       for (int k = 0; k < KR; ++k) {
-        const int r0 = 2 * tid + 2 * SS_T * k;
+        pd += wc[k][h].x * zr[k][h].x + wc[k][h].y * zr[k][h].y;
+        sq += wc[k][h].x * wc[k][h].x + wc[k][h].y * wc[k][h].y;
+      }
+      v[h] = pd;
+      v[Q + h] = sq;
+    }
+#pragma unroll
+    for (int e = 0; e < NV; ++e) v[e] = wave_sum_dpp(v[e]);
+    SS_CFENCE();
+    if (lane == 0) {
+#pragma unroll
+      for (int e = 0; e < NV; ++e) part[i & 1][e][wv] = v[e];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    SS_CFENCE();
+    // ---- every wave: the workgroup sums (row e of 16 lanes: value e over the 16 waves)
+    const int e_l = lane >> 4;
+    const double pv = part[i & 1][e_l < NV ? e_l : 0][lane & 15];
+    const double rsum = row_sum_dpp(e_l < NV ? pv : 0.0);
+    double g[Q], qd[Q];
+#pragma unroll
+    for (int h = 0; h < Q; ++h) {
+      g[h] = rlane_u(rsum, 16 * h);
+      qd[h] = rlane_u(rsum, 16 * (Q + h));
+    }
+    // ---- the site's MH steps (outcomes in order) and the z update
+    int fl = 0;
+#pragma unroll
+    for (int a = 0; a < Q; ++a) {
+      const double d = rfl_f64(dl_[a]);
+      double c = ai[a * q] * g[0];
+#pragma unroll
+      for (int h = 1; h < Q; ++h) c += ai[h + a * q] * g[h];
+      double dd = 0.0;
+#pragma unroll
+      for (int h = 0; h < Q; ++h) dd += (ai[h + a * q] * ai[h + a * q]) * qd[h];
+      const double ratio = rfl_f64(dll_[a]) - (d * c + 0.5 * d * d * dd);
+      if (rfl_f64(lg_[a]) <= ratio) {   // uniform
 #pragma unroll
         for (int h = 0; h < Q; ++h) {
-          wc[k][h].x = (r0 >= i) ? wr[u][k][h].x : 0.0;
-          wc[k][h].y = (r0 + 1 >= i && r0 + 1 < ns) ? wr[u][k][h].y : 0.0;
-        }
-      }
-      double v[NV];
+          const double coef = d * ai[h + a * q];
+          g[h] += coef * qd[h];
 #pragma unroll
-      for (int h = 0; h < Q; ++h) {
-        double pd = 0.0, sq = 0.0;
-#pragma unroll
-        for (int k = 0; k < KR; ++k) {
-          pd += wc[k][h].x * zr[k][h].x + wc[k][h].y * zr[k][h].y;
-          sq += wc[k][h].x * wc[k][h].x + wc[k][h].y * wc[k][h].y;
-        }
-        v[h] = pd;
-        v[Q + h] = sq;
-      }
-#pragma unroll
-      for (int e = 0; e < NV; ++e) v[e] = wave_sum_dpp(v[e]);
-      SS_CFENCE();
-      if (lane == 0) {
-#pragma unroll
-        for (int e = 0; e < NV; ++e) part[i & 1][e][wv] = v[e];
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      SS_CFENCE();
-      // ---- every wave: the workgroup sums (row e of 16 lanes: value e over the 16 waves)
-      const int e_l = lane >> 4;
-      const double pv = part[i & 1][e_l < NV ? e_l : 0][lane & 15];
-      const double rsum = row_sum_dpp(e_l < NV ? pv : 0.0);
-      double g[Q], qd[Q];
-#pragma unroll
-      for (int h = 0; h < Q; ++h) {
-        g[h] = rlane_u(rsum, 16 * h);
-        qd[h] = rlane_u(rsum, 16 * (Q + h));
-      }
-      // ---- the site's MH steps (outcomes in order) and the z update
-      int fl = 0;
-#pragma unroll
-      for (int a = 0; a < Q; ++a) {
-        const double d = rfl_f64(dl_[a]);
-        double c = ai[a * q] * g[0];
-#pragma unroll
-        for (int h = 1; h < Q; ++h) c += ai[h + a * q] * g[h];
-        double dd = 0.0;
-#pragma unroll
-        for (int h = 0; h < Q; ++h) dd += (ai[h + a * q] * ai[h + a * q]) * qd[h];
-        const double ratio = rfl_f64(dll_[a]) - (d * c + 0.5 * d * d * dd);
-        if (rfl_f64(lg_[a]) <= ratio) {   // uniform
-#pragma unroll
-          for (int h = 0; h < Q; ++h) {
-            const double coef = d * ai[h + a * q];
-            g[h] += coef * qd[h];
-#pragma unroll
-            for (int k = 0; k < KR; ++k) {
-              zr[k][h].x = fma(coef, wc[k][h].x, zr[k][h].x);
-              zr[k][h].y = fma(coef, wc[k][h].y, zr[k][h].y);
-            }
+          for (int k = 0; k < KR; ++k) {
+            zr[k][h].x = fma(coef, wc[k][h].x, zr[k][h].x);
+            zr[k][h].y = fma(coef, wc[k][h].y, zr[k][h].y);
           }
-          fl |= 1 << a;
         }
+        fl |= 1 << a;
       }
-      if (tid == 0 && live) sflag[i] = fl;
-      load_col(i + D, wr[u]);   // the ring slot's next column
     }
+    if (tid == 0 && live) sflag[i] = fl;
+  };
+  d2 wa[H][KR][Q], wb[H][KR][Q];
+#pragma unroll
+  for (int u = 0; u < H; ++u) load_col(u, wa[u]);
+  for (int i0 = 0; i0 < ns; i0 += 2 * H) {
+#pragma unroll
+    for (int u = 0; u < H; ++u) load_col(i0 + H + u, wb[u]);
+#pragma unroll
+    for (int u = 0; u < H; ++u) step(i0 + u, wa[u]);
+#pragma unroll
+    for (int u = 0; u < H; ++u) load_col(i0 + 2 * H + u, wa[u]);
+#pragma unroll
+    for (int u = 0; u < H; ++u) step(i0 + H + u, wb[u]);
   }
   // ---- write back own z rows; the accept flags to sw_acc; apply accepted moves
 #pragma unroll
