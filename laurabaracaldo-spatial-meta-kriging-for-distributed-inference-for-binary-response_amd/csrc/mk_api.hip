@@ -1597,14 +1597,19 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
     // No default path launches a kernel whose workgroups wait on each other: the cooperative kernel
     // (opt-in) was followed by intermittent stalls of the GPU suite -- once more in
     // round 3, on the sequential schedule where it had been the default for <= 64 subsets.
-    s->sweep_split = mode == 3 || mode == 4 || (mode == 0 && q >= 2 && S <= 16);
+    // MK_SWEEP=6 and the default (0): the one-pass site sweep (k_sweep_site; W read once, no Q_BB
+    // tiles, no inter-workgroup waits) wherever it fits: n_pad <= 4096 (q = 4: 2048) and the sites'
+    // data in LDS (configs[3]: n_s = 2,000, q = 3 takes 152 KB).  1-5 select the 64-site-block kernels,
+    // which remain the fallback: split launches (3, 4) for multi-outcome small shards, else one
+    // workgroup per subset.
+    const bool site_fits = sweep_site_kernel(q, n_pad <= 2 * MK_SW_T ? 1 : 2) != nullptr && n_pad <= 4 * MK_SW_T &&
+                           sweep_site_lds_bytes(nmax, q) <= 156 * 1024;
+    const bool site = (mode == 0 || mode == 6) && site_fits;
+    s->sweep_split = mode == 3 || mode == 4 || (mode == 0 && !site && q >= 2 && S <= 16);
     s->sweep_step = s->sweep_split && mode != 4 && nt <= 32;   // k_sweep_step sums <= 32 tile partials
     s->sweep_mg = !s->sweep_split && fits && mode == 2;
     s->sweep_rows = mode == 5 && q <= 3 && nt <= 32;
-    // MK_SWEEP=6 or the default (0) for q <= 2 where the split-launch sweep is not chosen: the one-pass
-    // site sweep (k_sweep_site; W read once, no Q_BB tiles).  1-5 select the 64-site-block kernels.
-    if ((mode == 0 || mode == 6) && !s->sweep_split && q <= 2 && n_pad <= 2 * 2 * MK_SW_T &&
-        sweep_site_lds_bytes(nmax, q) <= 150 * 1024) {
+    if (site) {
       s->sweep_site = n_pad <= 2 * MK_SW_T ? 1 : 2;
       s->sweep_site_lds = sweep_site_lds_bytes(nmax, q);
       s->sweep_mg = false;

@@ -65,10 +65,15 @@ template <int Q, int KR>
 __global__ void k_sweep_site(Model md, MatSet ms, int iter);
 // its dynamic LDS: the sites' proposal / likelihood difference / accept draw + the accept flags
 inline size_t sweep_site_lds_bytes(int ns_max, int q) { return (size_t)ns_max * q * 3 * 8 + (size_t)ns_max * 4; }
-// the one-pass site sweep for q <= 2 outcomes and n_pad <= 4096 (kr: row pairs per thread, 1 or 2)
+// the one-pass site sweep (kr: row pairs per thread, 1 for n_pad <= 2048 or 2 for <= 4096); NULL
+// where its registers would spill (q = 3 with kr = 2, q = 4): the 64-site-block kernels run there
 inline const void* sweep_site_kernel(int q, int kr) {
-  if (q == 1) return kr == 1 ? (const void*)k_sweep_site<1, 1> : (const void*)k_sweep_site<1, 2>;
-  return kr == 1 ? (const void*)k_sweep_site<2, 1> : (const void*)k_sweep_site<2, 2>;
+  switch (q) {
+    case 1: return kr == 1 ? (const void*)k_sweep_site<1, 1> : (const void*)k_sweep_site<1, 2>;
+    case 2: return kr == 1 ? (const void*)k_sweep_site<2, 1> : (const void*)k_sweep_site<2, 2>;
+    case 3: return kr == 1 ? (const void*)k_sweep_site<3, 1> : nullptr;
+    default: return nullptr;
+  }
 }
 template <int Q>
 __global__ void k_sweep_step(Model md, MatSet ms, int iter, int B, double* part);

@@ -1236,7 +1236,7 @@ MK_INST_SPLIT(2)
 MK_INST_SPLIT(3)
 MK_INST_SPLIT(4)
 
-// ---------------------------------------------------------------- 5b. one-pass site sweep (default, q <= 2)
+// ---------------------------------------------------------------- 5b. one-pass site sweep (default)
 // The single-site w updates of spMvGLM (MK.R:80-84) with every column of W_h = L_h^-1 read from HBM
 // exactly once per sweep.  One 1024-thread workgroup per subset; thread t owns the row pairs
 // 2t + 2048k (k < KR) of every z_h and keeps them in registers for the whole sweep; the W columns
@@ -1287,8 +1287,10 @@ typedef unsigned int u4v __attribute__((ext_vector_type(4)));
 template <int Q, int KR>
 __global__ __launch_bounds__(SS_T) void k_sweep_site(Model md, MatSet ms, int iter) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  constexpr int q = Q, H = (8 / (Q * Q * KR)) > 0 ? 8 / (Q * Q * KR) : 1, NV = 2 * Q;   // ring: 2H columns (VGPRs)
-  static_assert(NV <= 4, "the row-sum exchange carries at most four values");
+  // ring: 2H columns (VGPRs: 8 H Q KR); NV values exchanged per site, four per row-sum round
+  constexpr int q = Q, H = Q == 1 ? 8 / KR : (Q == 2 ? 2 / KR : 1), NV = 2 * Q;
+  constexpr int NR = (NV + 3) / 4;
+  static_assert(H >= 1 && NV <= 8, "q <= 4");   // instantiated for q <= 2 and (q = 3, KR = 1): no spills
   __shared__ double part[2][NV][SS_W];
   __shared__ double Ai_s[MK_QMAX * MK_QMAX];
   const int s = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -1402,14 +1404,20 @@ __global__ __launch_bounds__(SS_T) void k_sweep_site(Model md, MatSet ms, int it
     __builtin_amdgcn_s_barrier();
     SS_CFENCE();
     // ---- every wave: the workgroup sums (row e of 16 lanes: value e over the 16 waves)
-    const int e_l = lane >> 4;
-    const double pv = part[i & 1][e_l < NV ? e_l : 0][lane & 15];
-    const double rsum = row_sum_dpp(e_l < NV ? pv : 0.0);
+    double tot[4 * NR];
+#pragma unroll
+    for (int rr = 0; rr < NR; ++rr) {
+      const int e_l = 4 * rr + (lane >> 4);
+      const double pv = part[i & 1][e_l < NV ? e_l : 0][lane & 15];
+      const double rsum = row_sum_dpp(e_l < NV ? pv : 0.0);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) tot[4 * rr + e] = rlane_u(rsum, 16 * e);
+    }
     double g[Q], qd[Q];
 #pragma unroll
     for (int h = 0; h < Q; ++h) {
-      g[h] = rlane_u(rsum, 16 * h);
-      qd[h] = rlane_u(rsum, 16 * (Q + h));
+      g[h] = tot[h];
+      qd[h] = tot[Q + h];
     }
     // ---- the site's MH steps (outcomes in order) and the z update
     int fl = 0;
@@ -1471,6 +1479,7 @@ template __global__ void k_sweep_site<1, 1>(Model, MatSet, int);
 template __global__ void k_sweep_site<1, 2>(Model, MatSet, int);
 template __global__ void k_sweep_site<2, 1>(Model, MatSet, int);
 template __global__ void k_sweep_site<2, 2>(Model, MatSet, int);
+template __global__ void k_sweep_site<3, 1>(Model, MatSet, int);
 
 // ---------------------------------------------------------------- 6. record / adapt
 __global__ __launch_bounds__(64) void k_record(Model md, int iter) {
