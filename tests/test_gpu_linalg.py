@@ -170,7 +170,8 @@ def test_site_sweep_runs_the_block_sweeps_chain(tmp_path):
     the 64-site-block sweep (MK_SWEEP=1, k_sweep) run the same chain: the dot products are summed in
     a different order, so the chains agree to rounding -- identical accept decisions, samples, latent
     w and kriging draws within 1e-9 -- under both launch schedules (q = 1 and q = 2 LMC, ragged
-    subsets, the Matern model; q = 3 keeps the block sweeps)."""
+    subsets, the Matern model).  q = 3 and n_s > 2047 (two row pairs per thread) are covered by the
+    oracle replays of tests/test_gpu_sampler.py, which run the default (site) sweep."""
     import os
     import subprocess
     import sys
