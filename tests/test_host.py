@@ -150,3 +150,29 @@ def test_meta_fit_node_fails_loudly_without_gpu_and_checks_arguments(mk):
         with pytest.raises(mk.MkError) as e:
             mk.meta_fit_node(subs, cfg, coords_test=d["coords_test"], devices=[0, 0])
         assert e.value.code == -4
+
+
+def test_process_hygiene_entry_points_without_gpu(mk):
+    """mk_hip_initialized reports whether HIP already runs without starting it (no /dev/kfd here);
+    mk_shutdown is callable any time (idempotent) and the watchdog switch accepts on/off."""
+    lib = mk.load()
+    assert lib.mk_hip_initialized() == 0
+    lib.mk_shutdown()
+    lib.mk_shutdown()
+    assert lib.mk_set_watchdog(0) == 0
+
+
+def test_synthetic_generator_never_loads_torch():
+    """The random-Fourier-feature field (> 6,000 sites) runs on NumPy: a host that loaded torch after
+    libmk would map torch's own HIP runtime and RCCL beside libmk's."""
+    import subprocess
+    import sys
+    code = ("import sys, importlib; sys.path.insert(0, %r); "
+            "syn = importlib.import_module(%r + '.synthetic'); "
+            "d = syn.generate(7000, q=1, n_test=10); "
+            "assert d['w_true'].shape == (7000,); "
+            "assert 'torch' not in sys.modules, 'torch imported'; print('ok')") % (
+        __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))),
+        "laurabaracaldo-spatial-meta-kriging-for-distributed-inference-for-binary-response_amd")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
