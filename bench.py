@@ -139,16 +139,16 @@ def physical_cores():
     return len(sets) or None
 
 
-def shard_leg(mk, d, idx, S, beta0, bt, adapt_batches, warmup, steps):
-    """The per-GPU share of configs[2] on 8 GPUs (S = 32 of its 250 subsets, global indices 0..S-1)
-    over the same kind of window as the headline: adapt, warm up, then `steps` iterations timed with
-    the same 3:1 burn-in : kept split.  The rate an 8-GPU strong-scaling run's ranks each see."""
+def window_leg(mk, d, idx, S, q, cov, beta0, bt, adapt_batches, warmup, steps):
+    """S subsets (global indices 0..S-1 of the partition idx of data d) over the headline's kind of
+    window: adapt, warm up, then `steps` iterations timed with the 3:1 burn-in : kept split (kriging
+    on the kept ones).  Returns rate, ms per step, schedule and the k_chol_update union rate."""
     A = max(0, adapt_batches) * 50
     W = max(1, warmup) + A
     n_burn = int(round(0.75 * steps))
-    cfg = mk.SamplerConfig(1, 2, beta0, bt, n_batch=(W + steps + 49) // 50, batch_length=50,
+    cfg = mk.SamplerConfig(q, 2 * q, beta0, bt, cov_model=cov, n_batch=(W + steps + 49) // 50, batch_length=50,
                            burn_in=W + n_burn + 1, seed=20250114)
-    subs = [mk.subset_data(d["y"], d["x"], 1.0, d["coords"], 1, idx[i]) for i in range(S)]
+    subs = [mk.subset_data(d["y"], d["x"], 1.0, d["coords"], q, idx[i]) for i in range(S)]
     with mk.Session(subs, cfg, coords_test=d["coords_test"]) as ses:
         ses.run(W)
         ses.profile(True, kinds=[mk.session.KS_CHOL_UPDATE, mk.session.KS_CHOL_UPDATE_SUB])
@@ -159,16 +159,42 @@ def shard_leg(mk, d, idx, S, beta0, bt, adapt_batches, warmup, steps):
         la = ses.lookahead
     tf = st["flops"] / (st["ms"] * 1e-3) / 1e12 if st["ms"] > 0 else 0.0
     return {"value": S * steps / el, "unit": "subset-iters/s", "ms_per_step": el / steps * 1e3,
-            "workload": f"{S} of configs[2]'s subsets (the per-GPU share of K=250 on 8 GPUs), n_s=2000, exponential, "
-                        f"q=1, n_test=1000, window {n_burn} burn-in + {steps - n_burn} kept iterations at "
-                        f"{W + 1}-{W + steps} (after {A} adaptation + {W - A} warmup iterations)",
+            "window": f"{n_burn} burn-in + {steps - n_burn} kept iterations at {W + 1}-{W + steps} (after {A} "
+                      f"adaptation + {W - A} warmup iterations)",
             "schedule": "lookahead" if la else "sequential",
-            # an 8-GPU strong-scaling run: every rank holds <= S (31-32) of the 250 subsets at this chain rate
-            "projected_8gpu_value": 250 * steps / el,
             "roofline": {"kernel": "k_chol_update (union of its launch intervals)", "achieved": tf,
                          "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": tf / FP64_PEAK_TFLOPS,
-                         "note": "update launches share the chip with the main stream (lookahead schedule): "
-                                 "the fraction understates the kernel's own rate"}}
+                         "note": "lookahead schedule: update launches share the chip with the main stream, so "
+                                 "the fraction understates the kernel's own rate" if la else
+                                 "sequential schedule: update launches run alone"}}
+
+
+def shard_leg(mk, d, idx, S, beta0, bt, adapt_batches, warmup, steps):
+    """The per-GPU share of configs[2] on 8 GPUs (S = 32 of its 250 subsets): the rate an 8-GPU
+    strong-scaling run's ranks each see."""
+    r = window_leg(mk, d, idx, S, 1, "exponential", beta0, bt, adapt_batches, warmup, steps)
+    r["workload"] = (f"{S} of configs[2]'s subsets (the per-GPU share of K=250 on 8 GPUs), n_s=2000, exponential, "
+                     f"q=1, n_test=1000, window " + r.pop("window"))
+    # an 8-GPU strong-scaling run: every rank holds <= S (31-32) of the 250 subsets at this chain rate
+    r["projected_8gpu_value"] = 250 * 1e3 / r["ms_per_step"]
+    return r
+
+
+def config_leg(mk, which, adapt_batches, warmup, steps, subsets=None):
+    """configs[1] (Matern, n = 50,000, K = 50 subsets of 1,000) or configs[3] (q = 3 LMC, n = 100,000,
+    K = 50 subsets of 2,000) on one GPU -- all K subsets, or the first `subsets` (configs[3]'s per-GPU
+    share on 8 GPUs is 6-7) -- over the headline's kind of window; data from the SURVEY.md 8d
+    generator, R's partition, glm start values on the full data."""
+    n, K, q, cov = {1: (50_000, 50, 1, "matern"), 3: (100_000, 50, 3, "exponential")}[which]
+    d = mk.synthetic.generate(n, q=q, n_test=1000, cov_model=1 if cov == "matern" else 0, seed=20250114)
+    _, idx = mk.partition(n, K, seed=20250114, method="R")
+    beta0, bt = mk.start_values(d["y"], d["x"], 1.0, q)
+    S = K if subsets is None else min(subsets, K)
+    r = window_leg(mk, d, idx, S, q, cov, beta0, bt, adapt_batches, warmup, steps)
+    r["workload"] = (f"configs[{which}]: n={n}, K={K} subsets of {n // K}, {cov}, q={q}, n_test=1000; "
+                     + (f"all {K} subsets" if S == K else f"the first {S} (the per-GPU share on 8 GPUs)")
+                     + ", window " + r.pop("window"))
+    return r
 
 
 def host_cores():
@@ -357,11 +383,13 @@ def main():
     ses.close()
     legs = {}
     if world == 1 and not a.no_legs:
-        legs["shard32"] = shard_leg(mk, d, idx, min(a.shard_subsets, K), beta0, bt, a.adapt_batches, a.warmup, a.steps)
+        legs["configs[2]_share32"] = shard_leg(mk, d, idx, min(a.shard_subsets, K), beta0, bt, a.adapt_batches, a.warmup, a.steps)
         import bench_kriging
         kr_sites = np.random.default_rng(20250115).uniform(size=(a.krig_sites, 2))   # configs[4]: 1M held-out sites
         kr_subs = [mk.subset_data(d["y"], d["x"], 1.0, d["coords"], 1, idx[i]) for i in range(min(a.krig_subsets, K))]
-        legs["kriging_cfg5"] = bench_kriging.kriging_leg(mk, kr_subs, kr_sites, beta0, bt)
+        legs["configs[4]_kriging"] = bench_kriging.kriging_leg(mk, kr_subs, kr_sites, beta0, bt)
+        legs["configs[1]_matern"] = config_leg(mk, 1, a.adapt_batches, a.warmup, a.steps)
+        legs["configs[3]_lmc_share7"] = config_leg(mk, 3, a.adapt_batches, a.warmup, a.steps, subsets=7)
     e2e = None
     if world == 1 and not a.no_e2e:
         e2e = end_to_end(mk, d, K, tuple(int(x) for x in a.e2e_devices.split(",")))
