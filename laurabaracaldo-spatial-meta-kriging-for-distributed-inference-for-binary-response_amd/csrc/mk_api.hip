@@ -357,6 +357,7 @@ struct mk_session {
   bool sweep_rows = false;        // one-workgroup sweep with rows owned by waves (k_sweep_rows, MK_SWEEP=5)
   int sweep_site = 0;             // one-pass site sweep (k_sweep_site, default for q <= 2): row pairs per thread (0: off)
   size_t sweep_site_lds = 0;
+  bool sweep_pair = false;        // the site sweep two sites per barrier (MK_SWEEP=7, q = 1)
   double* sp_part = nullptr;
   double* sp_dacc = nullptr;
   int* sp_any = nullptr;
@@ -920,7 +921,7 @@ static void launch_sweep(mk_session* s, Group& g, int it) {
     MatSet ms = g.ms;
     int iter = it;
     void* args[] = {&md, &ms, &iter};
-    const hipError_t e = hipLaunchKernel(sweep_site_kernel(q, s->sweep_site), dim3(g.S), dim3(MK_SW_T), args,
+    const hipError_t e = hipLaunchKernel(sweep_site_kernel(q, s->sweep_site, s->sweep_pair), dim3(g.S), dim3(MK_SW_T), args,
                                          s->sweep_site_lds, g.stream);
     wd_trace(g.stream, "k_sweep_site");
     if (e != hipSuccess && s->launch_err == hipSuccess) s->launch_err = e;
@@ -1602,18 +1603,21 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
     // data in LDS (configs[3]: n_s = 2,000, q = 3 takes 152 KB).  1-5 select the 64-site-block kernels,
     // which remain the fallback: split launches (3, 4) for multi-outcome small shards, else one
     // workgroup per subset.
-    const bool site_fits = sweep_site_kernel(q, n_pad <= 2 * MK_SW_T ? 1 : 2) != nullptr && n_pad <= 4 * MK_SW_T &&
+    // MK_SWEEP=7: the site sweep two sites per barrier (q = 1)
+    const bool pair = mode == 7;
+    const bool site_fits = sweep_site_kernel(q, n_pad <= 2 * MK_SW_T ? 1 : 2, pair) != nullptr && n_pad <= 4 * MK_SW_T &&
                            sweep_site_lds_bytes(nmax, q) <= 156 * 1024;
-    const bool site = (mode == 0 || mode == 6) && site_fits;
+    const bool site = (mode == 0 || mode == 6 || mode == 7) && site_fits;
     s->sweep_split = mode == 3 || mode == 4 || (mode == 0 && !site && q >= 2 && S <= 16);
     s->sweep_step = s->sweep_split && mode != 4 && nt <= 32;   // k_sweep_step sums <= 32 tile partials
     s->sweep_mg = !s->sweep_split && fits && mode == 2;
     s->sweep_rows = mode == 5 && q <= 3 && nt <= 32;
     if (site) {
       s->sweep_site = n_pad <= 2 * MK_SW_T ? 1 : 2;
+      s->sweep_pair = pair;
       s->sweep_site_lds = sweep_site_lds_bytes(nmax, q);
       s->sweep_mg = false;
-      HIPCHK(hipFuncSetAttribute(sweep_site_kernel(q, s->sweep_site), hipFuncAttributeMaxDynamicSharedMemorySize,
+      HIPCHK(hipFuncSetAttribute(sweep_site_kernel(q, s->sweep_site, pair), hipFuncAttributeMaxDynamicSharedMemorySize,
                                  (int)s->sweep_site_lds));
     }
     if (s->sweep_rows)

@@ -1284,13 +1284,18 @@ typedef unsigned int u4v __attribute__((ext_vector_type(4)));
 // Dynamic LDS (sweep_site_lds_bytes): site data [3][n_s q] (proposal, likelihood difference, log
 // accept draw) + accept flags [n_s] (bit a: outcome a).
 
-template <int Q, int KR>
+// P = 2 (q = 1, MK_SWEEP=7): two sites per barrier.  The pair (i, i+1) exchanges five values --
+// both dots, both squared norms and c = W[:,i] . W[:,i+1] = (R^-1)_{i+1,i} -- so site i+1's dot
+// after a move at site i is g_{i+1} + coef_i c (the same carry the 64-site blocks make through Q_BB);
+// half the barriers, one more reduction per pair.
+template <int Q, int KR, int P = 1>
 __global__ __launch_bounds__(SS_T) void k_sweep_site(Model md, MatSet ms, int iter) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   // ring: 2H columns (VGPRs: 8 H Q KR); NV values exchanged per site, four per row-sum round
-  constexpr int q = Q, H = Q == 1 ? 8 / KR : (Q == 2 ? 2 / KR : 1), NV = 2 * Q;
+  constexpr int q = Q, H = Q == 1 ? 8 / KR : (Q == 2 ? 2 / KR : 1), NV = P == 2 ? 5 : 2 * Q;
   constexpr int NR = (NV + 3) / 4;
   static_assert(H >= 1 && NV <= 8, "q <= 4");   // instantiated for q <= 2 and (q = 3, KR = 1): no spills
+  static_assert(P == 1 || (Q == 1 && H % 2 == 0), "site pairs: q = 1");
   __shared__ double part[2][NV][SS_W];
   __shared__ double Ai_s[MK_QMAX * MK_QMAX];
   const int s = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -1447,18 +1452,104 @@ __global__ __launch_bounds__(SS_T) void k_sweep_site(Model md, MatSet ms, int it
     }
     if (tid == 0 && live) sflag[i] = fl;
   };
+  // sites i, i + 1 (q = 1): one exchange, the carry of site i's move into site i + 1's dot
+  auto pair_step = [&](const int i, d2 (&w0)[KR][Q], d2 (&w1)[KR][Q]) {
+    const bool live0 = i < ns, live1 = i + 1 < ns;
+    const int i0c = live0 ? i : ns - 1, i1c = live1 ? i + 1 : ns - 1;
+    const double dl0 = sd_dl[i0c], dll0 = sd_dll[i0c], lg0 = live0 ? sd_lgu[i0c] : __builtin_huge_val();
+    const double dl1 = sd_dl[i1c], dll1 = sd_dll[i1c], lg1 = live1 ? sd_lgu[i1c] : __builtin_huge_val();
+    d2 c0[KR], c1[KR];
+#pragma unroll
+    for (int k = 0; k < KR; ++k) {
+      const int r0 = 2 * tid + 2 * SS_T * k;
+      c0[k].x = (r0 >= i) ? w0[k][0].x : 0.0;
+      c0[k].y = (r0 + 1 >= i && r0 + 1 < ns) ? w0[k][0].y : 0.0;
+      c1[k].x = (r0 >= i + 1) ? w1[k][0].x : 0.0;
+      c1[k].y = (r0 + 1 >= i + 1 && r0 + 1 < ns) ? w1[k][0].y : 0.0;
+    }
+    double v[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int k = 0; k < KR; ++k) {
+      v[0] += c0[k].x * zr[k][0].x + c0[k].y * zr[k][0].y;
+      v[1] += c1[k].x * zr[k][0].x + c1[k].y * zr[k][0].y;
+      v[2] += c0[k].x * c0[k].x + c0[k].y * c0[k].y;
+      v[3] += c1[k].x * c1[k].x + c1[k].y * c1[k].y;
+      v[4] += c0[k].x * c1[k].x + c0[k].y * c1[k].y;
+    }
+#pragma unroll
+    for (int e = 0; e < 5; ++e) v[e] = wave_sum_dpp(v[e]);
+    const int par = (i >> 1) & 1;
+    SS_CFENCE();
+    if (lane == 0) {
+#pragma unroll
+      for (int e = 0; e < 5; ++e) part[par][e][wv] = v[e];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    SS_CFENCE();
+    double tot[8];
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {
+      const int e_l = 4 * rr + (lane >> 4);
+      const double pv = part[par][e_l < 5 ? e_l : 0][lane & 15];
+      const double rsum = row_sum_dpp(e_l < 5 ? pv : 0.0);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) tot[4 * rr + e] = rlane_u(rsum, 16 * e);
+    }
+    const double a0 = ai[0];
+    int f0 = 0, f1 = 0;
+    double coef0 = 0.0, coef1 = 0.0;
+    {
+      const double d = rfl_f64(dl0);
+      const double c = a0 * tot[0];
+      const double dd = (a0 * a0) * tot[2];
+      if (rfl_f64(lg0) <= rfl_f64(dll0) - (d * c + 0.5 * d * d * dd)) {
+        coef0 = d * a0;
+        f0 = 1;
+      }
+    }
+    {
+      const double d = rfl_f64(dl1);
+      const double g1 = f0 ? tot[1] + coef0 * tot[4] : tot[1];
+      const double c = a0 * g1;
+      const double dd = (a0 * a0) * tot[3];
+      if (rfl_f64(lg1) <= rfl_f64(dll1) - (d * c + 0.5 * d * d * dd)) {
+        coef1 = d * a0;
+        f1 = 1;
+      }
+    }
+    if (f0 | f1) {
+#pragma unroll
+      for (int k = 0; k < KR; ++k) {
+        zr[k][0].x = fma(coef1, c1[k].x, fma(coef0, c0[k].x, zr[k][0].x));
+        zr[k][0].y = fma(coef1, c1[k].y, fma(coef0, c0[k].y, zr[k][0].y));
+      }
+    }
+    if (tid == 0 && live0) sflag[i] = f0;
+    if (tid == 0 && live1) sflag[i + 1] = f1;
+  };
   d2 wa[H][KR][Q], wb[H][KR][Q];
 #pragma unroll
   for (int u = 0; u < H; ++u) load_col(u, wa[u]);
   for (int i0 = 0; i0 < ns; i0 += 2 * H) {
 #pragma unroll
     for (int u = 0; u < H; ++u) load_col(i0 + H + u, wb[u]);
+    if constexpr (P == 2) {
 #pragma unroll
-    for (int u = 0; u < H; ++u) step(i0 + u, wa[u]);
+      for (int u = 0; u < H; u += 2) pair_step(i0 + u, wa[u], wa[u + 1]);
+    } else {
+#pragma unroll
+      for (int u = 0; u < H; ++u) step(i0 + u, wa[u]);
+    }
 #pragma unroll
     for (int u = 0; u < H; ++u) load_col(i0 + 2 * H + u, wa[u]);
+    if constexpr (P == 2) {
 #pragma unroll
-    for (int u = 0; u < H; ++u) step(i0 + H + u, wb[u]);
+      for (int u = 0; u < H; u += 2) pair_step(i0 + H + u, wb[u], wb[u + 1]);
+    } else {
+#pragma unroll
+      for (int u = 0; u < H; ++u) step(i0 + H + u, wb[u]);
+    }
   }
   // ---- write back own z rows; the accept flags to sw_acc; apply accepted moves
 #pragma unroll
@@ -1475,11 +1566,13 @@ __global__ __launch_bounds__(SS_T) void k_sweep_site(Model md, MatSet ms, int it
   __syncthreads();
   sweep_apply(md, s, 0, ns, Ai_s, tid, SS_T);
 }
-template __global__ void k_sweep_site<1, 1>(Model, MatSet, int);
-template __global__ void k_sweep_site<1, 2>(Model, MatSet, int);
-template __global__ void k_sweep_site<2, 1>(Model, MatSet, int);
-template __global__ void k_sweep_site<2, 2>(Model, MatSet, int);
-template __global__ void k_sweep_site<3, 1>(Model, MatSet, int);
+template __global__ void k_sweep_site<1, 1, 1>(Model, MatSet, int);
+template __global__ void k_sweep_site<1, 2, 1>(Model, MatSet, int);
+template __global__ void k_sweep_site<2, 1, 1>(Model, MatSet, int);
+template __global__ void k_sweep_site<2, 2, 1>(Model, MatSet, int);
+template __global__ void k_sweep_site<3, 1, 1>(Model, MatSet, int);
+template __global__ void k_sweep_site<1, 1, 2>(Model, MatSet, int);
+template __global__ void k_sweep_site<1, 2, 2>(Model, MatSet, int);
 
 // ---------------------------------------------------------------- 6. record / adapt
 __global__ __launch_bounds__(64) void k_record(Model md, int iter) {

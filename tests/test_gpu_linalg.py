@@ -178,7 +178,7 @@ def test_site_sweep_runs_the_block_sweeps_chain(tmp_path):
     here = os.path.dirname(os.path.abspath(__file__))
     for la in ("1", "0"):
         res = {}
-        for sweep in ("1", "6"):
+        for sweep in ("1", "6", "7"):
             path = str(tmp_path / f"site_{sweep}_{la}.npz")
             env = dict(os.environ, MK_SWEEP=sweep, **({} if la == "1" else {"MK_LOOKAHEAD": "0"}))
             r = subprocess.run([sys.executable, os.path.join(here, "gpu_tile_run.py"), path], capture_output=True,
@@ -187,7 +187,8 @@ def test_site_sweep_runs_the_block_sweeps_chain(tmp_path):
             z = np.load(path)
             res[sweep] = {k: z[k] for k in z.files}
         for k in res["1"]:
-            np.testing.assert_allclose(res["6"][k], res["1"][k], rtol=0, atol=1e-9, err_msg=f"{k} la={la}")
+            for sw in ("6", "7"):   # 7: two sites per barrier (q = 1; q = 2 falls back to the block sweep)
+                np.testing.assert_allclose(res[sw][k], res["1"][k], rtol=0, atol=1e-9, err_msg=f"{k} la={la} {sw}")
 
 
 def test_chain_split_cholesky_is_bit_identical(tmp_path):
