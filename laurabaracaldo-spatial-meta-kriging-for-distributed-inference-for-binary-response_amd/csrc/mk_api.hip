@@ -126,6 +126,7 @@ struct Group {
   hipEvent_t done = nullptr;         // fork-join sweep: this group's pre-sweep work is queued
   hipStream_t bulk = nullptr;        // split Cholesky (launch_cholesky): CU-masked bulk-update stream
   hipStream_t near = nullptr;        // chain split (MK_CHOL_CHAIN): off-diagonal correction + trsm stream
+  CovGen gen{};                      // MK_COV_FUSE: the candidates being factored, generated at first touch
   std::vector<hipEvent_t> ev;        // 2 nt + 1 events reused every factorisation
 };
 
@@ -178,6 +179,7 @@ Model model_view(const Model& m, int s0, int S) {
   if (m.span_pt) v.span_pt = m.span_pt + s;
   if (m.chtab) v.chtab = m.chtab + s * q * MK_CH_TAB;
   if (m.chtab_p) v.chtab_p = m.chtab_p + s * q * MK_CH_TAB;
+  if (m.phi_c) v.phi_c = m.phi_c + s * q;
   return v;
 }
 
@@ -335,6 +337,7 @@ struct mk_session {
   int iter = 0;
   bool matern = false, record_samples = true, record_w = false;
   bool pred_gen = false;          // kriging P^T generated inside k_pred_var (exponential; no P^T buffer)
+  bool cov_fuse = false;          // MK_COV_FUSE=1 (exponential): candidate tiles generated by the update at first touch
   Group all;                      // the whole shard on `stream`
   bool tiled = false;             // kriging after the fit over test-site tiles (predict_tile)
   int pred_tile = 0, n_test_all = 0, n_test_pad_all = 0;
@@ -548,7 +551,8 @@ static void launch_candidates(const Model& md, const MatSet& ms, hipStream_t st,
                               int which, int iter, const int* slist = nullptr, const int* scount = nullptr) {
   if (md.cov_model == MK_COV_MATERN && md.chtab)
     MK_LAUNCH(k_matern_table, dim3(n_entries), dim3(256), 0, st, md, h0, hc, which, iter, slist, scount);
-  MK_LAUNCH(cov_candidate_kernel(md.cov_model), dim3(xcd_grid_h(n_entries, ms.nt * (ms.nt + 1) / 2)),
+  const int ntiles = (which & MK_CAND_COL0) ? ms.nt : ms.nt * (ms.nt + 1) / 2;
+  MK_LAUNCH(cov_candidate_kernel(md.cov_model), dim3(xcd_grid_h(n_entries, ntiles)),
                      dim3(256), 0, st, md, ms, h0, hc, which, iter, slist, scount);
 }
 
@@ -556,25 +560,42 @@ static void launch_candidates(const Model& md, const MatSet& ms, hipStream_t st,
 // Candidate tiles are in the free slot (k_cov_candidate, or k_load_plain for the test entry).
 // One launch per step covers outcomes h0 .. h0+hc-1 of every subset (hc = q in the sampler).
 // Launch pieces of the blocked Cholesky for panel k, tiles [ia, ib), on stream st.
+// MK_COV_FUSE: the candidate generation the update kernel does at a tile's first touch (j0 == 0), and
+// the covariance launch that then writes column 0 only (and each pair's phi').
+static CovGen cov_gen(const mk_session* s, const Model& md, bool border) {
+  CovGen c{};
+  if (!s->cov_fuse) return c;
+  c.coords = md.coords;
+  c.n_s = md.n_s;
+  c.u = md.u;
+  c.phi_c = md.phi_c;
+  c.n_pad = md.n_pad;
+  c.q = md.q;
+  c.border = border ? 1 : 0;
+  return c;
+}
+static int cand_flags(const mk_session* s) { return s->cov_fuse ? MK_CAND_COL0 : 0; }
+
 static void chol_update(mk_session* s, Group& g, hipStream_t st, int h0, int hc, int k, int ia, int ib, int j0, int j1,
                         const int* slist, const int* scount, double flops) {
   const int E = g.S * hc, nti = ib - ia;
   if (nti <= 0) return;
+  const CovGen cg = j0 == 0 ? g.gen : CovGen{};
   const int tm = tile_size((long)E * nti);
   if (tm == 32) {
     timed(s, st, KS_CHOL_UPDATE_SUB, flops, [&] {
       MK_LAUNCH(k_chol_update<32>, dim3(xcd_grid_h(E, nti * 16)), dim3(256), LDS_32, st, g.ms, g.S, h0, hc, k, ia,
-                         ib, j0, j1, slist, scount);
+                         ib, j0, j1, slist, scount, cg);
     });
   } else if (tm == 64) {
     timed(s, st, KS_CHOL_UPDATE_SUB, flops, [&] {
       MK_LAUNCH(k_chol_update<64>, dim3(xcd_grid_h(E, nti * 4)), dim3(256), LDS_64, st, g.ms, g.S, h0, hc, k, ia,
-                         ib, j0, j1, slist, scount);
+                         ib, j0, j1, slist, scount, cg);
     });
   } else {
     timed(s, st, KS_CHOL_UPDATE, flops, [&] {
       MK_LAUNCH(k_chol_update<128>, dim3(xcd_grid_h(E, nti)), dim3(256), LDS_128, st, g.ms, g.S, h0, hc, k, ia,
-                         ib, j0, j1, slist, scount);
+                         ib, j0, j1, slist, scount, cg);
     });
   }
 }
@@ -979,7 +1000,8 @@ static void iteration_pre_sweep(mk_session* s, Group& g, int it) {
   const int nkinds = s->matern ? 2 : 1;
   // the q outcomes' (phi_h, nu_h) steps are independent given u: one batched pass per kind
   for (int which = 0; which < nkinds; ++which) {
-    timed(s, st, KS_COV, 0.0, [&] { launch_candidates(md, g.ms, st, S * q, 0, q, which, it); });
+    timed(s, st, KS_COV, 0.0, [&] { launch_candidates(md, g.ms, st, S * q, 0, q, which | cand_flags(s), it); });
+    g.gen = cov_gen(s, md, true);
     launch_cholesky(s, g, 0, q);
     MK_LAUNCH(k_theta_mh, dim3((S * q + 63) / 64), dim3(64), 0, st, md, g.ms, 0, q, which, it);
   }
@@ -1023,7 +1045,9 @@ static int la_head(mk_session* s) {
 static void enqueue_candidates(mk_session* s, Group& g, int it, hipEvent_t after, int k_hi) {
   const int S = g.S, q = s->q, nt = s->nt;
   hipStreamWaitEvent(s->la_c, after, 0);
-  timed(s, s->la_c, KS_COV, 0.0, [&] { launch_candidates(g.md, g.ms, s->la_c, S * q, 0, q, 0 | MK_CAND_NOBORDER, it); });
+  timed(s, s->la_c, KS_COV, 0.0,
+        [&] { launch_candidates(g.md, g.ms, s->la_c, S * q, 0, q, 0 | MK_CAND_NOBORDER | cand_flags(s), it); });
+  g.gen = cov_gen(s, g.md, false);   // also the rest of this factorisation (enqueue_candidates_rest)
   launch_cholesky(s, g, 0, q, nullptr, nullptr, s->la_c, s->la_ev.data(), 0, k_hi);
   s->la_next = it;
   s->la_enq = k_hi;
@@ -1345,6 +1369,8 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
   // kriging memory, but 0.52 vs 0.74 of fp64 peak: the exp/sqrt per element are recomputed for
   // every row panel).  Default: stored P^T.
   s->pred_gen = !s->matern && tile_env("MK_PRED_GEN", 0) != 0;
+  // MK_COV_FUSE=1 (exponential): candidate tiles generated inside the update at their first touch
+  s->cov_fuse = !s->matern && tile_env("MK_COV_FUSE", 0) != 0;
   s->n_part.assign(pr->n_part, pr->n_part + S);
   s->bbox.assign((size_t)4 * S, 0.0);
   {
@@ -1443,6 +1469,7 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
       hs[i] = std::hypot(s->bbox[4 * i + 1] - s->bbox[4 * i], s->bbox[4 * i + 3] - s->bbox[4 * i + 2]);
     HIPCHK(hipMemcpy(d_span, hs.data(), (size_t)S * 8, hipMemcpyHostToDevice));
     md.span = d_span;
+    if ((rc = s->alloc(&md.phi_c, (size_t)S * q))) return rc;
     if (s->matern && ((rc = s->alloc(&md.chtab, (size_t)S * q * MK_CH_TAB)) ||
                       (rc = s->alloc(&md.chtab_p, (size_t)S * q * MK_CH_TAB))))
       return rc;
@@ -1647,8 +1674,10 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
   // ---------------- initial state: eta, u, factor every R_h at the starting values, W, z (whole shard)
   Group& a = s->all;
   MK_LAUNCH(k_init_state, dim3(S), dim3(256), 0, s->stream, md);
-  launch_candidates(md, ms, s->stream, S * q, 0, q, 2, 0);
+  launch_candidates(md, ms, s->stream, S * q, 0, q, 2 | cand_flags(s), 0);
+  a.gen = cov_gen(s, md, true);
   launch_cholesky(s, a, 0, q);
+  a.gen = CovGen{};
   MK_LAUNCH(k_theta_init, dim3((S * q + 63) / 64), dim3(64), 0, s->stream, md, ms, 0, q);
   MK_LAUNCH(k_dirty_list, dim3(1), dim3(256), 0, s->stream, md, 0, a.d_list, a.d_count, a.d_plist, a.d_pcount);
   launch_inverse(s, a);
@@ -1858,8 +1887,10 @@ static int predict_tile(mk_session* s, int t0, double* dq, mk_outputs* o) {
     MK_LAUNCH(k_kept_dirty, dim3(1), dim3(256), 0, st, mt, prev, s->d_slist, s->d_scount, g.d_plist,
                        g.d_pcount);
     for (int h = 0; h < q; ++h) {
-      launch_candidates(mt, g.ms, st, S, h, 1, 2, 0, s->d_slist + h * S, s->d_scount + h);
+      launch_candidates(mt, g.ms, st, S, h, 1, 2 | cand_flags(s), 0, s->d_slist + h * S, s->d_scount + h);
+      g.gen = cov_gen(s, mt, true);
       launch_cholesky(s, g, h, 1, s->d_slist + h * S, s->d_scount + h);
+      g.gen = CovGen{};
     }
     MK_LAUNCH(k_flip_pairs, dim3((S * q + 255) / 256), dim3(256), 0, st, g.ms, g.d_plist, g.d_pcount);
     launch_trinv(s, g, S * q, g.d_plist, g.d_pcount);

@@ -15,7 +15,7 @@ inline CovCandidateKernel cov_candidate_kernel(int model) {
 }
 template <int TM, int TN = TM>
 __global__ void k_chol_update(MatSet ms, int S, int h0, int hc, int k, int ia, int ib, int j0, int j1,
-                              const int* slist, const int* scount);
+                              const int* slist, const int* scount, CovGen cg);
 template <int TM>
 __global__ void k_chol_trsm(MatSet ms, int S, int h0, int hc, int k, int ia, int ib, const int* slist,
                             const int* scount);

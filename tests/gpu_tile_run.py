@@ -32,6 +32,18 @@ def main(path):
             out[f"q{q}c{cov}_samples_{s}"] = o["samples"][s]
             out[f"q{q}c{cov}_w_{s}"] = o["w_samples"][s]
             out[f"q{q}c{cov}_pred_{s}"] = o["w_pred_samples"][s]
+    # tiled kriging replay (predict_tile): its own candidate factorisations of the kept states
+    d = mk.synthetic.generate(557, q=1, n_test=300, seed=77)
+    cfg = mk.SamplerConfig(1, 2, np.zeros(2), np.full(2, 0.05), n_batch=2, batch_length=3, burn_in=4, seed=5,
+                           predict_tile=128)
+    subs = [dict(coords=d["coords"][:300], y=d["y"][:300], weights=np.ones(300), x=d["x"][:300]),
+            dict(coords=d["coords"][300:], y=d["y"][300:], weights=np.ones(257), x=d["x"][300:])]
+    with mk.Session(subs, cfg, coords_test=d["coords_test"]) as ses:
+        ses.run(cfg.n_samples)
+        o = ses.outputs(w_pred_samples=True)
+    for s in range(2):
+        out[f"tiled_pred_{s}"] = o["w_pred_samples"][s]
+        out[f"tiled_wq_{s}"] = o["w_predict"][s]
     L, ld = mk.cholesky_batched(np.stack([np.eye(300) + 0.5 * np.exp(-np.abs(np.subtract.outer(np.arange(300.0),
                                                                                                np.arange(300.0))) / 7)
                                           for _ in range(2)]), inverse=False)

@@ -217,3 +217,29 @@ def test_chain_split_cholesky_is_bit_identical(tmp_path):
         got, ref = runs[name], runs["ref0" if name in ("c1d1", "c2s") else "ref1"]
         for k in ref:
             assert np.array_equal(got[k], ref[k]), (name, k)
+
+
+def test_covariance_fused_into_the_update_is_bit_identical(tmp_path):
+    """MK_COV_FUSE=1 (exponential model): the candidate's tiles outside column 0 are generated by the
+    update kernel at their first touch (k_cov_candidate's expression, written in place and loaded back)
+    instead of by the covariance pass: the same bits as the default, under both launch schedules, with
+    the split and the chain-split Cholesky, and through the tiled kriging replay (its own candidates)."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    runs = {}
+    for name, env in (("ref1", {}), ("ref0", dict(MK_LOOKAHEAD="0")),
+                      ("f1", dict(MK_COV_FUSE="1")), ("f0", dict(MK_COV_FUSE="1", MK_LOOKAHEAD="0")),
+                      ("f1c", dict(MK_COV_FUSE="1", MK_CHOL_SPLIT="1", MK_CHOL_CHAIN="1")),
+                      ("f0s", dict(MK_COV_FUSE="1", MK_CHOL_SPLIT="1", MK_LOOKAHEAD="0"))):
+        path = str(tmp_path / f"{name}.npz")
+        r = subprocess.run([sys.executable, os.path.join(here, "gpu_tile_run.py"), path], capture_output=True,
+                           text=True, timeout=240, env=dict(os.environ, MK_SWEEP="1", **env))
+        assert r.returncode == 0, r.stderr[-4000:]
+        z = np.load(path)
+        runs[name] = {k: z[k] for k in z.files}
+    for name in ("f1", "f0", "f1c", "f0s"):
+        got, ref = runs[name], runs["ref0" if name in ("f0", "f0s") else "ref1"]
+        for k in ref:
+            assert np.array_equal(got[k], ref[k]), (name, k)
