@@ -14,6 +14,8 @@ run s32_block 32 MK_SWEEP=1
 run s32_pair 32 MK_SWEEP=7
 run s32_chain1 32 MK_CHOL_CHAIN=1
 run s32_chain2 32 MK_CHOL_CHAIN=2
+run s32_fuse 32 MK_COV_FUSE=1
 run s250_site 250
+run s250_fuse 250 MK_COV_FUSE=1
 run s250_block 250 MK_SWEEP=1
 run s250_pair 250 MK_SWEEP=7
