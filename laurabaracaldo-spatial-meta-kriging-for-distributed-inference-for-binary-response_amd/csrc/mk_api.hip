@@ -942,7 +942,7 @@ static void launch_sweep(mk_session* s, Group& g, int it) {
     MatSet ms = g.ms;
     int iter = it;
     void* args[] = {&md, &ms, &iter};
-    const hipError_t e = hipLaunchKernel(sweep_site_kernel(q, s->sweep_site, s->sweep_pair), dim3(g.S), dim3(MK_SW_T), args,
+    const hipError_t e = hipLaunchKernel(sweep_site_kernel(q, s->sweep_site, s->sweep_pair), dim3(g.S), dim3(MK_SS_T), args,
                                          s->sweep_site_lds, g.stream);
     wd_trace(g.stream, "k_sweep_site");
     if (e != hipSuccess && s->launch_err == hipSuccess) s->launch_err = e;
@@ -1632,7 +1632,7 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
     // workgroup per subset.
     // MK_SWEEP=7: the site sweep two sites per barrier (q = 1)
     const bool pair = mode == 7;
-    const bool site_fits = sweep_site_kernel(q, n_pad <= 2 * MK_SW_T ? 1 : 2, pair) != nullptr && n_pad <= 4 * MK_SW_T &&
+    const bool site_fits = sweep_site_kernel(q, n_pad <= 8 * MK_SS_T ? 1 : 2, pair) != nullptr && n_pad <= 16 * MK_SS_T &&
                            sweep_site_lds_bytes(nmax, q) <= 156 * 1024;
     const bool site = (mode == 0 || mode == 6 || mode == 7) && site_fits;
     s->sweep_split = mode == 3 || mode == 4 || (mode == 0 && !site && q >= 2 && S <= 16);
@@ -1640,7 +1640,7 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
     s->sweep_mg = !s->sweep_split && fits && mode == 2;
     s->sweep_rows = mode == 5 && q <= 3 && nt <= 32;
     if (site) {
-      s->sweep_site = n_pad <= 2 * MK_SW_T ? 1 : 2;
+      s->sweep_site = n_pad <= 8 * MK_SS_T ? 1 : 2;
       s->sweep_pair = pair;
       s->sweep_site_lds = sweep_site_lds_bytes(nmax, q);
       s->sweep_mg = false;

@@ -9,6 +9,7 @@
 #include <stdint.h>
 
 #define MK_NB 128          // Cholesky / GEMM tile edge (fp64)
+#define MK_SS_T 256        // threads of the site sweep workgroup (k_sweep_site: one wave per SIMD)
 #define MK_SW_T 1024       // threads of the latent-w sweep workgroup (one per subset): loads in flight for the W panels
 // dynamic LDS of the LDS-DMA GEMM (k_chol_update): 2 stages x (A, B) x 16 k-rows x 144 doubles
 #define MK_GD_LDS_BYTES (2 * 2 * 16 * 144 * 8)

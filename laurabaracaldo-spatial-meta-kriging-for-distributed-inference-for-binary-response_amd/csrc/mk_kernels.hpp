@@ -65,15 +65,15 @@ template <int Q, int KR, int P>
 __global__ void k_sweep_site(Model md, MatSet ms, int iter);
 // its dynamic LDS: the sites' proposal / likelihood difference / accept draw + the accept flags
 inline size_t sweep_site_lds_bytes(int ns_max, int q) { return (size_t)ns_max * q * 3 * 8 + (size_t)ns_max * 4; }
-// the one-pass site sweep (kr: row pairs per thread, 1 for n_pad <= 2048 or 2 for <= 4096); NULL
+// the one-pass site sweep (kr 1: n_pad <= 2048, four row pairs per thread; 2: <= 4096, eight); NULL
 // where its registers would spill (q = 3 with kr = 2, q = 4): the 64-site-block kernels run there
 // (pair: two sites per barrier, q = 1 only)
 inline const void* sweep_site_kernel(int q, int kr, bool pair = false) {
-  if (pair) return q != 1 ? nullptr : (kr == 1 ? (const void*)k_sweep_site<1, 1, 2> : (const void*)k_sweep_site<1, 2, 2>);
+  if (pair) return q != 1 ? nullptr : (kr == 1 ? (const void*)k_sweep_site<1, 4, 2> : (const void*)k_sweep_site<1, 8, 2>);
   switch (q) {
-    case 1: return kr == 1 ? (const void*)k_sweep_site<1, 1, 1> : (const void*)k_sweep_site<1, 2, 1>;
-    case 2: return kr == 1 ? (const void*)k_sweep_site<2, 1, 1> : (const void*)k_sweep_site<2, 2, 1>;
-    case 3: return kr == 1 ? (const void*)k_sweep_site<3, 1, 1> : nullptr;
+    case 1: return kr == 1 ? (const void*)k_sweep_site<1, 4, 1> : (const void*)k_sweep_site<1, 8, 1>;
+    case 2: return kr == 1 ? (const void*)k_sweep_site<2, 4, 1> : (const void*)k_sweep_site<2, 8, 1>;
+    case 3: return kr == 1 ? (const void*)k_sweep_site<3, 4, 1> : nullptr;
     default: return nullptr;
   }
 }

@@ -1238,14 +1238,17 @@ MK_INST_SPLIT(4)
 
 // ---------------------------------------------------------------- 5b. one-pass site sweep (default)
 // The single-site w updates of spMvGLM (MK.R:80-84) with every column of W_h = L_h^-1 read from HBM
-// exactly once per sweep.  One 1024-thread workgroup per subset; thread t owns the row pairs
-// 2t + 2048k (k < KR) of every z_h and keeps them in registers for the whole sweep; the W columns
+// exactly once per sweep.  One 256-thread workgroup per subset (a wave per SIMD: the per-site work every
+// wave repeats is issued once per SIMD -- with 16 waves the site took ~3,000 cycles, issue-bound);
+// thread t owns the row pairs 2t + 512k (k < KR = 4, or 8 beyond 2,048 rows) of every z_h and keeps
+// them in registers for the whole sweep; the W columns
 // stream through a register ring D sites ahead of use.  Site i, outcomes a = 0 .. q-1 in order:
 //   every wave: p_h = sum over its rows of W_h[r,i] z_h[r] and s_h = sum of W_h[r,i]^2 (rows
-//     i <= r < n_s; one DPP tree each) into LDS slot [i & 1][value][wave], then one s_barrier --
-//     LDS writes drained (lgkmcnt) but no wait on the W loads in flight;
-//   every wave: g_h = the 16 wave partials summed by a 16-lane DPP row tree (the same order in
-//     every wave, so the same bits) and Q_ii,h = (R_h^-1)_ii the same way from s_h; the site's q MH
+//     i <= r < n_s), one 16-lane DPP row tree each, the four row sums into LDS slots
+//     [i & 1][value][4 wave + row], then one s_barrier -- LDS writes drained (lgkmcnt) but no wait on
+//     the W loads in flight;
+//   every wave: g_h = the 16 row sums summed by a 16-lane DPP row tree (the same order in every
+//     wave, so the same bits) and Q_ii,h = (R_h^-1)_ii the same way from s_h; the site's q MH
 //     steps, computed redundantly by every wave with identical decisions (accept iff
 //     log U <= dll - (d c + 0.5 d^2 dd), c = sum_h A^-1_ha g_h, dd = sum_h (A^-1_ha)^2 Q_ii,h), the
 //     carry to the site's next outcome g_h += coef_h Q_ii,h, and on acceptance
@@ -1258,16 +1261,24 @@ MK_INST_SPLIT(4)
 // skipped row pairs (the zero upper triangle, the border and padding rows) take an out-of-range
 // offset and return zero without touching memory; the sites' proposals, likelihood differences
 // and accept draws (sweep_precompute) and the accept flags live in LDS.
-#define SS_T 1024
-#define SS_W (SS_T / 64)
+#define SS_T MK_SS_T
+#define SS_W (SS_T / 64)   // four waves: one per SIMD, so the per-site work each wave repeats is issued once per SIMD
 #define SS_OOB 0x7ffffff0u   // buffer offset beyond every W matrix: the load returns zero
 // Sums of the 16-lane rows of a wave, in every lane of the row (quad xor 1, quad xor 2, half-row
 // mirror, row mirror: the first four steps of wave_sum_dpp).
+// (mov_dpp: every lane reads a lane of its own row, so no `old` value has to be materialised first)
+template <int CTRL>
+__device__ inline double dpp_f64_mov(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)(b & 0xffffffffll), CTRL, 0xf, 0xf, true);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xf, 0xf, true);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
 __device__ inline double row_sum_dpp(double x) {
-  x += dpp_f64<0xB1>(x);
-  x += dpp_f64<0x4E>(x);
-  x += dpp_f64<0x141>(x);
-  x += dpp_f64<0x140>(x);
+  x += dpp_f64_mov<0xB1>(x);
+  x += dpp_f64_mov<0x4E>(x);
+  x += dpp_f64_mov<0x141>(x);
+  x += dpp_f64_mov<0x140>(x);
   return x;
 }
 __device__ inline double rfl_f64(double v) {   // a wave-uniform VGPR value as a scalar
@@ -1292,11 +1303,11 @@ template <int Q, int KR, int P = 1>
 __global__ __launch_bounds__(SS_T) void k_sweep_site(Model md, MatSet ms, int iter) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   // ring: 2H columns (VGPRs: 8 H Q KR); NV values exchanged per site, four per row-sum round
-  constexpr int q = Q, H = Q == 1 ? 8 / KR : (Q == 2 ? 2 / KR : 1), NV = P == 2 ? 5 : 2 * Q;
+  constexpr int q = Q, H = (16 / (Q * KR)) > 0 ? 16 / (Q * KR) : 1, NV = P == 2 ? 5 : 2 * Q;
   constexpr int NR = (NV + 3) / 4;
   static_assert(H >= 1 && NV <= 8, "q <= 4");   // instantiated for q <= 2 and (q = 3, KR = 1): no spills
   static_assert(P == 1 || (Q == 1 && H % 2 == 0), "site pairs: q = 1");
-  __shared__ double part[2][NV][SS_W];
+  __shared__ double part[2][NV][16];   // per value: the 16-lane row sums of the four waves
   __shared__ double Ai_s[MK_QMAX * MK_QMAX];
   const int s = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int ns = md.n_s[s];
@@ -1399,11 +1410,11 @@ __global__ __launch_bounds__(SS_T) void k_sweep_site(Model md, MatSet ms, int it
       v[Q + h] = sq;
     }
 #pragma unroll
-    for (int e = 0; e < NV; ++e) v[e] = wave_sum_dpp(v[e]);
+    for (int e = 0; e < NV; ++e) v[e] = row_sum_dpp(v[e]);
     SS_CFENCE();
-    if (lane == 0) {
+    if ((lane & 15) == 0) {
 #pragma unroll
-      for (int e = 0; e < NV; ++e) part[i & 1][e][wv] = v[e];
+      for (int e = 0; e < NV; ++e) part[i & 1][e][4 * wv + (lane >> 4)] = v[e];
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -1477,12 +1488,12 @@ __global__ __launch_bounds__(SS_T) void k_sweep_site(Model md, MatSet ms, int it
       v[4] += c0[k].x * c1[k].x + c0[k].y * c1[k].y;
     }
 #pragma unroll
-    for (int e = 0; e < 5; ++e) v[e] = wave_sum_dpp(v[e]);
+    for (int e = 0; e < 5; ++e) v[e] = row_sum_dpp(v[e]);
     const int par = (i >> 1) & 1;
     SS_CFENCE();
-    if (lane == 0) {
+    if ((lane & 15) == 0) {
 #pragma unroll
-      for (int e = 0; e < 5; ++e) part[par][e][wv] = v[e];
+      for (int e = 0; e < 5; ++e) part[par][e][4 * wv + (lane >> 4)] = v[e];
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -1566,13 +1577,13 @@ __global__ __launch_bounds__(SS_T) void k_sweep_site(Model md, MatSet ms, int it
   __syncthreads();
   sweep_apply(md, s, 0, ns, Ai_s, tid, SS_T);
 }
-template __global__ void k_sweep_site<1, 1, 1>(Model, MatSet, int);
-template __global__ void k_sweep_site<1, 2, 1>(Model, MatSet, int);
-template __global__ void k_sweep_site<2, 1, 1>(Model, MatSet, int);
-template __global__ void k_sweep_site<2, 2, 1>(Model, MatSet, int);
-template __global__ void k_sweep_site<3, 1, 1>(Model, MatSet, int);
-template __global__ void k_sweep_site<1, 1, 2>(Model, MatSet, int);
-template __global__ void k_sweep_site<1, 2, 2>(Model, MatSet, int);
+template __global__ void k_sweep_site<1, 4, 1>(Model, MatSet, int);
+template __global__ void k_sweep_site<1, 8, 1>(Model, MatSet, int);
+template __global__ void k_sweep_site<2, 4, 1>(Model, MatSet, int);
+template __global__ void k_sweep_site<2, 8, 1>(Model, MatSet, int);
+template __global__ void k_sweep_site<3, 4, 1>(Model, MatSet, int);
+template __global__ void k_sweep_site<1, 4, 2>(Model, MatSet, int);
+template __global__ void k_sweep_site<1, 8, 2>(Model, MatSet, int);
 
 // ---------------------------------------------------------------- 6. record / adapt
 __global__ __launch_bounds__(64) void k_record(Model md, int iter) {

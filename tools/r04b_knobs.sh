@@ -2,7 +2,7 @@
 # Round 4: the site sweep and the chain-split Cholesky against the round-3 defaults, one bench window
 # each (no CPU baseline, no end-to-end, no legs): 32 subsets (the 8-GPU share) and 250.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/r04b
+O=${O:-gpurun_out/r04b}
 mkdir -p $O
 run() {   # name, subsets, env...
   local name=$1 S=$2; shift 2
