@@ -57,6 +57,9 @@ def parse():
                     help="subsets of the shard leg (the per-GPU share of configs[2] on 8 GPUs)")
     ap.add_argument("--krig-subsets", type=int, default=32, help="subsets of the configs[4] kriging leg")
     ap.add_argument("--krig-sites", type=int, default=1_000_000, help="test sites of the configs[4] kriging leg")
+    ap.add_argument("--leg", choices=("configs1", "configs3", "configs3_share7"), default=None,
+                    help="run only this window leg (configs[1] Matern K=50, configs[3] q=3 K=50 or its 7-subset "
+                         "8-GPU share) and print its JSON")
     ap.add_argument("--no-kernel-events", action="store_true",
                     help="diagnostic: no per-kernel HIP events in the timed region (roofline fields then null)")
     ap.add_argument("--scaling", choices=("weak", "strong"), default="strong",
@@ -291,6 +294,11 @@ def node_end_to_end(a, world):
 
 def main():
     a = parse()
+    if a.leg:
+        mk = importlib.import_module(PKG)
+        which, sub = {"configs1": (1, None), "configs3": (3, None), "configs3_share7": (3, 7)}[a.leg]
+        print(json.dumps(config_leg(mk, which, a.adapt_batches, a.warmup, a.steps, subsets=sub)), flush=True)
+        return
     if a.e2e_only:
         mk = importlib.import_module(PKG)
         d = mk.synthetic.generate(a.n, q=1, n_test=a.n_test, seed=20250114)
