@@ -1630,12 +1630,18 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
     // data in LDS (configs[3]: n_s = 2,000, q = 3 takes 152 KB).  1-5 select the 64-site-block kernels,
     // which remain the fallback: split launches (3, 4) for multi-outcome small shards, else one
     // workgroup per subset.
-    // MK_SWEEP=7: the site sweep two sites per barrier (q = 1)
-    const bool pair = mode == 7;
+    // MK_SWEEP=7: the site sweep two sites per barrier (q = 1); the default for q = 1.  Measured
+    // (subset-iters/s, 40-step windows, profiles/r04/knobs, r04e): configs[2] 250 subsets block sweep
+    // 10,143 / site 10,506 / pair 10,527; its 32-subset share 7,744 / 7,784 / 7,758 (not the bound
+    // there); configs[1] 15,198 / 15,055 / 15,626; configs[3] (q = 3, 50 subsets) block 3,016 / site
+    // 3,106; configs[3]'s 7-subset share split launches 1,476 / site 1,340 / block 1,107 -- so q >= 2
+    // small shards keep the split-launch sweep.
+    const bool small_multi = q >= 2 && S <= 16;
+    const bool pair = mode == 7 || (mode == 0 && q == 1);
     const bool site_fits = sweep_site_kernel(q, n_pad <= 8 * MK_SS_T ? 1 : 2, pair) != nullptr && n_pad <= 16 * MK_SS_T &&
                            sweep_site_lds_bytes(nmax, q) <= 156 * 1024;
-    const bool site = (mode == 0 || mode == 6 || mode == 7) && site_fits;
-    s->sweep_split = mode == 3 || mode == 4 || (mode == 0 && !site && q >= 2 && S <= 16);
+    const bool site = ((mode == 0 && !small_multi) || mode == 6 || mode == 7) && site_fits;
+    s->sweep_split = mode == 3 || mode == 4 || (mode == 0 && !site && small_multi);
     s->sweep_step = s->sweep_split && mode != 4 && nt <= 32;   // k_sweep_step sums <= 32 tile partials
     s->sweep_mg = !s->sweep_split && fits && mode == 2;
     s->sweep_rows = mode == 5 && q <= 3 && nt <= 32;

@@ -3,7 +3,7 @@
 # FETCH_SIZE / WRITE_SIZE passes at 250 (one counter group per run) for the HBM traffic of the
 # update kernel and of the site sweep.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/r04c
+O=${O:-gpurun_out/r04c}
 mkdir -p $O
 B="python3 bench.py --no-cpu-baseline --no-e2e --no-legs"
 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/prof250 -o run -- $B > $O/prof250.log 2>&1 || { echo "prof250 rc $?"; exit 1; }
