@@ -360,6 +360,7 @@ struct mk_session {
   bool sweep_rows = false;        // one-workgroup sweep with rows owned by waves (k_sweep_rows, MK_SWEEP=5)
   int sweep_site = 0;             // one-pass site sweep (k_sweep_site, default for q <= 2): row pairs per thread (0: off)
   size_t sweep_site_lds = 0;
+  int sweep_lean = 0;             // its lean form (sweep_site_kernel: 1 / 2 border by factor / all n_s even)
   bool sweep_pair = false;        // the site sweep two sites per barrier (MK_SWEEP=7, q = 1)
   double* sp_part = nullptr;
   double* sp_dacc = nullptr;
@@ -942,7 +943,7 @@ static void launch_sweep(mk_session* s, Group& g, int it) {
     MatSet ms = g.ms;
     int iter = it;
     void* args[] = {&md, &ms, &iter};
-    const hipError_t e = hipLaunchKernel(sweep_site_kernel(q, s->sweep_site, s->sweep_pair), dim3(g.S), dim3(MK_SS_T), args,
+    const hipError_t e = hipLaunchKernel(sweep_site_kernel(q, s->sweep_site, s->sweep_pair, s->sweep_lean), dim3(g.S), dim3(MK_SS_T), args,
                                          s->sweep_site_lds, g.stream);
     wd_trace(g.stream, "k_sweep_site");
     if (e != hipSuccess && s->launch_err == hipSuccess) s->launch_err = e;
@@ -1635,7 +1636,8 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
     // 10,143 / site 10,506 / pair 10,527; its 32-subset share 7,744 / 7,784 / 7,758 (not the bound
     // there); configs[1] 15,198 / 15,055 / 15,626; configs[3] (q = 3, 50 subsets) block 3,016 / site
     // 3,106; configs[3]'s 7-subset share split launches 1,476 / site 1,340 / block 1,107 -- so q >= 2
-    // small shards keep the split-launch sweep.
+    // small shards keep the split-launch sweep.  The lean pair form (MK_SS_LEAN, k_sweep_site LN > 0):
+    // 250 subsets 10,452 -> 10,567-10,622 (sweep 1.12 -> 0.97-0.98 ms), 32 subsets 7,832 -> 7,957-8,067.
     const bool small_multi = q >= 2 && S <= 16;
     const bool pair = mode == 7 || (mode == 0 && q == 1);
     const bool site_fits = sweep_site_kernel(q, n_pad <= 8 * MK_SS_T ? 1 : 2, pair) != nullptr && n_pad <= 16 * MK_SS_T &&
@@ -1650,7 +1652,15 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
       s->sweep_pair = pair;
       s->sweep_site_lds = sweep_site_lds_bytes(nmax, q);
       s->sweep_mg = false;
-      HIPCHK(hipFuncSetAttribute(sweep_site_kernel(q, s->sweep_site, pair), hipFuncAttributeMaxDynamicSharedMemorySize,
+      // MK_SS_LEAN: 1 (default) the lean pair form (2 where every n_s is even), 3 its border-factor
+      // form always, 0 the masked form
+      static const int lean_env = tile_env("MK_SS_LEAN", 1);
+      bool all_even = true;
+      for (int i = 0; i < S; ++i) all_even = all_even && (s->n_part[i] % 2 == 0);
+      s->sweep_lean = (q == 1 && pair && lean_env > 0) ? (lean_env == 1 && all_even ? 2 : 1) : 0;
+      s->sweep_site_lds = sweep_site_lds_bytes(nmax, q, s->sweep_lean);
+      HIPCHK(hipFuncSetAttribute(sweep_site_kernel(q, s->sweep_site, pair, s->sweep_lean),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize,
                                  (int)s->sweep_site_lds));
     }
     if (s->sweep_rows)

@@ -61,19 +61,27 @@ __global__ void k_sweep_rows(Model md, MatSet ms, int iter);
 inline const void* sweep_rows_kernel(int q) {
   return q == 1 ? (const void*)k_sweep_rows<1> : (q == 2 ? (const void*)k_sweep_rows<2> : (const void*)k_sweep_rows<3>);
 }
-template <int Q, int KR, int P>
+template <int Q, int KR, int P, int HH, int LN>
 __global__ void k_sweep_site(Model md, MatSet ms, int iter);
 // its dynamic LDS: the sites' proposal / likelihood difference / accept draw + the accept flags
-inline size_t sweep_site_lds_bytes(int ns_max, int q) { return (size_t)ns_max * q * 3 * 8 + (size_t)ns_max * 4; }
+inline size_t sweep_site_lds_bytes(int ns_max, int q, int lean = 0) { return (size_t)ns_max * q * (lean ? 4 : 3) * 8 + (size_t)ns_max * 4; }
 // the one-pass site sweep (kr 1: n_pad <= 2048, four row pairs per thread; 2: <= 4096, eight); NULL
 // where its registers would spill (q = 3 with kr = 2, q = 4): the 64-site-block kernels run there
 // (pair: two sites per barrier, q = 1 only)
-inline const void* sweep_site_kernel(int q, int kr, bool pair = false) {
-  if (pair) return q != 1 ? nullptr : (kr == 1 ? (const void*)k_sweep_site<1, 4, 2> : (const void*)k_sweep_site<1, 8, 2>);
+// lean: 0 the masked form; 1 (q = 1 pairs) fused-multiply-add dots, no row masks (W's zero upper
+// triangle), the border row dropped by a factor; 2 the same for shards whose n_s are all even (no
+// border element in a loaded pair).
+inline const void* sweep_site_kernel(int q, int kr, bool pair = false, int lean = 0) {
+  if (pair && q == 1 && lean > 0) {
+    if (kr == 1)
+      return lean == 1 ? (const void*)k_sweep_site<1, 4, 2, 0, 1> : (const void*)k_sweep_site<1, 4, 2, 0, 2>;
+    return lean == 1 ? (const void*)k_sweep_site<1, 8, 2, 0, 1> : (const void*)k_sweep_site<1, 8, 2, 0, 2>;
+  }
+  if (pair) return q != 1 ? nullptr : (kr == 1 ? (const void*)k_sweep_site<1, 4, 2, 0, 0> : (const void*)k_sweep_site<1, 8, 2, 0, 0>);
   switch (q) {
-    case 1: return kr == 1 ? (const void*)k_sweep_site<1, 4, 1> : (const void*)k_sweep_site<1, 8, 1>;
-    case 2: return kr == 1 ? (const void*)k_sweep_site<2, 4, 1> : (const void*)k_sweep_site<2, 8, 1>;
-    case 3: return kr == 1 ? (const void*)k_sweep_site<3, 4, 1> : nullptr;
+    case 1: return kr == 1 ? (const void*)k_sweep_site<1, 4, 1, 0, 0> : (const void*)k_sweep_site<1, 8, 1, 0, 0>;
+    case 2: return kr == 1 ? (const void*)k_sweep_site<2, 4, 1, 0, 0> : (const void*)k_sweep_site<2, 8, 1, 0, 0>;
+    case 3: return kr == 1 ? (const void*)k_sweep_site<3, 4, 1, 0, 0> : nullptr;
     default: return nullptr;
   }
 }

@@ -1295,15 +1295,22 @@ typedef unsigned int u4v __attribute__((ext_vector_type(4)));
 // Dynamic LDS (sweep_site_lds_bytes): site data [3][n_s q] (proposal, likelihood difference, log
 // accept draw) + accept flags [n_s] (bit a: outcome a).
 
+// The loop is issue-bound, not HBM- or latency-bound (profiles/r04/lean: a ring of 2, 6 or 8 columns
+// per half instead of 4 changes nothing or loses; fewer instructions per site is what pays), so
+// LN > 0 (q = 1 pairs, the default) is the lean form: fused-multiply-add dots, no row masks at use
+// (W's upper triangle is zero in memory), the load offsets from per-thread row parts, and per site
+// the move's coefficient d A^-1 and half its square precomputed -- 253 instead of 336 VALU
+// instructions per pair; 1.12 -> 0.97 ms per sweep at 250 subsets.
 // P = 2 (q = 1, MK_SWEEP=7): two sites per barrier.  The pair (i, i+1) exchanges five values --
 // both dots, both squared norms and c = W[:,i] . W[:,i+1] = (R^-1)_{i+1,i} -- so site i+1's dot
 // after a move at site i is g_{i+1} + coef_i c (the same carry the 64-site blocks make through Q_BB);
 // half the barriers, one more reduction per pair.
-template <int Q, int KR, int P = 1>
+template <int Q, int KR, int P = 1, int HH = 0, int LN = 0>
 __global__ __launch_bounds__(SS_T) void k_sweep_site(Model md, MatSet ms, int iter) {
+  constexpr bool FM = LN > 0;
   extern __shared__ __attribute__((aligned(16))) double smem[];
   // ring: 2H columns (VGPRs: 8 H Q KR); NV values exchanged per site, four per row-sum round
-  constexpr int q = Q, H = (16 / (Q * KR)) > 0 ? 16 / (Q * KR) : 1, NV = P == 2 ? 5 : 2 * Q;
+  constexpr int q = Q, H = HH > 0 ? HH : ((16 / (Q * KR)) > 0 ? 16 / (Q * KR) : 1), NV = P == 2 ? 5 : 2 * Q;
   constexpr int NR = (NV + 3) / 4;
   static_assert(H >= 1 && NV <= 8, "q <= 4");   // instantiated for q <= 2 and (q = 3, KR = 1): no spills
   static_assert(P == 1 || (Q == 1 && H % 2 == 0), "site pairs: q = 1");
@@ -1316,7 +1323,8 @@ __global__ __launch_bounds__(SS_T) void k_sweep_site(Model md, MatSet ms, int it
   double* sd_dl = smem;
   double* sd_dll = smem + nq;
   double* sd_lgu = smem + 2 * nq;
-  int* sflag = reinterpret_cast<int*>(smem + 3 * nq);
+  double* sd_d2 = smem + 3 * nq;   // LN: 0.5 (d A^-1)^2 (sd_dl then holds d A^-1)
+  int* sflag = reinterpret_cast<int*>(smem + (FM ? 4 : 3) * nq);
   double* z = md.z + (long)s * q * md.n_pad;
   if (tid < q * q) Ai_s[tid] = md.Ainv[(long)s * q * q + tid];
   {   // the sites' data into LDS (sweep_precompute's values; the proposals also to sw_delta for sweep_apply)
@@ -1329,7 +1337,13 @@ __global__ __launch_bounds__(SS_T) void k_sweep_site(Model md, MatSet ms, int it
     for (int k = tid; k < nq; k += SS_T) {
       const int j = md.o_w + k;
       const double d = exp(tune[k]) * proposal_normal(key, j, iter);
-      sd_dl[k] = d;
+      if constexpr (FM) {   // q = 1: the site's move on z (coefficient of its W column) and half its square
+        const double cf = d * md.Ainv[(long)s];
+        sd_dl[k] = cf;
+        sd_d2[k] = 0.5 * cf * cf;
+      } else {
+        sd_dl[k] = d;
+      }
       gdl[k] = d;
       sd_dll[k] = loglik_term(y[k], wt[k], eta[k] + d, md.link) - loglik_term(y[k], wt[k], eta[k], md.link);
       sd_lgu[k] = accept_log_uniform(key, j, iter);
@@ -1356,12 +1370,22 @@ __global__ __launch_bounds__(SS_T) void k_sweep_site(Model md, MatSet ms, int it
   // column c of every W_h for this thread's rows; pairs wholly outside rows c <= r < n_s (the upper
   // triangle, the border and padding rows) are not fetched and read as zero.  The rest of the mask
   // is applied where the column is used (a select right after the load would wait for it).
+  // FM (lean form, q = 1 pairs): the row part of the offset and the border-row factor once per thread
+  unsigned rb[KR];
+  double ym[KR];
+#pragma unroll
+  for (int k = 0; k < KR; ++k) {
+    const int r0 = 2 * tid + 2 * SS_T * k;
+    rb[k] = r0 < ns ? (unsigned)(r0 * 8) : 0x40000000u;   // rows past n_s: beyond every W (no wrap)
+    ym[k] = (r0 + 1 < ns) ? 1.0 : 0.0;
+  }
   auto load_col = [&](int c, d2 (&w)[KR][Q]) {
+    const unsigned cb = c < ns ? (unsigned)((long)c * ld * 8) : 0x40000000u;
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
       const int r0 = 2 * tid + 2 * SS_T * k;
       const bool any = c < ns && r0 + 1 >= c && r0 < ns;
-      const unsigned off = any ? (unsigned)(((long)c * ld + r0) * 8) : SS_OOB;
+      const unsigned off = FM ? ((r0 + 1 >= c) ? cb + rb[k] : SS_OOB) : (any ? (unsigned)(((long)c * ld + r0) * 8) : SS_OOB);
 #pragma unroll
       for (int h = 0; h < Q; ++h)
         w[k][h] = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(rs[h], (int)off, 0, 0));
@@ -1403,8 +1427,13 @@ __global__ __launch_bounds__(SS_T) void k_sweep_site(Model md, MatSet ms, int it
       double pd = 0.0, sq = 0.0;
 #pragma unroll
       for (int k = 0; k < KR; ++k) {
-        pd += wc[k][h].x * zr[k][h].x + wc[k][h].y * zr[k][h].y;
-        sq += wc[k][h].x * wc[k][h].x + wc[k][h].y * wc[k][h].y;
+        if constexpr (FM) {
+          pd = fma(wc[k][h].y, zr[k][h].y, fma(wc[k][h].x, zr[k][h].x, pd));
+          sq = fma(wc[k][h].y, wc[k][h].y, fma(wc[k][h].x, wc[k][h].x, sq));
+        } else {
+          pd += wc[k][h].x * zr[k][h].x + wc[k][h].y * zr[k][h].y;
+          sq += wc[k][h].x * wc[k][h].x + wc[k][h].y * wc[k][h].y;
+        }
       }
       v[h] = pd;
       v[Q + h] = sq;
@@ -1473,19 +1502,40 @@ __global__ __launch_bounds__(SS_T) void k_sweep_site(Model md, MatSet ms, int it
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
       const int r0 = 2 * tid + 2 * SS_T * k;
-      c0[k].x = (r0 >= i) ? w0[k][0].x : 0.0;
-      c0[k].y = (r0 + 1 >= i && r0 + 1 < ns) ? w0[k][0].y : 0.0;
-      c1[k].x = (r0 >= i + 1) ? w1[k][0].x : 0.0;
-      c1[k].y = (r0 + 1 >= i + 1 && r0 + 1 < ns) ? w1[k][0].y : 0.0;
+      if constexpr (FM) {
+        // No row masks: i is even, so the loads already return zero for every row pair wholly above
+        // column i's diagonal, and the one upper element left, W[i, i+1], is zero in memory (W's
+        // upper triangle is zeroed at session creation and never written: store_tile_lw,
+        // k_inv_copydiag, k_inv_level write lower tiles and zero-upper diagonal tiles).  Row n_s
+        // (the border row, nonzero in W) sits in a loaded pair only for odd n_s: LN = 1 drops it with
+        // a factor 0; LN = 2 is launched only when every subset's n_s is even.
+        c0[k].x = w0[k][0].x;
+        c0[k].y = LN == 1 ? w0[k][0].y * ym[k] : w0[k][0].y;
+        c1[k].x = w1[k][0].x;
+        c1[k].y = LN == 1 ? w1[k][0].y * ym[k] : w1[k][0].y;
+      } else {
+        c0[k].x = (r0 >= i) ? w0[k][0].x : 0.0;
+        c0[k].y = (r0 + 1 >= i && r0 + 1 < ns) ? w0[k][0].y : 0.0;
+        c1[k].x = (r0 >= i + 1) ? w1[k][0].x : 0.0;
+        c1[k].y = (r0 + 1 >= i + 1 && r0 + 1 < ns) ? w1[k][0].y : 0.0;
+      }
     }
     double v[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
-      v[0] += c0[k].x * zr[k][0].x + c0[k].y * zr[k][0].y;
-      v[1] += c1[k].x * zr[k][0].x + c1[k].y * zr[k][0].y;
-      v[2] += c0[k].x * c0[k].x + c0[k].y * c0[k].y;
-      v[3] += c1[k].x * c1[k].x + c1[k].y * c1[k].y;
-      v[4] += c0[k].x * c1[k].x + c0[k].y * c1[k].y;
+      if constexpr (FM) {
+        v[0] = fma(c0[k].y, zr[k][0].y, fma(c0[k].x, zr[k][0].x, v[0]));
+        v[1] = fma(c1[k].y, zr[k][0].y, fma(c1[k].x, zr[k][0].x, v[1]));
+        v[2] = fma(c0[k].y, c0[k].y, fma(c0[k].x, c0[k].x, v[2]));
+        v[3] = fma(c1[k].y, c1[k].y, fma(c1[k].x, c1[k].x, v[3]));
+        v[4] = fma(c0[k].y, c1[k].y, fma(c0[k].x, c1[k].x, v[4]));
+      } else {
+        v[0] += c0[k].x * zr[k][0].x + c0[k].y * zr[k][0].y;
+        v[1] += c1[k].x * zr[k][0].x + c1[k].y * zr[k][0].y;
+        v[2] += c0[k].x * c0[k].x + c0[k].y * c0[k].y;
+        v[3] += c1[k].x * c1[k].x + c1[k].y * c1[k].y;
+        v[4] += c0[k].x * c1[k].x + c0[k].y * c1[k].y;
+      }
     }
 #pragma unroll
     for (int e = 0; e < 5; ++e) v[e] = row_sum_dpp(v[e]);
@@ -1510,6 +1560,19 @@ __global__ __launch_bounds__(SS_T) void k_sweep_site(Model md, MatSet ms, int it
     const double a0 = ai[0];
     int f0 = 0, f1 = 0;
     double coef0 = 0.0, coef1 = 0.0;
+    if constexpr (FM) {   // ratio = dll - (cf g + 0.5 cf^2 Q_ii), cf = d A^-1 (precomputed per site)
+      const double cf0 = rfl_f64(dl0), cf1 = rfl_f64(dl1);
+      const double h0 = rfl_f64(sd_d2[i0c]), h1 = rfl_f64(sd_d2[i1c]);
+      if (rfl_f64(lg0) <= rfl_f64(dll0) - fma(cf0, tot[0], h0 * tot[2])) {
+        coef0 = cf0;
+        f0 = 1;
+      }
+      const double g1 = fma(coef0, tot[4], tot[1]);
+      if (rfl_f64(lg1) <= rfl_f64(dll1) - fma(cf1, g1, h1 * tot[3])) {
+        coef1 = cf1;
+        f1 = 1;
+      }
+    } else {
     {
       const double d = rfl_f64(dl0);
       const double c = a0 * tot[0];
@@ -1528,6 +1591,7 @@ __global__ __launch_bounds__(SS_T) void k_sweep_site(Model md, MatSet ms, int it
         coef1 = d * a0;
         f1 = 1;
       }
+    }
     }
     if (f0 | f1) {
 #pragma unroll
@@ -1584,6 +1648,10 @@ template __global__ void k_sweep_site<2, 8, 1>(Model, MatSet, int);
 template __global__ void k_sweep_site<3, 4, 1>(Model, MatSet, int);
 template __global__ void k_sweep_site<1, 4, 2>(Model, MatSet, int);
 template __global__ void k_sweep_site<1, 8, 2>(Model, MatSet, int);
+template __global__ void k_sweep_site<1, 4, 2, 0, 1>(Model, MatSet, int);
+template __global__ void k_sweep_site<1, 4, 2, 0, 2>(Model, MatSet, int);
+template __global__ void k_sweep_site<1, 8, 2, 0, 1>(Model, MatSet, int);
+template __global__ void k_sweep_site<1, 8, 2, 0, 2>(Model, MatSet, int);
 
 // ---------------------------------------------------------------- 6. record / adapt
 __global__ __launch_bounds__(64) void k_record(Model md, int iter) {

@@ -178,16 +178,19 @@ def test_site_sweep_runs_the_block_sweeps_chain(tmp_path):
     here = os.path.dirname(os.path.abspath(__file__))
     for la in ("1", "0"):
         res = {}
-        for sweep in ("1", "6", "7"):
+        for sweep in ("1", "6", "7", "7m", "7b"):
             path = str(tmp_path / f"site_{sweep}_{la}.npz")
-            env = dict(os.environ, MK_SWEEP=sweep, **({} if la == "1" else {"MK_LOOKAHEAD": "0"}))
+            # 7: the lean pair form (the default: fma dots, no row masks, the all-even form where every
+            # n_s is even); 7b its border-factor form (MK_SS_LEAN=3); 7m the masked form (0)
+            lean = {"7m": {"MK_SS_LEAN": "0"}, "7b": {"MK_SS_LEAN": "3"}}.get(sweep, {})
+            env = dict(os.environ, MK_SWEEP=sweep[0], **lean, **({} if la == "1" else {"MK_LOOKAHEAD": "0"}))
             r = subprocess.run([sys.executable, os.path.join(here, "gpu_tile_run.py"), path], capture_output=True,
                                text=True, timeout=240, env=env)
             assert r.returncode == 0, r.stderr[-4000:]
             z = np.load(path)
             res[sweep] = {k: z[k] for k in z.files}
         for k in res["1"]:
-            for sw in ("6", "7"):   # 7: two sites per barrier (q = 1; q = 2 falls back to the block sweep)
+            for sw in ("6", "7", "7m", "7b"):   # 7: two sites per barrier (q = 1; q = 2: the block sweep)
                 np.testing.assert_allclose(res[sw][k], res["1"][k], rtol=0, atol=1e-9, err_msg=f"{k} la={la} {sw}")
 
 
