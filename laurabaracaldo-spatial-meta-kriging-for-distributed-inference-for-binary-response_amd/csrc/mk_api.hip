@@ -890,10 +890,10 @@ static bool la_auto(const mk_session* s) { return (long)s->S * s->q <= 224; }
 // sweep (q W panels per block, q x 64 MH steps) is the iteration's longest chain and the
 // cooperative kernel wins: q = 3, 7 subsets 1,050 -> 1,601, 13 subsets 1,553 -> 1,956 subset-iters/s
 // (25 subsets: equal).
-// The cooperative kernel's q >= 2 gain is not taken by default: runs of the GPU suite with it
-// stalled in session create / destroy.  q >= 2 small shards use the split-launch
-// sweep instead (no inter-workgroup waits; q = 3: 7 subsets 1,050 -> 1,213, 13 subsets 1,553 ->
-// 1,657 subset-iters/s, r03b); MK_SWEEP=2 opts in to the cooperative kernel.
+// Rounds 2-3 did not take the cooperative kernel's q >= 2 gain by default (GPU-suite stalls, DESIGN.md
+// 4.2 10, whose cause round 4 found: 4.5) and ran split launches there (q = 3: 7 subsets 1,050 ->
+// 1,213, 13 subsets 1,553 -> 1,657 subset-iters/s, r03b); since round 4 the cooperative kernel is
+// the default for q >= 2 small shards again (MK_SWEEP=3 selects the split launches).
 static bool use_sweep_mg(const mk_session* s) { return s->sweep_mg && (!s->la || s->sweep_mg_forced); }
 
 static void launch_sweep(mk_session* s, Group& g, int it) {
@@ -1620,12 +1620,11 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
     const int mode = tile_env("MK_SWEEP", 0);
     const bool fits = coop && grid <= (long)per_cu * n_cu && nt <= 32;
     // MK_SWEEP: 1 one workgroup per subset, 2 cooperative multi-workgroup, 3 split launches (one per
-    // block), 4 split launches (two per block); 0 (default): split launches for multi-outcome small
-    // shards (q >= 2, <= 16 subsets: the one-workgroup sweep's q x 64 MH steps and q W panels per
-    // block on one CU per subset are the iteration's longest chain), else one workgroup per subset.
-    // No default path launches a kernel whose workgroups wait on each other: the cooperative kernel
-    // (opt-in) was followed by intermittent stalls of the GPU suite -- once more in
-    // round 3, on the sequential schedule where it had been the default for <= 64 subsets.
+    // block), 4 split launches (two per block); 0 (default): for multi-outcome small shards (q >= 2,
+    // <= 16 subsets: the one-workgroup sweep's q x 64 MH steps and q W panels per block on one CU per
+    // subset are the iteration's longest chain) the cooperative kernel where it fits, else split
+    // launches; one workgroup per subset elsewhere.  (Rounds 2-3 kept the cooperative kernel opt-in
+    // after intermittent GPU-suite stalls; their cause is in DESIGN.md 4.5.)
     // MK_SWEEP=6 and the default (0): the one-pass site sweep (k_sweep_site; W read once, no Q_BB
     // tiles, no inter-workgroup waits) wherever it fits: n_pad <= 4096 (q = 4: 2048) and the sites'
     // data in LDS (configs[3]: n_s = 2,000, q = 3 takes 152 KB).  1-5 select the 64-site-block kernels,
@@ -1643,9 +1642,17 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
     const bool site_fits = sweep_site_kernel(q, n_pad <= 8 * MK_SS_T ? 1 : 2, pair) != nullptr && n_pad <= 16 * MK_SS_T &&
                            sweep_site_lds_bytes(nmax, q) <= 156 * 1024;
     const bool site = ((mode == 0 && !small_multi) || mode == 6 || mode == 7) && site_fits;
-    s->sweep_split = mode == 3 || mode == 4 || (mode == 0 && !site && small_multi);
+    // Round 4: multi-outcome small shards take the cooperative sweep by default where its grid fits the
+    // CUs the lookahead mask leaves (configs[3]'s 7-subset share: 1,468-1,489 split launches ->
+    // 1,687-1,699 subset-iters/s, profiles/r04/lean/r04m_*).  The suite stalls that kept it opt-in
+    // shared one cause with RCCL's init failure -- a second HIP runtime in the process,
+    // gone since round 4 -- and the stall watchdog names the kernel of any future one.
+    const int mask_cu = tile_env("MK_LA_MASK", 32);
+    const bool coop_fits = fits && grid <= (long)per_cu * std::max(0, n_cu - mask_cu);
+    const bool coop_default = mode == 0 && !site && small_multi && coop_fits;
+    s->sweep_split = mode == 3 || mode == 4 || (mode == 0 && !site && small_multi && !coop_default);
     s->sweep_step = s->sweep_split && mode != 4 && nt <= 32;   // k_sweep_step sums <= 32 tile partials
-    s->sweep_mg = !s->sweep_split && fits && mode == 2;
+    s->sweep_mg = !s->sweep_split && fits && (mode == 2 || coop_default);
     s->sweep_rows = mode == 5 && q <= 3 && nt <= 32;
     if (site) {
       s->sweep_site = n_pad <= 8 * MK_SS_T ? 1 : 2;
@@ -1668,8 +1675,7 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
                                  q * (64 * 64 + 2 * 64) * 8 + nt * q * 64 * 8));
     // under the lookahead schedule the sweep runs on the CU-masked main stream, beside the candidates'
     // chain: MK_SWEEP=2 is honoured there only when its grid fits the CUs that mask leaves
-    const int mask_cu = tile_env("MK_LA_MASK", 32);
-    s->sweep_mg_forced = s->sweep_mg && mode == 2 && grid <= (long)per_cu * std::max(0, n_cu - mask_cu);
+    s->sweep_mg_forced = s->sweep_mg && (mode == 2 || coop_default) && coop_fits;
     if (s->sweep_split) {
       HIPCHK(hipFuncSetAttribute(sweep_split_kernel(q, true), hipFuncAttributeMaxDynamicSharedMemorySize,
                                  q * (64 * 64 + 2 * 64) * 8));

@@ -130,9 +130,11 @@ def test_sub_tile_gemm_split_cholesky_and_multi_wg_sweep_are_bit_identical(tmp_p
     res = {}
     # gi: the kriging GEMM raster (MK_PRED_GI row panels per group; placement only).  la: the launch
     # schedule; the two schedules agree to rounding, not bit for bit, so each configuration is
-    # compared with the reference of its schedule.  The cooperative sweep (MK_SWEEP=2) is opt-in and
-    # not exercised here (intermittent suite stalls after such launches).
+    # compared with the reference of its schedule.  MK_SWEEP=2: the cooperative multi-workgroup sweep
+    # (the default for q >= 2 small shards since round 4).
     configs = (("128", "1", "0", "0", "0", "2", "1", "1"),
+               ("128", "2", "0", "0", "0", "2", "1", "1"),
+               ("128", "2", "0", "0", "0", "2", "1", "0"),
                ("64", "3", "1", "0", "0", "1", "4", "0"),
                ("64", "1", "0", "0", "0", "2", "3", "1"),
                ("32", "1", "1", "0", "1", "2", "4", "1"),
