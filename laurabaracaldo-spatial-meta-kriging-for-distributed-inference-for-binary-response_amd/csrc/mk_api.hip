@@ -219,9 +219,21 @@ typedef std::vector<std::pair<PoolKey, hipStream_t>> StreamList;
 static std::mutex g_pool_mu;
 static StreamList g_pool;        // idle streams
 static bool g_pool_closed = false;   // mk_shutdown ran: returned streams are destroyed, not pooled
+static std::vector<int> g_pool_count;   // streams of the pool in existence per device (idle or owned)
+static int hw_queues();
+static int tile_env(const char* name, int dflt);
+
+static int& pool_count(int device) {   // g_pool_mu held
+  if ((int)g_pool_count.size() <= device) g_pool_count.resize(device + 1, 0);
+  return g_pool_count[device];
+}
 
 // Drain and destroy one stream on its device (the calling thread's device is restored).
 static void stream_destroy(const PoolKey& k, hipStream_t st) {
+  {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    --pool_count(k.device);
+  }
   DeviceGuard dg;
   if (hipSetDevice(k.device) == hipSuccess) {
     (void)hipStreamSynchronize(st);
@@ -259,6 +271,7 @@ static hipError_t pool_stream(StreamList& owned, hipStream_t* st, int device, in
   k.kind = kind;
   k.prio = prio;
   k.mask = mask;
+  StreamList evict;
   {
     std::lock_guard<std::mutex> lk(g_pool_mu);
     for (size_t i = 0; i < g_pool.size(); ++i)
@@ -268,7 +281,28 @@ static hipError_t pool_stream(StreamList& owned, hipStream_t* st, int device, in
         owned.push_back({k, *st});
         return hipSuccess;
       }
+    // No exact match: a session of another configuration (another shard size needs another CU mask).
+    // Idle streams left by earlier sessions still hold hardware queues, and a new queue among them
+    // ends up sharing one with another stream (serialising the split Cholesky's streams: 5,427 ->
+    // 4,087 subset-iters/s at 32 subsets) -- well before GPU_MAX_HW_QUEUES streams exist: configs[1]
+    // after the 32-subset shard in one process ran 15,045-15,356 -> 12,659-13,189 subset-iters/s,
+    // configs[3]'s share 1,666-1,701 -> 1,092.  So the idle streams on the device go (oldest first)
+    // until at most MK_POOL_CAP - 1 streams remain besides the new one (default 1: every idle one;
+    // measured cap 8 / 5 / 1: 12,659 / 15,261 / 15,532 and 1,092 / 1,678 / 1,714,
+    // profiles/r04/pool/).  Repeated sessions of one configuration still reuse their queues.
+    static const int cap_env = tile_env("MK_POOL_CAP", 1);
+    int over = pool_count(device) + 1 - std::max(1, cap_env);
+    for (size_t i = 0; i < g_pool.size() && over > 0;) {
+      if (g_pool[i].first.device == device) {
+        evict.push_back(g_pool[i]);
+        g_pool.erase(g_pool.begin() + (long)i);
+        --over;
+      } else {
+        ++i;
+      }
+    }
   }
+  for (auto& o : evict) stream_destroy(o.first, o.second);
   hipError_t e;
   if (kind == SK_CUMASK) {
     // cuMaskSize = the device's CU count (as before the pool); the array is padded to that many
@@ -284,6 +318,10 @@ static hipError_t pool_stream(StreamList& owned, hipStream_t* st, int device, in
   }
   if (e == hipSuccess) {
     owned.push_back({k, *st});
+    {
+      std::lock_guard<std::mutex> lk(g_pool_mu);
+      ++pool_count(device);
+    }
     static std::once_flag at_exit;
     std::call_once(at_exit, [] { std::atexit(shutdown_at_exit); });
   }

@@ -2,7 +2,7 @@
 # Round 4 pass on the chosen defaults: suite, smoke, the default bench (all legs, CPU baseline, end to
 # end), rocprofv3 kernel stats at 250 and 32 subsets, FETCH / WRITE passes at 250.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/r04f
+O=${O:-gpurun_out/r04f}
 mkdir -p $O
 timeout -k 10 420 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/gpu_tests.log 2>&1 || { echo "suite rc $?"; tail -30 $O/gpu_tests.log; exit 1; }
 tail -1 $O/gpu_tests.log
