@@ -395,15 +395,16 @@ def main():
         legs["configs[2]_share32"] = shard_leg(mk, d, idx, min(a.shard_subsets, K), beta0, bt, a.adapt_batches, a.warmup, ls)
         legs["configs[1]_matern"] = config_leg(mk, 1, a.adapt_batches, a.warmup, ls)
         legs["configs[3]_lmc_share7"] = config_leg(mk, 3, a.adapt_batches, a.warmup, ls, subsets=7)
+    e2e = None
+    if world == 1 and not a.no_e2e:
+        e2e = end_to_end(mk, d, K, tuple(int(x) for x in a.e2e_devices.split(",")))
+    if world == 1 and not a.no_legs:
         # the 1M-site kriging leg last: window legs run after it in one process measured 12-20 % slower
-        # (not the stream pool), so it cannot colour them
+        # (not the stream pool), so it cannot colour them or the end-to-end leg
         import bench_kriging
         kr_sites = np.random.default_rng(20250115).uniform(size=(a.krig_sites, 2))   # configs[4]: 1M held-out sites
         kr_subs = [mk.subset_data(d["y"], d["x"], 1.0, d["coords"], 1, idx[i]) for i in range(min(a.krig_subsets, K))]
         legs["configs[4]_kriging"] = bench_kriging.kriging_leg(mk, kr_subs, kr_sites, beta0, bt)
-    e2e = None
-    if world == 1 and not a.no_e2e:
-        e2e = end_to_end(mk, d, K, tuple(int(x) for x in a.e2e_devices.split(",")))
     elif world > 1 and not a.no_e2e and not weak:
         if rank == 0:
             e2e = node_end_to_end(a, world)
