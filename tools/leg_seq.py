@@ -28,6 +28,14 @@ for tag in sys.argv[1:]:
         _, idx = mk.partition(500_000, 250, seed=20250114, method="R")
         b0, bt = mk.start_values(d["y"], d["x"], 1.0, 1)
         r = bench.shard_leg(mk, d, idx, 250, b0, bt, 6, 3, 20)
+    elif tag == "k100":   # the kriging leg with 100,000 sites (a tenth of the buffers)
+        import bench_kriging
+        d = mk.synthetic.generate(64_000, q=1, n_test=1000, seed=20250114)
+        _, idx = mk.partition(64_000, 32, seed=20250114, method="R")
+        b0, bt = mk.start_values(d["y"], d["x"], 1.0, 1)
+        sites = np.random.default_rng(20250115).uniform(size=(100_000, 2))
+        subs = [mk.subset_data(d["y"], d["x"], 1.0, d["coords"], 1, idx[i]) for i in range(32)]
+        r = bench_kriging.kriging_leg(mk, subs, sites, b0, bt)
     elif tag == "k":
         import bench_kriging
         d = mk.synthetic.generate(64_000, q=1, n_test=1000, seed=20250114)
