@@ -4,6 +4,8 @@ geometries whose long-chain behaviour that fixture does not cover:
 
   cfg2_matern  BASELINE.json configs[1] geometry: Matern (nu free, U(0.1, 2)), q = 1, subsets of
                n_s = 1,000 (configs[1]'s subset size), K = 3, exact Matern GP field (nu = 0.5)
+  cfg3_exp     BASELINE.json configs[2] geometry: exponential, q = 1, subsets of n_s = 2,000 (the
+               headline's subset size), K = 3
   cfg4_lmc     BASELINE.json configs[3] geometry: q = 3 LMC (3n x 3n blocks), exponential,
                subsets of n_s = 500, K = 2, exact LMC field (beta)
 
@@ -15,6 +17,7 @@ combined result / result2.  The reference holds no fixtures and spBayes is absen
 this pins the device to the build's own oracle, not to spBayes.
 
     python tests/golden/stat/make_meta_fixture.py cfg2_matern   (~25 min on 3 cores: scipy kv)
+    python tests/golden/stat/make_meta_fixture.py cfg3_exp      (~3 min on 3 cores)
     python tests/golden/stat/make_meta_fixture.py cfg4_lmc      (~3 min on 2 cores)
 """
 import os
@@ -32,6 +35,7 @@ PKG = "laurabaracaldo-spatial-meta-kriging-for-distributed-inference-for-binary-
 
 CASES = {
     "cfg2_matern": dict(n=3000, K=3, q=1, cov_model=1, n_test=200),
+    "cfg3_exp": dict(n=6000, K=3, q=1, cov_model=0, n_test=200),
     "cfg4_lmc": dict(n=1000, K=2, q=3, cov_model=0, n_test=200),
 }
 N_BATCH, BATCH_LENGTH, SEED = 20, 50, 20250114
