@@ -919,6 +919,10 @@ static void launch_pred_refresh(mk_session* s, Group& g, hipStream_t st = nullpt
 // 7,719, 125 7,486 -> 8,303, 188 8,071 -> 8,486 subset-iters/s); at 250 subsets both saturate the
 // chip and the sequential schedule is as fast (8,572 vs 8,553-8,565) while its panel-update
 // launches run alone (roofline timing 0.71 of peak vs 0.52-0.57 beside the main stream's kernels).
+// Round 4 (lean sweep): at 250 subsets the lookahead schedule gains 0.9 % (10,574-10,579 sequential vs
+// 10,660-10,686, three interleaved 40-step windows each, profiles/r04/la250/) but its update launches
+// share the chip, so each launch's own rate reads ~0.55 instead of ~0.70 of peak; the sequential
+// schedule stays the default there (MK_LOOKAHEAD=1 takes the 0.9 %).
 static bool la_auto(const mk_session* s) { return (long)s->S * s->q <= 224; }
 
 // Under the lookahead schedule the one-workgroup kernel is the default for q = 1: the cooperative
