@@ -1493,7 +1493,22 @@ __global__ __launch_bounds__(SS_T) void k_sweep_site(Model md, MatSet ms, int it
     if (tid == 0 && live) sflag[i] = fl;
   };
   // sites i, i + 1 (q = 1): one exchange, the carry of site i's move into site i + 1's dot
+  // LN: the sites' data in registers, lane l holding site 64 b + l of the current block of 64 (refilled
+  // from LDS at each block's first pair); a pair reads its two sites with v_readlane at a uniform lane
+  // index instead of LDS reads, address arithmetic and readfirstlanes.  Sites past n_s: accept draw +inf.
+  double vcf = 0.0, vdll = 0.0, vh = 0.0, vlg = __builtin_huge_val();
   auto pair_step = [&](const int i, d2 (&w0)[KR][Q], d2 (&w1)[KR][Q]) {
+    if constexpr (FM) {
+      if ((i & 63) == 0) {   // uniform
+        const int kk = i + lane;
+        const bool lv = kk < ns;
+        const int kc = lv ? kk : ns - 1;
+        vcf = sd_dl[kc];
+        vdll = sd_dll[kc];
+        vh = sd_d2[kc];
+        vlg = lv ? sd_lgu[kc] : __builtin_huge_val();
+      }
+    }
     const bool live0 = i < ns, live1 = i + 1 < ns;
     const int i0c = live0 ? i : ns - 1, i1c = live1 ? i + 1 : ns - 1;
     const double dl0 = sd_dl[i0c], dll0 = sd_dll[i0c], lg0 = live0 ? sd_lgu[i0c] : __builtin_huge_val();
@@ -1561,14 +1576,15 @@ __global__ __launch_bounds__(SS_T) void k_sweep_site(Model md, MatSet ms, int it
     int f0 = 0, f1 = 0;
     double coef0 = 0.0, coef1 = 0.0;
     if constexpr (FM) {   // ratio = dll - (cf g + 0.5 cf^2 Q_ii), cf = d A^-1 (precomputed per site)
-      const double cf0 = rfl_f64(dl0), cf1 = rfl_f64(dl1);
-      const double h0 = rfl_f64(sd_d2[i0c]), h1 = rfl_f64(sd_d2[i1c]);
-      if (rfl_f64(lg0) <= rfl_f64(dll0) - fma(cf0, tot[0], h0 * tot[2])) {
+      const int l0 = i & 63, l1 = l0 + 1;
+      const double cf0 = rlane_u(vcf, l0), cf1 = rlane_u(vcf, l1);
+      const double h0 = rlane_u(vh, l0), h1 = rlane_u(vh, l1);
+      if (rlane_u(vlg, l0) <= rlane_u(vdll, l0) - fma(cf0, tot[0], h0 * tot[2])) {
         coef0 = cf0;
         f0 = 1;
       }
       const double g1 = fma(coef0, tot[4], tot[1]);
-      if (rfl_f64(lg1) <= rfl_f64(dll1) - fma(cf1, g1, h1 * tot[3])) {
+      if (rlane_u(vlg, l1) <= rlane_u(vdll, l1) - fma(cf1, g1, h1 * tot[3])) {
         coef1 = cf1;
         f1 = 1;
       }
