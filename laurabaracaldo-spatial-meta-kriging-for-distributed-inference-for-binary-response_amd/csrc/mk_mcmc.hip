@@ -1293,14 +1293,16 @@ typedef unsigned int u4v __attribute__((ext_vector_type(4)));
 #define SS_CFENCE() asm volatile("" ::: "memory")
 
 // Dynamic LDS (sweep_site_lds_bytes): site data [3][n_s q] (proposal, likelihood difference, log
-// accept draw) + accept flags [n_s] (bit a: outcome a).
+// accept draw; LN > 0: [4], the proposal as its coefficient d A^-1 plus half its square) + accept
+// flags [n_s] (bit a: outcome a).
 
 // The loop is issue-bound, not HBM- or latency-bound (profiles/r04/lean: a ring of 2, 6 or 8 columns
 // per half instead of 4 changes nothing or loses; fewer instructions per site is what pays), so
 // LN > 0 (q = 1 pairs, the default) is the lean form: fused-multiply-add dots, no row masks at use
 // (W's upper triangle is zero in memory), the load offsets from per-thread row parts, and per site
 // the move's coefficient d A^-1 and half its square precomputed -- 253 instead of 336 VALU
-// instructions per pair; 1.12 -> 0.97 ms per sweep at 250 subsets.
+// instructions per pair; 1.12 -> 0.97 ms per sweep at 250 subsets, 0.92-0.94 ms with the sites' data
+// read from registers (pair_step).
 // P = 2 (q = 1, MK_SWEEP=7): two sites per barrier.  The pair (i, i+1) exchanges five values --
 // both dots, both squared norms and c = W[:,i] . W[:,i+1] = (R^-1)_{i+1,i} -- so site i+1's dot
 // after a move at site i is g_{i+1} + coef_i c (the same carry the 64-site blocks make through Q_BB);
