@@ -276,6 +276,20 @@ def end_to_end(mk, d, K, devices=(0,)):
             "param_median": summ["param_quant"][0].tolist()}
 
 
+def kriging_leg_process(subsets, sites):
+    """bench_kriging.py's configs[4] leg (tiled spPredict of `sites` test sites from `subsets` subsets)
+    run as a child process; its JSON line, or the error."""
+    import subprocess
+    cmd = [sys.executable, os.path.join(ROOT, "bench_kriging.py"), "--subsets", str(subsets), "--n-test", str(sites)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    if r.returncode != 0 or not lines:
+        return {"error": f"bench_kriging.py rc {r.returncode}: {r.stderr[-2000:]}"}
+    res = json.loads(lines[-1])
+    res["process"] = "child (bench_kriging.py)"
+    return res
+
+
 def node_end_to_end(a, world):
     """N > 1 (strong scaling): the same whole configs[2] script over the node's N GPUs through
     mk_meta_fit (libmk's threads, RCCL combine) -- a fresh child process, started (not exec'd)
@@ -399,12 +413,11 @@ def main():
     if world == 1 and not a.no_e2e:
         e2e = end_to_end(mk, d, K, tuple(int(x) for x in a.e2e_devices.split(",")))
     if world == 1 and not a.no_legs:
-        # the 1M-site kriging leg last: window legs run after it in one process measured 12-20 % slower
-        # (not the stream pool), so it cannot colour them or the end-to-end leg
-        import bench_kriging
-        kr_sites = np.random.default_rng(20250115).uniform(size=(a.krig_sites, 2))   # configs[4]: 1M held-out sites
-        kr_subs = [mk.subset_data(d["y"], d["x"], 1.0, d["coords"], 1, idx[i]) for i in range(min(a.krig_subsets, K))]
-        legs["configs[4]_kriging"] = bench_kriging.kriging_leg(mk, kr_subs, kr_sites, beta0, bt)
+        # the 1M-site kriging leg in a fresh process (bench_kriging.py: the same kriging_leg on 32
+        # subsets of n_s = 2,000 from the same generator): sessions that follow one another in a process
+        # can inherit the HIP runtime's queue state -- in-process, after the other legs
+        # and the end-to-end leg, this leg read ~10 % low (16.9 vs 18.7-19.0 M draws/s)
+        legs["configs[4]_kriging"] = kriging_leg_process(min(a.krig_subsets, K), a.krig_sites)
     elif world > 1 and not a.no_e2e and not weak:
         if rank == 0:
             e2e = node_end_to_end(a, world)
