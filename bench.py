@@ -269,6 +269,7 @@ def end_to_end(mk, d, K, devices=(0,)):
             "chains_subset_iters_per_s": K * cfg.n_samples / ph["chains_s"],
             "devices": list(devices),
             "exchange": ph.get("exchange"),
+            "comm_ranks": ph.get("comm_ranks"),     # the ranks mk_meta_fit's RCCL communicators hold
             "workload": f"configs[2] end to end on {len(devices)} GPU(s), one process: n={len(d['coords'])}, K={K}, "
                         f"exponential, q=1, "
                         f"n_test={len(d['coords_test'])}, 100 x 50 amcmc iterations, burn.in 3,750 "
@@ -306,8 +307,43 @@ def node_end_to_end(a, world):
         return {"error": repr(e)[:500]}
 
 
+def launcher_cmd(a, argv, port):
+    """--gpus N > 1 without a launcher: the torch.distributed.run command that runs this same bench
+    as N ranks, one per GPU of this node (rendezvous on 127.0.0.1)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s_:
+        s_.bind(("127.0.0.1", 0))
+        return s_.getsockname()[1]
+
+
+def self_launch(a, argv):
+    """`python bench.py --gpus N` (N > 1, WORLD_SIZE unset): start torch.distributed.run as a CHILD
+    process -- before this process imports torch or libmk or touches a GPU -- let rank 0's JSON
+    line through on the shared stdout and exit with the child's code.  Returns None when this
+    process is itself a rank (or N = 1); raises when WORLD_SIZE contradicts --gpus."""
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != a.gpus and not (a.leg or a.e2e_only):
+            raise SystemExit(f"bench.py: WORLD_SIZE={ws} but --gpus {a.gpus}: the launcher and the flag disagree")
+        return None
+    if a.gpus <= 1 or a.leg or a.e2e_only:
+        return None
+    import subprocess
+    env = dict(os.environ, MK_BENCH_LAUNCHER="bench.py (torch.distributed.run child)")
+    r = subprocess.run(launcher_cmd(a, argv, _free_port()), env=env)
+    return r.returncode
+
+
 def main():
     a = parse()
+    rc = self_launch(a, sys.argv[1:])
+    if rc is not None:
+        sys.exit(rc)
     if a.leg:
         mk = importlib.import_module(PKG)
         which, sub = {"configs1": (1, None), "configs3": (3, None), "configs3_share7": (3, 7)}[a.leg]
@@ -332,6 +368,9 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", rank=rank, world_size=world)
         cpu_group = dist.new_group(backend="gloo")   # waits that must not hold a GPU kernel
+        if dist.get_world_size() != a.gpus:
+            raise SystemExit(f"bench.py: torch.distributed sees {dist.get_world_size()} ranks, --gpus {a.gpus}")
+    ranks_seen = dist.get_world_size() if dist is not None else 1
 
     mk = importlib.import_module(PKG)
     weak = a.scaling == "weak"
@@ -447,6 +486,9 @@ def main():
         "value": value,
         "unit": "subset-iters/s",
         "n_gpus": world,
+        # what actually ran: the ranks torch.distributed saw (RCCL backend) and who started them
+        "ranks_seen": ranks_seen,
+        "launcher": os.environ.get("MK_BENCH_LAUNCHER", "external torch.distributed.run" if world > 1 else "none"),
         "steps": a.steps,
         "warmup": W - A,
         "ms_per_step": elapsed / a.steps * 1e3,

@@ -189,6 +189,8 @@ typedef struct mk_combined {
   int32_t max_iter;   /* MEDIAN: Weiszfeld iterations (<= 0: 100)                                   */
   double tol;         /* MEDIAN: convergence tolerance (< 0: 1e-12)                                 */
   int32_t exchange;   /* out: 1 = RCCL, 0 = device copies                                           */
+  int32_t comm_ranks; /* out: ranks of the exchange (RCCL: ncclCommCount of the communicators; copies:
+                       * the number of device blocks)                                               */
 } mk_combined;
 /* Progress between batches: iterations done so far (a multiple of batch_length) of n_samples. */
 typedef int (*mk_progress_fn)(void* user, int32_t iterations, int32_t n_samples);

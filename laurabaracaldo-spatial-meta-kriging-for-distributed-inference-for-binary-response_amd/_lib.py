@@ -67,7 +67,7 @@ class Summary(ctypes.Structure):
 
 class Combined(ctypes.Structure):
     _fields_ = [("result", _dp), ("result2", _dp), ("method", ctypes.c_int32), ("max_iter", ctypes.c_int32),
-                ("tol", ctypes.c_double), ("exchange", ctypes.c_int32)]
+                ("tol", ctypes.c_double), ("exchange", ctypes.c_int32), ("comm_ranks", ctypes.c_int32)]
 
 
 # int (*mk_progress_fn)(void* user, int32_t iterations, int32_t n_samples)

@@ -125,8 +125,6 @@ struct Group {
   int* d_pcount = nullptr;
   hipEvent_t done = nullptr;         // fork-join sweep: this group's pre-sweep work is queued
   hipStream_t bulk = nullptr;        // split Cholesky (launch_cholesky): CU-masked bulk-update stream
-  hipStream_t near = nullptr;        // chain split (MK_CHOL_CHAIN): off-diagonal correction + trsm stream
-  CovGen gen{};                      // MK_COV_FUSE: the candidates being factored, generated at first touch
   std::vector<hipEvent_t> ev;        // 2 nt + 1 events reused every factorisation
 };
 
@@ -179,7 +177,6 @@ Model model_view(const Model& m, int s0, int S) {
   if (m.span_pt) v.span_pt = m.span_pt + s;
   if (m.chtab) v.chtab = m.chtab + s * q * MK_CH_TAB;
   if (m.chtab_p) v.chtab_p = m.chtab_p + s * q * MK_CH_TAB;
-  if (m.phi_c) v.phi_c = m.phi_c + s * q;
   return v;
 }
 
@@ -375,7 +372,6 @@ struct mk_session {
   int iter = 0;
   bool matern = false, record_samples = true, record_w = false;
   bool pred_gen = false;          // kriging P^T generated inside k_pred_var (exponential; no P^T buffer)
-  bool cov_fuse = false;          // MK_COV_FUSE=1 (exponential): candidate tiles generated by the update at first touch
   Group all;                      // the whole shard on `stream`
   bool tiled = false;             // kriging after the fit over test-site tiles (predict_tile)
   int pred_tile = 0, n_test_all = 0, n_test_pad_all = 0;
@@ -387,22 +383,18 @@ struct mk_session {
   int* d_slist = nullptr;         // tiled replay: per-outcome subset lists [q][S] + counts [q]
   int* d_scount = nullptr;
   std::vector<Group> groups;      // the run-time split, one stream each
-  // multi-workgroup sweep (k_sweep_mg, small shards): partial dots, per-block counters, error flag
-  bool sweep_mg = false;          // buffers allocated and chosen for the sequential schedule
-  bool sweep_mg_forced = false;   // MK_SWEEP=2: also under the lookahead schedule
-  size_t sweep_mg_lds = 0;
-  // split-launch sweep (k_sweep_tiles / k_sweep_block, no inter-workgroup waits): partial dots
-  // [S][nt][q][64], the block's coefficients [S][q][64] and any-moved flags [S]
-  bool sweep_split = false;
-  bool sweep_step = false;        // one launch per block (k_sweep_step); else two (MK_SWEEP=4)
-  bool sweep_rows = false;        // one-workgroup sweep with rows owned by waves (k_sweep_rows, MK_SWEEP=5)
-  int sweep_site = 0;             // one-pass site sweep (k_sweep_site, default for q <= 2): row pairs per thread (0: off)
+  // The latent sweep (launch_sweep).  sweep_site: the one-pass site sweep (default; row pairs per
+  // thread, 0: off) with its LDS and lean form; else, for multi-outcome small shards, the split-launch
+  // sweep (sweep_split: no inter-workgroup waits) and -- on the sequential schedule only, through a
+  // cooperative launch, which guarantees co-residency -- the multi-workgroup kernel (sweep_coop);
+  // else the 64-site-block kernel (k_sweep, one workgroup per subset).
+  int sweep_site = 0;
   size_t sweep_site_lds = 0;
-  int sweep_lean = 0;             // its lean form (sweep_site_kernel: 1 / 2 border by factor / all n_s even)
-  bool sweep_pair = false;        // the site sweep two sites per barrier (MK_SWEEP=7, q = 1)
+  int sweep_lean = 0;             // q = 1: 1 border row by factor, 2 every n_s even (sweep_site_kernel)
+  bool sweep_split = false;       // k_sweep_step, one launch per 64-site block
+  bool sweep_coop = false;        // k_sweep_mg by hipLaunchCooperativeKernel (sequential schedule only)
+  size_t sweep_mg_lds = 0;
   double* sp_part = nullptr;
-  double* sp_dacc = nullptr;
-  int* sp_any = nullptr;
   hipEvent_t swept = nullptr;     // fork-join sweep (several groups): the whole-shard sweep is queued
   double* sw_part = nullptr;
   int* sw_cnt = nullptr;
@@ -423,6 +415,7 @@ struct mk_session {
   hipStream_t la_k = nullptr;     // kept iterations' kriging refresh beside the sweep (MK_LA_KRIG)
   std::vector<hipEvent_t> la_ev;  // [nt] panel k final | decided (or adapted) | join | W ready | kriged
   hipError_t launch_err = hipSuccess;   // first failed hipLaunchKernel / cooperative launch of a run
+  const char* poisoned = nullptr;       // set when a run left the chain in a state that is not the sampler's
   std::vector<int> n_part;
   std::vector<void*> allocs;
   bool prof = false;
@@ -590,7 +583,7 @@ static void launch_candidates(const Model& md, const MatSet& ms, hipStream_t st,
                               int which, int iter, const int* slist = nullptr, const int* scount = nullptr) {
   if (md.cov_model == MK_COV_MATERN && md.chtab)
     MK_LAUNCH(k_matern_table, dim3(n_entries), dim3(256), 0, st, md, h0, hc, which, iter, slist, scount);
-  const int ntiles = (which & MK_CAND_COL0) ? ms.nt : ms.nt * (ms.nt + 1) / 2;
+  const int ntiles = ms.nt * (ms.nt + 1) / 2;
   MK_LAUNCH(cov_candidate_kernel(md.cov_model), dim3(xcd_grid_h(n_entries, ntiles)),
                      dim3(256), 0, st, md, ms, h0, hc, which, iter, slist, scount);
 }
@@ -599,42 +592,26 @@ static void launch_candidates(const Model& md, const MatSet& ms, hipStream_t st,
 // Candidate tiles are in the free slot (k_cov_candidate, or k_load_plain for the test entry).
 // One launch per step covers outcomes h0 .. h0+hc-1 of every subset (hc = q in the sampler).
 // Launch pieces of the blocked Cholesky for panel k, tiles [ia, ib), on stream st.
-// MK_COV_FUSE: the candidate generation the update kernel does at a tile's first touch (j0 == 0), and
-// the covariance launch that then writes column 0 only (and each pair's phi').
-static CovGen cov_gen(const mk_session* s, const Model& md, bool border) {
-  CovGen c{};
-  if (!s->cov_fuse) return c;
-  c.coords = md.coords;
-  c.n_s = md.n_s;
-  c.u = md.u;
-  c.phi_c = md.phi_c;
-  c.n_pad = md.n_pad;
-  c.q = md.q;
-  c.border = border ? 1 : 0;
-  return c;
-}
-static int cand_flags(const mk_session* s) { return s->cov_fuse ? MK_CAND_COL0 : 0; }
 
 static void chol_update(mk_session* s, Group& g, hipStream_t st, int h0, int hc, int k, int ia, int ib, int j0, int j1,
                         const int* slist, const int* scount, double flops) {
   const int E = g.S * hc, nti = ib - ia;
   if (nti <= 0) return;
-  const CovGen cg = j0 == 0 ? g.gen : CovGen{};
   const int tm = tile_size((long)E * nti);
   if (tm == 32) {
     timed(s, st, KS_CHOL_UPDATE_SUB, flops, [&] {
       MK_LAUNCH(k_chol_update<32>, dim3(xcd_grid_h(E, nti * 16)), dim3(256), LDS_32, st, g.ms, g.S, h0, hc, k, ia,
-                         ib, j0, j1, slist, scount, cg);
+                         ib, j0, j1, slist, scount);
     });
   } else if (tm == 64) {
     timed(s, st, KS_CHOL_UPDATE_SUB, flops, [&] {
       MK_LAUNCH(k_chol_update<64>, dim3(xcd_grid_h(E, nti * 4)), dim3(256), LDS_64, st, g.ms, g.S, h0, hc, k, ia,
-                         ib, j0, j1, slist, scount, cg);
+                         ib, j0, j1, slist, scount);
     });
   } else {
     timed(s, st, KS_CHOL_UPDATE, flops, [&] {
       MK_LAUNCH(k_chol_update<128>, dim3(xcd_grid_h(E, nti)), dim3(256), LDS_128, st, g.ms, g.S, h0, hc, k, ia,
-                         ib, j0, j1, slist, scount, cg);
+                         ib, j0, j1, slist, scount);
     });
   }
 }
@@ -731,95 +708,6 @@ static void launch_cholesky(mk_session* s, Group& g, int h0, int hc, const int* 
   if (k_lo == 0) {
     hipEventRecord(g.ev[2 * nt], A);             // the candidates are on A
     hipStreamWaitEvent(B, g.ev[2 * nt], 0);
-  }
-  if (g.near) {
-    // Chain split: only the diagonal tiles' dependency chain stays on the critical stream, as
-    // launches of one tile per matrix (S q workgroups: they fit the CUs the other streams' masks
-    // leave), the rest of each column's correction and trsm runs one column behind on `near`:
-    //   A (critical): [eU(k)] U(k; tile k; panels k-d..k-1), D(k) -> eD(k), [eUo(k)] T(k; tile k+1) -> eTn(k)
-    //   N (near):     [eU(k), eTn(k-1)] U(k; tiles > k; panels k-d..k-1) -> eUo(k),
-    //                 [eD(k)] T(k; tiles > k+1), [eTn(k)] -> eTr(k) = panel k final (evP(k))
-    //   B (bulk):     [eTr(k)] U(k+d+1; panels < k+1) -> eU(k+d+1)
-    // The critical chain per column is a one-tile correction, the diagonal factor and a one-tile
-    // trsm; the wide launches overlap it.  Every tile sees the same panels in the same order and
-    // chunking as in the other schedules (same bits).
-    hipStream_t N = g.near;
-    hipEvent_t* eD = g.ev.data() + 2 * nt + 1;
-    hipEvent_t* eTn = eD + nt;
-    hipEvent_t* eUo = eTn + nt;
-    hipEvent_t* eTr = eUo + nt;
-    if (k_lo == 0) hipStreamWaitEvent(N, g.ev[2 * nt], 0);   // the candidates are on A
-    for (int k = k_lo; k < k_hi; ++k) {
-      const int j0 = std::max(0, k - d);
-      if (k >= 1 && k + 1 < nt) {   // near: the off-diagonal tiles' correction of column k
-        if (k > d) hipStreamWaitEvent(N, eU[k], 0);
-        hipStreamWaitEvent(N, eTn[k - 1], 0);
-        chol_update(s, g, N, h0, hc, k, k + 1, nt, j0, k, nullptr, nullptr, panel_flops(s, g, hc, k, k + 1, nt, false, j0, k));
-        hipEventRecord(eUo[k], N);
-      }
-      if (k > d) hipStreamWaitEvent(A, eU[k], 0);
-      if (k >= 1)
-        chol_update(s, g, A, h0, hc, k, k, k + 1, j0, k, nullptr, nullptr, panel_flops(s, g, hc, k, k, k + 1, false, j0, k));
-      chol_diag(s, g, A, h0, hc, k, nullptr, nullptr);
-      if (k == nt - 1) {
-        if (evP) hipEventRecord(evP[k], A);
-        break;
-      }
-      hipEventRecord(eD[k], A);
-      if (k >= 1) hipStreamWaitEvent(A, eUo[k], 0);
-      chol_trsm(s, g, A, h0, hc, k, k + 1, k + 2, nullptr, nullptr, panel_flops(s, g, hc, k, k + 1, k + 2, true));
-      hipEventRecord(eTn[k], A);
-      hipStreamWaitEvent(N, eD[k], 0);
-      if (k + 2 < nt)
-        chol_trsm(s, g, N, h0, hc, k, k + 2, nt, nullptr, nullptr, panel_flops(s, g, hc, k, k + 2, nt, true));
-      hipStreamWaitEvent(N, eTn[k], 0);
-      hipEventRecord(eTr[k], N);
-      if (evP) hipEventRecord(evP[k], N);
-      if (k + d + 1 < nt) {
-        const int c = k + d + 1;
-        hipStreamWaitEvent(B, eTr[k], 0);
-        chol_update(s, g, B, h0, hc, c, c, nt, 0, c - d, nullptr, nullptr, panel_flops(s, g, hc, c, c, nt, false, 0, c - d));
-        hipEventRecord(eU[c], B);
-      }
-    }
-    return;
-  }
-  static const int fine_env = tile_env("MK_CHOL_FINE", 0);
-  if (fine_env) {
-    // Fine split: the critical stream keeps only the diagonal tile's correction, the diagonal
-    // factor and the trsm; the off-diagonal tiles' correction of column k+1 runs on the bulk stream
-    // right after T(k), beside D(k+1).
-    //   A: [eU(k)] U(k; tile k; panels k-d..k-1), D(k), [eO(k)] T(k), evP(k)
-    //   B: [evP(k)] U(k+1; tiles > k+1; panels k+1-d..k) -> eO(k+1); U(k+d+1; panels < k+1) -> eU
-    hipEvent_t* eO = g.ev.data() + 2 * nt + 1;     // eO[c]: off-diagonal correction of column c done
-    for (int k = k_lo; k < k_hi; ++k) {
-      if (k > d) hipStreamWaitEvent(A, eU[k], 0);
-      const int j0 = std::max(0, k - d);
-      if (k >= 1)
-        chol_update(s, g, A, h0, hc, k, k, k + 1, j0, k, nullptr, nullptr, panel_flops(s, g, hc, k, k, k + 1, false, j0, k));
-      chol_diag(s, g, A, h0, hc, k, nullptr, nullptr);
-      if (k < nt - 1) {
-        if (k >= 1) hipStreamWaitEvent(A, eO[k], 0);
-        chol_trsm(s, g, A, h0, hc, k, k + 1, nt, nullptr, nullptr, panel_flops(s, g, hc, k, k + 1, nt, true));
-      }
-      hipEventRecord(eT[k], A);
-      if (evP) hipEventRecord(evP[k], A);
-      if (k + 1 < nt) {
-        hipStreamWaitEvent(B, eT[k], 0);
-        const int c = k + 1, jc = std::max(0, c - d);
-        if (c + 1 < nt) {
-          chol_update(s, g, B, h0, hc, c, c + 1, nt, jc, c, nullptr, nullptr, panel_flops(s, g, hc, c, c + 1, nt, false, jc, c));
-          hipEventRecord(eO[c], B);
-        }
-        if (k + d + 1 < nt) {
-          const int cb = k + d + 1;
-          chol_update(s, g, B, h0, hc, cb, cb, nt, 0, cb - d, nullptr, nullptr,
-                      panel_flops(s, g, hc, cb, cb, nt, false, 0, cb - d));
-          hipEventRecord(eU[cb], B);
-        }
-      }
-    }
-    return;
   }
   for (int k = k_lo; k < k_hi; ++k) {
     if (k > d) hipStreamWaitEvent(A, eU[k], 0);
@@ -925,109 +813,51 @@ static void launch_pred_refresh(mk_session* s, Group& g, hipStream_t st = nullpt
 // schedule stays the default there (MK_LOOKAHEAD=1 takes the 0.9 %).
 static bool la_auto(const mk_session* s) { return (long)s->S * s->q <= 224; }
 
-// Under the lookahead schedule the one-workgroup kernel is the default for q = 1: the cooperative
-// kernel's gain (one W pass, 0.6 vs 1.2 ms at 32 subsets alone) is lost beside the concurrent
-// factorisation (6,635 vs 6,892 subset-iters/s at 32 subsets; configs[1] 14,832 vs 15,074).  With
-// q >= 2 outcomes on a few subsets -- configs[3]'s per-GPU share on 8 GPUs -- the one-workgroup
-// sweep (q W panels per block, q x 64 MH steps) is the iteration's longest chain and the
-// cooperative kernel wins: q = 3, 7 subsets 1,050 -> 1,601, 13 subsets 1,553 -> 1,956 subset-iters/s
-// (25 subsets: equal).
-// Rounds 2-3 did not take the cooperative kernel's q >= 2 gain by default (GPU-suite stalls, DESIGN.md
-// 4.2 10, whose cause round 4 found: 4.5) and ran split launches there (q = 3: 7 subsets 1,050 ->
-// 1,213, 13 subsets 1,553 -> 1,657 subset-iters/s, r03b); since round 4 the cooperative kernel is
-// the default for q >= 2 small shards again (MK_SWEEP=3 selects the split launches).
-static bool use_sweep_mg(const mk_session* s) { return s->sweep_mg && (!s->la || s->sweep_mg_forced); }
+// The cooperative multi-workgroup sweep runs only as a cooperative launch (every workgroup co-resident,
+// guaranteed by the runtime), which HIP does not dispatch beside other queues' work -- so only on the
+// sequential schedule.  Under the lookahead schedule multi-outcome small shards take the split-launch
+// sweep, which never waits across workgroups.  (Round 4 had launched the cooperative kernel plainly
+// beside the candidates' stream, relying on its workgroups becoming resident eventually)
+static bool use_sweep_mg(const mk_session* s) { return s->sweep_coop && !s->la; }
 
 static void launch_sweep(mk_session* s, Group& g, int it) {
   const int q = s->q;
-  if (s->sweep_split) {   // two launches per 64-site block, ordered by the stream (no waits on the device)
-    int nmax = 1;
-    for (int i = g.s0; i < g.s0 + g.S; ++i) nmax = std::max(nmax, s->n_part[i]);
-    const int nblk = (nmax + 63) / 64, nt = s->nt;
-    Model md = g.md;
-    MatSet ms = g.ms;
-    int iter = it;
-    double* part = s->sp_part + (long)g.s0 * (s->sweep_step ? 2 : 1) * nt * q * 64;
-    double* dacc = s->sp_dacc + (long)g.s0 * q * 64;
-    int* any = s->sp_any + g.s0;
-    const size_t lds = (size_t)q * (64 * 64 + 2 * 64) * sizeof(double);
-    if (s->sweep_step) {
-      const size_t lds_s = lds + 4 * MK_NB * sizeof(double);
-      for (int B = 0; B <= nblk; ++B) {
-        void* ta[] = {&md, &ms, &iter, &B, &part};
-        const hipError_t e = hipLaunchKernel(sweep_step_kernel(q), dim3(g.S * nt), dim3(256), ta, lds_s, g.stream);
-        wd_trace(g.stream, "k_sweep_step");
-        if (e != hipSuccess) {
-          if (s->launch_err == hipSuccess) s->launch_err = e;
-          return;
-        }
-      }
-      return;
-    }
-    for (int B = 0; B <= nblk; ++B) {
-      void* ta[] = {&md, &ms, &iter, &B, &part, &dacc, &any};
-      hipError_t e = hipLaunchKernel(sweep_split_kernel(q, false), dim3(g.S * nt), dim3(256), ta, 0, g.stream);
-      wd_trace(g.stream, "k_sweep_tiles");
-      if (e == hipSuccess && B < nblk) {
-        void* ba[] = {&md, &ms, &B, &part, &dacc, &any};
-        e = hipLaunchKernel(sweep_split_kernel(q, true), dim3(g.S), dim3(256), ba, lds, g.stream);
-        wd_trace(g.stream, "k_sweep_block");
-      }
-      if (e != hipSuccess) {
-        if (s->launch_err == hipSuccess) s->launch_err = e;
-        return;
-      }
-    }
-    return;
-  }
+  Model md = g.md;
+  MatSet ms = g.ms;
+  int iter = it;
+  hipError_t e = hipSuccess;
   if (s->sweep_site) {
-    Model md = g.md;
-    MatSet ms = g.ms;
-    int iter = it;
     void* args[] = {&md, &ms, &iter};
-    const hipError_t e = hipLaunchKernel(sweep_site_kernel(q, s->sweep_site, s->sweep_pair, s->sweep_lean), dim3(g.S), dim3(MK_SS_T), args,
-                                         s->sweep_site_lds, g.stream);
+    e = hipLaunchKernel(sweep_site_kernel(q, s->sweep_site, s->sweep_lean), dim3(g.S), dim3(MK_SS_T), args,
+                        s->sweep_site_lds, g.stream);
     wd_trace(g.stream, "k_sweep_site");
-    if (e != hipSuccess && s->launch_err == hipSuccess) s->launch_err = e;
-    return;
-  }
-  if (use_sweep_mg(s)) {
+  } else if (use_sweep_mg(s)) {
     hipMemsetAsync(s->sw_cnt, 0, (size_t)g.S * (s->n_pad / 64) * sizeof(int), g.stream);
-    Model md = g.md;
-    MatSet ms = g.ms;
-    int iter = it;
     double* part = s->sw_part;
     int* cnt = s->sw_cnt;
     int* xcc = s->sw_xcc;
     int* err = s->sw_err;
     void* args[] = {&md, &ms, &iter, &part, &cnt, &xcc, &err};
-    // A cooperative launch is not dispatched beside other queues' work; under the lookahead
-    // schedule the candidates' factorisation runs concurrently, so the grid goes out as a plain
-    // launch: the kernel's waits only need every workgroup resident eventually -- the other
-    // stream's kernels never wait on the sweep and drain -- and each wait has a time-out
-    // (MK_SWEEP_COOP=1 keeps the cooperative launch)
-    static const int coop_env = tile_env("MK_SWEEP_COOP", 0);
-    hipError_t e;
-    if (s->la && !coop_env)
-      e = hipLaunchKernel(sweep_kernel(q, true), dim3(xcd_grid(g.S, s->nt)), dim3(256), args, (unsigned)s->sweep_mg_lds,
-                          g.stream);
-    else
-      e = hipLaunchCooperativeKernel(sweep_kernel(q, true), dim3(xcd_grid(g.S, s->nt)), dim3(256), args,
-                                     (unsigned)s->sweep_mg_lds, g.stream);
+    e = hipLaunchCooperativeKernel(sweep_kernel(q, true), dim3(xcd_grid(g.S, s->nt)), dim3(256), args,
+                                   (unsigned)s->sweep_mg_lds, g.stream);
     wd_trace(g.stream, "k_sweep_mg");
-    if (e != hipSuccess && s->launch_err == hipSuccess) s->launch_err = e;
-    return;
+  } else if (s->sweep_split) {   // one launch per 64-site block, ordered by the stream (no waits on the device)
+    int nmax = 1;
+    for (int i = g.s0; i < g.s0 + g.S; ++i) nmax = std::max(nmax, s->n_part[i]);
+    const int nblk = (nmax + 63) / 64, nt = s->nt;
+    double* part = s->sp_part + (long)g.s0 * 2 * nt * q * 64;
+    const size_t lds = (size_t)q * (64 * 64 + 2 * 64) * sizeof(double) + 4 * MK_NB * sizeof(double);
+    for (int B = 0; B <= nblk && e == hipSuccess; ++B) {
+      void* ta[] = {&md, &ms, &iter, &B, &part};
+      e = hipLaunchKernel(sweep_step_kernel(q), dim3(g.S * nt), dim3(256), ta, lds, g.stream);
+      wd_trace(g.stream, "k_sweep_step");
+    }
+  } else {
+    const size_t sw_lds = (size_t)q * (64 * 64 + 2 * 64) * sizeof(double);
+    void* args[] = {&md, &ms, &iter};
+    e = hipLaunchKernel(sweep_kernel(q, false), dim3(g.S), dim3(MK_SW_T), args, sw_lds, g.stream);
+    wd_trace(g.stream, "k_sweep");
   }
-  const size_t sw_lds = (size_t)q * (64 * 64 + 2 * 64) * sizeof(double);
-  Model md = g.md;
-  MatSet ms = g.ms;
-  int iter = it;
-  void* args[] = {&md, &ms, &iter};
-  const hipError_t e =
-      s->sweep_rows ? hipLaunchKernel(sweep_rows_kernel(q), dim3(g.S), dim3(512), args,
-                                      sw_lds + (size_t)s->nt * q * 64 * sizeof(double), g.stream)
-                    : hipLaunchKernel(sweep_kernel(q, false), dim3(g.S), dim3(MK_SW_T), args, sw_lds, g.stream);
-  wd_trace(g.stream, s->sweep_rows ? "k_sweep_rows" : "k_sweep");
   if (e != hipSuccess && s->launch_err == hipSuccess) s->launch_err = e;
 }
 
@@ -1043,8 +873,7 @@ static void iteration_pre_sweep(mk_session* s, Group& g, int it) {
   const int nkinds = s->matern ? 2 : 1;
   // the q outcomes' (phi_h, nu_h) steps are independent given u: one batched pass per kind
   for (int which = 0; which < nkinds; ++which) {
-    timed(s, st, KS_COV, 0.0, [&] { launch_candidates(md, g.ms, st, S * q, 0, q, which | cand_flags(s), it); });
-    g.gen = cov_gen(s, md, true);
+    timed(s, st, KS_COV, 0.0, [&] { launch_candidates(md, g.ms, st, S * q, 0, q, which, it); });
     launch_cholesky(s, g, 0, q);
     MK_LAUNCH(k_theta_mh, dim3((S * q + 63) / 64), dim3(64), 0, st, md, g.ms, 0, q, which, it);
   }
@@ -1089,8 +918,7 @@ static void enqueue_candidates(mk_session* s, Group& g, int it, hipEvent_t after
   const int S = g.S, q = s->q, nt = s->nt;
   hipStreamWaitEvent(s->la_c, after, 0);
   timed(s, s->la_c, KS_COV, 0.0,
-        [&] { launch_candidates(g.md, g.ms, s->la_c, S * q, 0, q, 0 | MK_CAND_NOBORDER | cand_flags(s), it); });
-  g.gen = cov_gen(s, g.md, false);   // also the rest of this factorisation (enqueue_candidates_rest)
+        [&] { launch_candidates(g.md, g.ms, s->la_c, S * q, 0, q, MK_CAND_NOBORDER, it); });
   launch_cholesky(s, g, 0, q, nullptr, nullptr, s->la_c, s->la_ev.data(), 0, k_hi);
   s->la_next = it;
   s->la_enq = k_hi;
@@ -1284,19 +1112,7 @@ static int setup_groups(mk_session* s, int n_groups) {
     Group& g = s->groups[0];
     if (pool_stream(s->owned, &g.bulk, s->device, SK_CUMASK, 0, mask) != hipSuccess)
       return set_err(MK_E_HIP, "bulk stream");
-    // MK_CHOL_CHAIN=1: the chain split's near stream (1: high priority, all CUs; 2: the bulk mask)
-    static const int chain_env = tile_env("MK_CHOL_CHAIN", 0);
-    if (chain_env == 1) {
-      int lo = 0, hi = 0;
-      if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
-          pool_stream(s->owned, &g.near, s->device, SK_PRIO, hi) != hipSuccess)
-        return set_err(MK_E_HIP, "near stream");
-    } else if (chain_env == 2) {
-      if (pool_stream(s->owned, &g.near, s->device, SK_CUMASK, 0, mask) != hipSuccess)
-        return set_err(MK_E_HIP, "near stream");
-      // a second stream with the same mask: the pool hands out distinct streams per session
-    }
-    g.ev.assign(6 * s->nt + 2, nullptr);
+    g.ev.assign(2 * s->nt + 1, nullptr);
     for (auto& e : g.ev)
       if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return set_err(MK_E_HIP, "cholesky event");
   }
@@ -1412,8 +1228,6 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
   // kriging memory, but 0.52 vs 0.74 of fp64 peak: the exp/sqrt per element are recomputed for
   // every row panel).  Default: stored P^T.
   s->pred_gen = !s->matern && tile_env("MK_PRED_GEN", 0) != 0;
-  // MK_COV_FUSE=1 (exponential): candidate tiles generated inside the update at their first touch
-  s->cov_fuse = !s->matern && tile_env("MK_COV_FUSE", 0) != 0;
   s->n_part.assign(pr->n_part, pr->n_part + S);
   s->bbox.assign((size_t)4 * S, 0.0);
   {
@@ -1465,8 +1279,6 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
   md.seed = c->seed;
   md.accept_rate = c->accept_rate;
   md.P = P;
-  // kriging GEMM raster (k_pred_var): row panels per group; placement only, same bits for any value
-  md.pred_gi = std::max(1, std::min(tile_env("MK_PRED_GI", 1), 64));
   for (int h = 0; h < q; ++h) {
     md.phi_a[h] = c->phi_unif_a[h]; md.phi_b[h] = c->phi_unif_b[h];
     md.nu_a[h] = s->matern ? c->nu_unif_a[h] : 0.0;
@@ -1512,17 +1324,71 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
       hs[i] = std::hypot(s->bbox[4 * i + 1] - s->bbox[4 * i], s->bbox[4 * i + 3] - s->bbox[4 * i + 2]);
     HIPCHK(hipMemcpy(d_span, hs.data(), (size_t)S * 8, hipMemcpyHostToDevice));
     md.span = d_span;
-    if ((rc = s->alloc(&md.phi_c, (size_t)S * q))) return rc;
     if (s->matern && ((rc = s->alloc(&md.chtab, (size_t)S * q * MK_CH_TAB)) ||
                       (rc = s->alloc(&md.chtab_p, (size_t)S * q * MK_CH_TAB))))
       return rc;
+  }
+  // ---------------- the latent sweep (launch_sweep)
+  // MK_SWEEP (tests and measurements): 1 the 64-site-block kernel (k_sweep: the fallback for subsets
+  // too large for the site sweep), 2 the cooperative multi-workgroup kernel where a cooperative launch
+  // fits (sequential schedule; split launches under the lookahead schedule), 3 split launches.
+  // 0 (default): the one-pass site sweep (k_sweep_site; W read once, no Q_BB tiles, no inter-workgroup
+  // waits) wherever it fits -- n_pad <= 4096 (q = 4: not instantiated) and the sites' data in LDS
+  // (configs[3]: n_s = 2,000, q = 3 takes 152 KB) -- except multi-outcome small shards (q >= 2, <= 16
+  // subsets: one workgroup per subset is the iteration's longest chain there), which take the
+  // cooperative kernel on the sequential schedule and split launches on the lookahead schedule.
+  // Measured (subset-iters/s, 40-step windows, profiles/r04/knobs, r04e): configs[2] 250 subsets block
+  // sweep 10,143 / site pair 10,527; configs[1] 15,198 / 15,626; configs[3] (q = 3, 50 subsets) block
+  // 3,016 / site 3,106; configs[3]'s 7-subset share split launches 1,476 / site 1,340 / block 1,107
+  // (lookahead schedule).  q = 1 runs the lean pair form (k_sweep_site LN > 0: 250 subsets 10,452 ->
+  // 10,567-10,622, 32 subsets 7,832 -> 7,957-8,067).
+  {
+    HIPCHK(hipFuncSetAttribute(sweep_kernel(q, false), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               q * (64 * 64 + 2 * 64) * 8));
+    s->sweep_mg_lds = (size_t)q * (64 * 64 + 2 * 64) * 8 + 4 * MK_NB * 8;
+    const void* fn = sweep_kernel(q, true);
+    HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)s->sweep_mg_lds));
+    int per_cu = 0, n_cu = 0, coop = 0;
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, s->sweep_mg_lds));
+    HIPCHK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, c->device));
+    HIPCHK(hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, c->device));
+    const int mode = tile_env("MK_SWEEP", 0);
+    const bool coop_fits = coop && (long)xcd_grid(S, nt) <= (long)per_cu * n_cu && nt <= 32;
+    const bool small_multi = q >= 2 && S <= 16;
+    const bool site_fits = sweep_site_kernel(q, n_pad <= 8 * MK_SS_T ? 1 : 2) != nullptr && n_pad <= 16 * MK_SS_T &&
+                           sweep_site_lds_bytes(nmax, q, q == 1) <= 156 * 1024;
+    const bool site = mode == 0 && !small_multi && site_fits;
+    const bool multi = (mode == 0 && !site && small_multi) || mode == 2 || mode == 3;
+    s->sweep_coop = multi && mode != 3 && coop_fits;
+    s->sweep_split = multi && nt <= 32;   // k_sweep_step sums <= 32 tile partials
+    if (site) {
+      s->sweep_site = n_pad <= 8 * MK_SS_T ? 1 : 2;
+      bool all_even = true;
+      for (int i = 0; i < S; ++i) all_even = all_even && (s->n_part[i] % 2 == 0);
+      s->sweep_lean = q == 1 ? (all_even ? 2 : 1) : 0;
+      s->sweep_site_lds = sweep_site_lds_bytes(nmax, q, s->sweep_lean);
+      HIPCHK(hipFuncSetAttribute(sweep_site_kernel(q, s->sweep_site, s->sweep_lean),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)s->sweep_site_lds));
+    }
+    if (s->sweep_split) {
+      HIPCHK(hipFuncSetAttribute(sweep_step_kernel(q), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 q * (64 * 64 + 2 * 64) * 8 + 4 * MK_NB * 8));
+      if ((rc = s->alloc(&s->sp_part, (size_t)S * 2 * nt * q * 64))) return rc;
+    }
+    if (s->sweep_coop) {
+      if ((rc = s->alloc(&s->sw_part, (size_t)S * 2 * nt * q * 64)) || (rc = s->alloc(&s->sw_cnt, (size_t)S * (n_pad / 64))) ||
+          (rc = s->alloc(&s->sw_xcc, (size_t)S * nt)) || (rc = s->alloc(&s->sw_err, 1)))
+        return rc;
+      HIPCHK(hipMemsetAsync(s->sw_err, 0, sizeof(int), s->stream));
+    }
   }
   MatSet& ms = s->ms;
   ms.ld = n_pad; ms.nt = nt; ms.q = q;
   if ((rc = s->alloc(&ms.L, (size_t)S * q * 2 * n_pad * n_pad)) ||
       (rc = s->alloc(&ms.Winv, (size_t)S * q * 2 * nt * MK_NB * MK_NB)) ||
       (rc = s->alloc(&ms.W, (size_t)S * q * n_pad * n_pad)) ||
-      (rc = s->alloc(&ms.QB, (size_t)S * q * nt * MK_NB * MK_NB)) || (rc = s->alloc(&ms.cur, (size_t)S * q)) ||
+      (!s->sweep_site && (rc = s->alloc(&ms.QB, (size_t)S * q * nt * MK_NB * MK_NB))) ||   // Q_BB: block sweeps only
+      (rc = s->alloc(&ms.cur, (size_t)S * q)) ||
       (rc = s->alloc(&s->d_probs, MK_N_LEVELS)))
     return rc;
   // lookahead schedule buffers (run_iteration_la): one stream group (either covariance model)
@@ -1648,100 +1514,11 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
   if (!set_gemm_lds()) return set_err(MK_E_HIP, "gemm lds attribute");
   HIPCHK(hipFuncSetAttribute(sweep_kernel(q, false), hipFuncAttributeMaxDynamicSharedMemorySize,
                              q * (64 * 64 + 2 * 64) * 8));
-  // multi-workgroup sweep: chosen when the cooperative grid (S x nt workgroups) fits on the chip
-  // at once; MK_SWEEP=1 forces the one-workgroup kernel, 2 the multi-workgroup one (when it fits)
-  {
-    s->sweep_mg_lds = (size_t)q * (64 * 64 + 2 * 64) * 8 + 4 * MK_NB * 8;
-    const void* fn = sweep_kernel(q, true);
-    HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)s->sweep_mg_lds));
-    int per_cu = 0, n_cu = 0, coop = 0;
-    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, s->sweep_mg_lds));
-    HIPCHK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, c->device));
-    HIPCHK(hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, c->device));
-    const long grid = xcd_grid(S, nt);
-    const int mode = tile_env("MK_SWEEP", 0);
-    const bool fits = coop && grid <= (long)per_cu * n_cu && nt <= 32;
-    // MK_SWEEP: 1 one workgroup per subset, 2 cooperative multi-workgroup, 3 split launches (one per
-    // block), 4 split launches (two per block); 0 (default): for multi-outcome small shards (q >= 2,
-    // <= 16 subsets: the one-workgroup sweep's q x 64 MH steps and q W panels per block on one CU per
-    // subset are the iteration's longest chain) the cooperative kernel where it fits, else split
-    // launches; one workgroup per subset elsewhere.  (Rounds 2-3 kept the cooperative kernel opt-in
-    // after intermittent GPU-suite stalls; their cause is in DESIGN.md 4.5.)
-    // MK_SWEEP=6 and the default (0): the one-pass site sweep (k_sweep_site; W read once, no Q_BB
-    // tiles, no inter-workgroup waits) wherever it fits: n_pad <= 4096 (q = 4: 2048) and the sites'
-    // data in LDS (configs[3]: n_s = 2,000, q = 3 takes 152 KB).  1-5 select the 64-site-block kernels,
-    // which remain the fallback: split launches (3, 4) for multi-outcome small shards, else one
-    // workgroup per subset.
-    // MK_SWEEP=7: the site sweep two sites per barrier (q = 1); the default for q = 1.  Measured
-    // (subset-iters/s, 40-step windows, profiles/r04/knobs, r04e): configs[2] 250 subsets block sweep
-    // 10,143 / site 10,506 / pair 10,527; its 32-subset share 7,744 / 7,784 / 7,758 (not the bound
-    // there); configs[1] 15,198 / 15,055 / 15,626; configs[3] (q = 3, 50 subsets) block 3,016 / site
-    // 3,106; configs[3]'s 7-subset share split launches 1,476 / site 1,340 / block 1,107 -- so q >= 2
-    // small shards keep the split-launch sweep.  The lean pair form (MK_SS_LEAN, k_sweep_site LN > 0):
-    // 250 subsets 10,452 -> 10,567-10,622 (sweep 1.12 -> 0.97-0.98 ms), 32 subsets 7,832 -> 7,957-8,067.
-    const bool small_multi = q >= 2 && S <= 16;
-    const bool pair = mode == 7 || (mode == 0 && q == 1);
-    const bool site_fits = sweep_site_kernel(q, n_pad <= 8 * MK_SS_T ? 1 : 2, pair) != nullptr && n_pad <= 16 * MK_SS_T &&
-                           sweep_site_lds_bytes(nmax, q) <= 156 * 1024;
-    const bool site = ((mode == 0 && !small_multi) || mode == 6 || mode == 7) && site_fits;
-    // Round 4: multi-outcome small shards take the cooperative sweep by default where its grid fits the
-    // CUs the lookahead mask leaves (configs[3]'s 7-subset share: 1,468-1,489 split launches ->
-    // 1,687-1,699 subset-iters/s, profiles/r04/lean/r04m_*).  The suite stalls that kept it opt-in
-    // shared one cause with RCCL's init failure -- a second HIP runtime in the process,
-    // gone since round 4 -- and the stall watchdog names the kernel of any future one.
-    const int mask_cu = tile_env("MK_LA_MASK", 32);
-    const bool coop_fits = fits && grid <= (long)per_cu * std::max(0, n_cu - mask_cu);
-    const bool coop_default = mode == 0 && !site && small_multi && coop_fits;
-    s->sweep_split = mode == 3 || mode == 4 || (mode == 0 && !site && small_multi && !coop_default);
-    s->sweep_step = s->sweep_split && mode != 4 && nt <= 32;   // k_sweep_step sums <= 32 tile partials
-    s->sweep_mg = !s->sweep_split && fits && (mode == 2 || coop_default);
-    s->sweep_rows = mode == 5 && q <= 3 && nt <= 32;
-    if (site) {
-      s->sweep_site = n_pad <= 8 * MK_SS_T ? 1 : 2;
-      s->sweep_pair = pair;
-      s->sweep_site_lds = sweep_site_lds_bytes(nmax, q);
-      s->sweep_mg = false;
-      // MK_SS_LEAN: 1 (default) the lean pair form (2 where every n_s is even), 3 its border-factor
-      // form always, 0 the masked form
-      static const int lean_env = tile_env("MK_SS_LEAN", 1);
-      bool all_even = true;
-      for (int i = 0; i < S; ++i) all_even = all_even && (s->n_part[i] % 2 == 0);
-      s->sweep_lean = (q == 1 && pair && lean_env > 0) ? (lean_env == 1 && all_even ? 2 : 1) : 0;
-      s->sweep_site_lds = sweep_site_lds_bytes(nmax, q, s->sweep_lean);
-      HIPCHK(hipFuncSetAttribute(sweep_site_kernel(q, s->sweep_site, pair, s->sweep_lean),
-                                 hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 (int)s->sweep_site_lds));
-    }
-    if (s->sweep_rows)
-      HIPCHK(hipFuncSetAttribute(sweep_rows_kernel(q), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 q * (64 * 64 + 2 * 64) * 8 + nt * q * 64 * 8));
-    // under the lookahead schedule the sweep runs on the CU-masked main stream, beside the candidates'
-    // chain: MK_SWEEP=2 is honoured there only when its grid fits the CUs that mask leaves
-    s->sweep_mg_forced = s->sweep_mg && (mode == 2 || coop_default) && coop_fits;
-    if (s->sweep_split) {
-      HIPCHK(hipFuncSetAttribute(sweep_split_kernel(q, true), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 q * (64 * 64 + 2 * 64) * 8));
-      HIPCHK(hipFuncSetAttribute(sweep_step_kernel(q), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 q * (64 * 64 + 2 * 64) * 8 + 4 * MK_NB * 8));
-      if ((rc = s->alloc(&s->sp_part, (size_t)S * 2 * nt * q * 64)) || (rc = s->alloc(&s->sp_dacc, (size_t)S * q * 64)) ||
-          (rc = s->alloc(&s->sp_any, (size_t)S)))
-        return rc;
-    }
-    if (s->sweep_mg) {
-      if ((rc = s->alloc(&s->sw_part, (size_t)S * 2 * nt * q * 64)) || (rc = s->alloc(&s->sw_cnt, (size_t)S * (n_pad / 64))) ||
-          (rc = s->alloc(&s->sw_xcc, (size_t)S * nt)) || (rc = s->alloc(&s->sw_err, 1)))
-        return rc;
-      HIPCHK(hipMemsetAsync(s->sw_err, 0, sizeof(int), s->stream));
-    }
-  }
-
   // ---------------- initial state: eta, u, factor every R_h at the starting values, W, z (whole shard)
   Group& a = s->all;
   MK_LAUNCH(k_init_state, dim3(S), dim3(256), 0, s->stream, md);
-  launch_candidates(md, ms, s->stream, S * q, 0, q, 2 | cand_flags(s), 0);
-  a.gen = cov_gen(s, md, true);
+  launch_candidates(md, ms, s->stream, S * q, 0, q, 2, 0);
   launch_cholesky(s, a, 0, q);
-  a.gen = CovGen{};
   MK_LAUNCH(k_theta_init, dim3((S * q + 63) / 64), dim3(64), 0, s->stream, md, ms, 0, q);
   MK_LAUNCH(k_dirty_list, dim3(1), dim3(256), 0, s->stream, md, 0, a.d_list, a.d_count, a.d_plist, a.d_pcount);
   launch_inverse(s, a);
@@ -1758,6 +1535,7 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
 
 extern "C" int mk_session_run(mk_session* s, int32_t n_iter) {
   if (!s) return set_err(MK_E_ARG, "null session");
+  if (s->poisoned) return set_err(MK_E_HIP, std::string("session unusable after an earlier failure: ") + s->poisoned);
   MK_ENTRY_DEVICE(s->device);
   if (n_iter < 0 || s->iter + n_iter > s->md.n_samples) return set_err(MK_E_ARG, "n_iter beyond n.samples");
   if (s->la && !s->la_c) {
@@ -1824,11 +1602,16 @@ extern "C" int mk_session_run(mk_session* s, int32_t n_iter) {
   for (auto& g : s->groups) HIPCHK(hipStreamSynchronize(g.stream));
   if (s->la_c) HIPCHK(hipStreamSynchronize(s->la_c));   // the next iteration's candidates
   if (s->la_k) HIPCHK(hipStreamSynchronize(s->la_k));
-  if (s->sweep_mg) {
+  if (s->sweep_coop) {
+    // the cooperative sweep's own checks (a subset split over XCDs, a barrier time-out): its chain
+    // state is then not the sampler's -- the session is poisoned, every later call on it fails
     int e = 0;
     HIPCHK(hipMemcpy(&e, s->sw_err, sizeof(int), hipMemcpyDeviceToHost));
-    if (e & 2) return set_err(MK_E_HIP, "latent sweep: a subset's workgroups ran on different XCDs (set MK_SWEEP=1)");
-    if (e) return set_err(MK_E_HIP, "latent sweep: workgroup barrier timed out");
+    if (e) {
+      s->poisoned = e & 2 ? "latent sweep: a subset's workgroups ran on different XCDs (MK_SWEEP=3 avoids the kernel)"
+                          : "latent sweep: workgroup barrier timed out";
+      return set_err(MK_E_HIP, s->poisoned);
+    }
   }
   if (s->prof) {
     s->stats[KS_ITER].launches += n_iter;
@@ -1848,6 +1631,7 @@ extern "C" int32_t mk_session_iteration(const mk_session* s) { return s ? s->ite
 extern "C" int mk_session_chain_state(mk_session* s, int32_t subset, double* beta, double* theta, double* w,
                                       double* tune, double* accept) {
   if (!s) return set_err(MK_E_ARG, "null session");
+  if (s->poisoned) return set_err(MK_E_HIP, std::string("session unusable after an earlier failure: ") + s->poisoned);
   if (subset < 0 || subset >= s->S) return set_err(MK_E_ARG, "subset out of range");
   MK_ENTRY_DEVICE(s->device);
   const Model& md = s->md;
@@ -1951,10 +1735,8 @@ static int predict_tile(mk_session* s, int t0, double* dq, mk_outputs* o) {
     MK_LAUNCH(k_kept_dirty, dim3(1), dim3(256), 0, st, mt, prev, s->d_slist, s->d_scount, g.d_plist,
                        g.d_pcount);
     for (int h = 0; h < q; ++h) {
-      launch_candidates(mt, g.ms, st, S, h, 1, 2 | cand_flags(s), 0, s->d_slist + h * S, s->d_scount + h);
-      g.gen = cov_gen(s, mt, true);
+      launch_candidates(mt, g.ms, st, S, h, 1, 2, 0, s->d_slist + h * S, s->d_scount + h);
       launch_cholesky(s, g, h, 1, s->d_slist + h * S, s->d_scount + h);
-      g.gen = CovGen{};
     }
     MK_LAUNCH(k_flip_pairs, dim3((S * q + 255) / 256), dim3(256), 0, st, g.ms, g.d_plist, g.d_pcount);
     launch_trinv(s, g, S * q, g.d_plist, g.d_pcount);
@@ -2057,6 +1839,7 @@ int session_tile_grids(mk_session* s, int t0, double* d_out, mk_outputs* o) {
 
 extern "C" int mk_session_grids(mk_session* s, int32_t which, double* out, int32_t device_out) {
   if (!s || !out) return set_err(MK_E_ARG, "null session/output");
+  if (s->poisoned) return set_err(MK_E_HIP, std::string("session unusable after an earlier failure: ") + s->poisoned);
   if (which != 0 && which != 1) return set_err(MK_E_ARG, "which must be 0 (parameters) or 1 (w.predict)");
   if (which == 1 && s->tiled) return set_err(MK_E_ARG, "tiled sessions give w.predict grids per tile (mk_session_tile_grids)");
   if (which == 1 && s->md.n_test < 1) return set_err(MK_E_ARG, "the session has no test sites");
@@ -2073,6 +1856,7 @@ extern "C" int mk_session_grids(mk_session* s, int32_t which, double* out, int32
 
 extern "C" int mk_session_tile_grids(mk_session* s, int32_t t0, double* out, int32_t device_out) {
   if (!s || !out) return set_err(MK_E_ARG, "null session/output");
+  if (s->poisoned) return set_err(MK_E_HIP, std::string("session unusable after an earlier failure: ") + s->poisoned);
   if (!s->tiled) return set_err(MK_E_ARG, "tile grids need a session created with predict_tile > 0");
   if (device_out) return session_tile_grids(s, t0, out, nullptr);
   const long Tc = std::min(s->pred_tile, s->n_test_all - t0);
@@ -2088,6 +1872,7 @@ extern "C" int mk_session_tile_grids(mk_session* s, int32_t t0, double* out, int
 
 extern "C" int mk_session_outputs(mk_session* s, mk_outputs* o) {
   if (!s || !o) return set_err(MK_E_ARG, "null session/outputs");
+  if (s->poisoned) return set_err(MK_E_HIP, std::string("session unusable after an earlier failure: ") + s->poisoned);
   MK_ENTRY_DEVICE(s->device);
   Model& md = s->md;
   const int S = s->S, P = s->P, q = s->q;

@@ -14,7 +14,6 @@
 // dynamic LDS of the LDS-DMA GEMM (k_chol_update): 2 stages x (A, B) x 16 k-rows x 144 doubles
 #define MK_GD_LDS_BYTES (2 * 2 * 16 * 144 * 8)
 #define MK_CAND_NOBORDER 4  // k_cov_candidate `which` flag: no bordered row (lookahead schedule)
-#define MK_CAND_COL0 8      // k_cov_candidate `which` flag: column-0 tiles only + phi' to Model::phi_c
                             // (MK_COV_FUSE: the update kernel generates every other tile at its first touch)
 #define MK_TLD 129         // LDS column stride of the diagonal-tile factor/inverse (k_chol_diag)
 // dynamic LDS of k_chol_diag: tile + diag(L) + diag(L^-1) + 7 16 x 17 inverse stagings

@@ -15,7 +15,7 @@ inline CovCandidateKernel cov_candidate_kernel(int model) {
 }
 template <int TM, int TN = TM>
 __global__ void k_chol_update(MatSet ms, int S, int h0, int hc, int k, int ia, int ib, int j0, int j1,
-                              const int* slist, const int* scount, CovGen cg);
+                              const int* slist, const int* scount);
 template <int TM>
 __global__ void k_chol_trsm(MatSet ms, int S, int h0, int hc, int k, int ia, int ib, const int* slist,
                             const int* scount);
@@ -52,34 +52,22 @@ template <int Q>
 __global__ void k_sweep(Model md, MatSet ms, int iter);
 template <int Q>
 __global__ void k_sweep_mg(Model md, MatSet ms, int iter, double* part, int* cnt, int* xcc, int* err);
-template <int Q>
-__global__ void k_sweep_tiles(Model md, MatSet ms, int iter, int B, double* part, const double* dacc_g, const int* any_g);
-template <int Q>
-__global__ void k_sweep_block(Model md, MatSet ms, int B, const double* part, double* dacc_g, int* any_g);
-template <int Q>
-__global__ void k_sweep_rows(Model md, MatSet ms, int iter);
-inline const void* sweep_rows_kernel(int q) {
-  return q == 1 ? (const void*)k_sweep_rows<1> : (q == 2 ? (const void*)k_sweep_rows<2> : (const void*)k_sweep_rows<3>);
-}
 template <int Q, int KR, int P, int HH, int LN>
 __global__ void k_sweep_site(Model md, MatSet ms, int iter);
 // its dynamic LDS: the sites' proposal / likelihood difference / accept draw + the accept flags
 inline size_t sweep_site_lds_bytes(int ns_max, int q, int lean = 0) { return (size_t)ns_max * q * (lean ? 4 : 3) * 8 + (size_t)ns_max * 4; }
 // the one-pass site sweep (kr 1: n_pad <= 2048, four row pairs per thread; 2: <= 4096, eight); NULL
 // where its registers would spill (q = 3 with kr = 2, q = 4): the 64-site-block kernels run there
-// (pair: two sites per barrier, q = 1 only)
-// lean: 0 the masked form; 1 (q = 1 pairs) fused-multiply-add dots, no row masks (W's zero upper
-// triangle), the border row dropped by a factor; 2 the same for shards whose n_s are all even (no
-// border element in a loaded pair).
-inline const void* sweep_site_kernel(int q, int kr, bool pair = false, int lean = 0) {
-  if (pair && q == 1 && lean > 0) {
+// q = 1: the lean pair form (two sites per barrier, fused-multiply-add dots, no row masks beyond the
+// one upper element a pair loads; lean 1: the border row dropped by a factor; 2: for shards whose
+// n_s are all even, no border element in a loaded pair); q = 2, 3: one site per barrier, masked.
+inline const void* sweep_site_kernel(int q, int kr, int lean = 1) {
+  if (q == 1) {
     if (kr == 1)
       return lean == 1 ? (const void*)k_sweep_site<1, 4, 2, 0, 1> : (const void*)k_sweep_site<1, 4, 2, 0, 2>;
     return lean == 1 ? (const void*)k_sweep_site<1, 8, 2, 0, 1> : (const void*)k_sweep_site<1, 8, 2, 0, 2>;
   }
-  if (pair) return q != 1 ? nullptr : (kr == 1 ? (const void*)k_sweep_site<1, 4, 2, 0, 0> : (const void*)k_sweep_site<1, 8, 2, 0, 0>);
   switch (q) {
-    case 1: return kr == 1 ? (const void*)k_sweep_site<1, 4, 1, 0, 0> : (const void*)k_sweep_site<1, 8, 1, 0, 0>;
     case 2: return kr == 1 ? (const void*)k_sweep_site<2, 4, 1, 0, 0> : (const void*)k_sweep_site<2, 8, 1, 0, 0>;
     case 3: return kr == 1 ? (const void*)k_sweep_site<3, 4, 1, 0, 0> : nullptr;
     default: return nullptr;
@@ -93,15 +81,6 @@ inline const void* sweep_step_kernel(int q) {
     case 2: return (const void*)k_sweep_step<2>;
     case 3: return (const void*)k_sweep_step<3>;
     default: return (const void*)k_sweep_step<4>;
-  }
-}
-// the split-launch sweep's two kernels for q outcomes
-inline const void* sweep_split_kernel(int q, bool block) {
-  switch (q) {
-    case 1: return block ? (const void*)k_sweep_block<1> : (const void*)k_sweep_tiles<1>;
-    case 2: return block ? (const void*)k_sweep_block<2> : (const void*)k_sweep_tiles<2>;
-    case 3: return block ? (const void*)k_sweep_block<3> : (const void*)k_sweep_tiles<3>;
-    default: return block ? (const void*)k_sweep_block<4> : (const void*)k_sweep_tiles<4>;
   }
 }
 // the sweep kernels specialised for the session's number of outcomes

@@ -209,21 +209,15 @@ __device__ inline int cheb_load(const double* src, double* chtab) {
 template <int MODEL>
 __global__ __launch_bounds__(256) void k_cov_candidate(Model md, MatSet ms, int h0, int hc, int which, int iter,
                                                        const int* slist, const int* scount) {
-  const bool col0 = (which & MK_CAND_COL0) != 0;
-  const int ntiles = col0 ? ms.nt : ms.nt * (ms.nt + 1) / 2;
+  const int ntiles = ms.nt * (ms.nt + 1) / 2;
   int e, t, s, h;
   if (!xcd_map(active_pairs(slist, scount, md.S, hc), ntiles, &e, &t) || !pick_pair(slist, scount, e, h0, hc, &s, &h)) return;
   int ti = 0, tj = 0;
-  if (col0) {
-    ti = t;   // column-0 tiles only: every other tile is generated by the update at its first touch
-  } else {
-    while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
-    tj = t - ti * (ti + 1) / 2;
-  }
+  while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
+  tj = t - ti * (ti + 1) / 2;
   const int sh = s * md.q + h;
   CandGen g = make_gen(md, s, h, which & 3, iter);
   if (which & MK_CAND_NOBORDER) g.uh = nullptr;   // lookahead: u is not known yet (k_border_step)
-  if (col0 && ti == 0 && threadIdx.x == 0) md.phi_c[sh] = g.rho.phi;
   double* M = mat_slot(ms, sh, 1 - ms.cur[sh]);
   const long ld = ms.ld;
   if (MODEL == MK_COV_MATERN) {
@@ -295,17 +289,9 @@ template __global__ void k_cov_candidate<MK_COV_MATERN>(Model, MatSet, int, int,
 // The split schedule (launch_cholesky) runs panels [0, k-1) early on the bulk stream and panel
 // k-1 on the critical stream; the accumulator round-trips through fp64 memory between the two,
 // so every element sees the same MFMA sequence as one [0, k) launch (same bits).
-// Generated candidate element (R, C) of pair (s, h): k_cov_candidate's exponential expression.
-__device__ inline double gen_value(const CovGen& cg, const double* cx, const double* cy, const double* uh, int ns,
-                                   double phi, int R, int C) {
-  if (R < ns && C < ns) return (R == C) ? 1.0 : exp(-phi * dist2d(cx[R], cy[R], cx[C], cy[C]));
-  if (R == ns && C < ns) return uh ? uh[C] : 0.0;
-  return (R == C && R != ns) ? 1.0 : 0.0;
-}
-
 template <int TM, int TN>
 __global__ __launch_bounds__(256, 2) void k_chol_update(MatSet ms, int S, int h0, int hc, int k, int ia, int ib,
-                                                       int j0, int j1, const int* slist, const int* scount, CovGen cg) {
+                                                       int j0, int j1, const int* slist, const int* scount) {
   extern __shared__ __attribute__((aligned(16))) double lds[];   // gb_lds_bytes(TM, TN) (two DMA stages)
   constexpr int SUBR = MK_NB / TM, SUB = SUBR * (MK_NB / TN);
   const int ntk = ib - ia;
@@ -321,28 +307,6 @@ __global__ __launch_bounds__(256, 2) void k_chol_update(MatSet ms, int S, int h0
   double* M = mat_slot(ms, sh, 1 - ms.cur[sh]);
   const long ld = ms.ld;
   double* C = M + i * MK_NB + sr * TM + (long)(k * MK_NB + sc * TN) * ld;
-  if (cg.phi_c && j0 == 0) {
-    // first touch of this sub-tile (the update of column k starts from panel 0): its candidate
-    // elements are generated here and written in place -- two rows per lane, 16-byte stores, as
-    // k_cov_candidate writes them -- then loaded as usual (the workgroup's stores are visible to its
-    // loads after the barrier's fence)
-    const int ns = cg.n_s[s];
-    const double* cx = cg.coords + (long)s * 2 * cg.n_pad;
-    const double* cy = cx + cg.n_pad;
-    const double* uh = cg.border ? cg.u + ((long)s * cg.q + h) * cg.n_pad : nullptr;
-    const double phi = cg.phi_c[sh];
-    const int R0 = i * MK_NB + sr * TM, C0 = k * MK_NB + sc * TN;
-    for (int e2 = threadIdx.x; e2 < (TM / 2) * TN; e2 += 256) {
-      const int rp = e2 % (TM / 2), cc = e2 / (TM / 2);
-      const int R = R0 + 2 * rp, Cc = C0 + cc;
-      if (i == k && R + 1 < Cc) continue;   // above the diagonal: never read
-      d2 v;
-      v.x = gen_value(cg, cx, cy, uh, ns, phi, R, Cc);
-      v.y = gen_value(cg, cx, cy, uh, ns, phi, R + 1, Cc);
-      *reinterpret_cast<d2*>(M + R + (long)Cc * ld) = v;
-    }
-    __syncthreads();
-  }
   AccT<TM / 32, TN / 32> acc;
   acc_load(acc, C, ld);
   // (Skipping the diagonal tiles' unused upper quadrant -- per MFMA or per chunk -- measured slower.)
@@ -351,9 +315,9 @@ __global__ __launch_bounds__(256, 2) void k_chol_update(MatSet ms, int S, int h0
                                       (j1 - j0) * MK_NB, (j1 - j0) * MK_NB, acc, lds);
   store_tile(C, ld, acc);
 }
-template __global__ void k_chol_update<128, 128>(MatSet, int, int, int, int, int, int, int, int, const int*, const int*, CovGen);
-template __global__ void k_chol_update<64, 64>(MatSet, int, int, int, int, int, int, int, int, const int*, const int*, CovGen);
-template __global__ void k_chol_update<32, 32>(MatSet, int, int, int, int, int, int, int, int, const int*, const int*, CovGen);
+template __global__ void k_chol_update<128, 128>(MatSet, int, int, int, int, int, int, int, int, const int*, const int*);
+template __global__ void k_chol_update<64, 64>(MatSet, int, int, int, int, int, int, int, int, const int*, const int*);
+template __global__ void k_chol_update<32, 32>(MatSet, int, int, int, int, int, int, int, int, const int*, const int*);
 
 // TM = 64: the tile's two row halves on two workgroups (in place: each reads and writes its own
 // rows only), bit-identical.
@@ -1389,20 +1353,9 @@ __global__ __launch_bounds__(256, 2) void k_pred_var(Model md, MatSet ms, const 
   const int per = ms.nt * md.ntt;
   int e, t_;
   if (!xcd_map(*count, per, &e, &t_)) return;
-  // Grouped raster: groups of G = pred_gi row panels; inside a group the G row panels of one test
-  // block are consecutive, then the next test block.  The ~64 workgroups an XCD holds at once then
-  // cover G row panels x 64/G test blocks: each W row panel is shared by 64/G of them and each P^T
-  // block by G (through L2), where plain row-panel-major order (G = 1) shares W 64 ways and fetches
-  // every P^T block once per row panel (measured 8.7 x the P^T bytes).  (tb-major -- G = nt --
-  // re-reads W: 0.65 vs 0.74 of peak.)  Placement only: every tile's arithmetic is the same.
-  int i, tb;
-  {
-    const int G = md.pred_gi, gsz = G * md.ntt;
-    const int g0 = (t_ / gsz) * G, r = t_ % gsz;
-    const int ge = min(G, ms.nt - g0);      // short last group
-    tb = r / ge;
-    i = g0 + r % ge;
-  }
+  // row-panel-major raster: the ~64 workgroups an XCD holds at once share one W row panel (L2);
+  // grouped rasters that share P^T blocks instead measured slower
+  const int i = t_ / md.ntt, tb = t_ % md.ntt;
   const int sh = list[e];
   const int s = sh / md.q;
   const int ns = md.n_s[s];

@@ -593,144 +593,6 @@ __global__ __launch_bounds__(SW_T) void k_sweep(Model md, MatSet ms, int iter) {
   sweep_apply(md, s, 0, ns, Ai, tid, SW_T);
 }
 
-// One workgroup per subset, rows owned by waves (k_sweep's arithmetic, laid out for latency):
-// wave w of 8 owns the rows of tiles w, w + 8, w + 16, w + 24 (lane l: rows 128 t + 2 l, + 1) and
-// keeps their z in registers for the whole sweep, so a block's z update (panel B-1) and its dots (panel B) are one
-// pass over the wave's own rows -- no z round trip through memory and no per-column pass over
-// every tile: per block each wave issues its tile's loads of both panels in 16-column batches.
-// Same bits as k_sweep: the update is per row in the same column-residue FMA order (row pairs are
-// even-aligned in both, and a pair is never split by p0), the dots are the same per-tile DPP
-// reductions summed in tile order.  q <= 3 (LDS: Q_BB + the per-tile partials).
-#define SR_T 512                                  // k_sweep_rows: 8 waves, 2 per SIMD (256 VGPRs)
-#define SR_W (SR_T / 64)
-template <int Q>
-__global__ __launch_bounds__(SR_T) void k_sweep_rows(Model md, MatSet ms, int iter) {
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  constexpr int q = Q;
-  const int nt = ms.nt;
-  double* Qb = smem;                              // [q][SW_B*SW_B] column-major
-  double* gb = Qb + q * SW_B * SW_B;              // [q][SW_B]
-  double* dacc = gb + q * SW_B;                   // [q][SW_B]
-  double* part = dacc + q * SW_B;                 // [nt][q][SW_B] per-tile partial dots
-  __shared__ int any_acc;
-  __shared__ double Ai[MK_QMAX * MK_QMAX];
-  const int s = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int ns = md.n_s[s];
-  const long ld = ms.ld;
-  const int tl = (ns - 1) / MK_NB;
-  double* z = md.z + (long)s * q * md.n_pad;
-  if (tid < q * q) Ai[tid] = md.Ainv[(long)s * q * q + tid];
-  sweep_precompute(md, s, iter, 0, ns * q, tid, SR_T);
-  constexpr int NS = 4;                           // tile slots per wave: tiles wv, wv + 8, wv + 16, wv + 24
-  d2 zr[NS][Q];
-#pragma unroll
-  for (int k = 0; k < NS; ++k) {
-    const int r0 = MK_NB * (wv + SR_W * k) + 2 * lane;
-#pragma unroll
-    for (int h = 0; h < Q; ++h)
-      zr[k][h] = (wv + SR_W * k <= tl) ? *reinterpret_cast<const d2*>(z + (long)h * md.n_pad + r0) : d2{0.0, 0.0};
-  }
-  if (tid == 0) any_acc = 0;
-  __syncthreads();
-  int p0 = 0, pnb = 0;
-  for (int b0 = 0; b0 < ns + SW_B; b0 += SW_B) {
-    const int nb = min(SW_B, ns - b0);
-    const bool upd = pnb > 0 && any_acc;
-    const int tile = b0 / MK_NB;
-#pragma unroll
-    for (int k = 0; k < NS; ++k) {
-      const int t = wv + SR_W * k;
-      if (t > tl) continue;
-      const int r0 = MK_NB * t + 2 * lane;
-      // ---- (a) own rows >= p0: z += W[:, prev block] delta'_prev (k_sweep's column-residue order)
-      if (upd && MK_NB * t + MK_NB > p0) {
-#pragma unroll
-        for (int h = 0; h < Q; ++h) {
-          const double* Wp = ms.W + ((long)s * q + h) * (ld * ld) + (long)p0 * ld + r0;
-          const double* da = dacc + h * SW_B;
-          d2 v4[4] = {{0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}};
-          for (int k0 = 0; k0 < pnb; k0 += 16) {
-            d2 wv2[16];
-#pragma unroll
-            for (int u = 0; u < 16; ++u) wv2[u] = *reinterpret_cast<const d2*>(Wp + (long)min(k0 + u, pnb - 1) * ld);
-#pragma unroll
-            for (int u = 0; u < 16; ++u) {
-              const double c = (k0 + u < pnb) ? da[k0 + u] : 0.0;
-              v4[u & 3].x = fma(wv2[u].x, c, v4[u & 3].x);
-              v4[u & 3].y = fma(wv2[u].y, c, v4[u & 3].y);
-            }
-          }
-          const double vx = ((v4[0].x + v4[1].x) + v4[2].x) + v4[3].x;
-          const double vy = ((v4[0].y + v4[1].y) + v4[2].y) + v4[3].y;
-          if (r0 >= p0 && r0 < ns) zr[k][h].x += vx;
-          if (r0 >= p0 && r0 + 1 < ns) zr[k][h].y += vy;
-        }
-      }
-      // ---- (b) own tile's partial dots of the block's columns (tiles >= the block's first tile)
-      if (nb > 0 && t >= tile) {
-#pragma unroll
-        for (int h = 0; h < Q; ++h) {
-          const double* Wb = ms.W + ((long)s * q + h) * (ld * ld) + (long)b0 * ld + r0;
-          for (int i0 = 0; i0 < nb; i0 += 16) {
-            d2 wv2[16];
-#pragma unroll
-            for (int u = 0; u < 16; ++u) wv2[u] = *reinterpret_cast<const d2*>(Wb + (long)min(i0 + u, nb - 1) * ld);
-#pragma unroll
-            for (int u = 0; u < 16; ++u) {
-              const double a0 = (r0 >= b0 && r0 < ns) ? wv2[u].x * zr[k][h].x : 0.0;
-              const double a1 = (r0 + 1 >= b0 && r0 + 1 < ns) ? wv2[u].y * zr[k][h].y : 0.0;
-              const double pp = wave_sum_dpp(a0 + a1);
-              if (lane == 0 && i0 + u < nb) part[((long)t * q + h) * SW_B + i0 + u] = pp;
-            }
-          }
-        }
-      }
-    }
-    __syncthreads();
-    if (nb <= 0) break;
-    if (tid == 0) any_acc = 0;
-    // ---- dots summed in tile order; Q_BB into LDS
-    for (int e = tid; e < q * SW_B; e += SR_T) {
-      const int h = e / SW_B, i = e % SW_B;
-      double g = part[((long)tile * q + h) * SW_B + i];
-      for (int t = tile + 1; t <= tl; ++t) g = g + part[((long)t * q + h) * SW_B + i];
-      gb[e] = (i < nb) ? g : 0.0;
-    }
-    const int off = b0 % MK_NB;
-    for (int h = 0; h < q; ++h) {
-      const double* QBt = ms.QB + (((long)s * q + h) * ms.nt + tile) * MK_NB * MK_NB;
-      for (int e = tid; e < SW_B * SW_B; e += SR_T) {
-        const int r = e & (SW_B - 1), c = e / SW_B;
-        const double v = QBt[(off + r) + (off + c) * MK_NB];
-        Qb[h * SW_B * SW_B + e] = (r < nb && c < nb) ? v : 0.0;
-      }
-    }
-    __syncthreads();
-    // ---- the block's sequential Metropolis steps (wave 0)
-    if (wv == 0) {
-      const int anyl = sweep_block_mh_q<Q, false>(md, s, b0, nb, gb, Qb, Ai, dacc, true);
-      if (lane == 0) any_acc = anyl;
-    }
-    __syncthreads();
-    p0 = b0;
-    pnb = nb;
-  }
-  // ---- write back own z rows; apply accepted moves
-#pragma unroll
-  for (int k = 0; k < NS; ++k) {
-    const int t = wv + SR_W * k;
-    if (t > tl) continue;
-    const int r0 = MK_NB * t + 2 * lane;
-#pragma unroll
-    for (int h = 0; h < Q; ++h) *reinterpret_cast<d2*>(z + (long)h * md.n_pad + r0) = zr[k][h];
-  }
-  __syncthreads();
-  sweep_apply(md, s, 0, ns, Ai, tid, SR_T);
-}
-template __global__ void k_sweep_rows<1>(Model, MatSet, int);
-template __global__ void k_sweep_rows<2>(Model, MatSet, int);
-template __global__ void k_sweep_rows<3>(Model, MatSet, int);
-
 // Multi-workgroup sweep (small shards).  Grid: xcd_grid(S, nt) workgroups of 256 threads,
 // cooperative (all co-resident); workgroup (s, t) owns rows [128t, 128t + 128) of subset s
 // (its z rows in registers, replicated in the four waves; its sites' proposals and final
@@ -924,153 +786,18 @@ __global__ __launch_bounds__(256) void k_sweep_mg(Model md, MatSet ms, int iter,
 }
 // Split-launch sweep (small shards, no inter-workgroup waiting).  The sweep's only sequential
 // dependency -- block B's dots need z after block B-1's accepted moves -- is carried by stream
-// order instead of by barriers between co-resident workgroups: per 64-site block two launches,
-//   k_sweep_tiles(B): one 256-thread workgroup per (subset, 128-row tile): z rows of the tile
-//                     += W[:, B-1] delta'_{B-1} (if block B-1 moved a site), then the tile's partial
-//                     dots of block B's columns -> part[s][t][h][64]; B = 0 also computes the
-//                     tile's proposals, the launch after a subset's last block applies its moves;
-//   k_sweep_block(B): one workgroup per subset: the partials of tiles tf .. tl summed in tile
-//                     order, Q_BB, the block's MH steps (wave 0) -> delta' [s][h][64], any-moved.
-// A workgroup never waits on another, so nothing depends on co-residency, queue priority or CU
-// masks.  The arithmetic and its order are k_sweep's / k_sweep_mg's (per-tile DPP dot reductions
-// summed in tile order; per-wave column-residue FMA chains summed over the four waves): same bits.
-template <int Q>
-__global__ __launch_bounds__(256) void k_sweep_tiles(Model md, MatSet ms, int iter, int B, double* __restrict__ part,
-                                                     const double* __restrict__ dacc_g, const int* __restrict__ any_g) {
-  __shared__ double red[4 * MK_NB];
-  __shared__ double Ai[MK_QMAX * MK_QMAX];
-  constexpr int q = Q;
-  const int nt = ms.nt;
-  const int s = blockIdx.x / nt, t = blockIdx.x % nt;
-  const int ns = md.n_s[s];
-  const int tl = (ns - 1) / MK_NB;
-  if (t > tl) return;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const long ld = ms.ld;
-  const int r0 = MK_NB * t + 2 * lane;
-  const int n_blk = (ns + SW_B - 1) / SW_B;
-  if (B > n_blk) return;
-  if (B == 0) sweep_precompute(md, s, iter, MK_NB * t * q, min(MK_NB * (t + 1), ns) * q, tid, 256);
-  d2 zr[Q];
-#pragma unroll
-  for (int h = 0; h < Q; ++h) zr[h] = *reinterpret_cast<const d2*>(md.z + ((long)s * q + h) * md.n_pad + r0);
-  bool zdirty = false;
-  // ---- z rows of tile t (rows >= b0') += W[:, B-1] delta'_{B-1}
-  if (B > 0) {
-    const int bp = (B - 1) * SW_B, nbp = min(SW_B, ns - bp);
-    if (t >= bp / MK_NB && any_g[s]) {
-      zdirty = true;
-      for (int h = 0; h < q; ++h) {
-        const double* Wt = ms.W + ((long)s * q + h) * (ld * ld) + (long)bp * ld + r0;
-        const double* da = dacc_g + ((long)s * q + h) * SW_B;
-        d2 wreg[16];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) wreg[j] = *reinterpret_cast<const d2*>(Wt + (long)(wv + 4 * j) * ld);
-        d2 sw = {0.0, 0.0};
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          const int i = wv + 4 * j;
-          const double c = (i < nbp) ? da[i] : 0.0;
-          sw.x = fma(wreg[j].x, c, sw.x);
-          sw.y = fma(wreg[j].y, c, sw.y);
-        }
-        red[wv * MK_NB + 2 * lane] = sw.x;
-        red[wv * MK_NB + 2 * lane + 1] = sw.y;
-        __syncthreads();
-        const double vx = ((red[2 * lane] + red[MK_NB + 2 * lane]) + red[2 * MK_NB + 2 * lane]) + red[3 * MK_NB + 2 * lane];
-        const double vy = ((red[2 * lane + 1] + red[MK_NB + 2 * lane + 1]) + red[2 * MK_NB + 2 * lane + 1]) +
-                          red[3 * MK_NB + 2 * lane + 1];
-        __syncthreads();
-#pragma unroll
-        for (int hh = 0; hh < Q; ++hh) {
-          if (hh != h) continue;
-          if (r0 >= bp && r0 < ns) zr[hh].x += vx;
-          if (r0 + 1 >= bp && r0 + 1 < ns) zr[hh].y += vy;
-        }
-      }
-    }
-  }
-  if (B < n_blk) {
-    // ---- partial dots of tile t for block B's columns (tiles >= the block's first tile)
-    const int b0 = B * SW_B;
-    if (t >= b0 / MK_NB) {
-      double* pb = part + (((long)s * nt + t) * q) * SW_B;
-      for (int h = 0; h < q; ++h) {
-        const double* Wt = ms.W + ((long)s * q + h) * (ld * ld) + (long)b0 * ld + r0;
-        d2 wreg[16];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) wreg[j] = *reinterpret_cast<const d2*>(Wt + (long)(wv + 4 * j) * ld);
-        d2 zz = zr[0];
-#pragma unroll
-        for (int hh = 1; hh < Q; ++hh)
-          if (hh == h) zz = zr[hh];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          const double a0 = (r0 >= b0 && r0 < ns) ? wreg[j].x * zz.x : 0.0;
-          const double a1 = (r0 + 1 >= b0 && r0 + 1 < ns) ? wreg[j].y * zz.y : 0.0;
-          const double p = wave_sum_dpp(a0 + a1);
-          if (lane == 0) pb[h * SW_B + wv + 4 * j] = p;
-        }
-      }
-    }
-  }
-  if (zdirty && wv == 0) {
-#pragma unroll
-    for (int h = 0; h < Q; ++h) *reinterpret_cast<d2*>(md.z + ((long)s * q + h) * md.n_pad + r0) = zr[h];
-  }
-  if (B == n_blk) {   // the subset's last block is done: apply this tile's accepted moves
-    if (tid < q * q) Ai[tid] = md.Ainv[(long)s * q * q + tid];
-    __syncthreads();
-    sweep_apply(md, s, MK_NB * t, min(MK_NB * (t + 1), ns), Ai, tid, 256);
-  }
-}
-
-template <int Q>
-__global__ __launch_bounds__(256) void k_sweep_block(Model md, MatSet ms, int B, const double* __restrict__ part,
-                                                     double* __restrict__ dacc_g, int* __restrict__ any_g) {
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  constexpr int q = Q;
-  double* Qb = smem;                              // [q][SW_B*SW_B]
-  double* gb = Qb + q * SW_B * SW_B;              // [q][SW_B]
-  double* dacc = gb + q * SW_B;                   // [q][SW_B]
-  __shared__ double Ai[MK_QMAX * MK_QMAX];
-  const int s = blockIdx.x, tid = threadIdx.x;
-  const int ns = md.n_s[s];
-  const int b0 = B * SW_B;
-  if (b0 >= ns) return;
-  const int nb = min(SW_B, ns - b0), tf = b0 / MK_NB, tl = (ns - 1) / MK_NB, nt = ms.nt;
-  if (tid < q * q) Ai[tid] = md.Ainv[(long)s * q * q + tid];
-  const int tile = b0 / MK_NB, off = b0 % MK_NB;
-  for (int h = 0; h < q; ++h) {
-    const double* QBt = ms.QB + (((long)s * q + h) * nt + tile) * MK_NB * MK_NB;
-    for (int e = tid; e < SW_B * SW_B; e += 256) {
-      const int r = e & (SW_B - 1), c = e / SW_B;
-      Qb[h * SW_B * SW_B + e] = QBt[(off + r) + (off + c) * MK_NB];
-    }
-  }
-  // dots: partials of tiles tf .. tl summed in tile order
-  for (int e = tid; e < q * SW_B; e += 256) {
-    const int h = e / SW_B, i = e % SW_B;
-    const double* pp = part + ((long)s * nt * q + h) * SW_B + i;
-    double g = pp[(long)tf * q * SW_B];
-    for (int u = tf + 1; u <= tl; ++u) g = g + pp[(long)u * q * SW_B];
-    gb[e] = g;
-  }
-  __syncthreads();
-  if (tid < 64) {
-    const int anyl = sweep_block_mh_q<Q, false>(md, s, b0, nb, gb, Qb, Ai, dacc, true);
-#pragma unroll
-    for (int h = 0; h < Q; ++h) dacc_g[((long)s * q + h) * SW_B + tid] = dacc[h * SW_B + tid];
-    if (tid == 0) any_g[s] = anyl;
-  }
-}
-
-// Split-launch sweep, one launch per block: launch B is k_sweep_tiles(B) with k_sweep_block(B-1)
-// folded in as a prologue that every tile workgroup of the subset runs redundantly -- the same
-// partials summed in the same order, the same Q_BB and draws, so every copy makes the same
-// decisions and computes the same delta' (the owner tile, tf, records the accept flags).  Half the
-// launches of the two-kernel form.  The partials are double-buffered by block parity (launch B
-// reads block B-1's while it writes block B's).  part: [S][2][nt][q][64].
+// order instead of by barriers between co-resident workgroups: one launch per 64-site block, one
+// 256-thread workgroup per (subset, 128-row tile).  Launch B (i) runs block B-1's MH steps from the
+// partial dots of the previous launch, redundantly in every tile workgroup of the subset -- the
+// same partials summed in the same tile order, the same Q_BB and draws, so every copy makes the same
+// decisions and computes the same delta' (the owner tile, tf, records the accept flags); (ii) adds
+// W[:, B-1] delta'_{B-1} to its z rows; (iii) writes its partial dots of block B's columns.  B = 0
+// also computes the tile's proposals; the launch after a subset's last block applies its moves.  The
+// partials are double-buffered by block parity (launch B reads block B-1's while it writes block
+// B's).  part: [S][2][nt][q][64].  A workgroup never waits on another, so nothing depends on
+// co-residency, queue priority or CU masks.  The arithmetic and its order are k_sweep's /
+// k_sweep_mg's (per-tile DPP dot reductions summed in tile order; per-wave column-residue FMA chains
+// summed over the four waves): same bits.
 template <int Q>
 __global__ __launch_bounds__(256) void k_sweep_step(Model md, MatSet ms, int iter, int B, double* __restrict__ part) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -1223,18 +950,11 @@ template __global__ void k_sweep_mg<1>(Model, MatSet, int, double*, int*, int*, 
 template __global__ void k_sweep_mg<2>(Model, MatSet, int, double*, int*, int*, int*);
 template __global__ void k_sweep_mg<3>(Model, MatSet, int, double*, int*, int*, int*);
 template __global__ void k_sweep_mg<4>(Model, MatSet, int, double*, int*, int*, int*);
-#define MK_INST_SPLIT(Q)                                                                                   \
-  template __global__ void k_sweep_tiles<Q>(Model, MatSet, int, int, double*, const double*, const int*); \
-  template __global__ void k_sweep_block<Q>(Model, MatSet, int, const double*, double*, int*);
 #define MK_INST_STEP(Q) template __global__ void k_sweep_step<Q>(Model, MatSet, int, int, double*);
 MK_INST_STEP(1)
 MK_INST_STEP(2)
 MK_INST_STEP(3)
 MK_INST_STEP(4)
-MK_INST_SPLIT(1)
-MK_INST_SPLIT(2)
-MK_INST_SPLIT(3)
-MK_INST_SPLIT(4)
 
 // ---------------------------------------------------------------- 5b. one-pass site sweep (default)
 // The single-site w updates of spMvGLM (MK.R:80-84) with every column of W_h = L_h^-1 read from HBM
@@ -1303,7 +1023,7 @@ typedef unsigned int u4v __attribute__((ext_vector_type(4)));
 // the move's coefficient d A^-1 and half its square precomputed -- 253 instead of 336 VALU
 // instructions per pair; 1.12 -> 0.97 ms per sweep at 250 subsets, 0.92-0.94 ms with the sites' data
 // read from registers (pair_step).
-// P = 2 (q = 1, MK_SWEEP=7): two sites per barrier.  The pair (i, i+1) exchanges five values --
+// P = 2 (q = 1, always with LN > 0): two sites per barrier.  The pair (i, i+1) exchanges five values --
 // both dots, both squared norms and c = W[:,i] . W[:,i+1] = (R^-1)_{i+1,i} -- so site i+1's dot
 // after a move at site i is g_{i+1} + coef_i c (the same carry the 64-site blocks make through Q_BB);
 // half the barriers, one more reduction per pair.
@@ -1500,7 +1220,8 @@ __global__ __launch_bounds__(SS_T) void k_sweep_site(Model md, MatSet ms, int it
   // index instead of LDS reads, address arithmetic and readfirstlanes.  Sites past n_s: accept draw +inf.
   double vcf = 0.0, vdll = 0.0, vh = 0.0, vlg = __builtin_huge_val();
   auto pair_step = [&](const int i, d2 (&w0)[KR][Q], d2 (&w1)[KR][Q]) {
-    if constexpr (FM) {
+    static_assert(P == 1 || FM, "site pairs: the lean form");
+    {
       if ((i & 63) == 0) {   // uniform
         const int kk = i + lane;
         const bool lv = kk < ns;
@@ -1512,14 +1233,10 @@ __global__ __launch_bounds__(SS_T) void k_sweep_site(Model md, MatSet ms, int it
       }
     }
     const bool live0 = i < ns, live1 = i + 1 < ns;
-    const int i0c = live0 ? i : ns - 1, i1c = live1 ? i + 1 : ns - 1;
-    const double dl0 = sd_dl[i0c], dll0 = sd_dll[i0c], lg0 = live0 ? sd_lgu[i0c] : __builtin_huge_val();
-    const double dl1 = sd_dl[i1c], dll1 = sd_dll[i1c], lg1 = live1 ? sd_lgu[i1c] : __builtin_huge_val();
     d2 c0[KR], c1[KR];
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
-      const int r0 = 2 * tid + 2 * SS_T * k;
-      if constexpr (FM) {
+      {
         // No row masks: i is even, so the loads already return zero for every row pair wholly above
         // column i's diagonal, and the one upper element left, W[i, i+1], is zero in memory (W's
         // upper triangle is zeroed at session creation and never written: store_tile_lw,
@@ -1530,29 +1247,16 @@ __global__ __launch_bounds__(SS_T) void k_sweep_site(Model md, MatSet ms, int it
         c0[k].y = LN == 1 ? w0[k][0].y * ym[k] : w0[k][0].y;
         c1[k].x = w1[k][0].x;
         c1[k].y = LN == 1 ? w1[k][0].y * ym[k] : w1[k][0].y;
-      } else {
-        c0[k].x = (r0 >= i) ? w0[k][0].x : 0.0;
-        c0[k].y = (r0 + 1 >= i && r0 + 1 < ns) ? w0[k][0].y : 0.0;
-        c1[k].x = (r0 >= i + 1) ? w1[k][0].x : 0.0;
-        c1[k].y = (r0 + 1 >= i + 1 && r0 + 1 < ns) ? w1[k][0].y : 0.0;
       }
     }
     double v[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
-      if constexpr (FM) {
-        v[0] = fma(c0[k].y, zr[k][0].y, fma(c0[k].x, zr[k][0].x, v[0]));
-        v[1] = fma(c1[k].y, zr[k][0].y, fma(c1[k].x, zr[k][0].x, v[1]));
-        v[2] = fma(c0[k].y, c0[k].y, fma(c0[k].x, c0[k].x, v[2]));
-        v[3] = fma(c1[k].y, c1[k].y, fma(c1[k].x, c1[k].x, v[3]));
-        v[4] = fma(c0[k].y, c1[k].y, fma(c0[k].x, c1[k].x, v[4]));
-      } else {
-        v[0] += c0[k].x * zr[k][0].x + c0[k].y * zr[k][0].y;
-        v[1] += c1[k].x * zr[k][0].x + c1[k].y * zr[k][0].y;
-        v[2] += c0[k].x * c0[k].x + c0[k].y * c0[k].y;
-        v[3] += c1[k].x * c1[k].x + c1[k].y * c1[k].y;
-        v[4] += c0[k].x * c1[k].x + c0[k].y * c1[k].y;
-      }
+      v[0] = fma(c0[k].y, zr[k][0].y, fma(c0[k].x, zr[k][0].x, v[0]));
+      v[1] = fma(c1[k].y, zr[k][0].y, fma(c1[k].x, zr[k][0].x, v[1]));
+      v[2] = fma(c0[k].y, c0[k].y, fma(c0[k].x, c0[k].x, v[2]));
+      v[3] = fma(c1[k].y, c1[k].y, fma(c1[k].x, c1[k].x, v[3]));
+      v[4] = fma(c0[k].y, c1[k].y, fma(c0[k].x, c1[k].x, v[4]));
     }
 #pragma unroll
     for (int e = 0; e < 5; ++e) v[e] = row_sum_dpp(v[e]);
@@ -1574,10 +1278,9 @@ __global__ __launch_bounds__(SS_T) void k_sweep_site(Model md, MatSet ms, int it
 #pragma unroll
       for (int e = 0; e < 4; ++e) tot[4 * rr + e] = rlane_u(rsum, 16 * e);
     }
-    const double a0 = ai[0];
     int f0 = 0, f1 = 0;
     double coef0 = 0.0, coef1 = 0.0;
-    if constexpr (FM) {   // ratio = dll - (cf g + 0.5 cf^2 Q_ii), cf = d A^-1 (precomputed per site)
+    {   // ratio = dll - (cf g + 0.5 cf^2 Q_ii), cf = d A^-1 (precomputed per site)
       const int l0 = i & 63, l1 = l0 + 1;
       const double cf0 = rlane_u(vcf, l0), cf1 = rlane_u(vcf, l1);
       const double h0 = rlane_u(vh, l0), h1 = rlane_u(vh, l1);
@@ -1590,26 +1293,6 @@ __global__ __launch_bounds__(SS_T) void k_sweep_site(Model md, MatSet ms, int it
         coef1 = cf1;
         f1 = 1;
       }
-    } else {
-    {
-      const double d = rfl_f64(dl0);
-      const double c = a0 * tot[0];
-      const double dd = (a0 * a0) * tot[2];
-      if (rfl_f64(lg0) <= rfl_f64(dll0) - (d * c + 0.5 * d * d * dd)) {
-        coef0 = d * a0;
-        f0 = 1;
-      }
-    }
-    {
-      const double d = rfl_f64(dl1);
-      const double g1 = f0 ? tot[1] + coef0 * tot[4] : tot[1];
-      const double c = a0 * g1;
-      const double dd = (a0 * a0) * tot[3];
-      if (rfl_f64(lg1) <= rfl_f64(dll1) - (d * c + 0.5 * d * d * dd)) {
-        coef1 = d * a0;
-        f1 = 1;
-      }
-    }
     }
     if (f0 | f1) {
 #pragma unroll
@@ -1659,13 +1342,9 @@ __global__ __launch_bounds__(SS_T) void k_sweep_site(Model md, MatSet ms, int it
   __syncthreads();
   sweep_apply(md, s, 0, ns, Ai_s, tid, SS_T);
 }
-template __global__ void k_sweep_site<1, 4, 1>(Model, MatSet, int);
-template __global__ void k_sweep_site<1, 8, 1>(Model, MatSet, int);
 template __global__ void k_sweep_site<2, 4, 1>(Model, MatSet, int);
 template __global__ void k_sweep_site<2, 8, 1>(Model, MatSet, int);
 template __global__ void k_sweep_site<3, 4, 1>(Model, MatSet, int);
-template __global__ void k_sweep_site<1, 4, 2>(Model, MatSet, int);
-template __global__ void k_sweep_site<1, 8, 2>(Model, MatSet, int);
 template __global__ void k_sweep_site<1, 4, 2, 0, 1>(Model, MatSet, int);
 template __global__ void k_sweep_site<1, 4, 2, 0, 2>(Model, MatSet, int);
 template __global__ void k_sweep_site<1, 8, 2, 0, 1>(Model, MatSet, int);

@@ -60,6 +60,7 @@ struct Rccl {
   ncclResult_t (*send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
   ncclResult_t (*recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
   const char* (*error_string)(ncclResult_t) = nullptr;
+  ncclResult_t (*comm_count)(const ncclComm_t, int*) = nullptr;   // optional: ranks a communicator holds
 };
 
 // RCCL must run on the HIP runtime libmk runs on.  A process can hold two: a host that loads torch
@@ -105,6 +106,7 @@ const Rccl& rccl() {
     x.send = (decltype(x.send))dlsym(h, "ncclSend");
     x.recv = (decltype(x.recv))dlsym(h, "ncclRecv");
     x.error_string = (decltype(x.error_string))dlsym(h, "ncclGetErrorString");
+    x.comm_count = (decltype(x.comm_count))dlsym(h, "ncclCommCount");
     x.ok = x.comm_init_all && x.comm_destroy && x.comm_abort && x.group_start && x.group_end && x.send && x.recv && x.error_string;
     if (!x.ok) x.why = "librccl lacks a symbol";
     return x;
@@ -446,7 +448,13 @@ extern "C" int mk_meta_fit(const mk_problem* pr, const mk_config* c, const int32
                                 " (MK_EXCHANGE=copy selects the device-copy exchange)");
     }
   }
-  if (comb) comb->exchange = nd.use_rccl ? 1 : 0;
+  if (comb) {
+    comb->exchange = nd.use_rccl ? 1 : 0;
+    // the ranks the exchange spans, as RCCL itself counts them (communicator 0); copies: the blocks
+    int nr = G;
+    if (nd.use_rccl && rccl().comm_count && rccl().comm_count(nd.comms[0], &nr) != ncclSuccess) nr = -1;
+    comb->comm_ranks = nr;
+  }
 
   // ---- the chains, one amcmc batch at a time on every device; progress between batches
   for (int it = 0; it < n_samples; it += c->batch_length) {

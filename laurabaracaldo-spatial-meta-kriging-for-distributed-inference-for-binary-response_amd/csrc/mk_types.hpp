@@ -51,7 +51,6 @@ struct Model {
   const double* span_pt;       // [S] bound on the subset-to-test-site distances (Matern kriging tables)
   double* chtab;               // [S*q][MK_CH_TAB] Matern: Chebyshev tables of the pairs' candidates (k_matern_table)
   double* chtab_p;             // [S*q][MK_CH_TAB] Matern: tables of the current (phi, nu), kriging (k_matern_table_list)
-  double* phi_c;               // [S*q] phi of each pair's current candidate (MK_CAND_COL0; covariance fused into the update)
   // state
   double* beta;      // [S][p]
   double* theta;     // [S][n_theta]: A lower-tri (log diag) | logit phi | logit nu
@@ -94,17 +93,6 @@ struct Model {
   double* zc;          // [S][q][n_pad]     z'_h = L'_h^-1 u_h of the candidate
   int* la_nu;          // [S*q]             Matern: 1 where this iteration's nu step accepted (k_nu_border)
   int P;               // reported columns
-  int pred_gi;         // kriging GEMM raster: row panels per group (k_pred_var; 1 = row-panel-major)
-};
-
-// Candidate covariance generated inside k_chol_update at a tile's first touch (panels from 0):
-// the exponential model's elements, k_cov_candidate's expression (same bits).  phi_c == nullptr: off.
-struct CovGen {
-  const double* coords;   // [S][2][n_pad]
-  const int* n_s;
-  const double* u;        // [S][q][n_pad] the bordered row (border != 0)
-  const double* phi_c;    // [S*q]
-  int n_pad, q, border;
 };
 
 struct MatSet {

@@ -91,6 +91,7 @@ std::string report(const Call& c, double secs) {
   std::string out = line;
   int pending = 0;
   for (const Traced& t : g_streams) {
+    if (!t.st) continue;   // a free slot
     const unsigned done = __atomic_load_n(g_words + t.slot, __ATOMIC_ACQUIRE);
     if (done == t.enq) continue;
     ++pending;
@@ -162,14 +163,30 @@ void wd_trace(hipStream_t st, const char* name) {
   for (Traced& x : g_streams)
     if (x.st == st) t = &x;
   if (!t) {
-    if ((int)g_streams.size() >= MAX_STREAMS) return;
-    Traced n;
-    n.st = st;
-    (void)hipGetDevice(&n.device);
-    n.slot = (unsigned)g_streams.size();
-    g_words[n.slot] = 0;
-    g_streams.push_back(n);
-    t = &g_streams.back();
+    // a destroyed stream's entry (wd_forget) is reused first: the stream pool destroys and recreates
+    // streams when the shard configuration changes, so a long process would otherwise run out of slots
+    for (Traced& x : g_streams)
+      if (!x.st) {
+        t = &x;
+        break;
+      }
+    if (!t && (int)g_streams.size() < MAX_STREAMS) {
+      g_streams.push_back(Traced{});
+      t = &g_streams.back();
+      t->slot = (unsigned)(g_streams.size() - 1);
+    }
+    if (!t) {
+      static bool warned = false;
+      if (!warned) emit("libmk watchdog: stream table full; new streams are not traced\n");
+      warned = true;
+      return;
+    }
+    const unsigned slot = t->slot;
+    *t = Traced{};
+    t->slot = slot;
+    t->st = st;
+    (void)hipGetDevice(&t->device);
+    __atomic_store_n(g_words + slot, 0u, __ATOMIC_RELEASE);
   }
   const unsigned seq = ++t->enq;
   t->names[seq % RING] = name;
@@ -180,7 +197,7 @@ void wd_forget(hipStream_t st) {
   if (limit() <= 0) return;
   std::lock_guard<std::mutex> lk(g_mu);
   for (Traced& x : g_streams)
-    if (x.st == st) {   // keep its slot (stream handles can be reused): mark it idle and unowned
+    if (x.st == st) {   // the slot becomes free for the next new stream (wd_trace resets it)
       __atomic_store_n(g_words + x.slot, x.enq, __ATOMIC_RELEASE);
       x.st = nullptr;
     }

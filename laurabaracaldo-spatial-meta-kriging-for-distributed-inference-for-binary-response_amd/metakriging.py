@@ -189,4 +189,5 @@ def reference_flow(d, K, q, cov_model="exponential", n_batch=100, batch_length=5
     t["post_s"] = time.perf_counter() - t2
     t["end_to_end_s"] = time.perf_counter() - t0
     t["exchange"] = fit["exchange"]          # the combine's all-to-all: "rccl" (distinct GPUs) or "copy"
+    t["comm_ranks"] = fit["comm_ranks"]      # ranks RCCL's communicators hold (copies: device blocks)
     return t, fit["result"], fit["result2"], summ, cfg

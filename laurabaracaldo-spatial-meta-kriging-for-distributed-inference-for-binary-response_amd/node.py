@@ -25,6 +25,7 @@ def meta_fit_node(subsets, cfg, coords_test=None, devices=(0,), subset_base=0, m
                   progress=None, record_w=False, max_iter=100, tol=1e-12):
     """Fit all subsets over `devices` and combine.  Returns a dict with 'result' (200 x P, MK.R:127),
     'result2' (200 x q n_test, MK.R:133; None without test sites), 'exchange' ('rccl' / 'copy'),
+    'comm_ranks' (the ranks the exchange spans: RCCL's own ncclCommCount, or the blocks for copies),
     and per subset (lists, as Session.outputs lays them out) 'parameters' / 'w_predict' when
     per_subset, plus the optional 'samples', 'w_samples', 'w_pred_samples', 'acceptance',
     'w_predict_sum' (the sequential sum of all K w.predict grids)."""
@@ -78,7 +79,7 @@ def meta_fit_node(subsets, cfg, coords_test=None, devices=(0,), subset_base=0, m
                           ctypes.byref(o), ctypes.byref(cb)))
     del keep
     out = {"result": result.T.copy(), "result2": None if result2 is None else result2.T.copy(),
-           "exchange": "rccl" if cb.exchange else "copy"}
+           "exchange": "rccl" if cb.exchange else "copy", "comm_ranks": int(cb.comm_ranks)}
     if "parameters" in res:
         out["parameters"] = [res["parameters"][i].T.copy() for i in range(K)]
     if "w_predict" in res:

@@ -1,5 +1,5 @@
 """Helper run as a subprocess by tests/test_gpu_linalg.py (not a test module): a short chain
-under the code paths the environment forces (MK_TILE, MK_SWEEP, MK_CHOL_SPLIT, MK_PRED_GEN, MK_PRED_GI; read once per process), outputs
+under the code paths the environment forces (MK_TILE, MK_SWEEP, MK_CHOL_SPLIT, MK_CHOL_DEPTH, MK_PRED_GEN; read once per process), outputs
 saved to the .npz named on the command line."""
 import importlib
 import os

@@ -112,49 +112,42 @@ def test_combine_is_sequential_mean(mk):
 def test_sub_tile_gemm_split_cholesky_and_multi_wg_sweep_are_bit_identical(tmp_path):
     """Small-shard code paths give exactly the large-shard results: the 64- and 32-sub-tile GEMMs
     (Cholesky update / trsm, inverse levels; mk_gemm.hpp: same MFMA sequence per element), the
-    split two-stream Cholesky schedule (bulk update by panels < k-1 on a CU-masked stream, the
-    rank-128 correction on the critical stream; the accumulator passes through fp64 memory) and
-    the split-launch sweeps (MK_SWEEP=3: k_sweep_step, one launch per block; 4: k_sweep_tiles /
-    k_sweep_block, two) and the row-owning one-workgroup sweep (5: k_sweep_rows), under both launch
-    schedules,
-    and the kriging GEMM with P^T generated in LDS (MK_PRED_GEN=1, exponential model) against
-    the default stored-P^T path (k_pred_PT writes the same exp(-phi d) values to HBM first).
-    Also the split schedule's depth (MK_CHOL_DEPTH: the bulk update d critical steps ahead, the
-    critical correction rank-128d) and its fine form (MK_CHOL_FINE: the diagonal tile's correction
-    alone on the critical stream).  Chains, latent w, kriging draws and a plain factorisation, each
-    configuration forced in its own process (the MK_* switches are read once per process)."""
+    split two-stream Cholesky schedule (bulk update by panels < k-d on a CU-masked stream, the
+    rank-128d correction on the critical stream; the accumulator passes through fp64 memory) at
+    depths 1-3, the 64-site-block sweeps -- one workgroup per subset (MK_SWEEP=1, k_sweep), the
+    split launches (3: k_sweep_step, one launch per block) and the cooperative multi-workgroup kernel
+    (2: k_sweep_mg through a cooperative launch on the sequential schedule; split launches under the
+    lookahead schedule) -- and the kriging GEMM with P^T generated in LDS (MK_PRED_GEN=1,
+    exponential model) against the stored-P^T path.  Chains, latent w, kriging draws and a plain
+    factorisation, each configuration forced in its own process (the MK_* switches are read once
+    per process); the two launch schedules agree to rounding, not bit for bit, so each configuration
+    is compared with the reference of its schedule."""
     import os
     import subprocess
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     res = {}
-    # gi: the kriging GEMM raster (MK_PRED_GI row panels per group; placement only).  la: the launch
-    # schedule; the two schedules agree to rounding, not bit for bit, so each configuration is
-    # compared with the reference of its schedule.  MK_SWEEP=2: the cooperative multi-workgroup sweep
-    # (the default for q >= 2 small shards since round 4).
-    configs = (("128", "1", "0", "0", "0", "2", "1", "1"),
-               ("128", "2", "0", "0", "0", "2", "1", "1"),
-               ("128", "2", "0", "0", "0", "2", "1", "0"),
-               ("64", "3", "1", "0", "0", "1", "4", "0"),
-               ("64", "1", "0", "0", "0", "2", "3", "1"),
-               ("32", "1", "1", "0", "1", "2", "4", "1"),
-               ("128", "4", "1", "0", "0", "3", "4", "0"),
-               ("128", "1", "0", "1", "0", "2", "2", "1"),
-               ("64", "1", "1", "0", "1", "1", "4", "1"),
-               ("128", "3", "0", "0", "0", "2", "1", "1"),
-               ("64", "4", "0", "0", "0", "2", "1", "1"),
-               ("128", "5", "1", "0", "0", "2", "1", "1"),
-               ("128", "5", "0", "0", "0", "2", "1", "0"),
-               ("64", "3", "1", "0", "0", "2", "1", "0"),
-               ("128", "1", "0", "0", "0", "2", "1", "0"))
+    # (MK_TILE, MK_SWEEP, MK_CHOL_SPLIT, MK_PRED_GEN, MK_CHOL_DEPTH, lookahead)
+    configs = (("128", "1", "0", "0", "2", "1"),
+               ("128", "2", "0", "0", "2", "1"),
+               ("128", "2", "0", "0", "2", "0"),
+               ("64", "3", "1", "0", "1", "0"),
+               ("64", "1", "0", "0", "2", "1"),
+               ("32", "1", "1", "0", "2", "1"),
+               ("128", "3", "1", "0", "3", "0"),
+               ("128", "1", "0", "1", "2", "1"),
+               ("64", "1", "1", "0", "2", "1"),
+               ("128", "3", "0", "0", "2", "1"),
+               ("64", "2", "1", "0", "3", "0"),
+               ("64", "3", "1", "0", "2", "0"),
+               ("128", "1", "0", "0", "2", "0"))
     for cfg in configs:
-        tile, sweep, split, gen, fine, depth, gi, la = cfg
+        tile, sweep, split, gen, depth, la = cfg
         path = str(tmp_path / ("run_" + "_".join(cfg) + ".npz"))
         r = subprocess.run([sys.executable, os.path.join(here, "gpu_tile_run.py"), path], capture_output=True,
                            text=True, timeout=240,
                            env=dict(os.environ, MK_TILE=tile, MK_SWEEP=sweep, MK_CHOL_SPLIT=split, MK_PRED_GEN=gen,
-                                    MK_CHOL_FINE=fine, MK_CHOL_DEPTH=depth, MK_PRED_GI=gi,
-                                    **({} if la == "1" else {"MK_LOOKAHEAD": "0"})))
+                                    MK_CHOL_DEPTH=depth, **({} if la == "1" else {"MK_LOOKAHEAD": "0"})))
         assert r.returncode == 0, r.stderr[-4000:]
         z = np.load(path)
         res[cfg] = {k: z[k] for k in z.files}
@@ -166,85 +159,28 @@ def test_sub_tile_gemm_split_cholesky_and_multi_wg_sweep_are_bit_identical(tmp_p
             assert np.array_equal(got[k], ref[k]), (cfg, k)
 
 
-
 def test_site_sweep_runs_the_block_sweeps_chain(tmp_path):
-    """The one-pass site sweep (k_sweep_site, the default for q <= 2: W read once, no Q_BB tiles) and
-    the 64-site-block sweep (MK_SWEEP=1, k_sweep) run the same chain: the dot products are summed in
-    a different order, so the chains agree to rounding -- identical accept decisions, samples, latent
-    w and kriging draws within 1e-9 -- under both launch schedules (q = 1 and q = 2 LMC, ragged
-    subsets, the Matern model).  q = 3 and n_s > 2047 (two row pairs per thread) are covered by the
-    oracle replays of tests/test_gpu_sampler.py, which run the default (site) sweep."""
+    """The one-pass site sweep (k_sweep_site, the default: W read once, no Q_BB tiles; q = 1 its lean
+    pair form, with the border-row factor where a subset's n_s is odd) and the 64-site-block sweep
+    (MK_SWEEP=1, k_sweep) run the same chain: the dot products are summed in a different order, so
+    the chains agree to rounding -- identical accept decisions, samples, latent w and kriging draws
+    within 1e-9 -- under both launch schedules (q = 1 ragged subsets and the Matern model; q = 2 with
+    two subsets is a multi-outcome small shard and runs the block sweeps either way).  q = 3 and
+    n_s > 2047 (two row pairs per thread) are covered by the oracle replays of
+    tests/test_gpu_sampler.py, which run the default sweep."""
     import os
     import subprocess
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     for la in ("1", "0"):
         res = {}
-        for sweep in ("1", "6", "7", "7m", "7b"):
+        for sweep in ("1", "0"):
             path = str(tmp_path / f"site_{sweep}_{la}.npz")
-            # 7: the lean pair form (the default: fma dots, no row masks, the all-even form where every
-            # n_s is even); 7b its border-factor form (MK_SS_LEAN=3); 7m the masked form (0)
-            lean = {"7m": {"MK_SS_LEAN": "0"}, "7b": {"MK_SS_LEAN": "3"}}.get(sweep, {})
-            env = dict(os.environ, MK_SWEEP=sweep[0], **lean, **({} if la == "1" else {"MK_LOOKAHEAD": "0"}))
+            env = dict(os.environ, MK_SWEEP=sweep, **({} if la == "1" else {"MK_LOOKAHEAD": "0"}))
             r = subprocess.run([sys.executable, os.path.join(here, "gpu_tile_run.py"), path], capture_output=True,
                                text=True, timeout=240, env=env)
             assert r.returncode == 0, r.stderr[-4000:]
             z = np.load(path)
             res[sweep] = {k: z[k] for k in z.files}
         for k in res["1"]:
-            for sw in ("6", "7", "7m", "7b"):   # 7: two sites per barrier (q = 1; q = 2: the block sweep)
-                np.testing.assert_allclose(res[sw][k], res["1"][k], rtol=0, atol=1e-9, err_msg=f"{k} la={la} {sw}")
-
-
-def test_chain_split_cholesky_is_bit_identical(tmp_path):
-    """The chain split (MK_CHOL_CHAIN: the diagonal tiles' correction, factor and next-tile trsm on the
-    critical stream, the other tiles' correction and trsm on a near stream one column behind, the
-    early panels on the bulk stream) gives the sequential factorisation's bits: every tile sees the
-    same panels in the same order and chunking.  Both near-stream kinds (1: high priority; 2: the bulk
-    stream's CU mask), both launch schedules, depths 1-3."""
-    import os
-    import subprocess
-    import sys
-    here = os.path.dirname(os.path.abspath(__file__))
-    runs = {}
-    for name, env in (("ref1", dict(MK_CHOL_SPLIT="0")), ("ref0", dict(MK_CHOL_SPLIT="0", MK_LOOKAHEAD="0")),
-                      ("c1", dict(MK_CHOL_SPLIT="1", MK_CHOL_CHAIN="1")),
-                      ("c2", dict(MK_CHOL_SPLIT="1", MK_CHOL_CHAIN="2", MK_CHOL_DEPTH="3")),
-                      ("c1d1", dict(MK_CHOL_SPLIT="1", MK_CHOL_CHAIN="1", MK_CHOL_DEPTH="1", MK_LOOKAHEAD="0")),
-                      ("c2s", dict(MK_CHOL_SPLIT="1", MK_CHOL_CHAIN="2", MK_LOOKAHEAD="0"))):
-        path = str(tmp_path / f"{name}.npz")
-        r = subprocess.run([sys.executable, os.path.join(here, "gpu_tile_run.py"), path], capture_output=True,
-                           text=True, timeout=240, env=dict(os.environ, MK_SWEEP="1", MK_TILE="128", **env))
-        assert r.returncode == 0, r.stderr[-4000:]
-        z = np.load(path)
-        runs[name] = {k: z[k] for k in z.files}
-    for name in ("c1", "c2", "c1d1", "c2s"):   # the two schedules agree to rounding: each against its own
-        got, ref = runs[name], runs["ref0" if name in ("c1d1", "c2s") else "ref1"]
-        for k in ref:
-            assert np.array_equal(got[k], ref[k]), (name, k)
-
-
-def test_covariance_fused_into_the_update_is_bit_identical(tmp_path):
-    """MK_COV_FUSE=1 (exponential model): the candidate's tiles outside column 0 are generated by the
-    update kernel at their first touch (k_cov_candidate's expression, written in place and loaded back)
-    instead of by the covariance pass: the same bits as the default, under both launch schedules, with
-    the split and the chain-split Cholesky, and through the tiled kriging replay (its own candidates)."""
-    import os
-    import subprocess
-    import sys
-    here = os.path.dirname(os.path.abspath(__file__))
-    runs = {}
-    for name, env in (("ref1", {}), ("ref0", dict(MK_LOOKAHEAD="0")),
-                      ("f1", dict(MK_COV_FUSE="1")), ("f0", dict(MK_COV_FUSE="1", MK_LOOKAHEAD="0")),
-                      ("f1c", dict(MK_COV_FUSE="1", MK_CHOL_SPLIT="1", MK_CHOL_CHAIN="1")),
-                      ("f0s", dict(MK_COV_FUSE="1", MK_CHOL_SPLIT="1", MK_LOOKAHEAD="0"))):
-        path = str(tmp_path / f"{name}.npz")
-        r = subprocess.run([sys.executable, os.path.join(here, "gpu_tile_run.py"), path], capture_output=True,
-                           text=True, timeout=240, env=dict(os.environ, MK_SWEEP="1", **env))
-        assert r.returncode == 0, r.stderr[-4000:]
-        z = np.load(path)
-        runs[name] = {k: z[k] for k in z.files}
-    for name in ("f1", "f0", "f1c", "f0s"):
-        got, ref = runs[name], runs["ref0" if name in ("f0", "f0s") else "ref1"]
-        for k in ref:
-            assert np.array_equal(got[k], ref[k]), (name, k)
+            np.testing.assert_allclose(res["0"][k], res["1"][k], rtol=0, atol=1e-9, err_msg=f"{k} la={la}")
