@@ -1,0 +1,69 @@
+"""Independent oracle replicates of the meta-kriging fixtures (TEST INFRASTRUCTURE ONLY).
+
+make_meta_fixture.py stores ONE oracle meta-fit per case, on the Philox streams of global subsets
+0 .. K-1 -- the streams the device's replicate 0 also runs (the replay test).  The Monte Carlo-error
+comparison needs oracle chains that share no stream with any device replicate (a
+spec error shared by oracle and device would otherwise pass): this script runs R_O more oracle
+meta-fits of the same data, partition and start values, replicate r on global subsets
+BASE + r K .. BASE + r K + K - 1 (BASE = 1,000: the device test's 16 replicates use 0 .. 16 K - 1),
+and stores their combined grids (MK.R:123-133) -- result (200 x P) and result2 at the three
+levels the test reads.
+
+    python tests/golden/stat/make_indep_replicates.py [case ...]   (cfg3_exp / cfg4_lmc: minutes;
+                                                                   cfg2_matern: ~1 h on 6 cores)
+"""
+import os
+os.environ.setdefault("OPENBLAS_NUM_THREADS", "1")   # one BLAS thread per worker (set before numpy loads)
+import multiprocessing as mp  # noqa: E402
+import sys  # noqa: E402
+
+import numpy as np  # noqa: E402
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(HERE)))
+sys.path.insert(0, ROOT)
+
+CASES = ("cfg2_matern", "cfg3_exp", "cfg4_lmc")
+R_O = 4                 # oracle replicates
+BASE = 1000             # first global subset index of oracle replicate 0
+LEVELS3 = (4, 99, 194)
+WORKERS = int(os.environ.get("MK_FIXTURE_WORKERS", "6"))
+
+
+def _fit(args):
+    os.environ["OPENBLAS_NUM_THREADS"] = "1"
+    from oracle import spmvglm as om
+    coords, y, x, coords_test, beta0, bt, gsub, q, cov_model, n_batch, batch_length, seed = args
+    cfg = om.Config(q, x.shape[1], beta_starting=beta0, beta_tuning=bt, cov_model=cov_model, n_batch=n_batch,
+                    batch_length=batch_length, seed=seed)
+    r = om.fit_subset(coords, y, np.ones(y.size), x, cfg, subset=gsub, coords_test=coords_test)
+    return r["param_q"], r["w_q"][list(LEVELS3)]
+
+
+def make(case):
+    from oracle import spmvglm as om
+    z = np.load(os.path.join(HERE, case + ".npz"))
+    g = {k: z[k] for k in z.files}
+    K, q = int(g["K"]), int(g["q"])
+    offs = np.concatenate([[0], np.cumsum(g["n_part"])])
+    jobs = []
+    for r in range(R_O):
+        for s in range(K):
+            idx = g["index"][offs[s]:offs[s + 1]].astype(np.int64) - 1
+            rows = (idx[:, None] * q + np.arange(q)[None, :]).reshape(-1)
+            jobs.append((g["coords"][idx], g["y"][rows], g["x"][rows], g["coords_test"], g["beta_starting"],
+                         g["beta_tuning"], BASE + r * K + s, q, int(g["cov_model"]), int(g["n_batch"]),
+                         int(g["batch_length"]), int(g["seed"])))
+    with mp.get_context("spawn").Pool(min(WORKERS, len(jobs))) as pool:
+        res = pool.map(_fit, jobs)
+    result = np.stack([om.combine_mean([res[r * K + s][0] for s in range(K)]) for r in range(R_O)])
+    # the combine of the three stored levels is the same sequential mean, level by level
+    result2_3 = np.stack([om.combine_mean([res[r * K + s][1] for s in range(K)]) for r in range(R_O)])
+    np.savez_compressed(os.path.join(HERE, case + "_indep.npz"), base=BASE, R_O=R_O, K=K,
+                        levels3=np.asarray(LEVELS3), result=result, result2_3=result2_3)
+    print(case, "oracle replicates' medians", result[:, 99])
+
+
+if __name__ == "__main__":
+    for name in sys.argv[1:] or CASES:
+        make(name)
