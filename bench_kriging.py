@@ -89,6 +89,23 @@ def kriging_leg(mk, subs, coords_test, beta0, bt, kept=6, burn=14, tile=65536, k
     return res
 
 
+def kept_window_runs(mk, subs, beta0, bt, subset_base=0):
+    """The configs[4] replay's refresh count from a real kept window: the fit of MK.R:83 as written
+    (100 x 50 amcmc iterations, burn.in 3,750 -> 1,251 kept, MK.R:85) on `subs`, no test sites (the
+    fit alone, minutes-cheap), and the phi sequence of every subset's kept window.  The tiled replay
+    re-runs X = W P^T for a subset at its first kept state and wherever phi changed since the
+    previous one.  Returns (refreshes per kept sample, fit seconds)."""
+    cfg = mk.SamplerConfig(1, 2, beta0, bt, n_batch=100, batch_length=50, seed=20250114)
+    t0 = time.perf_counter()
+    with mk.Session(subs, cfg, subset_base=subset_base) as ses:
+        ses.run(cfg.n_samples)
+        out = ses.outputs(quantiles=False, samples=True)
+    fit_s = time.perf_counter() - t0
+    kept = np.stack([smp[cfg.burn_in - 1:, 3] for smp in out["samples"]])     # phi, iterations 3,750..5,000
+    runs = int(sum(1 + np.count_nonzero(np.diff(r)) for r in kept))
+    return runs / kept.size, fit_s, kept.shape[1]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--subsets", type=int, default=32)   # the per-GPU share of K = 250 on 8 GPUs
@@ -98,6 +115,8 @@ def main():
     ap.add_argument("--burn", type=int, default=14)
     ap.add_argument("--tile", type=int, default=65536)
     ap.add_argument("--kernel-events", type=int, default=1, help="HIP events around k_pred_var (0: off)")
+    ap.add_argument("--phi-window", type=int, default=1,
+                    help="price the configs[4] extrapolation from a full 5,000-iteration fit's kept window (0: off)")
     a = ap.parse_args()
     mk = importlib.import_module(PKG)
     S, ns = a.subsets, a.n_sub
@@ -107,6 +126,21 @@ def main():
                  x=d["x"][i * ns:(i + 1) * ns]) for i in range(S)]
     res = kriging_leg(mk, subs, d["coords_test"], beta0, bt, kept=a.kept, burn=a.burn, tile=a.tile,
                       kernel_events=bool(a.kernel_events))
+    if a.phi_window:
+        # price the full job from the phi sequence of a full 1,251-sample kept window (the sample above
+        # holds only a few kept states, the first always a refresh)
+        frac, fit_s, n_kept = kept_window_runs(mk, subs, beta0, bt)
+        ex = res["cfg5_extrapolation"]
+        rate_tf = res["roofline"]["achieved"]
+        cfg5_flops = 250 * 1251 * frac * ns * ns * 1_000_000
+        res["cfg5_extrapolation_sample"] = ex
+        res["cfg5_extrapolation"] = {
+            "flops": cfg5_flops, "seconds_1gpu": cfg5_flops / (rate_tf * 1e12),
+            "seconds_8gpu": cfg5_flops / (rate_tf * 1e12) / 8,
+            "refreshes_per_kept_sample": frac,
+            "assumes": f"X = W P^T refreshes per kept sample {frac:.3f}, measured on these {S} subsets' full kept "
+                       f"window ({n_kept} kept of 100 x 50 amcmc iterations, burn.in 3,750; fit {fit_s:.1f} s) at "
+                       f"the rate measured above"}
     print(json.dumps(res), flush=True)
 
 

@@ -528,7 +528,7 @@ static inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
 // Every tile-GEMM kernel takes gb_lds_bytes(TM, TN) of dynamic LDS: two DMA stages (> 64 KiB at 128 x 128).
 static constexpr size_t LDS_128 = gb_lds_bytes(128, 128), LDS_64 = gb_lds_bytes(64, 64),
                         LDS_64x128 = gb_lds_bytes(64, 128), LDS_32 = gb_lds_bytes(32, 32),
-                        LDS_32x128 = gb_lds_bytes(32, 128);
+                        LDS_32x128 = gb_lds_bytes(32, 128), LDS_WIDE = gw_lds_bytes();
 static bool set_gemm_lds() {
   const std::pair<const void*, size_t> fns[] = {
       {(const void*)k_chol_update<128>, LDS_128}, {(const void*)k_chol_update<64>, LDS_64},
@@ -537,7 +537,8 @@ static bool set_gemm_lds() {
       {(const void*)k_chol_update<32>, LDS_32},   {(const void*)k_chol_trsm<32>, LDS_32x128},
       {(const void*)k_inv_level<32>, LDS_32},
       {(const void*)k_qblocks, LDS_64},           {(const void*)k_lauum, LDS_128},
-      {(const void*)k_pred_var<true>, LDS_128},   {(const void*)k_pred_var<false>, LDS_128}};
+      {(const void*)k_pred_var<true>, LDS_128},   {(const void*)k_pred_var<false>, LDS_128},
+      {(const void*)k_pred_var_w, LDS_WIDE}};
   for (const auto& f : fns)
     if (hipFuncSetAttribute(f.first, hipFuncAttributeMaxDynamicSharedMemorySize, (int)f.second) != hipSuccess)
       return false;
@@ -791,9 +792,17 @@ static void launch_pred_refresh(mk_session* s, Group& g, hipStream_t st = nullpt
   else if (!s->pred_gen)
     MK_LAUNCH(pred_PT_kernel(md.cov_model), dim3(max_entries * md.n_pad), dim3(256), 0, st, md, g.d_plist,
                        g.d_pcount);
+  // stored P^T: the wide three-stage GEMM (k_pred_var_w, 128 x 256 tiles, one 8-wave workgroup per CU);
+  // MK_PRED_GEN: P^T generated in LDS by the 128 x 128 body; MK_PRED_NARROW=1: the stored-P^T
+  // 128 x 128 body (k_pred_var<false>, two workgroups per CU; same bits)
+  static const int narrow_env = tile_env("MK_PRED_NARROW", 0);
   timed(s, st, KS_PRED_VAR, pred_flops(s, g), [&] {
-    MK_LAUNCH(s->pred_gen ? k_pred_var<true> : k_pred_var<false>, dim3(xcd_grid_h(max_entries, nt * md.ntt)),
-                       dim3(256), LDS_128, st, md, g.ms, g.d_plist, g.d_pcount);
+    if (s->pred_gen || narrow_env)
+      MK_LAUNCH(s->pred_gen ? k_pred_var<true> : k_pred_var<false>, dim3(xcd_grid_h(max_entries, nt * md.ntt)),
+                dim3(256), LDS_128, st, md, g.ms, g.d_plist, g.d_pcount);
+    else
+      MK_LAUNCH(k_pred_var_w, dim3(xcd_grid_h(max_entries, nt * (md.ntt / 2))), dim3(512), LDS_WIDE, st, md,
+                g.ms, g.d_plist, g.d_pcount);
   });
   MK_LAUNCH(k_pred_var_reduce, dim3(max_entries * (md.n_test_pad / 256)), dim3(256), 0, st, md, nt,
                      g.d_plist, g.d_pcount);

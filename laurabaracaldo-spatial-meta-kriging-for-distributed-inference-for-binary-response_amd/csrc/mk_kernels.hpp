@@ -42,6 +42,7 @@ inline PredPTKernel pred_PT_kernel(int model) {
 }
 template <bool GEN>
 __global__ void k_pred_var(Model md, MatSet ms, const int* list, const int* count);
+__global__ void k_pred_var_w(Model md, MatSet ms, const int* list, const int* count);
 __global__ void k_pred_var_reduce(Model md, int nt, const int* list, const int* count);
 // mk_mcmc.hip
 __global__ void k_beta(Model md, int iter);

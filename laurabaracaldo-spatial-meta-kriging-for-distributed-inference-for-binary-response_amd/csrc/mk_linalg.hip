@@ -1435,6 +1435,56 @@ __global__ __launch_bounds__(256, 2) void k_pred_var(Model md, MatSet ms, const 
 template __global__ void k_pred_var<true>(Model, MatSet, const int*, const int*);
 template __global__ void k_pred_var<false>(Model, MatSet, const int*, const int*);
 
+// The stored-P^T kriging GEMM in its wide form (the default): 128 x 256 output tiles (one W row
+// panel x 256 test sites) on one 512-thread workgroup per CU with the three-stage body gemm_wide.
+// X = W P^T and the column sums of squares exactly as k_pred_var<false> computes them -- the same
+// MFMA sequence per element (each wave the same 64 x 64 quadrant layout) and the same reduction
+// order -- so the same bits.
+__global__ __launch_bounds__(512, 1) void k_pred_var_w(Model md, MatSet ms, const int* __restrict__ list,
+                                                       const int* __restrict__ count) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];   // gw_lds_bytes()
+  const int ntw = md.ntt / 2;                                     // 256-site column tiles
+  int e, t_;
+  if (!xcd_map(*count, ms.nt * ntw, &e, &t_)) return;
+  const int i = t_ / ntw, tw = t_ % ntw;   // row-panel-major: an XCD's workgroups share W's row panel
+  const int sh = list[e];
+  const int s = sh / md.q;
+  const int ns = md.n_s[s];
+  const long ld = ms.ld;
+  const double* Wm = wmat(ms, sh);
+  Acc acc;
+  acc_zero(acc);
+  const double* PT = md.PT + (long)sh * md.n_pad * md.n_test_pad + tw * 256;
+  gemm_wide(Wm + i * MK_NB, ld, PT, md.n_test_pad, (i + 1) * MK_NB, acc, lds);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w & 1, wn = w >> 1;
+  // wave (wm, wn): rows 64 wm + 16 bm + (lane & 15), columns 64 wn + 16 bn + (lane >> 4) + 4 r
+  double* XK = md.XK + (long)sh * md.n_test_pad * md.n_pad + (long)(tw * 256 + wn * 64) * md.n_pad + i * MK_NB +
+               wm * 64;
+  double* red = lds;   // [2][256] (the GEMM ended with a barrier)
+#pragma unroll
+  for (int bn = 0; bn < 4; ++bn)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = bn * 16 + (lane >> 4) + 4 * r;
+      double v = 0.0;
+#pragma unroll
+      for (int bm = 0; bm < 4; ++bm) {
+        const int mr = bm * 16 + (lane & 15);
+        const double x = acc.v[bm][bn][r];
+        XK[mr + (long)n * md.n_pad] = x;
+        v += (i * MK_NB + wm * 64 + mr < ns) ? x * x : 0.0;
+      }
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+      if ((lane & 15) == 0) red[wm * 256 + wn * 64 + n] = v;
+    }
+  __syncthreads();
+  if (threadIdx.x < 256) {
+    const int n = threadIdx.x;
+    md.s_part[((long)sh * ms.nt + i) * md.n_test_pad + tw * 256 + n] = red[n] + red[256 + n];
+  }
+}
+
 __global__ __launch_bounds__(256) void k_pred_var_reduce(Model md, int nt, const int* __restrict__ list,
                                                          const int* __restrict__ count) {
   const int per = md.n_test_pad / 256;

@@ -13,14 +13,21 @@ Both: R's partition after set.seed (MK.R:15-41), glm start values on the full da
 per-subset spMvGLM + spPredict + 200 quantiles (MK.R:46-96), combine MK.R:123-133.
 
 GPU: one session of 16 replicate meta-fits per case (replicate r = global subsets rK .. rK + K - 1, so
-replicate 0 runs the oracle's Philox streams and replicates 1..15 are independent chains):
+replicate 0 runs the oracle fixture's Philox streams and replicates 1..15 are independent chains):
   * replicate 0 replays the oracle over all 1,000 iterations (adaptation across 20 batch ends, the
     K and nu chains' drift included): samples, per-subset grids and the combined grids within 1e-6;
-  * the oracle's combined quantiles lie within Monte Carlo error of the device's independent
-    replicates: per parameter and level |z| <= 4 with z = (oracle - mean_r) / (sd_r sqrt(1 + 1/15));
-    over the w.predict (site, level) pairs at most 2 % with |z| > 3 and mean z^2 in [0.5, 2].
-CPU: the fixtures' own consistency (inputs regenerate, the combine is the sequential mean).
-The fixtures pin the device to the build's oracle, not to spBayes (absent).
+  * Monte Carlo-error parity against INDEPENDENT oracle chains: tests/golden/stat/<case>_indep.npz
+    (tests/golden/stat/make_indep_replicates.py) holds 4 more oracle meta-fits of the same data on
+    global subsets 1,000 + rK .. -- streams no device replicate runs -- and their combined grids are
+    compared with the device's replicates 1..15 by a two-sample t statistic per (column, level),
+    t = (mean_oracle - mean_device) / (s_pooled sqrt(1/4 + 1/15)), 17 df: every parameter |t| <= 5;
+    over the w.predict (site, level) pairs at most 3 % with |t| > 3.5 and mean t^2 in [0.5, 2].
+    (Round 4 compared the oracle's own fixture with replicates 1..15 -- but that fixture IS replicate
+    0's chain, so the test measured the device's spread against itself.)
+CPU: the fixtures' own consistency (inputs regenerate, the combine is the sequential mean, the
+independent replicates are distinct chains of the same fit).
+The fixtures pin the device to the build's oracle, not to spBayes (absent); the oracle
+itself is pinned to the model by tests/test_geweke.py.
 """
 import importlib
 import os
@@ -121,19 +128,43 @@ def test_replica0_replays_oracle(mk, case):
     np.testing.assert_allclose(res2[0], g["result2"], rtol=0, atol=1e-6)
 
 
-def _z(oracle, reps):
-    m = reps.mean(axis=0)
-    sd = reps.std(axis=0, ddof=1) * np.sqrt(1.0 + 1.0 / reps.shape[0])
-    return (oracle - m) / np.where(sd > 0, sd, np.inf)
+def _load_indep(case):
+    z = np.load(os.path.join(HERE, "golden", "stat", case + "_indep.npz"))   # allow_pickle=False (default)
+    return {k: z[k] for k in z.files}
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_independent_oracle_replicates_are_distinct_chains(case):
+    """The independent oracle replicates run other Philox streams than the fixture (replicate 0's):
+    same data and start values, different chains, similar answers."""
+    g, ind = _load(case), _load_indep(case)
+    assert int(ind["base"]) >= R_REP * int(g["K"])            # no device replicate's streams
+    assert ind["result"].shape == (int(ind["R_O"]), 200, g["result"].shape[1])
+    assert ind["result2_3"].shape == (int(ind["R_O"]), len(LEVELS3), g["result2"].shape[1])
+    for r in range(int(ind["R_O"])):
+        assert not np.array_equal(ind["result"][r], g["result"])
+    # the regression coefficients' medians within a loose band of the fixture's (a gross drift check, not
+    # the MC test; phi is weakly identified at 1,000 iterations and its chains' medians spread widely)
+    p = 2 * int(g["q"])
+    assert np.all(np.abs(ind["result"][:, 99, :p] - g["result"][99, :p]) < 0.5)
+
+
+def _t2(a, b):
+    """Two-sample t (pooled variance) of the replicate means, per element: a [n_a, ...], b [n_b, ...]."""
+    na, nb = a.shape[0], b.shape[0]
+    sp2 = ((na - 1) * a.var(axis=0, ddof=1) + (nb - 1) * b.var(axis=0, ddof=1)) / (na + nb - 2)
+    se = np.sqrt(sp2 * (1.0 / na + 1.0 / nb))
+    return (a.mean(axis=0) - b.mean(axis=0)) / np.where(se > 0, se, np.inf)
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", CASES)
-def test_oracle_within_mc_error_of_device(mk, case):
+def test_independent_oracle_chains_within_mc_error_of_device(mk, case):
     g, _, res, res2 = _device_replicates(mk, case)
+    ind = _load_indep(case)
     L = list(LEVELS3)
-    zp = _z(g["result"][L], res[1:, L])                 # 3 levels x P parameters
-    assert np.all(np.abs(zp) <= 4.0), zp
-    zw = _z(g["result2"][L], res2[1:, L])               # 3 levels x q n_test columns
-    assert np.mean(np.abs(zw) > 3.0) <= 0.02, np.mean(np.abs(zw) > 3.0)
-    assert 0.5 <= np.mean(zw ** 2) <= 2.0, np.mean(zw ** 2)
+    tp = _t2(ind["result"][:, L], res[1:, L])            # 3 levels x P parameters
+    assert np.all(np.abs(tp) <= 5.0), tp
+    tw = _t2(ind["result2_3"], res2[1:, L])              # 3 levels x q n_test columns
+    assert np.mean(np.abs(tw) > 3.5) <= 0.03, np.mean(np.abs(tw) > 3.5)
+    assert 0.5 <= np.mean(tw ** 2) <= 2.0, np.mean(tw ** 2)
