@@ -391,6 +391,7 @@ struct mk_session {
   int sweep_site = 0;
   size_t sweep_site_lds = 0;
   int sweep_lean = 0;             // q = 1: 1 border row by factor, 2 every n_s even (sweep_site_kernel)
+  bool sweep_quad = false;        // q = 1, n_pad <= 2048: four sites per barrier
   bool sweep_split = false;       // k_sweep_step, one launch per 64-site block
   bool sweep_coop = false;        // k_sweep_mg by hipLaunchCooperativeKernel (sequential schedule only)
   size_t sweep_mg_lds = 0;
@@ -837,7 +838,7 @@ static void launch_sweep(mk_session* s, Group& g, int it) {
   hipError_t e = hipSuccess;
   if (s->sweep_site) {
     void* args[] = {&md, &ms, &iter};
-    e = hipLaunchKernel(sweep_site_kernel(q, s->sweep_site, s->sweep_lean), dim3(g.S), dim3(MK_SS_T), args,
+    e = hipLaunchKernel(sweep_site_kernel(q, s->sweep_site, s->sweep_lean, s->sweep_quad), dim3(g.S), dim3(MK_SS_T), args,
                         s->sweep_site_lds, g.stream);
     wd_trace(g.stream, "k_sweep_site");
   } else if (use_sweep_mg(s)) {
@@ -1375,8 +1376,10 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
       bool all_even = true;
       for (int i = 0; i < S; ++i) all_even = all_even && (s->n_part[i] % 2 == 0);
       s->sweep_lean = q == 1 ? (all_even ? 2 : 1) : 0;
+      static const int quad_env = tile_env("MK_SS_QUAD", 0);
+      s->sweep_quad = q == 1 && s->sweep_site == 1 && quad_env == 1;
       s->sweep_site_lds = sweep_site_lds_bytes(nmax, q, s->sweep_lean);
-      HIPCHK(hipFuncSetAttribute(sweep_site_kernel(q, s->sweep_site, s->sweep_lean),
+      HIPCHK(hipFuncSetAttribute(sweep_site_kernel(q, s->sweep_site, s->sweep_lean, s->sweep_quad),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)s->sweep_site_lds));
     }
     if (s->sweep_split) {

@@ -62,8 +62,11 @@ inline size_t sweep_site_lds_bytes(int ns_max, int q, int lean = 0) { return (si
 // q = 1: the lean pair form (two sites per barrier, fused-multiply-add dots, no row masks beyond the
 // one upper element a pair loads; lean 1: the border row dropped by a factor; 2: for shards whose
 // n_s are all even, no border element in a loaded pair); q = 2, 3: one site per barrier, masked.
-inline const void* sweep_site_kernel(int q, int kr, int lean = 1) {
+// quad: four sites per barrier (q = 1, n_pad <= 2048).
+inline const void* sweep_site_kernel(int q, int kr, int lean = 1, bool quad = false) {
   if (q == 1) {
+    if (kr == 1 && quad)
+      return lean == 1 ? (const void*)k_sweep_site<1, 4, 4, 0, 1> : (const void*)k_sweep_site<1, 4, 4, 0, 2>;
     if (kr == 1)
       return lean == 1 ? (const void*)k_sweep_site<1, 4, 2, 0, 1> : (const void*)k_sweep_site<1, 4, 2, 0, 2>;
     return lean == 1 ? (const void*)k_sweep_site<1, 8, 2, 0, 1> : (const void*)k_sweep_site<1, 8, 2, 0, 2>;

@@ -174,13 +174,16 @@ def test_site_sweep_runs_the_block_sweeps_chain(tmp_path):
     here = os.path.dirname(os.path.abspath(__file__))
     for la in ("1", "0"):
         res = {}
-        for sweep in ("1", "0"):
+        for sweep in ("1", "0", "0q"):
             path = str(tmp_path / f"site_{sweep}_{la}.npz")
-            env = dict(os.environ, MK_SWEEP=sweep, **({} if la == "1" else {"MK_LOOKAHEAD": "0"}))
+            # 0q: the q = 1 site sweep four sites per barrier (MK_SS_QUAD=1)
+            env = dict(os.environ, MK_SWEEP=sweep[0], **({"MK_SS_QUAD": "1"} if sweep == "0q" else {}),
+                       **({} if la == "1" else {"MK_LOOKAHEAD": "0"}))
             r = subprocess.run([sys.executable, os.path.join(here, "gpu_tile_run.py"), path], capture_output=True,
                                text=True, timeout=240, env=env)
             assert r.returncode == 0, r.stderr[-4000:]
             z = np.load(path)
             res[sweep] = {k: z[k] for k in z.files}
         for k in res["1"]:
-            np.testing.assert_allclose(res["0"][k], res["1"][k], rtol=0, atol=1e-9, err_msg=f"{k} la={la}")
+            for sw in ("0", "0q"):
+                np.testing.assert_allclose(res[sw][k], res["1"][k], rtol=0, atol=1e-9, err_msg=f"{k} la={la} {sw}")
