@@ -1205,6 +1205,11 @@ __device__ inline void current_phi_nu(const Model& md, int s, int h, double* phi
   *nu = (md.cov_model == MK_COV_MATERN) ? logit_inv(th[md.ntri + md.q + h], md.nu_a[h], md.nu_b[h]) : 0.0;
 }
 
+// Columns of P^T the kriging GEMM reads: the 128-site blocks of the tile (ntt, odd for a short last
+// tile of the tiled replay) rounded up to the wide GEMM's 256-site tiles (<= n_test_pad, a multiple of
+// 256); columns past n_test are written as zeros.
+__device__ inline int pt_cols(const Model& md) { return ((md.ntt + 1) / 2) * 2 * MK_NB; }
+
 // P^T[k][t] = rho(|obs_k - test_t|) for the listed pairs (zero outside the valid block).
 // MODEL = MK_COV_EXPONENTIAL: exp(-phi d) inline, as in cand_value (bit-identical to CorrFn).
 template <int MODEL>
@@ -1229,7 +1234,7 @@ __global__ __launch_bounds__(256) void k_pred_PT(Model md, const int* __restrict
   const double* cx = md.coords + (long)s * 2 * md.n_pad;
   const double ox = cx[k], oy = cx[md.n_pad + k];
   double* row = md.PT + ((long)sh * md.n_pad + k) * md.n_test_pad;
-  const int tlim = md.ntt * MK_NB;   // the column blocks k_pred_var reads (all of n_test_pad when fused)
+  const int tlim = pt_cols(md);   // the column blocks the kriging GEMM reads (all of n_test_pad when fused)
   for (int t = threadIdx.x; t < tlim; t += 256) {
     double v = 0.0;
     if (k < ns && t < md.n_test) {
@@ -1276,7 +1281,7 @@ __global__ __launch_bounds__(256) void k_pred_PT_matern(Model md, const int* __r
   const int s = sh / md.q, h = sh % md.q;
   const int ns = md.n_s[s];
   const int tid = threadIdx.x, lane = tid & 63;
-  const int tlim = md.ntt * MK_NB;   // the column blocks k_pred_var reads
+  const int tlim = pt_cols(md);      // the column blocks the kriging GEMM reads
   double* PT = md.PT + ((long)sh * md.n_pad + k0) * md.n_test_pad;
   if (k0 >= ns) {                    // padding rows
     for (int rr = 0; rr < MK_PT_RB; ++rr)
@@ -1443,7 +1448,7 @@ template __global__ void k_pred_var<false>(Model, MatSet, const int*, const int*
 __global__ __launch_bounds__(512, 1) void k_pred_var_w(Model md, MatSet ms, const int* __restrict__ list,
                                                        const int* __restrict__ count) {
   extern __shared__ __attribute__((aligned(16))) double lds[];   // gw_lds_bytes()
-  const int ntw = md.ntt / 2;                                     // 256-site column tiles
+  const int ntw = (md.ntt + 1) / 2;                               // 256-site column tiles (pt_cols)
   int e, t_;
   if (!xcd_map(*count, ms.nt * ntw, &e, &t_)) return;
   const int i = t_ / ntw, tw = t_ % ntw;   // row-panel-major: an XCD's workgroups share W's row panel

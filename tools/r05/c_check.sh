@@ -3,7 +3,7 @@
 set -o pipefail
 O=gpurun_out/r05c
 mkdir -p $O
-timeout -k 10 700 python -u -m pytest tests/test_gpu_cfg5.py tests/test_gpu_linalg.py tests/test_gpu_sampler.py -x -v --timeout 240 --timeout-method thread > $O/tests.log 2>&1 || { echo "tests failed"; tail -40 $O/tests.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread > $O/tests.log 2>&1 || { echo "tests failed"; tail -40 $O/tests.log; exit 1; }
 tail -2 $O/tests.log
 timeout -k 10 300 python bench_kriging.py > $O/krig_wide.json 2> $O/krig.err || { echo krig wide failed; tail $O/krig.err; exit 1; }
 MK_PRED_NARROW=1 timeout -k 10 300 python bench_kriging.py --phi-window 0 > $O/krig_narrow.json 2>> $O/krig.err || { echo krig narrow failed; exit 1; }

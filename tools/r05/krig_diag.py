@@ -1,0 +1,21 @@
+"""Diagnostic: the tiled kriging draws of test_gpu_cfg5's setup under the current library
+configuration, saved to the .npz named on the command line (compare MK_PRED_NARROW=0 / 1)."""
+import importlib
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+mk = importlib.import_module("laurabaracaldo-spatial-meta-kriging-for-distributed-inference-for-binary-response_amd")
+n, n_test, tile, S, base = 2000, int(sys.argv[2]) if len(sys.argv) > 2 else 70_000, 65536, 2, 3
+d = mk.synthetic.generate(S * n, q=1, n_test=n_test, seed=505, cov_model=0)
+kw = dict(n_batch=2, batch_length=3, burn_in=3, seed=21)
+cfg = mk.SamplerConfig(1, 2, beta_starting=np.zeros(2), beta_tuning=np.full(2, 0.05), predict_tile=tile, **kw)
+subs = [dict(coords=d["coords"][s * n:(s + 1) * n], y=d["y"][s * n:(s + 1) * n], weights=np.ones(n),
+             x=d["x"][s * n:(s + 1) * n]) for s in range(S)]
+with mk.Session(subs, cfg, coords_test=d["coords_test"], subset_base=base) as ses:
+    ses.run(cfg.n_samples)
+    dev = ses.outputs(samples=True, w_pred_samples=True)
+np.savez(sys.argv[1], pred=np.stack(dev["w_pred_samples"]), samples=np.stack(dev["samples"]))
