@@ -539,7 +539,7 @@ static bool set_gemm_lds() {
       {(const void*)k_inv_level<32>, LDS_32},
       {(const void*)k_qblocks, LDS_64},           {(const void*)k_lauum, LDS_128},
       {(const void*)k_pred_var<true>, LDS_128},   {(const void*)k_pred_var<false>, LDS_128},
-      {(const void*)k_pred_var_w, LDS_WIDE}};
+      {(const void*)k_pred_var_w, LDS_WIDE},     {(const void*)k_chol_trsm_w, LDS_WIDE}};
   for (const auto& f : fns)
     if (hipFuncSetAttribute(f.first, hipFuncAttributeMaxDynamicSharedMemorySize, (int)f.second) != hipSuccess)
       return false;
@@ -622,8 +622,15 @@ static void chol_trsm(mk_session* s, Group& g, hipStream_t st, int h0, int hc, i
   const int E = g.S * hc, nti = ib - ia;
   if (nti <= 0) return;
   const int tm = tile_size((long)E * nti);
+  // MK_TRSM_WIDE=1: two tiles per 8-wave workgroup, three stages (k_chol_trsm_w), where the pair grid
+  // still covers every CU (2: wherever the 128-tile shape is chosen -- tests); same bits
+  static const int wide_env = tile_env("MK_TRSM_WIDE", 0);
+  const long pairs = (long)E * ((nti + 1) / 2);
   timed(s, st, KS_CHOL_TRSM, flops, [&] {
-    if (tm == 32)
+    if (tm == 128 && (wide_env == 2 || (wide_env == 1 && pairs >= 256)))
+      MK_LAUNCH(k_chol_trsm_w, dim3(xcd_grid_h(E, (nti + 1) / 2)), dim3(512), LDS_WIDE, st, g.ms, g.S, h0, hc, k, ia,
+                ib, slist, scount);
+    else if (tm == 32)
       MK_LAUNCH(k_chol_trsm<32>, dim3(xcd_grid_h(E, nti * 4)), dim3(256), LDS_32x128, st, g.ms, g.S, h0, hc, k,
                          ia, ib, slist, scount);
     else if (tm == 64)

@@ -346,6 +346,101 @@ __global__ __launch_bounds__(256, 2) void k_chol_trsm(MatSet ms, int S, int h0, 
   gemm_tile<TM, 128, true, true, false, false, false, SKIP_TRI_B>(C, ld, W, MK_NB, MK_NB, MK_NB, acc, lds);
   store_tile(C, ld, acc);
 }
+// Wide trsm (MK_TRSM_WIDE): two consecutive tiles (i, i+1) of panel k per 512-thread workgroup, one
+// workgroup per CU, all 160 KiB of LDS as three stages of (C chunk 256 x 16, Winv_k chunk 128 x 16):
+// two chunks in flight per CU against one per workgroup (two per CU) in k_chol_trsm<128>, and each
+// Winv chunk staged once for two tiles.  Waves 0-3 own tile i, 4-7 tile i+1, each the 64 x 64 quadrant
+// layout of gemm_tile with the same SKIP_TRI_B skips: the same MFMA sequence per element, the same bits.
+// A pair's odd last tile reads its own rows twice (no read past the matrix) and stores once.
+__global__ __launch_bounds__(512, 1) void k_chol_trsm_w(MatSet ms, int S, int h0, int hc, int k, int ia, int ib,
+                                                        const int* slist, const int* scount) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];   // gw_lds_bytes()
+  constexpr int IA = 16 * 272;                                    // C image: 256-long m-contiguous
+  constexpr int STAGE = IA + 16 * 144;                            // + Winv_k^T image [16][128] (n-contiguous)
+  static_assert(3 * STAGE * 8 <= 163840, "one workgroup per CU");
+  constexpr int NDMA = 6;                                         // per wave per chunk: C 2 rows x 2, Winv 2
+  const int npr = (ib - ia + 1) / 2;
+  int e, t, s, h;
+  if (!xcd_map(active_pairs(slist, scount, S, hc), npr, &e, &t) || !pick_pair(slist, scount, e, h0, hc, &s, &h))
+    return;
+  const int i = ia + 2 * t;
+  const bool two = i + 1 < ib;
+  const int sh = s * ms.q + h;
+  const int slot = 1 - ms.cur[sh];
+  double* M = mat_slot(ms, sh, slot);
+  const double* Wv = winv_slot(ms, sh, slot, k);
+  const long ld = ms.ld;
+  double* C = M + i * MK_NB + (long)k * MK_NB * ld;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int tt = w >> 2, wq = w & 3, wm = wq & 1, wn = wq >> 1;
+  const int li = lane & 15, lk = lane >> 4;
+  auto issue = [&](int c) {
+    double* st = lds + (c % 3) * STAGE;
+    const int k0 = GB_K * c;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int r = w + 8 * j;   // k-row of the chunk
+#pragma unroll
+      for (int pc = 0; pc < 2; ++pc)   // rows 128 pc .. : tile i + pc (tile i again for a lone last tile)
+        __builtin_amdgcn_global_load_lds((const void*)(C + (long)(k0 + r) * ld + (two ? 128 * pc : 0) + 2 * lane),
+                                         (void*)(st + r * 272 + 128 * pc), 16, 0, 0);
+      // op(B)(k, n) = Winv_k(n, k) = Wv[k * 128 + n]: k-row r of the chunk is 128 contiguous doubles
+      __builtin_amdgcn_global_load_lds((const void*)(Wv + (long)(k0 + r) * MK_NB + 2 * lane),
+                                       (void*)(st + IA + r * 144), 16, 0, 0);
+    }
+  };
+  Acc acc;
+  acc_zero(acc);
+  auto chunk = [&](int c) {
+    const double* st = lds + (c % 3) * STAGE;
+    const double* As = st + tt * 128;
+    const double* Bs = st + IA;
+#pragma unroll
+    for (int ks = 0; ks < GB_K / 4; ++ks) {
+      const int kk = ks * 4 + lk;
+      double ya[4], xb[4];
+#pragma unroll
+      for (int b = 0; b < 4; ++b) ya[b] = As[kk * 272 + wm * 64 + b * 16 + li];
+#pragma unroll
+      for (int b = 0; b < 4; ++b) xb[b] = Bs[kk * 144 + wn * 64 + b * 16 + li];
+#pragma unroll
+      for (int bm = 0; bm < 4; ++bm)
+#pragma unroll
+        for (int bn = 0; bn < 4; ++bn) {
+          if (c > wn * 4 + bn) continue;   // SKIP_TRI_B: Winv_k lower triangular, chunk c feeds column blocks >= c
+          acc.v[bm][bn] = __builtin_amdgcn_mfma_f64_16x16x4f64(xb[bn], ya[bm], acc.v[bm][bn], 0, 0, 0);
+        }
+    }
+  };
+  constexpr int nch = MK_NB / GB_K;   // 8
+  issue(0);
+  issue(1);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NDMA) : "memory");
+  __syncthreads();
+#pragma unroll 1
+  for (int c = 0; c + 2 < nch; ++c) {
+    issue(c + 2);
+    chunk(c);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NDMA) : "memory");
+    __syncthreads();
+  }
+#pragma unroll 1
+  for (int c = nch - 2; c < nch; ++c) {
+    chunk(c);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  if (tt == 0 || two) {
+    double* Ct = C + tt * 128 + wm * 64 + (long)(wn * 64) * ld;
+#pragma unroll
+    for (int bm = 0; bm < 4; ++bm)
+#pragma unroll
+      for (int bn = 0; bn < 4; ++bn)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Ct[bm * 16 + li + (long)(bn * 16 + lk + 4 * r) * ld] = acc.v[bm][bn][r];
+  }
+}
+
 template __global__ void k_chol_trsm<128>(MatSet, int, int, int, int, int, int, const int*, const int*);
 template __global__ void k_chol_trsm<64>(MatSet, int, int, int, int, int, int, const int*, const int*);
 template __global__ void k_chol_trsm<32>(MatSet, int, int, int, int, int, int, const int*, const int*);

@@ -127,8 +127,10 @@ def test_sub_tile_gemm_split_cholesky_and_multi_wg_sweep_are_bit_identical(tmp_p
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     res = {}
-    # (MK_TILE, MK_SWEEP, MK_CHOL_SPLIT, MK_PRED_GEN, MK_CHOL_DEPTH, lookahead)
+    # (MK_TILE, MK_SWEEP, MK_CHOL_SPLIT, MK_PRED_GEN, MK_CHOL_DEPTH, lookahead[, MK_TRSM_WIDE])
     configs = (("128", "1", "0", "0", "2", "1"),
+               ("128", "1", "1", "0", "2", "1", "2"),
+               ("128", "3", "0", "0", "2", "0", "2"),
                ("128", "2", "0", "0", "2", "1"),
                ("128", "2", "0", "0", "2", "0"),
                ("64", "3", "1", "0", "1", "0"),
@@ -142,18 +144,20 @@ def test_sub_tile_gemm_split_cholesky_and_multi_wg_sweep_are_bit_identical(tmp_p
                ("64", "3", "1", "0", "2", "0"),
                ("128", "1", "0", "0", "2", "0"))
     for cfg in configs:
-        tile, sweep, split, gen, depth, la = cfg
+        tile, sweep, split, gen, depth, la = cfg[:6]
+        wide = cfg[6] if len(cfg) > 6 else "0"   # 2: the two-tile trsm (k_chol_trsm_w) wherever 128-tiles run
         path = str(tmp_path / ("run_" + "_".join(cfg) + ".npz"))
         r = subprocess.run([sys.executable, os.path.join(here, "gpu_tile_run.py"), path], capture_output=True,
                            text=True, timeout=240,
                            env=dict(os.environ, MK_TILE=tile, MK_SWEEP=sweep, MK_CHOL_SPLIT=split, MK_PRED_GEN=gen,
-                                    MK_CHOL_DEPTH=depth, **({} if la == "1" else {"MK_LOOKAHEAD": "0"})))
+                                    MK_CHOL_DEPTH=depth, MK_TRSM_WIDE=wide,
+                                    **({} if la == "1" else {"MK_LOOKAHEAD": "0"})))
         assert r.returncode == 0, r.stderr[-4000:]
         z = np.load(path)
         res[cfg] = {k: z[k] for k in z.files}
     refs = {"1": res[configs[0]], "0": res[configs[-1]]}
     for cfg, got in res.items():
-        ref = refs[cfg[-1]]
+        ref = refs[cfg[5]]
         assert got.keys() == ref.keys()
         for k in ref:
             assert np.array_equal(got[k], ref[k]), (cfg, k)
