@@ -9,6 +9,6 @@ B="python3 -u bench.py --steps 4 --warmup 1 --no-cpu-baseline"
 KR="python3 -u bench_kriging.py --subsets 8 --n-test 262144 --kept 2 --kernel-events 0"
 for c in FETCH_SIZE WRITE_SIZE; do
   lc=$(echo $c | cut -d_ -f1 | tr A-Z a-z)
-  MK_SWEEP=1 timeout -s KILL 150 rocprofv3 --pmc $c --output-format csv -d gpurun_out/pmc_${T}_bench_$lc -- $B > gpurun_out/pmc_${T}_bench_$lc.log 2>&1
-  MK_SWEEP=1 timeout -s KILL 150 rocprofv3 --pmc $c --output-format csv -d gpurun_out/pmc_${T}_krig_$lc -- $KR > gpurun_out/pmc_${T}_krig_$lc.log 2>&1
+  timeout -s KILL 150 rocprofv3 --pmc $c --output-format csv -d gpurun_out/pmc_${T}_bench_$lc -- $B > gpurun_out/pmc_${T}_bench_$lc.log 2>&1
+  timeout -s KILL 150 rocprofv3 --pmc $c --output-format csv -d gpurun_out/pmc_${T}_krig_$lc -- $KR > gpurun_out/pmc_${T}_krig_$lc.log 2>&1
 done
