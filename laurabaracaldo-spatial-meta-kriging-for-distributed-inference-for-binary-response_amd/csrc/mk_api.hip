@@ -391,7 +391,6 @@ struct mk_session {
   int sweep_site = 0;
   size_t sweep_site_lds = 0;
   int sweep_lean = 0;             // q = 1: 1 border row by factor, 2 every n_s even (sweep_site_kernel)
-  bool sweep_quad = false;        // q = 1, n_pad <= 2048: four sites per barrier
   bool sweep_split = false;       // k_sweep_step, one launch per 64-site block
   bool sweep_coop = false;        // k_sweep_mg by hipLaunchCooperativeKernel (sequential schedule only)
   size_t sweep_mg_lds = 0;
@@ -529,7 +528,7 @@ static inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
 // Every tile-GEMM kernel takes gb_lds_bytes(TM, TN) of dynamic LDS: two DMA stages (> 64 KiB at 128 x 128).
 static constexpr size_t LDS_128 = gb_lds_bytes(128, 128), LDS_64 = gb_lds_bytes(64, 64),
                         LDS_64x128 = gb_lds_bytes(64, 128), LDS_32 = gb_lds_bytes(32, 32),
-                        LDS_32x128 = gb_lds_bytes(32, 128), LDS_WIDE = gw_lds_bytes();
+                        LDS_32x128 = gb_lds_bytes(32, 128);
 static bool set_gemm_lds() {
   const std::pair<const void*, size_t> fns[] = {
       {(const void*)k_chol_update<128>, LDS_128}, {(const void*)k_chol_update<64>, LDS_64},
@@ -539,7 +538,7 @@ static bool set_gemm_lds() {
       {(const void*)k_inv_level<32>, LDS_32},
       {(const void*)k_qblocks, LDS_64},           {(const void*)k_lauum, LDS_128},
       {(const void*)k_pred_var<true>, LDS_128},   {(const void*)k_pred_var<false>, LDS_128},
-      {(const void*)k_pred_var_w, LDS_WIDE},     {(const void*)k_chol_trsm_w, LDS_WIDE}};
+      {(const void*)k_chol_trsm_r, (size_t)TRSM_R_LDS}};
   for (const auto& f : fns)
     if (hipFuncSetAttribute(f.first, hipFuncAttributeMaxDynamicSharedMemorySize, (int)f.second) != hipSuccess)
       return false;
@@ -622,13 +621,12 @@ static void chol_trsm(mk_session* s, Group& g, hipStream_t st, int h0, int hc, i
   const int E = g.S * hc, nti = ib - ia;
   if (nti <= 0) return;
   const int tm = tile_size((long)E * nti);
-  // MK_TRSM_WIDE=1: two tiles per 8-wave workgroup, three stages (k_chol_trsm_w), where the pair grid
-  // still covers every CU (2: wherever the 128-tile shape is chosen -- tests); same bits
-  static const int wide_env = tile_env("MK_TRSM_WIDE", 0);
-  const long pairs = (long)E * ((nti + 1) / 2);
+  // 128-tiles: the register-resident trsm (k_chol_trsm_r, one 8-wave workgroup per tile and CU);
+  // MK_TRSM_REG=0: the two-stage LDS form k_chol_trsm<128> (same bits)
+  static const int reg_env = tile_env("MK_TRSM_REG", 1);
   timed(s, st, KS_CHOL_TRSM, flops, [&] {
-    if (tm == 128 && (wide_env == 2 || (wide_env == 1 && pairs >= 256)))
-      MK_LAUNCH(k_chol_trsm_w, dim3(xcd_grid_h(E, (nti + 1) / 2)), dim3(512), LDS_WIDE, st, g.ms, g.S, h0, hc, k, ia,
+    if (tm == 128 && reg_env)
+      MK_LAUNCH(k_chol_trsm_r, dim3(xcd_grid_h(E, nti)), dim3(512), (size_t)TRSM_R_LDS, st, g.ms, g.S, h0, hc, k, ia,
                 ib, slist, scount);
     else if (tm == 32)
       MK_LAUNCH(k_chol_trsm<32>, dim3(xcd_grid_h(E, nti * 4)), dim3(256), LDS_32x128, st, g.ms, g.S, h0, hc, k,
@@ -800,17 +798,9 @@ static void launch_pred_refresh(mk_session* s, Group& g, hipStream_t st = nullpt
   else if (!s->pred_gen)
     MK_LAUNCH(pred_PT_kernel(md.cov_model), dim3(max_entries * md.n_pad), dim3(256), 0, st, md, g.d_plist,
                        g.d_pcount);
-  // stored P^T: the wide three-stage GEMM (k_pred_var_w, 128 x 256 tiles, one 8-wave workgroup per CU);
-  // MK_PRED_GEN: P^T generated in LDS by the 128 x 128 body; MK_PRED_NARROW=1: the stored-P^T
-  // 128 x 128 body (k_pred_var<false>, two workgroups per CU; same bits)
-  static const int narrow_env = tile_env("MK_PRED_NARROW", 0);
   timed(s, st, KS_PRED_VAR, pred_flops(s, g), [&] {
-    if (s->pred_gen || narrow_env)
-      MK_LAUNCH(s->pred_gen ? k_pred_var<true> : k_pred_var<false>, dim3(xcd_grid_h(max_entries, nt * md.ntt)),
-                dim3(256), LDS_128, st, md, g.ms, g.d_plist, g.d_pcount);
-    else
-      MK_LAUNCH(k_pred_var_w, dim3(xcd_grid_h(max_entries, nt * ((md.ntt + 1) / 2))), dim3(512), LDS_WIDE, st, md,
-                g.ms, g.d_plist, g.d_pcount);
+    MK_LAUNCH(s->pred_gen ? k_pred_var<true> : k_pred_var<false>, dim3(xcd_grid_h(max_entries, nt * md.ntt)),
+              dim3(256), LDS_128, st, md, g.ms, g.d_plist, g.d_pcount);
   });
   MK_LAUNCH(k_pred_var_reduce, dim3(max_entries * (md.n_test_pad / 256)), dim3(256), 0, st, md, nt,
                      g.d_plist, g.d_pcount);
@@ -845,7 +835,7 @@ static void launch_sweep(mk_session* s, Group& g, int it) {
   hipError_t e = hipSuccess;
   if (s->sweep_site) {
     void* args[] = {&md, &ms, &iter};
-    e = hipLaunchKernel(sweep_site_kernel(q, s->sweep_site, s->sweep_lean, s->sweep_quad), dim3(g.S), dim3(MK_SS_T), args,
+    e = hipLaunchKernel(sweep_site_kernel(q, s->sweep_site, s->sweep_lean), dim3(g.S), dim3(MK_SS_T), args,
                         s->sweep_site_lds, g.stream);
     wd_trace(g.stream, "k_sweep_site");
   } else if (use_sweep_mg(s)) {
@@ -1383,10 +1373,8 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
       bool all_even = true;
       for (int i = 0; i < S; ++i) all_even = all_even && (s->n_part[i] % 2 == 0);
       s->sweep_lean = q == 1 ? (all_even ? 2 : 1) : 0;
-      static const int quad_env = tile_env("MK_SS_QUAD", 0);
-      s->sweep_quad = q == 1 && s->sweep_site == 1 && quad_env == 1;
       s->sweep_site_lds = sweep_site_lds_bytes(nmax, q, s->sweep_lean);
-      HIPCHK(hipFuncSetAttribute(sweep_site_kernel(q, s->sweep_site, s->sweep_lean, s->sweep_quad),
+      HIPCHK(hipFuncSetAttribute(sweep_site_kernel(q, s->sweep_site, s->sweep_lean),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)s->sweep_site_lds));
     }
     if (s->sweep_split) {

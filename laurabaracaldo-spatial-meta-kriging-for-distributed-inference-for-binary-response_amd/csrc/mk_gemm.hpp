@@ -211,83 +211,6 @@ __device__ inline void gemm_tile_genb(const double* __restrict__ A, long sA, int
   }
 }
 
-// Wide three-stage form for long-K products (the kriging GEMM X = W P^T): a 128 x 256 output tile
-// on ONE 512-thread workgroup per CU -- 8 waves (2 x 4), each the proven 64 x 64 quadrant (64
-// accumulator doubles, two waves per SIMD at <= 256 registers) -- with all 160 KiB of LDS as three
-// stages of (A image 128 x 16, B image 256 x 16): chunks c+1 and c+2 stream in while chunk c is
-// multiplied, and the barrier after chunk c waits only for chunk c+1's DMA (vmcnt counts the younger
-// chunk's six instructions per wave out).  A and B m-contiguous (W column-major, P^T site-major).
-// Against two 4-wave 128 x 128 workgroups per CU: a quarter less DMA per flop (each B chunk feeds
-// 128 rows, each A chunk 256 columns) and one more chunk of latency cover.  Every element gets the
-// MFMA sequence of gemm_tile (16-deep chunks in order, four k-steps each, the same fragments): the
-// same bits.
-constexpr int GW_STAGE = 16 * 144 + 16 * 272;   // doubles per stage (A 128-long + B 256-long images)
-__host__ __device__ constexpr int gw_lds_bytes() { return 3 * GW_STAGE * 8; }
-static_assert(gw_lds_bytes() <= 163840, "one workgroup per CU");
-
-__device__ inline void gemm_wide(const double* __restrict__ A, long sA, const double* __restrict__ B, long sB, int K,
-                                 Acc& acc, double* lds) {
-  constexpr int IA = 16 * 144;
-  constexpr int NDMA = 6;   // per wave per chunk: A 2 rows, B 2 rows x 2 pieces
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int wm = w & 1, wn = w >> 1;
-  const int li = lane & 15, lk = lane >> 4;
-  if (K <= 0) return;
-  const int nch = K / GB_K;
-  auto issue = [&](int c) {
-    double* st = lds + (c % 3) * GW_STAGE;
-    const int k0 = GB_K * c;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int r = w + 8 * j;
-      __builtin_amdgcn_global_load_lds((const void*)(A + (long)(k0 + r) * sA + 2 * lane), (void*)(st + r * 144), 16,
-                                       0, 0);
-#pragma unroll
-      for (int pc = 0; pc < 2; ++pc)
-        __builtin_amdgcn_global_load_lds((const void*)(B + (long)(k0 + r) * sB + 128 * pc + 2 * lane),
-                                         (void*)(st + IA + r * 272 + 128 * pc), 16, 0, 0);
-    }
-  };
-  auto chunk = [&](const double* st) {
-    const double* As = st;
-    const double* Bs = st + IA;
-#pragma unroll
-    for (int ks = 0; ks < GB_K / 4; ++ks) {
-      const int k = ks * 4 + lk;
-      double ya[4], xb[4];
-#pragma unroll
-      for (int b = 0; b < 4; ++b) ya[b] = As[k * 144 + wm * 64 + b * 16 + li];
-#pragma unroll
-      for (int b = 0; b < 4; ++b) xb[b] = Bs[k * 272 + wn * 64 + b * 16 + li];
-#pragma unroll
-      for (int bm = 0; bm < 4; ++bm)
-#pragma unroll
-        for (int bn = 0; bn < 4; ++bn)
-          acc.v[bm][bn] = __builtin_amdgcn_mfma_f64_16x16x4f64(xb[bn], ya[bm], acc.v[bm][bn], 0, 0, 0);
-    }
-  };
-  issue(0);
-  if (nch > 1) {
-    issue(1);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NDMA) : "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-  int c = 0;
-  for (; c + 2 < nch; ++c) {   // steady state: branch-free body; the last two chunks are peeled
-    issue(c + 2);              // stage (c+2) % 3 was last read in iteration c-1, which every wave has left
-    chunk(lds + (c % 3) * GW_STAGE);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NDMA) : "memory");   // chunk c+1 landed, c+2 in flight
-    __syncthreads();
-  }
-  for (; c < nch; ++c) {
-    chunk(lds + (c % 3) * GW_STAGE);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-}
-
 // The 128 x 128 form every kernel started from.
 template <bool A_MU, bool B_NU, bool NEG = false, bool REV = false, bool SAME = false, int SKIP = SKIP_NONE,
           bool MASK = false>

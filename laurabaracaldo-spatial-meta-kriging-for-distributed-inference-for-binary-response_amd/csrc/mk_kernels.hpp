@@ -19,8 +19,10 @@ __global__ void k_chol_update(MatSet ms, int S, int h0, int hc, int k, int ia, i
 template <int TM>
 __global__ void k_chol_trsm(MatSet ms, int S, int h0, int hc, int k, int ia, int ib, const int* slist,
                             const int* scount);
-__global__ void k_chol_trsm_w(MatSet ms, int S, int h0, int hc, int k, int ia, int ib, const int* slist,
+__global__ void k_chol_trsm_r(MatSet ms, int S, int h0, int hc, int k, int ia, int ib, const int* slist,
                               const int* scount);
+constexpr int TRSM_R_LDS = MK_NB * 144 * 8;   // k_chol_trsm_r: Winv_k^T image [k][n], row stride 144
+static_assert(TRSM_R_LDS <= 163840, "one workgroup per CU");
 __global__ void k_chol_diag(MatSet ms, const int* n_s, int h0, int hc, int k, double* ld_part, double* quad_c, int* info,
                             const int* slist, const int* scount);
 __global__ void k_inv_copydiag(MatSet ms, const int* list, const int* count);
@@ -44,7 +46,6 @@ inline PredPTKernel pred_PT_kernel(int model) {
 }
 template <bool GEN>
 __global__ void k_pred_var(Model md, MatSet ms, const int* list, const int* count);
-__global__ void k_pred_var_w(Model md, MatSet ms, const int* list, const int* count);
 __global__ void k_pred_var_reduce(Model md, int nt, const int* list, const int* count);
 // mk_mcmc.hip
 __global__ void k_beta(Model md, int iter);
@@ -64,11 +65,8 @@ inline size_t sweep_site_lds_bytes(int ns_max, int q, int lean = 0) { return (si
 // q = 1: the lean pair form (two sites per barrier, fused-multiply-add dots, no row masks beyond the
 // one upper element a pair loads; lean 1: the border row dropped by a factor; 2: for shards whose
 // n_s are all even, no border element in a loaded pair); q = 2, 3: one site per barrier, masked.
-// quad: four sites per barrier (q = 1, n_pad <= 2048).
-inline const void* sweep_site_kernel(int q, int kr, int lean = 1, bool quad = false) {
+inline const void* sweep_site_kernel(int q, int kr, int lean = 1) {
   if (q == 1) {
-    if (kr == 1 && quad)
-      return lean == 1 ? (const void*)k_sweep_site<1, 4, 4, 0, 1> : (const void*)k_sweep_site<1, 4, 4, 0, 2>;
     if (kr == 1)
       return lean == 1 ? (const void*)k_sweep_site<1, 4, 2, 0, 1> : (const void*)k_sweep_site<1, 4, 2, 0, 2>;
     return lean == 1 ? (const void*)k_sweep_site<1, 8, 2, 0, 1> : (const void*)k_sweep_site<1, 8, 2, 0, 2>;

@@ -346,99 +346,70 @@ __global__ __launch_bounds__(256, 2) void k_chol_trsm(MatSet ms, int S, int h0, 
   gemm_tile<TM, 128, true, true, false, false, false, SKIP_TRI_B>(C, ld, W, MK_NB, MK_NB, MK_NB, acc, lds);
   store_tile(C, ld, acc);
 }
-// Wide trsm (MK_TRSM_WIDE): two consecutive tiles (i, i+1) of panel k per 512-thread workgroup, one
-// workgroup per CU, all 160 KiB of LDS as three stages of (C chunk 256 x 16, Winv_k chunk 128 x 16):
-// two chunks in flight per CU against one per workgroup (two per CU) in k_chol_trsm<128>, and each
-// Winv chunk staged once for two tiles.  Waves 0-3 own tile i, 4-7 tile i+1, each the 64 x 64 quadrant
-// layout of gemm_tile with the same SKIP_TRI_B skips: the same MFMA sequence per element, the same bits.
-// A pair's odd last tile reads its own rows twice (no read past the matrix) and stores once.
-__global__ __launch_bounds__(512, 1) void k_chol_trsm_w(MatSet ms, int S, int h0, int hc, int k, int ia, int ib,
+// Register-resident trsm (default for 128-tiles): L(i,k) = C(i,k) Winv_k^T with the whole C tile
+// in registers and the whole Winv_k^T in LDS.  k_chol_trsm<128> streams both through two 16-deep
+// LDS stages, one chunk ahead, so a workgroup has 32 KB in flight (two per CU: 64 KB) and each chunk
+// waits out an HBM round trip under load (PMC: 0.59 GB per launch at 3.9 TB/s, MFMA 0.45 busy).  Here
+// one 512-thread workgroup per CU issues its 128 KB C read at once -- each lane 32 16-byte loads, the
+// rows 2l, 2l+1 of its row group for the 32 k's it feeds -- and DMAs Winv_k^T (144 KB image) beside
+// it; after one barrier the MFMAs run with no further synchronisation, each k-step as its C loads
+// land (the compiler's in-order vmcnt waits).  Wave w: row group w & 3 (32 rows), column half w >> 2
+// (the two halves' unequal triangular work paired on each SIMD).  The MFMA row block b of lane l is
+// row 2l + b of the row group (so a lane's two rows are one 16-byte load and one 16-byte store); per
+// element the k-steps, fragments and SKIP_TRI_B skips of gemm_tile: the same bits.
+__global__ __launch_bounds__(512, 1) void k_chol_trsm_r(MatSet ms, int S, int h0, int hc, int k, int ia, int ib,
                                                         const int* slist, const int* scount) {
-  extern __shared__ __attribute__((aligned(16))) double lds[];   // gw_lds_bytes()
-  constexpr int IA = 16 * 272;                                    // C image: 256-long m-contiguous
-  constexpr int STAGE = IA + 16 * 144;                            // + Winv_k^T image [16][128] (n-contiguous)
-  static_assert(3 * STAGE * 8 <= 163840, "one workgroup per CU");
-  constexpr int NDMA = 6;                                         // per wave per chunk: C 2 rows x 2, Winv 2
-  const int npr = (ib - ia + 1) / 2;
+  extern __shared__ __attribute__((aligned(16))) double lds[];   // TRSM_R_LDS
+  const int ntk = ib - ia;
   int e, t, s, h;
-  if (!xcd_map(active_pairs(slist, scount, S, hc), npr, &e, &t) || !pick_pair(slist, scount, e, h0, hc, &s, &h))
+  if (!xcd_map(active_pairs(slist, scount, S, hc), ntk, &e, &t) || !pick_pair(slist, scount, e, h0, hc, &s, &h))
     return;
-  const int i = ia + 2 * t;
-  const bool two = i + 1 < ib;
+  const int i = ia + t;
   const int sh = s * ms.q + h;
   const int slot = 1 - ms.cur[sh];
   double* M = mat_slot(ms, sh, slot);
   const double* Wv = winv_slot(ms, sh, slot, k);
   const long ld = ms.ld;
-  double* C = M + i * MK_NB + (long)k * MK_NB * ld;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int tt = w >> 2, wq = w & 3, wm = wq & 1, wn = wq >> 1;
-  const int li = lane & 15, lk = lane >> 4;
-  auto issue = [&](int c) {
-    double* st = lds + (c % 3) * STAGE;
-    const int k0 = GB_K * c;
+  const int rg = w & 3, wn = w >> 2, li = lane & 15, lk = lane >> 4;
+  double* C = M + i * MK_NB + rg * 32 + 2 * li + (long)k * MK_NB * ld;   // this lane's row pair, column 0
+  // Winv_k^T into LDS: row k of the image = Wv[k * 128 .. k * 128 + 127] (16 DMA instructions per wave)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int r = w + 8 * j;   // k-row of the chunk
+  for (int j = 0; j < 16; ++j) {
+    const int r = w + 8 * j;
+    __builtin_amdgcn_global_load_lds((const void*)(Wv + (long)r * MK_NB + 2 * lane), (void*)(lds + r * 144), 16, 0, 0);
+  }
+  asm volatile("" ::: "memory");   // the DMAs are older than the C loads (the vmcnt below counts on it)
+  d2 a[32];
 #pragma unroll
-      for (int pc = 0; pc < 2; ++pc)   // rows 128 pc .. : tile i + pc (tile i again for a lone last tile)
-        __builtin_amdgcn_global_load_lds((const void*)(C + (long)(k0 + r) * ld + (two ? 128 * pc : 0) + 2 * lane),
-                                         (void*)(st + r * 272 + 128 * pc), 16, 0, 0);
-      // op(B)(k, n) = Winv_k(n, k) = Wv[k * 128 + n]: k-row r of the chunk is 128 contiguous doubles
-      __builtin_amdgcn_global_load_lds((const void*)(Wv + (long)(k0 + r) * MK_NB + 2 * lane),
-                                       (void*)(st + IA + r * 144), 16, 0, 0);
-    }
-  };
-  Acc acc;
-  acc_zero(acc);
-  auto chunk = [&](int c) {
-    const double* st = lds + (c % 3) * STAGE;
-    const double* As = st + tt * 128;
-    const double* Bs = st + IA;
-#pragma unroll
-    for (int ks = 0; ks < GB_K / 4; ++ks) {
-      const int kk = ks * 4 + lk;
-      double ya[4], xb[4];
-#pragma unroll
-      for (int b = 0; b < 4; ++b) ya[b] = As[kk * 272 + wm * 64 + b * 16 + li];
-#pragma unroll
-      for (int b = 0; b < 4; ++b) xb[b] = Bs[kk * 144 + wn * 64 + b * 16 + li];
-#pragma unroll
-      for (int bm = 0; bm < 4; ++bm)
-#pragma unroll
-        for (int bn = 0; bn < 4; ++bn) {
-          if (c > wn * 4 + bn) continue;   // SKIP_TRI_B: Winv_k lower triangular, chunk c feeds column blocks >= c
-          acc.v[bm][bn] = __builtin_amdgcn_mfma_f64_16x16x4f64(xb[bn], ya[bm], acc.v[bm][bn], 0, 0, 0);
-        }
-    }
-  };
-  constexpr int nch = MK_NB / GB_K;   // 8
-  issue(0);
-  issue(1);
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NDMA) : "memory");
+  for (int ks = 0; ks < 32; ++ks) a[ks] = *reinterpret_cast<const d2*>(C + (long)(4 * ks + lk) * ld);
+  asm volatile("s_waitcnt vmcnt(32)" ::: "memory");   // this wave's DMAs landed; its 32 C loads may not have
   __syncthreads();
-#pragma unroll 1
-  for (int c = 0; c + 2 < nch; ++c) {
-    issue(c + 2);
-    chunk(c);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NDMA) : "memory");
-    __syncthreads();
-  }
-#pragma unroll 1
-  for (int c = nch - 2; c < nch; ++c) {
-    chunk(c);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-  if (tt == 0 || two) {
-    double* Ct = C + tt * 128 + wm * 64 + (long)(wn * 64) * ld;
+  AccT<2, 4> acc;
+  acc_zero(acc);
 #pragma unroll
-    for (int bm = 0; bm < 4; ++bm)
+  for (int ks = 0; ks < 32; ++ks) {
+    const int kk = 4 * ks + lk, c = ks >> 2;
+    double xb[4];
 #pragma unroll
-      for (int bn = 0; bn < 4; ++bn)
+    for (int bn = 0; bn < 4; ++bn) xb[bn] = lds[kk * 144 + wn * 64 + bn * 16 + li];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) Ct[bm * 16 + li + (long)(bn * 16 + lk + 4 * r) * ld] = acc.v[bm][bn][r];
+    for (int bn = 0; bn < 4; ++bn) {
+      if (c > wn * 4 + bn) continue;   // SKIP_TRI_B: chunk c feeds column blocks >= c
+      acc.v[0][bn] = __builtin_amdgcn_mfma_f64_16x16x4f64(xb[bn], a[ks].x, acc.v[0][bn], 0, 0, 0);
+      acc.v[1][bn] = __builtin_amdgcn_mfma_f64_16x16x4f64(xb[bn], a[ks].y, acc.v[1][bn], 0, 0, 0);
+    }
   }
+  // acc.v[b][bn][r]: row 2 li + b of the row group, column wn * 64 + 16 bn + lk + 4 r
+#pragma unroll
+  for (int bn = 0; bn < 4; ++bn)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      d2 v;
+      v.x = acc.v[0][bn][r];
+      v.y = acc.v[1][bn][r];
+      *reinterpret_cast<d2*>(C + (long)(wn * 64 + 16 * bn + lk + 4 * r) * ld) = v;
+    }
 }
 
 template __global__ void k_chol_trsm<128>(MatSet, int, int, int, int, int, int, const int*, const int*);
@@ -1300,11 +1271,6 @@ __device__ inline void current_phi_nu(const Model& md, int s, int h, double* phi
   *nu = (md.cov_model == MK_COV_MATERN) ? logit_inv(th[md.ntri + md.q + h], md.nu_a[h], md.nu_b[h]) : 0.0;
 }
 
-// Columns of P^T the kriging GEMM reads: the 128-site blocks of the tile (ntt, odd for a short last
-// tile of the tiled replay) rounded up to the wide GEMM's 256-site tiles (<= n_test_pad, a multiple of
-// 256); columns past n_test are written as zeros.
-__device__ inline int pt_cols(const Model& md) { return ((md.ntt + 1) / 2) * 2 * MK_NB; }
-
 // P^T[k][t] = rho(|obs_k - test_t|) for the listed pairs (zero outside the valid block).
 // MODEL = MK_COV_EXPONENTIAL: exp(-phi d) inline, as in cand_value (bit-identical to CorrFn).
 template <int MODEL>
@@ -1329,7 +1295,7 @@ __global__ __launch_bounds__(256) void k_pred_PT(Model md, const int* __restrict
   const double* cx = md.coords + (long)s * 2 * md.n_pad;
   const double ox = cx[k], oy = cx[md.n_pad + k];
   double* row = md.PT + ((long)sh * md.n_pad + k) * md.n_test_pad;
-  const int tlim = pt_cols(md);   // the column blocks the kriging GEMM reads (all of n_test_pad when fused)
+  const int tlim = md.ntt * MK_NB;   // the column blocks k_pred_var reads (all of n_test_pad when fused)
   for (int t = threadIdx.x; t < tlim; t += 256) {
     double v = 0.0;
     if (k < ns && t < md.n_test) {
@@ -1376,7 +1342,7 @@ __global__ __launch_bounds__(256) void k_pred_PT_matern(Model md, const int* __r
   const int s = sh / md.q, h = sh % md.q;
   const int ns = md.n_s[s];
   const int tid = threadIdx.x, lane = tid & 63;
-  const int tlim = pt_cols(md);      // the column blocks the kriging GEMM reads
+  const int tlim = md.ntt * MK_NB;   // the column blocks k_pred_var reads
   double* PT = md.PT + ((long)sh * md.n_pad + k0) * md.n_test_pad;
   if (k0 >= ns) {                    // padding rows
     for (int rr = 0; rr < MK_PT_RB; ++rr)
@@ -1534,56 +1500,6 @@ __global__ __launch_bounds__(256, 2) void k_pred_var(Model md, MatSet ms, const 
 }
 template __global__ void k_pred_var<true>(Model, MatSet, const int*, const int*);
 template __global__ void k_pred_var<false>(Model, MatSet, const int*, const int*);
-
-// The stored-P^T kriging GEMM in its wide form (the default): 128 x 256 output tiles (one W row
-// panel x 256 test sites) on one 512-thread workgroup per CU with the three-stage body gemm_wide.
-// X = W P^T and the column sums of squares exactly as k_pred_var<false> computes them -- the same
-// MFMA sequence per element (each wave the same 64 x 64 quadrant layout) and the same reduction
-// order -- so the same bits.
-__global__ __launch_bounds__(512, 1) void k_pred_var_w(Model md, MatSet ms, const int* __restrict__ list,
-                                                       const int* __restrict__ count) {
-  extern __shared__ __attribute__((aligned(16))) double lds[];   // gw_lds_bytes()
-  const int ntw = (md.ntt + 1) / 2;                               // 256-site column tiles (pt_cols)
-  int e, t_;
-  if (!xcd_map(*count, ms.nt * ntw, &e, &t_)) return;
-  const int i = t_ / ntw, tw = t_ % ntw;   // row-panel-major: an XCD's workgroups share W's row panel
-  const int sh = list[e];
-  const int s = sh / md.q;
-  const int ns = md.n_s[s];
-  const long ld = ms.ld;
-  const double* Wm = wmat(ms, sh);
-  Acc acc;
-  acc_zero(acc);
-  const double* PT = md.PT + (long)sh * md.n_pad * md.n_test_pad + tw * 256;
-  gemm_wide(Wm + i * MK_NB, ld, PT, md.n_test_pad, (i + 1) * MK_NB, acc, lds);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w & 1, wn = w >> 1;
-  // wave (wm, wn): rows 64 wm + 16 bm + (lane & 15), columns 64 wn + 16 bn + (lane >> 4) + 4 r
-  double* XK = md.XK + (long)sh * md.n_test_pad * md.n_pad + (long)(tw * 256 + wn * 64) * md.n_pad + i * MK_NB +
-               wm * 64;
-  double* red = lds;   // [2][256] (the GEMM ended with a barrier)
-#pragma unroll
-  for (int bn = 0; bn < 4; ++bn)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int n = bn * 16 + (lane >> 4) + 4 * r;
-      double v = 0.0;
-#pragma unroll
-      for (int bm = 0; bm < 4; ++bm) {
-        const int mr = bm * 16 + (lane & 15);
-        const double x = acc.v[bm][bn][r];
-        XK[mr + (long)n * md.n_pad] = x;
-        v += (i * MK_NB + wm * 64 + mr < ns) ? x * x : 0.0;
-      }
-#pragma unroll
-      for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-      if ((lane & 15) == 0) red[wm * 256 + wn * 64 + n] = v;
-    }
-  __syncthreads();
-  if (threadIdx.x < 256) {
-    const int n = threadIdx.x;
-    md.s_part[((long)sh * ms.nt + i) * md.n_test_pad + tw * 256 + n] = red[n] + red[256 + n];
-  }
-}
 
 __global__ __launch_bounds__(256) void k_pred_var_reduce(Model md, int nt, const int* __restrict__ list,
                                                          const int* __restrict__ count) {

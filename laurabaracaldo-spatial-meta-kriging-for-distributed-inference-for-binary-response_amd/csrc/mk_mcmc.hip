@@ -1032,11 +1032,10 @@ __global__ __launch_bounds__(SS_T) void k_sweep_site(Model md, MatSet ms, int it
   constexpr bool FM = LN > 0;
   extern __shared__ __attribute__((aligned(16))) double smem[];
   // ring: 2H columns (VGPRs: 8 H Q KR); NV values exchanged per site, four per row-sum round
-  constexpr int q = Q, H = HH > 0 ? HH : ((16 / (Q * KR)) > 0 ? 16 / (Q * KR) : 1);
-  constexpr int NV = P == 4 ? 14 : (P == 2 ? 5 : 2 * Q);
+  constexpr int q = Q, H = HH > 0 ? HH : ((16 / (Q * KR)) > 0 ? 16 / (Q * KR) : 1), NV = P == 2 ? 5 : 2 * Q;
   constexpr int NR = (NV + 3) / 4;
-  static_assert(H >= 1 && (NV <= 8 || P == 4), "q <= 4");   // instantiated for q <= 2 and (q = 3, KR = 1): no spills
-  static_assert(P == 1 || (Q == 1 && H % P == 0), "site pairs / quads: q = 1, whole groups per ring half");
+  static_assert(H >= 1 && NV <= 8, "q <= 4");   // instantiated for q <= 2 and (q = 3, KR = 1): no spills
+  static_assert(P == 1 || (Q == 1 && H % 2 == 0), "site pairs: q = 1");
   __shared__ double part[2][NV][16];   // per value: the 16-lane row sums of the four waves
   __shared__ double Ai_s[MK_QMAX * MK_QMAX];
   const int s = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -1305,112 +1304,13 @@ __global__ __launch_bounds__(SS_T) void k_sweep_site(Model md, MatSet ms, int it
     if (tid == 0 && live0) sflag[i] = f0;
     if (tid == 0 && live1) sflag[i + 1] = f1;
   };
-  // P = 4 (q = 1, lean): sites i .. i+3 (i % 4 == 0) per barrier.  Fourteen sums per exchange -- the
-  // four dots, the four squared norms and the six couplings c_jk = W[:,j] . W[:,k] = (R^-1)_{kj} -- so
-  // site k's dot after the moves at the sites before it is g_k + sum_{j<k} coef_j c_jk (the carry the
-  // pair form makes once).  A quarter of the barriers of the single-site form, and fewer instructions
-  // per site than the pair form (the reductions of the couplings are shared by four sites).  The same
-  // zero-upper invariant covers every element a quad loads (W[i, i+1] and W[i+2, i+3]).
-  auto quad_step = [&](const int i, d2 (&w0)[KR][Q], d2 (&w1)[KR][Q], d2 (&w2)[KR][Q], d2 (&w3)[KR][Q]) {
-    static_assert(P != 4 || FM, "site quads: the lean form");
-    if ((i & 63) == 0) {   // uniform
-      const int kk = i + lane;
-      const bool lv = kk < ns;
-      const int kc = lv ? kk : ns - 1;
-      vcf = sd_dl[kc];
-      vdll = sd_dll[kc];
-      vh = sd_d2[kc];
-      vlg = lv ? sd_lgu[kc] : __builtin_huge_val();
-    }
-    d2 c[4][KR];
-#pragma unroll
-    for (int k = 0; k < KR; ++k) {
-      c[0][k].x = w0[k][0].x;
-      c[1][k].x = w1[k][0].x;
-      c[2][k].x = w2[k][0].x;
-      c[3][k].x = w3[k][0].x;
-      c[0][k].y = LN == 1 ? w0[k][0].y * ym[k] : w0[k][0].y;
-      c[1][k].y = LN == 1 ? w1[k][0].y * ym[k] : w1[k][0].y;
-      c[2][k].y = LN == 1 ? w2[k][0].y * ym[k] : w2[k][0].y;
-      c[3][k].y = LN == 1 ? w3[k][0].y * ym[k] : w3[k][0].y;
-    }
-    // v: dots 0-3, norms 4-7, couplings 8: 01, 9: 02, 10: 03, 11: 12, 12: 13, 13: 23
-    double v[14];
-#pragma unroll
-    for (int e = 0; e < 14; ++e) v[e] = 0.0;
-#pragma unroll
-    for (int k = 0; k < KR; ++k) {
-#pragma unroll
-      for (int a = 0; a < 4; ++a) {
-        v[a] = fma(c[a][k].y, zr[k][0].y, fma(c[a][k].x, zr[k][0].x, v[a]));
-        v[4 + a] = fma(c[a][k].y, c[a][k].y, fma(c[a][k].x, c[a][k].x, v[4 + a]));
-      }
-      v[8] = fma(c[0][k].y, c[1][k].y, fma(c[0][k].x, c[1][k].x, v[8]));
-      v[9] = fma(c[0][k].y, c[2][k].y, fma(c[0][k].x, c[2][k].x, v[9]));
-      v[10] = fma(c[0][k].y, c[3][k].y, fma(c[0][k].x, c[3][k].x, v[10]));
-      v[11] = fma(c[1][k].y, c[2][k].y, fma(c[1][k].x, c[2][k].x, v[11]));
-      v[12] = fma(c[1][k].y, c[3][k].y, fma(c[1][k].x, c[3][k].x, v[12]));
-      v[13] = fma(c[2][k].y, c[3][k].y, fma(c[2][k].x, c[3][k].x, v[13]));
-    }
-#pragma unroll
-    for (int e = 0; e < 14; ++e) v[e] = row_sum_dpp(v[e]);
-    const int par = (i >> 2) & 1;
-    SS_CFENCE();
-    if ((lane & 15) == 0) {
-#pragma unroll
-      for (int e = 0; e < 14; ++e) part[par][e][4 * wv + (lane >> 4)] = v[e];
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    SS_CFENCE();
-    double tot[16];
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      const int e_l = 4 * rr + (lane >> 4);
-      const double pv = part[par][e_l < 14 ? e_l : 0][lane & 15];
-      const double rsum = row_sum_dpp(e_l < 14 ? pv : 0.0);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) tot[4 * rr + e] = rlane_u(rsum, 16 * e);
-    }
-    // sites in order; ratio = dll - (cf g + 0.5 cf^2 Q_ii), cf = d A^-1 (precomputed per site)
-    double coef[4] = {0.0, 0.0, 0.0, 0.0};
-    int f[4] = {0, 0, 0, 0};
-    const int l0 = i & 63;
-#pragma unroll
-    for (int a = 0; a < 4; ++a) {
-      double g = tot[a];
-      if (a >= 1) g = fma(coef[0], tot[8 + a - 1], g);                 // c_0a: 8 (01), 9 (02), 10 (03)
-      if (a >= 2) g = fma(coef[1], tot[a == 2 ? 11 : 12], g);         // c_12, c_13
-      if (a >= 3) g = fma(coef[2], tot[13], g);                        // c_23
-      const double cf = rlane_u(vcf, l0 + a), hh = rlane_u(vh, l0 + a);
-      if (rlane_u(vlg, l0 + a) <= rlane_u(vdll, l0 + a) - fma(cf, g, hh * tot[4 + a])) {
-        coef[a] = cf;
-        f[a] = 1;
-      }
-    }
-    if (f[0] | f[1] | f[2] | f[3]) {
-#pragma unroll
-      for (int k = 0; k < KR; ++k) {
-        zr[k][0].x = fma(coef[3], c[3][k].x, fma(coef[2], c[2][k].x, fma(coef[1], c[1][k].x, fma(coef[0], c[0][k].x, zr[k][0].x))));
-        zr[k][0].y = fma(coef[3], c[3][k].y, fma(coef[2], c[2][k].y, fma(coef[1], c[1][k].y, fma(coef[0], c[0][k].y, zr[k][0].y))));
-      }
-    }
-    if (tid == 0) {
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-        if (i + a < ns) sflag[i + a] = f[a];
-    }
-  };
   d2 wa[H][KR][Q], wb[H][KR][Q];
 #pragma unroll
   for (int u = 0; u < H; ++u) load_col(u, wa[u]);
   for (int i0 = 0; i0 < ns; i0 += 2 * H) {
 #pragma unroll
     for (int u = 0; u < H; ++u) load_col(i0 + H + u, wb[u]);
-    if constexpr (P == 4) {
-#pragma unroll
-      for (int u = 0; u < H; u += 4) quad_step(i0 + u, wa[u], wa[u + 1], wa[u + 2], wa[u + 3]);
-    } else if constexpr (P == 2) {
+    if constexpr (P == 2) {
 #pragma unroll
       for (int u = 0; u < H; u += 2) pair_step(i0 + u, wa[u], wa[u + 1]);
     } else {
@@ -1419,10 +1319,7 @@ __global__ __launch_bounds__(SS_T) void k_sweep_site(Model md, MatSet ms, int it
     }
 #pragma unroll
     for (int u = 0; u < H; ++u) load_col(i0 + 2 * H + u, wa[u]);
-    if constexpr (P == 4) {
-#pragma unroll
-      for (int u = 0; u < H; u += 4) quad_step(i0 + H + u, wb[u], wb[u + 1], wb[u + 2], wb[u + 3]);
-    } else if constexpr (P == 2) {
+    if constexpr (P == 2) {
 #pragma unroll
       for (int u = 0; u < H; u += 2) pair_step(i0 + H + u, wb[u], wb[u + 1]);
     } else {
@@ -1452,8 +1349,6 @@ template __global__ void k_sweep_site<1, 4, 2, 0, 1>(Model, MatSet, int);
 template __global__ void k_sweep_site<1, 4, 2, 0, 2>(Model, MatSet, int);
 template __global__ void k_sweep_site<1, 8, 2, 0, 1>(Model, MatSet, int);
 template __global__ void k_sweep_site<1, 8, 2, 0, 2>(Model, MatSet, int);
-template __global__ void k_sweep_site<1, 4, 4, 0, 1>(Model, MatSet, int);
-template __global__ void k_sweep_site<1, 4, 4, 0, 2>(Model, MatSet, int);
 
 // ---------------------------------------------------------------- 6. record / adapt
 __global__ __launch_bounds__(64) void k_record(Model md, int iter) {

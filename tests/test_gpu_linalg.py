@@ -112,6 +112,7 @@ def test_combine_is_sequential_mean(mk):
 def test_sub_tile_gemm_split_cholesky_and_multi_wg_sweep_are_bit_identical(tmp_path):
     """Small-shard code paths give exactly the large-shard results: the 64- and 32-sub-tile GEMMs
     (Cholesky update / trsm, inverse levels; mk_gemm.hpp: same MFMA sequence per element), the
+    register-resident trsm against the two-stage LDS one (MK_TRSM_REG=0), the
     split two-stream Cholesky schedule (bulk update by panels < k-d on a CU-masked stream, the
     rank-128d correction on the critical stream; the accumulator passes through fp64 memory) at
     depths 1-3, the 64-site-block sweeps -- one workgroup per subset (MK_SWEEP=1, k_sweep), the
@@ -127,10 +128,10 @@ def test_sub_tile_gemm_split_cholesky_and_multi_wg_sweep_are_bit_identical(tmp_p
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     res = {}
-    # (MK_TILE, MK_SWEEP, MK_CHOL_SPLIT, MK_PRED_GEN, MK_CHOL_DEPTH, lookahead[, MK_TRSM_WIDE])
+    # (MK_TILE, MK_SWEEP, MK_CHOL_SPLIT, MK_PRED_GEN, MK_CHOL_DEPTH, lookahead[, MK_TRSM_REG])
     configs = (("128", "1", "0", "0", "2", "1"),
-               ("128", "1", "1", "0", "2", "1", "2"),
-               ("128", "3", "0", "0", "2", "0", "2"),
+               ("128", "1", "1", "0", "2", "1", "0"),
+               ("128", "3", "0", "0", "2", "0", "0"),
                ("128", "2", "0", "0", "2", "1"),
                ("128", "2", "0", "0", "2", "0"),
                ("64", "3", "1", "0", "1", "0"),
@@ -145,12 +146,12 @@ def test_sub_tile_gemm_split_cholesky_and_multi_wg_sweep_are_bit_identical(tmp_p
                ("128", "1", "0", "0", "2", "0"))
     for cfg in configs:
         tile, sweep, split, gen, depth, la = cfg[:6]
-        wide = cfg[6] if len(cfg) > 6 else "0"   # 2: the two-tile trsm (k_chol_trsm_w) wherever 128-tiles run
+        reg = cfg[6] if len(cfg) > 6 else "1"    # 0: the two-stage LDS trsm k_chol_trsm<128> instead of k_chol_trsm_r
         path = str(tmp_path / ("run_" + "_".join(cfg) + ".npz"))
         r = subprocess.run([sys.executable, os.path.join(here, "gpu_tile_run.py"), path], capture_output=True,
                            text=True, timeout=240,
                            env=dict(os.environ, MK_TILE=tile, MK_SWEEP=sweep, MK_CHOL_SPLIT=split, MK_PRED_GEN=gen,
-                                    MK_CHOL_DEPTH=depth, MK_TRSM_WIDE=wide,
+                                    MK_CHOL_DEPTH=depth, MK_TRSM_REG=reg,
                                     **({} if la == "1" else {"MK_LOOKAHEAD": "0"})))
         assert r.returncode == 0, r.stderr[-4000:]
         z = np.load(path)
@@ -178,16 +179,13 @@ def test_site_sweep_runs_the_block_sweeps_chain(tmp_path):
     here = os.path.dirname(os.path.abspath(__file__))
     for la in ("1", "0"):
         res = {}
-        for sweep in ("1", "0", "0q"):
+        for sweep in ("1", "0"):
             path = str(tmp_path / f"site_{sweep}_{la}.npz")
-            # 0q: the q = 1 site sweep four sites per barrier (MK_SS_QUAD=1)
-            env = dict(os.environ, MK_SWEEP=sweep[0], **({"MK_SS_QUAD": "1"} if sweep == "0q" else {}),
-                       **({} if la == "1" else {"MK_LOOKAHEAD": "0"}))
+            env = dict(os.environ, MK_SWEEP=sweep, **({} if la == "1" else {"MK_LOOKAHEAD": "0"}))
             r = subprocess.run([sys.executable, os.path.join(here, "gpu_tile_run.py"), path], capture_output=True,
                                text=True, timeout=240, env=env)
             assert r.returncode == 0, r.stderr[-4000:]
             z = np.load(path)
             res[sweep] = {k: z[k] for k in z.files}
         for k in res["1"]:
-            for sw in ("0", "0q"):
-                np.testing.assert_allclose(res[sw][k], res["1"][k], rtol=0, atol=1e-9, err_msg=f"{k} la={la} {sw}")
+            np.testing.assert_allclose(res["0"][k], res["1"][k], rtol=0, atol=1e-9, err_msg=f"{k} la={la}")
