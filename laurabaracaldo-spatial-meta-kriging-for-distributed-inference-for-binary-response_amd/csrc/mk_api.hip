@@ -537,8 +537,7 @@ static bool set_gemm_lds() {
       {(const void*)k_chol_update<32>, LDS_32},   {(const void*)k_chol_trsm<32>, LDS_32x128},
       {(const void*)k_inv_level<32>, LDS_32},
       {(const void*)k_qblocks, LDS_64},           {(const void*)k_lauum, LDS_128},
-      {(const void*)k_pred_var<true>, LDS_128},   {(const void*)k_pred_var<false>, LDS_128},
-      {(const void*)k_chol_trsm_r, (size_t)TRSM_R_LDS}};
+      {(const void*)k_pred_var<true>, LDS_128},   {(const void*)k_pred_var<false>, LDS_128}};
   for (const auto& f : fns)
     if (hipFuncSetAttribute(f.first, hipFuncAttributeMaxDynamicSharedMemorySize, (int)f.second) != hipSuccess)
       return false;
@@ -621,14 +620,8 @@ static void chol_trsm(mk_session* s, Group& g, hipStream_t st, int h0, int hc, i
   const int E = g.S * hc, nti = ib - ia;
   if (nti <= 0) return;
   const int tm = tile_size((long)E * nti);
-  // 128-tiles: the register-resident trsm (k_chol_trsm_r, one 8-wave workgroup per tile and CU);
-  // MK_TRSM_REG=0: the two-stage LDS form k_chol_trsm<128> (same bits)
-  static const int reg_env = tile_env("MK_TRSM_REG", 1);
   timed(s, st, KS_CHOL_TRSM, flops, [&] {
-    if (tm == 128 && reg_env)
-      MK_LAUNCH(k_chol_trsm_r, dim3(xcd_grid_h(E, nti)), dim3(512), (size_t)TRSM_R_LDS, st, g.ms, g.S, h0, hc, k, ia,
-                ib, slist, scount);
-    else if (tm == 32)
+    if (tm == 32)
       MK_LAUNCH(k_chol_trsm<32>, dim3(xcd_grid_h(E, nti * 4)), dim3(256), LDS_32x128, st, g.ms, g.S, h0, hc, k,
                          ia, ib, slist, scount);
     else if (tm == 64)

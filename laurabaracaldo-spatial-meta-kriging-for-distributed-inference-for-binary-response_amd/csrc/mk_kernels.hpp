@@ -19,10 +19,6 @@ __global__ void k_chol_update(MatSet ms, int S, int h0, int hc, int k, int ia, i
 template <int TM>
 __global__ void k_chol_trsm(MatSet ms, int S, int h0, int hc, int k, int ia, int ib, const int* slist,
                             const int* scount);
-__global__ void k_chol_trsm_r(MatSet ms, int S, int h0, int hc, int k, int ia, int ib, const int* slist,
-                              const int* scount);
-constexpr int TRSM_R_LDS = MK_NB * 144 * 8;   // k_chol_trsm_r: Winv_k^T image [k][n], row stride 144
-static_assert(TRSM_R_LDS <= 163840, "one workgroup per CU");
 __global__ void k_chol_diag(MatSet ms, const int* n_s, int h0, int hc, int k, double* ld_part, double* quad_c, int* info,
                             const int* slist, const int* scount);
 __global__ void k_inv_copydiag(MatSet ms, const int* list, const int* count);

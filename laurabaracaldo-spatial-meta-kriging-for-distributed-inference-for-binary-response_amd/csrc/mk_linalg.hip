@@ -346,72 +346,6 @@ __global__ __launch_bounds__(256, 2) void k_chol_trsm(MatSet ms, int S, int h0, 
   gemm_tile<TM, 128, true, true, false, false, false, SKIP_TRI_B>(C, ld, W, MK_NB, MK_NB, MK_NB, acc, lds);
   store_tile(C, ld, acc);
 }
-// Register-resident trsm (default for 128-tiles): L(i,k) = C(i,k) Winv_k^T with the whole C tile
-// in registers and the whole Winv_k^T in LDS.  k_chol_trsm<128> streams both through two 16-deep
-// LDS stages, one chunk ahead, so a workgroup has 32 KB in flight (two per CU: 64 KB) and each chunk
-// waits out an HBM round trip under load (PMC: 0.59 GB per launch at 3.9 TB/s, MFMA 0.45 busy).  Here
-// one 512-thread workgroup per CU issues its 128 KB C read at once -- each lane 32 16-byte loads, the
-// rows 2l, 2l+1 of its row group for the 32 k's it feeds -- and DMAs Winv_k^T (144 KB image) beside
-// it; after one barrier the MFMAs run with no further synchronisation, each k-step as its C loads
-// land (the compiler's in-order vmcnt waits).  Wave w: row group w & 3 (32 rows), column half w >> 2
-// (the two halves' unequal triangular work paired on each SIMD).  The MFMA row block b of lane l is
-// row 2l + b of the row group (so a lane's two rows are one 16-byte load and one 16-byte store); per
-// element the k-steps, fragments and SKIP_TRI_B skips of gemm_tile: the same bits.
-__global__ __launch_bounds__(512, 1) void k_chol_trsm_r(MatSet ms, int S, int h0, int hc, int k, int ia, int ib,
-                                                        const int* slist, const int* scount) {
-  extern __shared__ __attribute__((aligned(16))) double lds[];   // TRSM_R_LDS
-  const int ntk = ib - ia;
-  int e, t, s, h;
-  if (!xcd_map(active_pairs(slist, scount, S, hc), ntk, &e, &t) || !pick_pair(slist, scount, e, h0, hc, &s, &h))
-    return;
-  const int i = ia + t;
-  const int sh = s * ms.q + h;
-  const int slot = 1 - ms.cur[sh];
-  double* M = mat_slot(ms, sh, slot);
-  const double* Wv = winv_slot(ms, sh, slot, k);
-  const long ld = ms.ld;
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int rg = w & 3, wn = w >> 2, li = lane & 15, lk = lane >> 4;
-  double* C = M + i * MK_NB + rg * 32 + 2 * li + (long)k * MK_NB * ld;   // this lane's row pair, column 0
-  // Winv_k^T into LDS: row k of the image = Wv[k * 128 .. k * 128 + 127] (16 DMA instructions per wave)
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const int r = w + 8 * j;
-    __builtin_amdgcn_global_load_lds((const void*)(Wv + (long)r * MK_NB + 2 * lane), (void*)(lds + r * 144), 16, 0, 0);
-  }
-  asm volatile("" ::: "memory");   // the DMAs are older than the C loads (the vmcnt below counts on it)
-  d2 a[32];
-#pragma unroll
-  for (int ks = 0; ks < 32; ++ks) a[ks] = *reinterpret_cast<const d2*>(C + (long)(4 * ks + lk) * ld);
-  asm volatile("s_waitcnt vmcnt(32)" ::: "memory");   // this wave's DMAs landed; its 32 C loads may not have
-  __syncthreads();
-  AccT<2, 4> acc;
-  acc_zero(acc);
-#pragma unroll
-  for (int ks = 0; ks < 32; ++ks) {
-    const int kk = 4 * ks + lk, c = ks >> 2;
-    double xb[4];
-#pragma unroll
-    for (int bn = 0; bn < 4; ++bn) xb[bn] = lds[kk * 144 + wn * 64 + bn * 16 + li];
-#pragma unroll
-    for (int bn = 0; bn < 4; ++bn) {
-      if (c > wn * 4 + bn) continue;   // SKIP_TRI_B: chunk c feeds column blocks >= c
-      acc.v[0][bn] = __builtin_amdgcn_mfma_f64_16x16x4f64(xb[bn], a[ks].x, acc.v[0][bn], 0, 0, 0);
-      acc.v[1][bn] = __builtin_amdgcn_mfma_f64_16x16x4f64(xb[bn], a[ks].y, acc.v[1][bn], 0, 0, 0);
-    }
-  }
-  // acc.v[b][bn][r]: row 2 li + b of the row group, column wn * 64 + 16 bn + lk + 4 r
-#pragma unroll
-  for (int bn = 0; bn < 4; ++bn)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      d2 v;
-      v.x = acc.v[0][bn][r];
-      v.y = acc.v[1][bn][r];
-      *reinterpret_cast<d2*>(C + (long)(wn * 64 + 16 * bn + lk + 4 * r) * ld) = v;
-    }
-}
-
 template __global__ void k_chol_trsm<128>(MatSet, int, int, int, int, int, int, const int*, const int*);
 template __global__ void k_chol_trsm<64>(MatSet, int, int, int, int, int, int, const int*, const int*);
 template __global__ void k_chol_trsm<32>(MatSet, int, int, int, int, int, int, const int*, const int*);

@@ -112,7 +112,6 @@ def test_combine_is_sequential_mean(mk):
 def test_sub_tile_gemm_split_cholesky_and_multi_wg_sweep_are_bit_identical(tmp_path):
     """Small-shard code paths give exactly the large-shard results: the 64- and 32-sub-tile GEMMs
     (Cholesky update / trsm, inverse levels; mk_gemm.hpp: same MFMA sequence per element), the
-    register-resident trsm against the two-stage LDS one (MK_TRSM_REG=0), the
     split two-stream Cholesky schedule (bulk update by panels < k-d on a CU-masked stream, the
     rank-128d correction on the critical stream; the accumulator passes through fp64 memory) at
     depths 1-3, the 64-site-block sweeps -- one workgroup per subset (MK_SWEEP=1, k_sweep), the
@@ -128,10 +127,8 @@ def test_sub_tile_gemm_split_cholesky_and_multi_wg_sweep_are_bit_identical(tmp_p
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     res = {}
-    # (MK_TILE, MK_SWEEP, MK_CHOL_SPLIT, MK_PRED_GEN, MK_CHOL_DEPTH, lookahead[, MK_TRSM_REG])
+    # (MK_TILE, MK_SWEEP, MK_CHOL_SPLIT, MK_PRED_GEN, MK_CHOL_DEPTH, lookahead)
     configs = (("128", "1", "0", "0", "2", "1"),
-               ("128", "1", "1", "0", "2", "1", "0"),
-               ("128", "3", "0", "0", "2", "0", "0"),
                ("128", "2", "0", "0", "2", "1"),
                ("128", "2", "0", "0", "2", "0"),
                ("64", "3", "1", "0", "1", "0"),
@@ -145,20 +142,19 @@ def test_sub_tile_gemm_split_cholesky_and_multi_wg_sweep_are_bit_identical(tmp_p
                ("64", "3", "1", "0", "2", "0"),
                ("128", "1", "0", "0", "2", "0"))
     for cfg in configs:
-        tile, sweep, split, gen, depth, la = cfg[:6]
-        reg = cfg[6] if len(cfg) > 6 else "1"    # 0: the two-stage LDS trsm k_chol_trsm<128> instead of k_chol_trsm_r
+        tile, sweep, split, gen, depth, la = cfg
         path = str(tmp_path / ("run_" + "_".join(cfg) + ".npz"))
         r = subprocess.run([sys.executable, os.path.join(here, "gpu_tile_run.py"), path], capture_output=True,
                            text=True, timeout=240,
                            env=dict(os.environ, MK_TILE=tile, MK_SWEEP=sweep, MK_CHOL_SPLIT=split, MK_PRED_GEN=gen,
-                                    MK_CHOL_DEPTH=depth, MK_TRSM_REG=reg,
+                                    MK_CHOL_DEPTH=depth,
                                     **({} if la == "1" else {"MK_LOOKAHEAD": "0"})))
         assert r.returncode == 0, r.stderr[-4000:]
         z = np.load(path)
         res[cfg] = {k: z[k] for k in z.files}
     refs = {"1": res[configs[0]], "0": res[configs[-1]]}
     for cfg, got in res.items():
-        ref = refs[cfg[5]]
+        ref = refs[cfg[-1]]
         assert got.keys() == ref.keys()
         for k in ref:
             assert np.array_equal(got[k], ref[k]), (cfg, k)
