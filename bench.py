@@ -159,9 +159,11 @@ def window_leg(mk, d, idx, S, q, cov, beta0, bt, adapt_batches, warmup, steps):
         ses.run(steps)
         el = time.perf_counter() - t0
         st = ses.kernel_stats(mk.session.KS_UPDATE_BUSY)
+        fb = ses.kernel_stats(mk.session.KS_SWEEP_FALLBACK)["launches"]
         la = ses.lookahead
     tf = st["flops"] / (st["ms"] * 1e-3) / 1e12 if st["ms"] > 0 else 0.0
     return {"value": S * steps / el, "unit": "subset-iters/s", "ms_per_step": el / steps * 1e3,
+            "sweep_fallbacks": fb,   # (subset, iteration) sweeps k_sweep_mg refused admission (k_sweep ran them)
             "window": f"{n_burn} burn-in + {steps - n_burn} kept iterations at {W + 1}-{W + steps} (after {A} "
                       f"adaptation + {W - A} warmup iterations)",
             "schedule": "lookahead" if la else "sequential",

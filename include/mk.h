@@ -151,7 +151,8 @@ int mk_session_tile_grids(mk_session* s, int32_t t0, double* out, int32_t device
  * algorithmic flops per kernel kind (0 Cholesky panel update, 128-tiles; 1 diagonal tile;
  * 2 panel trsm; 3 latent sweep; 4 R^-1 diagonal tiles; 5 whole iterations; 6 inverse levels;
  * 7 panel update, 64/32-sub-tiles; 8 kinds 0 + 7 with overlapping launches counted once;
- * 9 kriging GEMM k_pred_var; 10 candidate covariance assembly).  mk_session_profile(s, enable) before mk_session_run:
+ * 9 kriging GEMM k_pred_var; 10 candidate covariance assembly; 11 latent sweeps the multi-workgroup
+ * kernel refused admission and its fallback ran -- launches = (subset, iteration) count, no timing).  mk_session_profile(s, enable) before mk_session_run:
  * enable 0 = off, 1 = every kind, otherwise a mask with bit (1 + kind) per kind
  * bracketed (e.g. 2 << 0 = the panel update only; fewer events, less overhead). */
 int mk_session_profile(mk_session* s, int32_t enable);

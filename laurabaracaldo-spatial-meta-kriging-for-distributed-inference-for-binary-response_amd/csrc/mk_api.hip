@@ -91,7 +91,7 @@ extern "C" int mk_device_memory(int32_t device, int64_t* free_bytes, int64_t* to
 
 namespace {
 
-constexpr int NKSTAT = 11;
+constexpr int NKSTAT = 12;
 // KS_CHOL_UPDATE: the 128-tile panel-update launches (k_chol_update<128>); KS_CHOL_UPDATE_SUB:
 // the 64- / 32-sub-tile ones (small grids).  Together: the roofline kernel k_chol_update.
 // KS_UPDATE_BUSY: both, with the time of launches that overlap (the split schedule's bulk and
@@ -100,7 +100,9 @@ constexpr int NKSTAT = 11;
 // bound: only the pairs whose factor changed are in the list -- bench_kriging counts exactly).
 // KS_COV: the candidates' covariance assembly (k_cov_candidate, with k_matern_table for Matern).
 enum { KS_CHOL_UPDATE = 0, KS_CHOL_DIAG, KS_CHOL_TRSM, KS_SWEEP, KS_LAUUM, KS_ITER, KS_INV, KS_CHOL_UPDATE_SUB,
-       KS_UPDATE_BUSY, KS_PRED_VAR, KS_COV };
+       KS_UPDATE_BUSY, KS_PRED_VAR, KS_COV, KS_SWEEP_FALLBACK };
+// KS_SWEEP_FALLBACK: launches = (subset, iteration) sweeps k_sweep_mg refused admission and its
+// k_sweep fallback ran (counted on the device, read at the end of every mk_session_run; no timing).
 
 struct Stat {
   long launches = 0;
@@ -385,19 +387,21 @@ struct mk_session {
   std::vector<Group> groups;      // the run-time split, one stream each
   // The latent sweep (launch_sweep).  sweep_site: the one-pass site sweep (default; row pairs per
   // thread, 0: off) with its LDS and lean form; else, for multi-outcome small shards, the split-launch
-  // sweep (sweep_split: no inter-workgroup waits) and -- on the sequential schedule only, through a
-  // cooperative launch, which guarantees co-residency -- the multi-workgroup kernel (sweep_coop);
+  // multi-workgroup kernel behind its admission consensus, k_sweep sweeping the subsets it did not
+  // admit (sweep_coop), or the split-launch sweep (sweep_split: no inter-workgroup waits);
   // else the 64-site-block kernel (k_sweep, one workgroup per subset).
   int sweep_site = 0;
   size_t sweep_site_lds = 0;
   int sweep_lean = 0;             // q = 1: 1 border row by factor, 2 every n_s even (sweep_site_kernel)
   bool sweep_split = false;       // k_sweep_step, one launch per 64-site block
-  bool sweep_coop = false;        // k_sweep_mg by hipLaunchCooperativeKernel (sequential schedule only)
+  bool sweep_coop = false;        // k_sweep_mg (admission consensus) + k_sweep for the subsets not admitted
   size_t sweep_mg_lds = 0;
   double* sp_part = nullptr;
   hipEvent_t swept = nullptr;     // fork-join sweep (several groups): the whole-shard sweep is queued
   double* sw_part = nullptr;
-  int* sw_cnt = nullptr;
+  int* sw_cnt = nullptr;           // [S][n_pad / 64] block counters, then [S] admission words (sw_adm)
+  int* sw_adm = nullptr;
+  int adm_spins = MK_ADM_SPINS;
   int* sw_xcc = nullptr;
   int* sw_err = nullptr;
   double* d_probs = nullptr;
@@ -813,12 +817,12 @@ static void launch_pred_refresh(mk_session* s, Group& g, hipStream_t st = nullpt
 // schedule stays the default there (MK_LOOKAHEAD=1 takes the 0.9 %).
 static bool la_auto(const mk_session* s) { return (long)s->S * s->q <= 224; }
 
-// The cooperative multi-workgroup sweep runs only as a cooperative launch (every workgroup co-resident,
-// guaranteed by the runtime), which HIP does not dispatch beside other queues' work -- so only on the
-// sequential schedule.  Under the lookahead schedule multi-outcome small shards take the split-launch
-// sweep, which never waits across workgroups.  (Round 4 had launched the cooperative kernel plainly
-// beside the candidates' stream, relying on its workgroups becoming resident eventually)
-static bool use_sweep_mg(const mk_session* s) { return s->sweep_coop && !s->la; }
+// The multi-workgroup sweep is a plain launch on either schedule: its admission consensus
+// (k_sweep_mg) sweeps a subset only once all its workgroups are resident, and the k_sweep launch
+// queued behind it sweeps the rest -- no wait depends on co-residency the hardware does not give.
+// (Round 4 had relied on the workgroups becoming resident eventually; round 5's first answer ran the
+// kernel only as a cooperative launch, i.e. not beside the lookahead schedule's other streams.)
+static bool use_sweep_mg(const mk_session* s) { return s->sweep_coop; }
 
 static void launch_sweep(mk_session* s, Group& g, int it) {
   const int q = s->q;
@@ -832,15 +836,25 @@ static void launch_sweep(mk_session* s, Group& g, int it) {
                         s->sweep_site_lds, g.stream);
     wd_trace(g.stream, "k_sweep_site");
   } else if (use_sweep_mg(s)) {
-    hipMemsetAsync(s->sw_cnt, 0, (size_t)g.S * (s->n_pad / 64) * sizeof(int), g.stream);
+    hipMemsetAsync(s->sw_cnt, 0, (size_t)s->S * (s->n_pad / 64 + 1) * sizeof(int), g.stream);   // g: the whole shard
     double* part = s->sw_part;
     int* cnt = s->sw_cnt;
     int* xcc = s->sw_xcc;
     int* err = s->sw_err;
-    void* args[] = {&md, &ms, &iter, &part, &cnt, &xcc, &err};
-    e = hipLaunchCooperativeKernel(sweep_kernel(q, true), dim3(xcd_grid(g.S, s->nt)), dim3(256), args,
-                                   (unsigned)s->sweep_mg_lds, g.stream);
+    int* adm = s->sw_adm;
+    int spins = s->adm_spins;
+    void* args[] = {&md, &ms, &iter, &part, &cnt, &xcc, &err, &adm, &spins};
+    e = hipLaunchKernel(sweep_kernel(q, true), dim3(xcd_grid(g.S, s->nt)), dim3(256), args, s->sweep_mg_lds,
+                        g.stream);
     wd_trace(g.stream, "k_sweep_mg");
+    if (e == hipSuccess) {   // the subsets k_sweep_mg did not admit (normally none: every workgroup returns at once)
+      const size_t sw_lds = (size_t)q * (64 * 64 + 2 * 64) * sizeof(double);
+      const int* cadm = adm;
+      int* fb = s->sw_err + 1;
+      void* fa[] = {&md, &ms, &iter, &cadm, &fb};
+      e = hipLaunchKernel(sweep_kernel(q, false), dim3(g.S), dim3(MK_SW_T), fa, sw_lds, g.stream);
+      wd_trace(g.stream, "k_sweep(fallback)");
+    }
   } else if (s->sweep_split) {   // one launch per 64-site block, ordered by the stream (no waits on the device)
     int nmax = 1;
     for (int i = g.s0; i < g.s0 + g.S; ++i) nmax = std::max(nmax, s->n_part[i]);
@@ -854,7 +868,9 @@ static void launch_sweep(mk_session* s, Group& g, int it) {
     }
   } else {
     const size_t sw_lds = (size_t)q * (64 * 64 + 2 * 64) * sizeof(double);
-    void* args[] = {&md, &ms, &iter};
+    const int* adm = nullptr;
+    int* fb = nullptr;
+    void* args[] = {&md, &ms, &iter, &adm, &fb};
     e = hipLaunchKernel(sweep_kernel(q, false), dim3(g.S), dim3(MK_SW_T), args, sw_lds, g.stream);
     wd_trace(g.stream, "k_sweep");
   }
@@ -1330,13 +1346,13 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
   }
   // ---------------- the latent sweep (launch_sweep)
   // MK_SWEEP (tests and measurements): 1 the 64-site-block kernel (k_sweep: the fallback for subsets
-  // too large for the site sweep), 2 the cooperative multi-workgroup kernel where a cooperative launch
-  // fits (sequential schedule; split launches under the lookahead schedule), 3 split launches.
+  // too large for the site sweep), 2 the multi-workgroup kernel (k_sweep_mg + the k_sweep fallback;
+  // where its grid fits the chip at once, else split launches), 3 split launches.
   // 0 (default): the one-pass site sweep (k_sweep_site; W read once, no Q_BB tiles, no inter-workgroup
   // waits) wherever it fits -- n_pad <= 4096 (q = 4: not instantiated) and the sites' data in LDS
   // (configs[3]: n_s = 2,000, q = 3 takes 152 KB) -- except multi-outcome small shards (q >= 2, <= 16
   // subsets: one workgroup per subset is the iteration's longest chain there), which take the
-  // cooperative kernel on the sequential schedule and split launches on the lookahead schedule.
+  // multi-workgroup kernel on either schedule.
   // Measured (subset-iters/s, 40-step windows, profiles/r04/knobs, r04e): configs[2] 250 subsets block
   // sweep 10,143 / site pair 10,527; configs[1] 15,198 / 15,626; configs[3] (q = 3, 50 subsets) block
   // 3,016 / site 3,106; configs[3]'s 7-subset share split launches 1,476 / site 1,340 / block 1,107
@@ -1348,19 +1364,19 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
     s->sweep_mg_lds = (size_t)q * (64 * 64 + 2 * 64) * 8 + 4 * MK_NB * 8;
     const void* fn = sweep_kernel(q, true);
     HIPCHK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)s->sweep_mg_lds));
-    int per_cu = 0, n_cu = 0, coop = 0;
+    int per_cu = 0, n_cu = 0;
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, s->sweep_mg_lds));
     HIPCHK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, c->device));
-    HIPCHK(hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, c->device));
     const int mode = tile_env("MK_SWEEP", 0);
-    const bool coop_fits = coop && (long)xcd_grid(S, nt) <= (long)per_cu * n_cu && nt <= 32;
+    // the whole grid fits the chip at once (else admission would mostly fall back)
+    const bool coop_fits = (long)xcd_grid(S, nt) <= (long)per_cu * n_cu && nt <= 32;
     const bool small_multi = q >= 2 && S <= 16;
     const bool site_fits = sweep_site_kernel(q, n_pad <= 8 * MK_SS_T ? 1 : 2) != nullptr && n_pad <= 16 * MK_SS_T &&
                            sweep_site_lds_bytes(nmax, q, q == 1) <= 156 * 1024;
     const bool site = mode == 0 && !small_multi && site_fits;
     const bool multi = (mode == 0 && !site && small_multi) || mode == 2 || mode == 3;
     s->sweep_coop = multi && mode != 3 && coop_fits;
-    s->sweep_split = multi && nt <= 32;   // k_sweep_step sums <= 32 tile partials
+    s->sweep_split = multi && !s->sweep_coop && nt <= 32;   // k_sweep_step sums <= 32 tile partials
     if (site) {
       s->sweep_site = n_pad <= 8 * MK_SS_T ? 1 : 2;
       bool all_even = true;
@@ -1376,10 +1392,13 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
       if ((rc = s->alloc(&s->sp_part, (size_t)S * 2 * nt * q * 64))) return rc;
     }
     if (s->sweep_coop) {
-      if ((rc = s->alloc(&s->sw_part, (size_t)S * 2 * nt * q * 64)) || (rc = s->alloc(&s->sw_cnt, (size_t)S * (n_pad / 64))) ||
-          (rc = s->alloc(&s->sw_xcc, (size_t)S * nt)) || (rc = s->alloc(&s->sw_err, 1)))
+      if ((rc = s->alloc(&s->sw_part, (size_t)S * 2 * nt * q * 64)) ||
+          (rc = s->alloc(&s->sw_cnt, (size_t)S * (n_pad / 64 + 1))) || (rc = s->alloc(&s->sw_xcc, (size_t)S * nt)) ||
+          (rc = s->alloc(&s->sw_err, 2)))
         return rc;
-      HIPCHK(hipMemsetAsync(s->sw_err, 0, sizeof(int), s->stream));
+      s->sw_adm = s->sw_cnt + (size_t)S * (n_pad / 64);
+      s->adm_spins = tile_env("MK_ADM_SPINS", MK_ADM_SPINS);
+      HIPCHK(hipMemsetAsync(s->sw_err, 0, 2 * sizeof(int), s->stream));
     }
   }
   MatSet& ms = s->ms;
@@ -1603,13 +1622,17 @@ extern "C" int mk_session_run(mk_session* s, int32_t n_iter) {
   if (s->la_c) HIPCHK(hipStreamSynchronize(s->la_c));   // the next iteration's candidates
   if (s->la_k) HIPCHK(hipStreamSynchronize(s->la_k));
   if (s->sweep_coop) {
-    // the cooperative sweep's own checks (a subset split over XCDs, a barrier time-out): its chain
-    // state is then not the sampler's -- the session is poisoned, every later call on it fails
-    int e = 0;
-    HIPCHK(hipMemcpy(&e, s->sw_err, sizeof(int), hipMemcpyDeviceToHost));
-    if (e) {
-      s->poisoned = e & 2 ? "latent sweep: a subset's workgroups ran on different XCDs (MK_SWEEP=3 avoids the kernel)"
-                          : "latent sweep: workgroup barrier timed out";
+    // the multi-workgroup sweep's barrier time-out (after admission every wait completes: this is the
+    // net under that argument): its chain state is then not the sampler's -- the session is
+    // poisoned, every later call on it fails
+    int e[2] = {0, 0};
+    HIPCHK(hipMemcpy(e, s->sw_err, 2 * sizeof(int), hipMemcpyDeviceToHost));
+    if (e[1]) {
+      s->stats[KS_SWEEP_FALLBACK].launches += e[1];
+      HIPCHK(hipMemset(s->sw_err + 1, 0, sizeof(int)));
+    }
+    if (e[0]) {
+      s->poisoned = "latent sweep: workgroup barrier timed out (MK_SWEEP=3 avoids the kernel)";
       return set_err(MK_E_HIP, s->poisoned);
     }
   }

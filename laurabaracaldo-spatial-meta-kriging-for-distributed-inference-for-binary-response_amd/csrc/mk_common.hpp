@@ -11,6 +11,11 @@
 #define MK_NB 128          // Cholesky / GEMM tile edge (fp64)
 #define MK_SS_T 256        // threads of the site sweep workgroup (k_sweep_site: one wave per SIMD)
 #define MK_SW_T 1024       // threads of the latent-w sweep workgroup (one per subset): loads in flight for the W panels
+// k_sweep_mg's per-subset admission word: arrival count | aborted | swept (k_sweep's fallback skips it)
+constexpr int MK_ADM_COUNT = 0xffff, MK_ADM_ABORT = 1 << 16, MK_ADM_DONE = 1 << 17;
+// bounded admission wait: ~2^15 x s_sleep 2 (~128 cycles) ~ 2 ms -- above the other streams' longest
+// kernels at small shards, which the sweep's missing workgroups may wait behind for CUs
+constexpr int MK_ADM_SPINS = 1 << 15;   // MK_ADM_SPINS overrides (tests: 0 sends some subsets to the fallback, -1 all)
 // dynamic LDS of the LDS-DMA GEMM (k_chol_update): 2 stages x (A, B) x 16 k-rows x 144 doubles
 #define MK_GD_LDS_BYTES (2 * 2 * 16 * 144 * 8)
 #define MK_CAND_NOBORDER 4  // k_cov_candidate `which` flag: no bordered row (lookahead schedule)

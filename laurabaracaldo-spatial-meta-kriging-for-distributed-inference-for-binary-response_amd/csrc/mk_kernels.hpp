@@ -49,9 +49,9 @@ __global__ void k_Aphase(Model md, int iter);
 __global__ void k_theta_mh(Model md, MatSet ms, int h0, int hc, int which, int iter);
 __global__ void k_dirty_list(Model md, int force, int* list_inv, int* count_inv, int* list_pred, int* count_pred);
 template <int Q>
-__global__ void k_sweep(Model md, MatSet ms, int iter);
+__global__ void k_sweep(Model md, MatSet ms, int iter, const int* adm, int* fb);
 template <int Q>
-__global__ void k_sweep_mg(Model md, MatSet ms, int iter, double* part, int* cnt, int* xcc, int* err);
+__global__ void k_sweep_mg(Model md, MatSet ms, int iter, double* part, int* cnt, int* xcc, int* err, int* adm, int spins_max);
 template <int Q, int KR, int P, int HH, int LN>
 __global__ void k_sweep_site(Model md, MatSet ms, int iter);
 // its dynamic LDS: the sites' proposal / likelihood difference / accept draw + the accept flags

@@ -487,10 +487,17 @@ __device__ inline void sweep_apply(const Model& md, int s, int i0, int i1, const
   }
 }
 
+// adm (optional): the multi-workgroup sweep's admission words; subsets it swept (MK_ADM_DONE) are
+// skipped, so this launch is the fallback for the subsets it did not admit (same bits, §4.3); fb counts them.
 template <int Q>
-__global__ __launch_bounds__(SW_T) void k_sweep(Model md, MatSet ms, int iter) {
+__global__ __launch_bounds__(SW_T) void k_sweep(Model md, MatSet ms, int iter, const int* __restrict__ adm,
+                                                int* __restrict__ fb) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   constexpr int q = Q;
+  if (adm) {
+    if (adm[blockIdx.x] & MK_ADM_DONE) return;
+    if (threadIdx.x == 0) atomicAdd(fb, 1);   // KS_SWEEP_FALLBACK
+  }
   double* Qb = smem;                              // [q][SW_B*SW_B] column-major
   double* gb = smem + q * SW_B * SW_B;            // [q][SW_B]
   double* dacc = gb + q * SW_B;                   // [q][SW_B]
@@ -593,8 +600,18 @@ __global__ __launch_bounds__(SW_T) void k_sweep(Model md, MatSet ms, int iter) {
   sweep_apply(md, s, 0, ns, Ai, tid, SW_T);
 }
 
-// Multi-workgroup sweep (small shards).  Grid: xcd_grid(S, nt) workgroups of 256 threads,
-// cooperative (all co-resident); workgroup (s, t) owns rows [128t, 128t + 128) of subset s
+// Multi-workgroup sweep (small shards).  Grid: xcd_grid(S, nt) workgroups of 256 threads, a plain
+// launch.  ADMISSION (before any chain state is touched): every workgroup of subset s arrives on
+// the subset's admission word adm[s] (release) and waits -- bounded -- until all tl + 1 of them have
+// arrived; a workgroup that times out marks the subset aborted (compare-and-swap, only while the
+// count is short), and a late arrival that finds the mark leaves.  The decision is a consensus: every
+// workgroup of s reads the same word.  Admitted, the subset's workgroups are co-resident -- a resident
+// workgroup is never descheduled -- so every later wait among them completes; they also check that
+// they share one XCD (the L2 exchange below needs it) and tile 0 marks the subset MK_ADM_DONE.  A
+// subset not admitted leaves its state untouched and the next launch on the stream, k_sweep with
+// adm, sweeps it (the same bits: the shared summation order below).  So no wait here depends on
+// co-residency the hardware does not give, under any schedule (round 4 had relied on it).
+// Workgroup (s, t) owns rows [128t, 128t + 128) of subset s
 // (its z rows in registers, replicated in the four waves; its sites' proposals and final
 // moves) and takes part in blocks b0 < min(n_s, 128t + 128).  Per block: partial dots of its
 // tile for every column (wave w: columns w + 4j, lane l: rows 2l, 2l+1) into part[s][B & 1][t],
@@ -602,8 +619,8 @@ __global__ __launch_bounds__(SW_T) void k_sweep(Model md, MatSet ms, int iter) {
 // tile order, run the MH steps, update z from the same registers.  REG (q == 1): the panel
 // stays in registers across the wait; else it is reloaded for the update.  The partial dots and
 // the sites' proposals move through the subset's XCD L2 (ld_l2); the counters are atomics.  A
-// barrier wait gives up after ~2^22 sleeps (err |= 1) and a subset split over XCDs sets err |= 2;
-// the host reports either, and every wave always exits.
+// barrier wait gives up after ~2^22 sleeps (err |= 1: the net under the admission argument; the host
+// poisons the session) and every wave always exits; a subset split over XCDs is refused at admission.
 // Q_BB of the block at b0 (q 64 x 64 column-major tiles of R_h^-1) straight into LDS by
 // LDS-DMA: one wave instruction moves two columns (lanes 0-31 column 2j, 32-63 column 2j+1),
 // no registers; completion is covered by the s_waitcnt before the next barrier arrival.  Entries
@@ -634,7 +651,8 @@ namespace mk {
 #endif
 template <int Q>
 __global__ __launch_bounds__(256) void k_sweep_mg(Model md, MatSet ms, int iter, double* __restrict__ part,
-                                                  int* __restrict__ cnt, int* __restrict__ xcc, int* __restrict__ err) {
+                                                  int* __restrict__ cnt, int* __restrict__ xcc, int* __restrict__ err,
+                                                  int* __restrict__ adm, int spins_max) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   constexpr int q = Q;
   constexpr bool REG = (Q == 1);
@@ -644,7 +662,7 @@ __global__ __launch_bounds__(256) void k_sweep_mg(Model md, MatSet ms, int iter,
   double* dacc = gb + q * SW_B;                   // [q][SW_B]
   double* red = dacc + q * SW_B;                  // [4][MK_NB] per-wave update sums
   __shared__ double Ai[MK_QMAX * MK_QMAX];
-  __shared__ int any_acc;
+  __shared__ int any_acc, admitted;
   // block map: block b runs on XCD b % 8 (the dispatch order every kernel here relies on); subset
   // s takes slots (s / 8) * nt ... of XCD s % 8, so all of its tiles share one L2
   const int j = blockIdx.x >> 3;
@@ -653,12 +671,41 @@ __global__ __launch_bounds__(256) void k_sweep_mg(Model md, MatSet ms, int iter,
   const int ns = md.n_s[s];
   const int tl = (ns - 1) / MK_NB;
   if (t > tl) return;                             // rows >= n_s only: no sites, no dots
-  // the exchange through L2 is sound only if the subset's workgroups share an XCD: each
-  // publishes its XCC id (device-coherent atomic), checked against the others after block 0
+  // the exchange through L2 is sound only if the subset's workgroups share an XCD: each publishes
+  // its XCC id before it arrives, and the admitted ones compare them
   const unsigned my_xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);   // hwreg(HW_REG_XCC_ID, 0, 4)
-  if (threadIdx.x == 0)
-    __hip_atomic_store(xcc + (long)s * nt + t, (int)my_xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (tid == 0) {
+    __hip_atomic_store(xcc + (long)s * nt + t, (int)my_xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int target = tl + 1;
+    int* a = adm + s;
+    int v = __hip_atomic_fetch_add(a, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) + 1;
+    int ok = 0;
+    for (int spins = 0; spins_max >= 0; ++spins) {   // spins_max < 0 (tests): refuse every subset
+      if (v & MK_ADM_ABORT) break;
+      if ((v & MK_ADM_COUNT) == target) {
+        ok = 1;
+        break;
+      }
+      if (spins >= spins_max) {   // give up on this subset unless the count completed meanwhile
+        int expected = v;
+        if (__hip_atomic_compare_exchange_strong(a, &expected, v | MK_ADM_ABORT, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE,
+                                                 __HIP_MEMORY_SCOPE_AGENT))
+          break;
+        v = expected;
+        continue;
+      }
+      __builtin_amdgcn_s_sleep(2);
+      v = __hip_atomic_load(a, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (ok)   // every id was published before its arrival (release), this read follows all of them
+      for (int u = 0; u <= tl; ++u)
+        if (__hip_atomic_load(xcc + (long)s * nt + u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != (int)my_xcc) ok = 0;
+    if (ok && t == 0) __hip_atomic_fetch_or(a, MK_ADM_DONE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    admitted = ok;
+  }
+  __syncthreads();
+  if (!admitted) return;   // nothing written yet: k_sweep (adm) sweeps this subset
   const long ld = ms.ld;
   const int r0 = MK_NB * t + 2 * lane;            // this lane's rows r0, r0 + 1
   if (tid < q * q) Ai[tid] = md.Ainv[(long)s * q * q + tid];
@@ -715,10 +762,6 @@ __global__ __launch_bounds__(256) void k_sweep_mg(Model md, MatSet ms, int iter,
     }
     __syncthreads();
     SW_STAMP(B, 3);
-    if (B == 0 && threadIdx.x <= tl) {              // every tile of the subset has arrived: same XCD?
-      const int other = __hip_atomic_load(xcc + (long)s * nt + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (other != (int)my_xcc) __hip_atomic_fetch_or(err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
     // ---- dots: partials of tiles tf .. tl summed in tile order (every workgroup, same bits);
     // L1-bypassing loads, all issued before the adds
     for (int e = tid; e < q * SW_B; e += 256) {
@@ -942,14 +985,14 @@ __global__ __launch_bounds__(256) void k_sweep_step(Model md, MatSet ms, int ite
   }
 }
 
-template __global__ void k_sweep<1>(Model, MatSet, int);
-template __global__ void k_sweep<2>(Model, MatSet, int);
-template __global__ void k_sweep<3>(Model, MatSet, int);
-template __global__ void k_sweep<4>(Model, MatSet, int);
-template __global__ void k_sweep_mg<1>(Model, MatSet, int, double*, int*, int*, int*);
-template __global__ void k_sweep_mg<2>(Model, MatSet, int, double*, int*, int*, int*);
-template __global__ void k_sweep_mg<3>(Model, MatSet, int, double*, int*, int*, int*);
-template __global__ void k_sweep_mg<4>(Model, MatSet, int, double*, int*, int*, int*);
+template __global__ void k_sweep<1>(Model, MatSet, int, const int*, int*);
+template __global__ void k_sweep<2>(Model, MatSet, int, const int*, int*);
+template __global__ void k_sweep<3>(Model, MatSet, int, const int*, int*);
+template __global__ void k_sweep<4>(Model, MatSet, int, const int*, int*);
+template __global__ void k_sweep_mg<1>(Model, MatSet, int, double*, int*, int*, int*, int*, int);
+template __global__ void k_sweep_mg<2>(Model, MatSet, int, double*, int*, int*, int*, int*, int);
+template __global__ void k_sweep_mg<3>(Model, MatSet, int, double*, int*, int*, int*, int*, int);
+template __global__ void k_sweep_mg<4>(Model, MatSet, int, double*, int*, int*, int*, int*, int);
 #define MK_INST_STEP(Q) template __global__ void k_sweep_step<Q>(Model, MatSet, int, int, double*);
 MK_INST_STEP(1)
 MK_INST_STEP(2)

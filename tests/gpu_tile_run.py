@@ -1,6 +1,7 @@
 """Helper run as a subprocess by tests/test_gpu_linalg.py (not a test module): a short chain
 under the code paths the environment forces (MK_TILE, MK_SWEEP, MK_CHOL_SPLIT, MK_CHOL_DEPTH, MK_PRED_GEN; read once per process), outputs
-saved to the .npz named on the command line."""
+saved to the .npz named on the command line; the latent sweeps k_sweep_mg refused admission (its
+k_sweep fallback ran) are counted into <path>.fallback."""
 import importlib
 import os
 import sys
@@ -15,6 +16,7 @@ PKG = "laurabaracaldo-spatial-meta-kriging-for-distributed-inference-for-binary-
 def main(path):
     mk = importlib.import_module(PKG)
     out = {}
+    fallback = 0
     for q, sizes, cov in ((1, [700, 640, 333], 0), (2, [300, 257], 0), (1, [500, 260], 1)):
         d = mk.synthetic.generate(sum(sizes), q=q, n_test=300, seed=71 + q + cov, cov_model=cov)
         p = 2 * q
@@ -27,6 +29,7 @@ def main(path):
             off += m
         with mk.Session(subs, cfg, coords_test=d["coords_test"], record_w=True) as ses:
             ses.run(cfg.n_samples)
+            fallback += ses.kernel_stats(mk.session.KS_SWEEP_FALLBACK)["launches"]
             o = ses.outputs(samples=True, w_samples=True, w_pred_samples=True)
         for s in range(len(sizes)):
             out[f"q{q}c{cov}_samples_{s}"] = o["samples"][s]
@@ -49,6 +52,8 @@ def main(path):
                                           for _ in range(2)]), inverse=False)
     out["chol_L"], out["chol_ld"] = L, ld
     np.savez(path, **out)
+    with open(path + ".fallback", "w") as f:
+        f.write(str(fallback))
 
 
 if __name__ == "__main__":

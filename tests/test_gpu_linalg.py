@@ -115,9 +115,10 @@ def test_sub_tile_gemm_split_cholesky_and_multi_wg_sweep_are_bit_identical(tmp_p
     split two-stream Cholesky schedule (bulk update by panels < k-d on a CU-masked stream, the
     rank-128d correction on the critical stream; the accumulator passes through fp64 memory) at
     depths 1-3, the 64-site-block sweeps -- one workgroup per subset (MK_SWEEP=1, k_sweep), the
-    split launches (3: k_sweep_step, one launch per block) and the cooperative multi-workgroup kernel
-    (2: k_sweep_mg through a cooperative launch on the sequential schedule; split launches under the
-    lookahead schedule) -- and the kriging GEMM with P^T generated in LDS (MK_PRED_GEN=1,
+    split launches (3: k_sweep_step, one launch per block) and the multi-workgroup kernel (2:
+    k_sweep_mg behind its admission consensus, on both schedules; MK_ADM_SPINS=0 refuses the subsets
+    whose workgroups do not arrive together, -1 every subset, and the k_sweep fallback queued behind
+    it sweeps them) -- and the kriging GEMM with P^T generated in LDS (MK_PRED_GEN=1,
     exponential model) against the stored-P^T path.  Chains, latent w, kriging draws and a plain
     factorisation, each configuration forced in its own process (the MK_* switches are read once
     per process); the two launch schedules agree to rounding, not bit for bit, so each configuration
@@ -141,20 +142,26 @@ def test_sub_tile_gemm_split_cholesky_and_multi_wg_sweep_are_bit_identical(tmp_p
                ("64", "2", "1", "0", "3", "0"),
                ("64", "3", "1", "0", "2", "0"),
                ("128", "1", "0", "0", "2", "0"))
-    for cfg in configs:
+    runs = [(cfg, {}) for cfg in configs] + [(("128", "2", "0", "0", "2", "1"), {"MK_ADM_SPINS": "0"}),
+                                              (("64", "2", "1", "0", "3", "0"), {"MK_ADM_SPINS": "-1"}),
+                                              (("128", "2", "0", "0", "2", "1"), {"MK_ADM_SPINS": "-1"})]
+    for cfg, extra in runs:
         tile, sweep, split, gen, depth, la = cfg
-        path = str(tmp_path / ("run_" + "_".join(cfg) + ".npz"))
+        key = cfg + tuple("adm" + v for v in extra.values())
+        path = str(tmp_path / ("run_" + "_".join(key) + ".npz"))
         r = subprocess.run([sys.executable, os.path.join(here, "gpu_tile_run.py"), path], capture_output=True,
                            text=True, timeout=240,
                            env=dict(os.environ, MK_TILE=tile, MK_SWEEP=sweep, MK_CHOL_SPLIT=split, MK_PRED_GEN=gen,
-                                    MK_CHOL_DEPTH=depth,
+                                    MK_CHOL_DEPTH=depth, **extra,
                                     **({} if la == "1" else {"MK_LOOKAHEAD": "0"})))
         assert r.returncode == 0, r.stderr[-4000:]
         z = np.load(path)
-        res[cfg] = {k: z[k] for k in z.files}
+        res[key] = {k: z[k] for k in z.files}
+        if extra.get("MK_ADM_SPINS") == "-1":   # the fallback did run (with 0 it depends on arrival timing)
+            assert int(open(path + ".fallback").read()) > 0, key
     refs = {"1": res[configs[0]], "0": res[configs[-1]]}
     for cfg, got in res.items():
-        ref = refs[cfg[-1]]
+        ref = refs[cfg[5]]
         assert got.keys() == ref.keys()
         for k in ref:
             assert np.array_equal(got[k], ref[k]), (cfg, k)
