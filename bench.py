@@ -316,6 +316,21 @@ def launcher_cmd(a, argv, port):
             "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
 
 
+class _stdout_to_stderr:
+    """fd 1 -> fd 2 for a block: process-group setup prints its connection lines ("[Gloo] Rank 0 is
+    connected to ...") from C++ onto stdout, where rank 0's one JSON line must stand alone."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+
+
 def _free_port():
     import socket
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s_:
@@ -359,6 +374,12 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # MK_BENCH_REHEARSE=1 (one-GPU boxes only): every rank on device 0, the process group on gloo, no
+    # end-to-end leg -- runs the N-rank code path (launcher, sharding, barriers, max-over-ranks) where
+    # only one GPU exists; the numbers are not a scaling measurement (the ranks share one GPU)
+    rehearse = os.environ.get("MK_BENCH_REHEARSE") == "1" and world > 1
+    if rehearse:
+        local, a.no_e2e = 0, True
     K, n, n_test = a.subsets, a.n, a.n_test
     want_cpu = rank == 0 and world == 1 and not a.no_cpu_baseline
     host = host_cores() if want_cpu else None
@@ -368,8 +389,10 @@ def main():
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", rank=rank, world_size=world)
-        cpu_group = dist.new_group(backend="gloo")   # waits that must not hold a GPU kernel
+        with _stdout_to_stderr():
+            dist.init_process_group("gloo" if rehearse else "nccl", rank=rank, world_size=world)
+            cpu_group = dist.new_group(backend="gloo")   # waits that must not hold a GPU kernel
+            dist.barrier()                               # the backend's communicator is created here
         if dist.get_world_size() != a.gpus:
             raise SystemExit(f"bench.py: torch.distributed sees {dist.get_world_size()} ranks, --gpus {a.gpus}")
     ranks_seen = dist.get_world_size() if dist is not None else 1
@@ -425,7 +448,7 @@ def main():
     elapsed = t1 - t0
     if dist is not None:
         import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if rehearse else "cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -435,6 +458,7 @@ def main():
     # bulk and correction updates of a panel concurrently on two streams; each moment counts once
     st = ses.kernel_stats(mk.session.KS_UPDATE_BUSY)
     summed_ms = sts[0]["ms"] + sts[1]["ms"]
+    sweep_fallbacks = ses.kernel_stats(mk.session.KS_SWEEP_FALLBACK)["launches"]
     # per-kernel breakdown: a separate untimed pass of n_post (kept) iterations, every kind evented
     kinds = [("chol_update", 0), ("chol_update_sub", 7), ("chol_diag", 1), ("chol_trsm", 2), ("w_sweep", 3),
              ("qblocks", 4), ("inverse", 6), ("cov_candidate", 10)]
@@ -490,6 +514,8 @@ def main():
         "n_gpus": world,
         # what actually ran: the ranks torch.distributed saw (RCCL backend) and who started them
         "ranks_seen": ranks_seen,
+        **({"rehearsal": "MK_BENCH_REHEARSE: every rank on GPU 0, gloo process group -- not a scaling measurement"}
+           if rehearse else {}),
         "launcher": os.environ.get("MK_BENCH_LAUNCHER", "external torch.distributed.run" if world > 1 else "none"),
         "steps": a.steps,
         "warmup": W - A,
@@ -522,6 +548,7 @@ def main():
                                      "(lookahead schedule, DESIGN.md 4.2): their union interval includes time "
                                      "shared with those kernels, so frac understates the kernel's own rate"
                                      if la else "update launches run alone on the stream (sequential schedule)")},
+        "sweep_fallbacks": sweep_fallbacks,   # multi-workgroup sweep only: subsets refused admission
         "kernels_ms_per_step": {k: v["ms"] / n_post for k, v in kern.items()},
         "kernels_ms_per_step_note": f"untimed post-window pass of {n_post} iterations, every kernel kind evented",
         # the HBM-bound sub-phases in GB/s, on algorithmic bytes per subset-iteration --

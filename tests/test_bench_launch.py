@@ -77,3 +77,14 @@ def test_world_size_contradicting_gpus_fails(monkeypatch):
     monkeypatch.setenv("WORLD_SIZE", "2")
     with pytest.raises(SystemExit, match="--gpus 1"):
         m.self_launch(_args(m, []), [])
+
+
+def test_process_group_setup_output_stays_off_stdout(capfd):
+    """Rank 0's JSON line must be alone on stdout: what C++ prints to fd 1 while the process groups
+    are set up ("[Gloo] Rank 0 is connected to ...") goes to stderr."""
+    m = _bench()
+    with m._stdout_to_stderr():
+        os.write(1, b"[Gloo] Rank 0 is connected to 1 peer ranks.\n")
+    print('{"metric": 1}')
+    out, err = capfd.readouterr()
+    assert out == '{"metric": 1}\n' and "[Gloo]" in err
