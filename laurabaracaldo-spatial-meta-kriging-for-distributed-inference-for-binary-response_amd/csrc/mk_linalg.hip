@@ -350,6 +350,104 @@ template __global__ void k_chol_trsm<128>(MatSet, int, int, int, int, int, int, 
 template __global__ void k_chol_trsm<64>(MatSet, int, int, int, int, int, int, const int*, const int*);
 template __global__ void k_chol_trsm<32>(MatSet, int, int, int, int, int, int, const int*, const int*);
 
+// Column k's update with the panel solve in its epilogue (sequential schedule, 128-tiles):
+//   jobs t < ntk: tile i = ia + t (ia = k + 1): C(i,k) -= sum_{j<k} L(i,j) L(k,j)^T (k_chol_update's
+//     MFMA sequence, in the row-wave form: wave w holds rows 32w.. of all 128 columns), then
+//     L(i,k) = C(i,k) Winv_k^T straight from the accumulator (k_chol_trsm's sequence: chunks of 16
+//     in order from zero, the same fragment values) -- C(i,k) never goes through HBM between the two,
+//     and every wave solves its own rows: the same triangular work on all four SIMDs;
+//   job t = ntk (when i = k + 1 < nt): the next diagonal tile's update by panels [0, k), stored
+//     partial; its correction by panel k (k_chol_update, accumulator from memory) follows the
+//     launch, then its factor -- so Winv_k exists before this launch starts.
+// Same per-element sequences as U(k), T(k): same bits (tests/test_gpu_linalg.py).
+// Epilogue: the accumulator's block (bm, c), k-step r is chunk c's A fragment, in registers; the
+// output accumulates 32 columns at a time (the kernel stays within the 256 registers of two
+// workgroups per CU).
+__global__ __launch_bounds__(256, 2) void k_chol_update_trsm(MatSet ms, int S, int h0, int hc, int k, int ia, int ib,
+                                                            const int* slist, const int* scount) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];   // gb_lds_bytes(128, 128)
+  const int ntk = ib - ia;
+  const int extra = ia < ms.nt ? 1 : 0;   // the next diagonal tile's partial update
+  int e, t, s, h;
+  if (!xcd_map(active_pairs(slist, scount, S, hc), ntk + extra, &e, &t) ||
+      !pick_pair(slist, scount, e, h0, hc, &s, &h))
+    return;
+  const int sh = s * ms.q + h;
+  const int slot = 1 - ms.cur[sh];
+  double* M = mat_slot(ms, sh, slot);
+  const long ld = ms.ld;
+  if (t == ntk) {   // tile (ia, ia) of column ia, panels [0, k)
+    double* C = M + ia * MK_NB + (long)ia * MK_NB * ld;
+    Acc acc;
+    acc_load(acc, C, ld);
+    gemm_tile<128, 128, true, true, true>(M + ia * MK_NB, ld, M + ia * MK_NB, ld, k * MK_NB, k * MK_NB, acc, lds);
+    store_tile(C, ld, acc);
+    return;
+  }
+  const int i = ia + t;
+  double* C = M + i * MK_NB + (long)k * MK_NB * ld;
+  AccRW c;
+  acc_load_rw(c, C, ld);
+  gemm_tile_rw<true>(M + i * MK_NB, ld, M + k * MK_NB, ld, k * MK_NB, c, lds);   // ends with a barrier
+  // opaque copies: the output addresses are computed here, not hoisted over the main loop beside
+  // the accumulator (the compiler would otherwise keep acc_load's 64 addresses live for the stores)
+  double* Co = C;
+  long ldo = ld;
+  asm volatile("" : "+s"(Co), "+s"(ldo));
+  const double* Wt = winv_slot(ms, sh, slot, k);   // op(B)(j, n) = Wt[j * 128 + n]
+  // four passes of 32 output columns, P = 3, 0, 2, 1 (pass P: n-blocks 2P, 2P+1, chunks 0 .. 2P+1);
+  // each pass's 16 x 32 slices of Winv_k^T arrive by LDS-DMA while the previous pass multiplies
+  // (buffers: passes 3, 2 at lds, passes 0, 1 behind pass 3's 48 KiB)
+  constexpr int IMG = gb_img(32);
+  auto issue = [&](int P, double* buf) {   // a rolled loop: one chunk's addresses live at a time
+#pragma nounroll
+    for (int ch = 0; ch < 2 * P + 2; ++ch) dma_chunk<true, 32>(Wt + 32 * P, MK_NB, GB_K * ch, buf + ch * IMG);
+  };
+  double* bufA = lds;
+  double* bufB = lds + 8 * IMG;
+  issue(3, bufA);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
+#pragma unroll
+  for (int idx = 0; idx < 4; ++idx) {
+    const int P = idx == 0 ? 3 : (idx == 1 ? 0 : (idx == 2 ? 2 : 1));
+    const double* buf = (idx & 1) ? bufB : bufA;
+    if (idx < 3) {
+      const int Pn = idx == 0 ? 0 : (idx == 1 ? 2 : 1);
+      issue(Pn, (idx & 1) ? bufA : bufB);
+    }
+    AccT<2, 2> o;
+    acc_zero(o);
+#pragma unroll
+    for (int ch = 0; ch < 8; ++ch) {
+      if (ch >= 2 * P + 2) break;
+#pragma unroll
+      for (int ks = 0; ks < GB_K / 4; ++ks) {
+        const int kk = ks * 4 + lk;
+        double xb[2];
+#pragma unroll
+        for (int b = 0; b < 2; ++b) xb[b] = frag<true, 32>(buf + ch * IMG, b * 16 + li, kk);
+#pragma unroll
+        for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+          for (int b = 0; b < 2; ++b) {
+            if (ch > 2 * P + b) continue;   // Winv(n, j) = 0 for j > n (k_chol_trsm's SKIP_TRI_B)
+            o.v[bm][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(xb[b], c.v[bm][ch][ks], o.v[bm][b], 0, 0, 0);
+          }
+      }
+    }
+#pragma unroll
+    for (int bm = 0; bm < 2; ++bm)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Co[rw_row(bm) + (long)rw_col(2 * P + b, r) * ldo] = o.v[bm][b][r];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+}
+
 // ---------------------------------------------------------------- diagonal tile: factor + invert in LDS
 // 128x128 tile T (column-major, stride TLD) in LDS, 256 threads, blocked by 16 (see
 // factor_invert_tile): F1 factor + invert of the 16x16 pivot in one wave's registers, F2 panel

@@ -94,6 +94,43 @@ def test_cholesky_logdet_inverse(mk, n):
         assert np.linalg.norm(inv[s] - Ir) <= 1e-9 * np.linalg.norm(Ir)
 
 
+_FUSED_RUN = """
+import importlib, sys, numpy as np
+sys.path.insert(0, {root!r})
+mk = importlib.import_module({pkg!r})
+rng = np.random.default_rng(11)
+S, n = 136, 700                     # >= 128 factors of 6 tiles: every launch takes 128-tiles
+c = rng.uniform(size=(S, n, 2))
+d = np.sqrt(((c[:, :, None, :] - c[:, None, :, :]) ** 2).sum(-1))
+A = np.exp(-(3.0 + rng.uniform(size=(S, 1, 1)) * 6.0) * d)
+L, ld = mk.cholesky_batched(A, inverse=False)
+np.savez({path!r}, A=A[:4], L=L, ld=ld)
+"""
+
+
+def test_fused_update_trsm_is_bit_identical(tmp_path):
+    """The fused column update + panel solve (k_chol_update_trsm, the default where every launch of a
+    factorisation takes 128-tiles: >= 128 factors) gives the bits of the separate update, diagonal
+    and trsm launches (MK_CHOL_FUSED=0), and a factor LAPACK agrees with."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    pkg = "laurabaracaldo-spatial-meta-kriging-for-distributed-inference-for-binary-response_amd"
+    res = {}
+    for fused in ("1", "0"):
+        path = str(tmp_path / f"fused{fused}.npz")
+        r = subprocess.run([sys.executable, "-c", _FUSED_RUN.format(root=root, pkg=pkg, path=path)],
+                           capture_output=True, text=True, timeout=240, env=dict(os.environ, MK_CHOL_FUSED=fused))
+        assert r.returncode == 0, r.stderr[-4000:]
+        z = np.load(path)
+        res[fused] = {k: z[k] for k in z.files}
+    assert np.array_equal(res["1"]["L"], res["0"]["L"]) and np.array_equal(res["1"]["ld"], res["0"]["ld"])
+    for s in range(4):
+        Lr = sla.cholesky(res["1"]["A"][s], lower=True)
+        assert np.linalg.norm(res["1"]["L"][s] - Lr) <= REL * np.linalg.norm(Lr)
+
+
 def test_cholesky_rejects_non_pd(mk):
     A = np.eye(4)[None].copy()
     A[0, 3, 3] = -1.0
@@ -115,7 +152,9 @@ def test_sub_tile_gemm_split_cholesky_and_multi_wg_sweep_are_bit_identical(tmp_p
     split two-stream Cholesky schedule (bulk update by panels < k-d on a CU-masked stream, the
     rank-128d correction on the critical stream; the accumulator passes through fp64 memory) at
     depths 1-3, the 64-site-block sweeps -- one workgroup per subset (MK_SWEEP=1, k_sweep), the
-    split launches (3: k_sweep_step, one launch per block) and the multi-workgroup kernel (2:
+    fused column update + panel solve (k_chol_update_trsm: MK_TILE=128 sessions take it, MK_CHOL_FUSED=0
+    the separate U, D, T launches), the split launches (3: k_sweep_step, one launch per block) and the
+    multi-workgroup kernel (2:
     k_sweep_mg behind its admission consensus, on both schedules; MK_ADM_SPINS=0 refuses the subsets
     whose workgroups do not arrive together, -1 every subset, and the k_sweep fallback queued behind
     it sweeps them) -- and the kriging GEMM with P^T generated in LDS (MK_PRED_GEN=1,
@@ -144,10 +183,12 @@ def test_sub_tile_gemm_split_cholesky_and_multi_wg_sweep_are_bit_identical(tmp_p
                ("128", "1", "0", "0", "2", "0"))
     runs = [(cfg, {}) for cfg in configs] + [(("128", "2", "0", "0", "2", "1"), {"MK_ADM_SPINS": "0"}),
                                               (("64", "2", "1", "0", "3", "0"), {"MK_ADM_SPINS": "-1"}),
-                                              (("128", "2", "0", "0", "2", "1"), {"MK_ADM_SPINS": "-1"})]
+                                              (("128", "2", "0", "0", "2", "1"), {"MK_ADM_SPINS": "-1"}),
+                                              (("128", "1", "0", "0", "2", "0"), {"MK_CHOL_FUSED": "0"}),
+                                              (("128", "1", "0", "0", "2", "1"), {"MK_CHOL_FUSED": "0"})]
     for cfg, extra in runs:
         tile, sweep, split, gen, depth, la = cfg
-        key = cfg + tuple("adm" + v for v in extra.values())
+        key = cfg + tuple(k_[3:] + v for k_, v in extra.items())
         path = str(tmp_path / ("run_" + "_".join(key) + ".npz"))
         r = subprocess.run([sys.executable, os.path.join(here, "gpu_tile_run.py"), path], capture_output=True,
                            text=True, timeout=240,
