@@ -228,7 +228,8 @@ def host_cores():
 
 
 def _pmc_traffic():
-    """HBM bytes per k_chol_update launch from the committed rocprofv3 --pmc passes (or None)."""
+    """HBM bytes per column-update launch (k_chol_update_trsm + k_chol_update, launch-weighted) from
+    the committed rocprofv3 --pmc passes (or None)."""
     path = os.path.join(ROOT, "profiles", "pmc_chol_update.json")
     try:
         with open(path) as f:
@@ -533,8 +534,9 @@ def main():
                                f"{W + 1}-{W + a.steps} (after {A} untimed adaptation + {W - A} warmup iterations)",
                    "subsets_per_gpu": per, "total_subsets": K_job, "streams_per_gpu": a.streams or 1,
                    "parallelism": f"subset-sharded x{world}"},
-        "roofline": {"bound": "mfma", "kernel": "k_chol_update (left-looking Cholesky panel GEMM, fp64 MFMA; "
-                               "128-tile and 64/32-sub-tile instances together)",
+        "roofline": {"bound": "mfma", "kernel": "the column-update launches of the left-looking Cholesky (fp64 MFMA): "
+                               "k_chol_update_trsm (update + panel solve fused, 128-tiles) and k_chol_update "
+                               "(diagonal corrections; 128-tile and 64/32-sub-tile instances) together",
                      "sub_tile_launch_share": sub_share,
                      "busy_ms_union": st["ms"], "launch_ms_summed": summed_ms,
                      "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",

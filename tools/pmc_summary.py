@@ -2,8 +2,9 @@
 
 usage: python tools/pmc_summary.py <fetch_pass_dir> <write_pass_dir> <out.json> "<command profiled>" [kernel]
 
-[kernel] (default mk::k_chol_update) is a name prefix: template instances (k_chol_update<128>,
-<64>, ...) are folded into one launch-weighted entry.
+[kernel] (default "mk::k_chol_update,mk::k_chol_update_trsm") is a comma-separated list of names:
+each name's template instances (k_chol_update<128>, <64>, ...) and the names themselves are folded
+into one launch-weighted entry (bench.py's roofline kernel: every column-update launch).
 
 gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE reports half the bytes of
 16-B/lane coalesced reads -> x2; WRITE_SIZE as reported.  Both are in KB -> x1024.
@@ -16,7 +17,7 @@ import os
 import sys
 from collections import defaultdict
 
-KERNEL = "mk::k_chol_update"
+KERNEL = "mk::k_chol_update,mk::k_chol_update_trsm"
 
 
 def _per_kernel(d, counter):
@@ -47,7 +48,8 @@ def main():
         allk[k] = {"launches": max(fn, wn), "fetch_kb_avg": fkb, "write_kb_avg": wkb,
                    "hbm_bytes_per_launch_corrected": (2.0 * fkb + wkb) * 1024.0}
     kernel = sys.argv[5] if len(sys.argv) > 5 else KERNEL
-    inst = {k: v for k, v in allk.items() if k == kernel or k.startswith(kernel + "<")}
+    names = kernel.split(",")
+    inst = {k: v for k, v in allk.items() if any(k == nm or k.startswith(nm + "<") for nm in names)}
     if not inst:
         raise SystemExit(f"{kernel} not in the profile")
     n = sum(v["launches"] for v in inst.values())
