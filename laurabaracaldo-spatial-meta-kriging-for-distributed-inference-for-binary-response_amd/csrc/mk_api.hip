@@ -539,7 +539,7 @@ static bool set_gemm_lds() {
       {(const void*)k_chol_trsm<128>, LDS_128},   {(const void*)k_chol_trsm<64>, LDS_64x128},
       {(const void*)k_inv_level<128>, LDS_128},   {(const void*)k_inv_level<64>, LDS_64},
       {(const void*)k_chol_update<32>, LDS_32},   {(const void*)k_chol_trsm<32>, LDS_32x128},
-      {(const void*)k_chol_update_trsm, LDS_128},
+      {(const void*)k_chol_update_trsm<128>, LDS_128}, {(const void*)k_chol_update_trsm<64>, LDS_128},
       {(const void*)k_inv_level<32>, LDS_32},
       {(const void*)k_qblocks, LDS_64},           {(const void*)k_lauum, LDS_128},
       {(const void*)k_pred_var<true>, LDS_128},   {(const void*)k_pred_var<false>, LDS_128}};
@@ -637,14 +637,19 @@ static void chol_trsm(mk_session* s, Group& g, hipStream_t st, int h0, int hc, i
                          slist, scount);
   });
 }
-// F(k): column k's update of tiles k+1.. with the panel solve in the epilogue, plus the next diagonal
-// tile's update by panels [0, k) (k_chol_update_trsm; 128-tiles, k >= 1, k < nt - 1).
-static void chol_update_trsm(mk_session* s, Group& g, hipStream_t st, int h0, int hc, int k, const int* slist,
-                             const int* scount, double flops) {
+// F(k): column k's update of tiles k+1.. by panels [j0, k) with the panel solve in the epilogue
+// (k_chol_update_trsm, 1 <= k < nt - 1), plus (extra) the next diagonal tile's update by panels [0, k).
+static void chol_update_trsm(mk_session* s, Group& g, hipStream_t st, int h0, int hc, int k, int j0, int extra,
+                             const int* slist, const int* scount, double flops) {
   const int E = g.S * hc, nt = s->nt, nti = nt - (k + 1);
-  timed(s, st, KS_CHOL_UPDATE, flops, [&] {
-    MK_LAUNCH(k_chol_update_trsm, dim3(xcd_grid_h(E, nti + 1)), dim3(256), LDS_128, st, g.ms, g.S, h0, hc, k, k + 1,
-              nt, slist, scount);
+  const int tm = tile_size((long)E * (nti + extra));
+  timed(s, st, tm == 128 ? KS_CHOL_UPDATE : KS_CHOL_UPDATE_SUB, flops, [&] {
+    if (tm == 128)
+      MK_LAUNCH(k_chol_update_trsm<128>, dim3(xcd_grid_h(E, nti + extra)), dim3(256), LDS_128, st, g.ms, g.S, h0, hc,
+                k, k + 1, nt, j0, extra, slist, scount);
+    else
+      MK_LAUNCH(k_chol_update_trsm<64>, dim3(xcd_grid_h(E, 2 * nti + extra)), dim3(256), LDS_128, st, g.ms, g.S, h0,
+                hc, k, k + 1, nt, j0, extra, slist, scount);
   });
 }
 static void chol_diag(mk_session* s, Group& g, hipStream_t st, int h0, int hc, int k, const int* slist,
@@ -677,13 +682,16 @@ static double panel_flops(mk_session* s, Group& g, int hc, int k, int ia, int ib
 // looking by 128-panels: per column k the update by panels < k, the diagonal tile, the trsm of
 // tiles k+1.. .
 //
-// Sequential form (one stream): U(k; panels 0..k-1), D(k), T(k).  Fused (MK_CHOL_FUSED, default on
-// where every launch takes 128-tiles: >= 128 factors): D(0), T(0), then per k >= 1
+// Sequential form (one stream): U(k; panels 0..k-1), D(k), T(k).  Fused (MK_CHOL_FUSED, default on;
+// 0 restores U, D, T): D(0), T(0), then per k >= 1
 //   X(k)  the diagonal tile's last panel k-1 (its panels [0, k-1) came with F(k-1); k = 1: panel 0),
 //   D(k),
 //   F(k)  tiles k+1.. of column k, update and solve in one launch (C(i,k) stays in registers), plus
 //         the next diagonal tile by panels [0, k)
-// -- one launch per column fewer than U, D, T and no C(i,k) round trip through HBM; same bits.
+// -- no C(i,k) round trip through HBM between the update and the solve; same bits.  (The split form
+// below stays unfused: there F(k) would put the off-diagonal tiles' critical correction after the
+// diagonal factor instead of beside the diagonal tile's -- a longer chain; 32 subsets 7,479-7,597 vs
+// 8,059-8,078 subset-iters/s)
 //
 // Split form (small shards, g.bulk set): the update of column c by panels 0..c-2 only needs
 // panels that are final two steps earlier, so it runs on the CU-masked bulk stream beside the
@@ -707,8 +715,8 @@ static void launch_cholesky(mk_session* s, Group& g, int h0, int hc, const int* 
   const int nt = s->nt;
   if (k_hi < 0) k_hi = nt;
   hipStream_t A = crit ? crit : g.stream;
-  static const int fused_env = tile_env("MK_CHOL_FUSED", 1);
-  if ((slist || !g.bulk) && fused_env && tile_size((long)g.S * hc * 2) == 128) {
+  static const int fused = tile_env("MK_CHOL_FUSED", 1);
+  if ((slist || !g.bulk) && fused) {
     for (int k = k_lo; k < k_hi; ++k) {
       if (k > 0) {
         const int j0 = k >= 2 ? k - 1 : 0;
@@ -718,7 +726,7 @@ static void launch_cholesky(mk_session* s, Group& g, int h0, int hc, const int* 
       if (k == 0 && nt > 1)
         chol_trsm(s, g, A, h0, hc, 0, 1, nt, slist, scount, panel_flops(s, g, hc, 0, 1, nt, true));
       else if (k > 0 && k < nt - 1)
-        chol_update_trsm(s, g, A, h0, hc, k, slist, scount,
+        chol_update_trsm(s, g, A, h0, hc, k, 0, 1, slist, scount,
                          panel_flops(s, g, hc, k, k + 1, nt, false) + panel_flops(s, g, hc, k, k + 1, nt, true) +
                              panel_flops(s, g, hc, k + 1, k + 1, k + 2, false, 0, k));
       if (evP) hipEventRecord(evP[k], A);

@@ -211,48 +211,52 @@ __device__ inline void gemm_tile_genb(const double* __restrict__ A, long sA, int
   }
 }
 
-// Row-wave form of the 128 x 128 tile (k_chol_update_trsm): wave w owns rows 32w .. 32w + 31 and all
-// 128 columns (2 x 8 MFMA blocks) instead of a 64 x 64 quadrant -- the same MFMA sequence per element
-// (same chunks, k-steps, fragment values), so the same bits; what changes is which wave holds which
-// rows, and a wave then holds whole rows of C: the operand of a solve applied from the right.
-// Accumulator: lane l, register r of block (bm, bn) is C[32w + 16bm + (l & 15)][16bn + (l >> 4) + 4r].
-typedef AccT<2, 8> AccRW;
-__device__ inline int rw_row(int bm) { return (threadIdx.x >> 6) * 32 + bm * 16 + (threadIdx.x & 15); }
+// Row-wave form of a TM x 128 tile, TM in {128, 64} (k_chol_update_trsm): wave w owns rows
+// TM/4 * w .. of all 128 columns (TM/64 x 8 MFMA blocks) instead of a quadrant -- the same MFMA
+// sequence per element (same chunks, k-steps, fragment values), so the same bits; what changes is
+// which wave holds which rows, and a wave then holds whole rows of C: the operand of a solve
+// applied from the right.
+// Accumulator: lane l, register r of block (bm, bn) is C[TM/4 w + 16bm + (l & 15)][16bn + (l >> 4) + 4r].
+template <int TM>
+using AccRW = AccT<TM / 64, 8>;
+template <int TM>
+__device__ inline int rw_row(int bm) { return (threadIdx.x >> 6) * (TM / 4) + bm * 16 + (threadIdx.x & 15); }
 __device__ inline int rw_col(int bn, int r) { return bn * 16 + ((threadIdx.x & 63) >> 4) + 4 * r; }
 
-template <bool NEG>
-__device__ inline void mma_chunk_rw(const double* As, const double* Bs, AccRW& acc) {
+template <int TM, bool NEG>
+__device__ inline void mma_chunk_rw(const double* As, const double* Bs, AccRW<TM>& acc) {
+  constexpr int BM = TM / 64;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int li = lane & 15, lk = lane >> 4;
 #pragma unroll
   for (int ks = 0; ks < GB_K / 4; ++ks) {
     const int k = ks * 4 + lk;
-    double ya[2], xb[8];
+    double ya[BM], xb[8];
 #pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      const double av = frag<true, 128>(As, w * 32 + b * 16 + li, k);
+    for (int b = 0; b < BM; ++b) {
+      const double av = frag<true, TM>(As, w * (TM / 4) + b * 16 + li, k);
       ya[b] = NEG ? -av : av;
     }
 #pragma unroll
     for (int b = 0; b < 8; ++b) xb[b] = frag<true, 128>(Bs, b * 16 + li, k);
 #pragma unroll
-    for (int bm = 0; bm < 2; ++bm)
+    for (int bm = 0; bm < BM; ++bm)
 #pragma unroll
       for (int bn = 0; bn < 8; ++bn)
         acc.v[bm][bn] = __builtin_amdgcn_mfma_f64_16x16x4f64(xb[bn], ya[bm], acc.v[bm][bn], 0, 0, 0);
   }
 }
 
-// gemm_tile<128, 128, true, true, NEG> in the row-wave form (A m-contiguous, B n-contiguous), K > 0.
-template <bool NEG>
+// gemm_tile<TM, 128, true, true, NEG> in the row-wave form (A m-contiguous, B n-contiguous), K > 0.
+template <int TM, bool NEG>
 __device__ inline void gemm_tile_rw(const double* __restrict__ A, long sA, const double* __restrict__ B, long sB, int K,
-                                    AccRW& acc, double* lds) {
-  constexpr int STAGE = gb_img(128) + gb_img(128);
+                                    AccRW<TM>& acc, double* lds) {
+  constexpr int STAGE = gb_img(TM) + gb_img(128);
   const int nch = K / GB_K;   // K > 0
   auto issue = [&](int c) {
     double* st = lds + (c & 1) * STAGE;
-    dma_chunk<true, 128>(A, sA, GB_K * c, st);
-    dma_chunk<true, 128>(B, sB, GB_K * c, st + gb_img(128));
+    dma_chunk<true, TM>(A, sA, GB_K * c, st);
+    dma_chunk<true, 128>(B, sB, GB_K * c, st + gb_img(TM));
   };
   issue(0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -260,19 +264,20 @@ __device__ inline void gemm_tile_rw(const double* __restrict__ A, long sA, const
   for (int c = 0; c < nch; ++c) {
     const double* st = lds + (c & 1) * STAGE;
     if (c + 1 < nch) issue(c + 1);
-    mma_chunk_rw<NEG>(st, st + gb_img(128), acc);
+    mma_chunk_rw<TM, NEG>(st, st + gb_img(TM), acc);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
 }
 
-__device__ inline void acc_load_rw(AccRW& acc, const double* C, long ldc) {
+template <int TM>
+__device__ inline void acc_load_rw(AccRW<TM>& acc, const double* C, long ldc) {
 #pragma unroll
-  for (int bm = 0; bm < 2; ++bm)
+  for (int bm = 0; bm < TM / 64; ++bm)
 #pragma unroll
     for (int bn = 0; bn < 8; ++bn)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) acc.v[bm][bn][r] = C[rw_row(bm) + (long)rw_col(bn, r) * ldc];
+      for (int r = 0; r < 4; ++r) acc.v[bm][bn][r] = C[rw_row<TM>(bm) + (long)rw_col(bn, r) * ldc];
 }
 
 // The 128 x 128 form every kernel started from.

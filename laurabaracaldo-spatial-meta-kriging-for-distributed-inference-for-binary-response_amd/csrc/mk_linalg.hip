@@ -350,33 +350,37 @@ template __global__ void k_chol_trsm<128>(MatSet, int, int, int, int, int, int, 
 template __global__ void k_chol_trsm<64>(MatSet, int, int, int, int, int, int, const int*, const int*);
 template __global__ void k_chol_trsm<32>(MatSet, int, int, int, int, int, int, const int*, const int*);
 
-// Column k's update with the panel solve in its epilogue (sequential schedule, 128-tiles):
-//   jobs t < ntk: tile i = ia + t (ia = k + 1): C(i,k) -= sum_{j<k} L(i,j) L(k,j)^T (k_chol_update's
-//     MFMA sequence, in the row-wave form: wave w holds rows 32w.. of all 128 columns), then
+// Column k's update with the panel solve in its epilogue (k_chol_update_trsm):
+//   jobs t < ntk * 128/TM: rows of tile i = ia + t / (128/TM) (ia = k + 1, TM-row parts):
+//     C(i,k) -= sum_{j0 <= j < k} L(i,j) L(k,j)^T (k_chol_update's MFMA sequence, in the row-wave
+//     form: wave w holds TM/4 rows of all 128 columns; the accumulator starts from C in memory, so
+//     panels [0, j0) may have come from an earlier launch -- the split schedule's bulk stream), then
 //     L(i,k) = C(i,k) Winv_k^T straight from the accumulator (k_chol_trsm's sequence: chunks of 16
-//     in order from zero, the same fragment values) -- C(i,k) never goes through HBM between the two,
-//     and every wave solves its own rows: the same triangular work on all four SIMDs;
-//   job t = ntk (when i = k + 1 < nt): the next diagonal tile's update by panels [0, k), stored
-//     partial; its correction by panel k (k_chol_update, accumulator from memory) follows the
-//     launch, then its factor -- so Winv_k exists before this launch starts.
-// Same per-element sequences as U(k), T(k): same bits (tests/test_gpu_linalg.py).
+//     in order from zero, the same fragment values) -- C(i,k) never goes through HBM between the
+//     two, and every wave solves its own rows: the same triangular work on all four SIMDs;
+//   job t = ntk * 128/TM (extra = 1, sequential schedule): the next diagonal tile's update by
+//     panels [0, k), stored partial; its correction by panel k (k_chol_update, accumulator from
+//     memory) follows the launch, then its factor.
+// Winv_k exists before the launch starts.  Same per-element sequences as U(k), T(k): same bits
+// (tests/test_gpu_linalg.py).
 // Epilogue: the accumulator's block (bm, c), k-step r is chunk c's A fragment, in registers; the
 // output accumulates 32 columns at a time (the kernel stays within the 256 registers of two
 // workgroups per CU).
+template <int TM>
 __global__ __launch_bounds__(256, 2) void k_chol_update_trsm(MatSet ms, int S, int h0, int hc, int k, int ia, int ib,
-                                                            const int* slist, const int* scount) {
+                                                            int j0, int extra, const int* slist, const int* scount) {
   extern __shared__ __attribute__((aligned(16))) double lds[];   // gb_lds_bytes(128, 128)
+  constexpr int SUB = MK_NB / TM, BM = TM / 64;
   const int ntk = ib - ia;
-  const int extra = ia < ms.nt ? 1 : 0;   // the next diagonal tile's partial update
   int e, t, s, h;
-  if (!xcd_map(active_pairs(slist, scount, S, hc), ntk + extra, &e, &t) ||
+  if (!xcd_map(active_pairs(slist, scount, S, hc), ntk * SUB + extra, &e, &t) ||
       !pick_pair(slist, scount, e, h0, hc, &s, &h))
     return;
   const int sh = s * ms.q + h;
   const int slot = 1 - ms.cur[sh];
   double* M = mat_slot(ms, sh, slot);
   const long ld = ms.ld;
-  if (t == ntk) {   // tile (ia, ia) of column ia, panels [0, k)
+  if (t == ntk * SUB) {   // tile (ia, ia) of column ia, panels [0, k)
     double* C = M + ia * MK_NB + (long)ia * MK_NB * ld;
     Acc acc;
     acc_load(acc, C, ld);
@@ -384,17 +388,19 @@ __global__ __launch_bounds__(256, 2) void k_chol_update_trsm(MatSet ms, int S, i
     store_tile(C, ld, acc);
     return;
   }
-  const int i = ia + t;
-  double* C = M + i * MK_NB + (long)k * MK_NB * ld;
-  AccRW c;
-  acc_load_rw(c, C, ld);
-  gemm_tile_rw<true>(M + i * MK_NB, ld, M + k * MK_NB, ld, k * MK_NB, c, lds);   // ends with a barrier
+  const int i = ia + t / SUB, r0 = i * MK_NB + (t % SUB) * TM;
+  double* C = M + r0 + (long)k * MK_NB * ld;
+  AccRW<TM> c;
+  acc_load_rw<TM>(c, C, ld);
+  const long jo = (long)j0 * MK_NB * ld;
+  gemm_tile_rw<TM, true>(M + r0 + jo, ld, M + k * MK_NB + jo, ld, (k - j0) * MK_NB, c, lds);   // ends with a barrier
   // opaque copies: the output addresses are computed here, not hoisted over the main loop beside
-  // the accumulator (the compiler would otherwise keep acc_load's 64 addresses live for the stores)
+  // the accumulator (the compiler would otherwise keep acc_load's addresses live for the stores)
   double* Co = C;
   long ldo = ld;
   asm volatile("" : "+s"(Co), "+s"(ldo));
   const double* Wt = winv_slot(ms, sh, slot, k);   // op(B)(j, n) = Wt[j * 128 + n]
+  asm volatile("" : "+s"(Wt));
   // four passes of 32 output columns, P = 3, 0, 2, 1 (pass P: n-blocks 2P, 2P+1, chunks 0 .. 2P+1);
   // each pass's 16 x 32 slices of Winv_k^T arrive by LDS-DMA while the previous pass multiplies
   // (buffers: passes 3, 2 at lds, passes 0, 1 behind pass 3's 48 KiB)
@@ -417,7 +423,7 @@ __global__ __launch_bounds__(256, 2) void k_chol_update_trsm(MatSet ms, int S, i
       const int Pn = idx == 0 ? 0 : (idx == 1 ? 2 : 1);
       issue(Pn, (idx & 1) ? bufA : bufB);
     }
-    AccT<2, 2> o;
+    AccT<BM, 2> o;
     acc_zero(o);
 #pragma unroll
     for (int ch = 0; ch < 8; ++ch) {
@@ -429,7 +435,7 @@ __global__ __launch_bounds__(256, 2) void k_chol_update_trsm(MatSet ms, int S, i
 #pragma unroll
         for (int b = 0; b < 2; ++b) xb[b] = frag<true, 32>(buf + ch * IMG, b * 16 + li, kk);
 #pragma unroll
-        for (int bm = 0; bm < 2; ++bm)
+        for (int bm = 0; bm < BM; ++bm)
 #pragma unroll
           for (int b = 0; b < 2; ++b) {
             if (ch > 2 * P + b) continue;   // Winv(n, j) = 0 for j > n (k_chol_trsm's SKIP_TRI_B)
@@ -438,15 +444,17 @@ __global__ __launch_bounds__(256, 2) void k_chol_update_trsm(MatSet ms, int S, i
       }
     }
 #pragma unroll
-    for (int bm = 0; bm < 2; ++bm)
+    for (int bm = 0; bm < BM; ++bm)
 #pragma unroll
       for (int b = 0; b < 2; ++b)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) Co[rw_row(bm) + (long)rw_col(2 * P + b, r) * ldo] = o.v[bm][b][r];
+        for (int r = 0; r < 4; ++r) Co[rw_row<TM>(bm) + (long)rw_col(2 * P + b, r) * ldo] = o.v[bm][b][r];
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
 }
+template __global__ void k_chol_update_trsm<128>(MatSet, int, int, int, int, int, int, int, int, const int*, const int*);
+template __global__ void k_chol_update_trsm<64>(MatSet, int, int, int, int, int, int, int, int, const int*, const int*);
 
 // ---------------------------------------------------------------- diagonal tile: factor + invert in LDS
 // 128x128 tile T (column-major, stride TLD) in LDS, 256 threads, blocked by 16 (see
