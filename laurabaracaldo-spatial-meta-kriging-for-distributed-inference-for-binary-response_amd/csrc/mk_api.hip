@@ -652,11 +652,12 @@ static void chol_update_trsm(mk_session* s, Group& g, hipStream_t st, int h0, in
                 hc, k, k + 1, nt, j0, extra, slist, scount);
   });
 }
+// cj0 < cj1: the diagonal tile's update by panels [cj0, cj1) first, in the same launch (fused form).
 static void chol_diag(mk_session* s, Group& g, hipStream_t st, int h0, int hc, int k, const int* slist,
-                      const int* scount) {
-  timed(s, st, KS_CHOL_DIAG, 0.0, [&] {
+                      const int* scount, int cj0 = 0, int cj1 = 0, double flops = 0.0) {
+  timed(s, st, KS_CHOL_DIAG, flops, [&] {
     MK_LAUNCH(k_chol_diag, dim3(g.S * hc), dim3(256), (size_t)MK_DIAG_LDS_BYTES, st, g.ms, g.md.n_s, h0, hc, k,
-                       g.md.ld_part, g.md.quad_c, g.md.info, slist, scount);
+                       g.md.ld_part, g.md.quad_c, g.md.info, slist, scount, cj0, cj1);
   });
 }
 
@@ -684,8 +685,8 @@ static double panel_flops(mk_session* s, Group& g, int hc, int k, int ia, int ib
 //
 // Sequential form (one stream): U(k; panels 0..k-1), D(k), T(k).  Fused (MK_CHOL_FUSED, default on;
 // 0 restores U, D, T): D(0), T(0), then per k >= 1
-//   X(k)  the diagonal tile's last panel k-1 (its panels [0, k-1) came with F(k-1); k = 1: panel 0),
-//   D(k),
+//   D(k)  the diagonal tile's last panel k-1 (its panels [0, k-1) came with F(k-1); k = 1: panel 0)
+//         applied inside the diagonal launch, then the factor,
 //   F(k)  tiles k+1.. of column k, update and solve in one launch (C(i,k) stays in registers), plus
 //         the next diagonal tile by panels [0, k)
 // -- no C(i,k) round trip through HBM between the update and the solve; same bits.  (The split form
@@ -718,11 +719,9 @@ static void launch_cholesky(mk_session* s, Group& g, int h0, int hc, const int* 
   static const int fused = tile_env("MK_CHOL_FUSED", 1);
   if ((slist || !g.bulk) && fused) {
     for (int k = k_lo; k < k_hi; ++k) {
-      if (k > 0) {
-        const int j0 = k >= 2 ? k - 1 : 0;
-        chol_update(s, g, A, h0, hc, k, k, k + 1, j0, k, slist, scount, panel_flops(s, g, hc, k, k, k + 1, false, j0, k));
-      }
-      chol_diag(s, g, A, h0, hc, k, slist, scount);
+      // X(k) inside D(k): the diagonal tile's last panel (k = 1: panel 0) before it factors
+      const int j0 = k >= 2 ? k - 1 : 0;
+      chol_diag(s, g, A, h0, hc, k, slist, scount, j0, k, k > 0 ? panel_flops(s, g, hc, k, k, k + 1, false, j0, k) : 0.0);
       if (k == 0 && nt > 1)
         chol_trsm(s, g, A, h0, hc, 0, 1, nt, slist, scount, panel_flops(s, g, hc, 0, 1, nt, true));
       else if (k > 0 && k < nt - 1)

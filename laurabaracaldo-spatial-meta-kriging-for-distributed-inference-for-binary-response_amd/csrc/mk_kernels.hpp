@@ -23,7 +23,7 @@ template <int TM>
 __global__ void k_chol_update_trsm(MatSet ms, int S, int h0, int hc, int k, int ia, int ib, int j0, int extra,
                                    const int* slist, const int* scount);
 __global__ void k_chol_diag(MatSet ms, const int* n_s, int h0, int hc, int k, double* ld_part, double* quad_c, int* info,
-                            const int* slist, const int* scount);
+                            const int* slist, const int* scount, int cj0, int cj1);
 __global__ void k_inv_copydiag(MatSet ms, const int* list, const int* count);
 template <int TM>
 __global__ void k_inv_level(MatSet ms, const int* list, const int* count, int sz, int phase);

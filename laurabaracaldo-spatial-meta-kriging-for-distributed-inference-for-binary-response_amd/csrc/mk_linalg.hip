@@ -899,9 +899,13 @@ __device__ void factor_invert_tile(double* T, double* dg, double* xd, double* Sb
 // Factor + invert the 128x128 diagonal tile k of each candidate.  Row rb = n_s - 128k
 // (if inside the tile) is the bordered row: its pivot is -(u' R^-1 u) and it is not
 // factored (pivot set to 1).
+// cj0 < cj1 (the fused factorisation, launch_cholesky): the tile first takes its update by panels
+// [cj0, cj1) -- k_chol_update's MFMA sequence from the tile in memory, the accumulator written
+// straight into the LDS image instead of back to HBM (the launch it replaces would have stored
+// exactly these values) -- then factors.
 __global__ __launch_bounds__(256) void k_chol_diag(MatSet ms, const int* __restrict__ n_s, int h0, int hc, int k,
                                                    double* ld_part, double* quad_c, int* info, const int* slist,
-                                                   const int* scount) {
+                                                   const int* scount, int cj0, int cj1) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
   double* T = sm;                      // [128*128]
   double* dg = T + MK_NB * TLD;        // [128]
@@ -918,10 +922,25 @@ __global__ __launch_bounds__(256) void k_chol_diag(MatSet ms, const int* __restr
   const int base = k * MK_NB;
   const int ns = n_s[s];
   double* Mt = M + base + (long)base * ld;
+  if (cj1 > cj0) {
+    Acc acc;
+    acc_load(acc, Mt, ld);
+    const long jo = (long)cj0 * MK_NB * ld;
+    gemm_tile<128, 128, true, true, true>(M + base + jo, ld, M + base + jo, ld, (cj1 - cj0) * MK_NB,
+                                          (cj1 - cj0) * MK_NB, acc, sm);   // stages in T's space; ends with a barrier
+#pragma unroll
+    for (int bm = 0; bm < 4; ++bm)
+#pragma unroll
+      for (int bn = 0; bn < 4; ++bn)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int rr = acc_row<128>(bm), cc = acc_col<128>(bn, r);
+          T[rr + cc * TLD] = rr >= cc ? acc.v[bm][bn][r] : 0.0;
+        }
+  } else {
   // Unconditional 16-byte loads, all 32 per thread in flight at once (one memory round trip
   // instead of four), then the upper triangle is zeroed in LDS (a masked load per element
   // compiled to one dependent round trip each: 64 per thread).
-  {
     constexpr int NL = MK_NB * MK_NB / (256 * 2);
     d2 v[NL];
 #pragma unroll
