@@ -1280,15 +1280,17 @@ __global__ __launch_bounds__(SS_T) void k_sweep_site(Model md, MatSet ms, int it
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
       {
-        // No row masks: i is even, so the loads already return zero for every row pair wholly above
-        // column i's diagonal, and the one upper element left, W[i, i+1], is zero in memory (W's
-        // upper triangle is zeroed at session creation and never written: store_tile_lw,
-        // k_inv_copydiag, k_inv_level write lower tiles and zero-upper diagonal tiles).  Row n_s
-        // (the border row, nonzero in W) sits in a loaded pair only for odd n_s: LN = 1 drops it with
-        // a factor 0; LN = 2 is launched only when every subset's n_s is even.
+        // No row masks but one: i is even, so the loads already return zero for every row pair wholly
+        // above column i's diagonal; the one upper element left, W[i, i+1] (column i+1 in the pair
+        // starting at row i), is zero in memory (W's upper triangle is zeroed at session creation and
+        // store_tile_lw, k_inv_copydiag, k_inv_level write lower tiles and zero-upper diagonal tiles)
+        // and is masked here anyway -- one select per pair, so no future writer of W's upper triangle
+        // can reach z.  Row n_s (the border row, nonzero in W) sits in a loaded pair only
+        // for odd n_s: LN = 1 drops it with a factor 0; LN = 2 is launched only when every subset's n_s
+        // is even.
         c0[k].x = w0[k][0].x;
         c0[k].y = LN == 1 ? w0[k][0].y * ym[k] : w0[k][0].y;
-        c1[k].x = w1[k][0].x;
+        c1[k].x = (2 * tid + 2 * SS_T * k == i) ? 0.0 : w1[k][0].x;
         c1[k].y = LN == 1 ? w1[k][0].y * ym[k] : w1[k][0].y;
       }
     }
