@@ -838,7 +838,7 @@ static void launch_pred_refresh(mk_session* s, Group& g, hipStream_t st = nullpt
     MK_LAUNCH(pred_PT_kernel(md.cov_model), dim3(max_entries * md.n_pad), dim3(256), 0, st, md, g.d_plist,
                        g.d_pcount);
   timed(s, st, KS_PRED_VAR, pred_flops(s, g), [&] {
-    MK_LAUNCH(s->pred_gen ? k_pred_var<true> : k_pred_var<false>, dim3(xcd_grid_h(max_entries, nt * md.ntt)),
+    MK_LAUNCH(s->pred_gen ? k_pred_var<true> : k_pred_var<false>, dim3(pv_grid(max_entries, nt, md.ntt)),
               dim3(256), LDS_128, st, md, g.ms, g.d_plist, g.d_pcount);
   });
   MK_LAUNCH(k_pred_var_reduce, dim3(max_entries * (md.n_test_pad / 256)), dim3(256), 0, st, md, nt,

@@ -19,6 +19,7 @@ __global__ void k_chol_update(MatSet ms, int S, int h0, int hc, int k, int ia, i
 template <int TM>
 __global__ void k_chol_trsm(MatSet ms, int S, int h0, int hc, int k, int ia, int ib, const int* slist,
                             const int* scount);
+int pv_grid(int max_entries, int nt, int ntt);   // k_pred_var's grid (mk_linalg.hip)
 template <int TM>
 __global__ void k_chol_update_trsm(MatSet ms, int S, int h0, int hc, int k, int ia, int ib, int j0, int extra,
                                    const int* slist, const int* scount);

@@ -1470,17 +1470,45 @@ __global__ __launch_bounds__(256) void k_pred_PT_matern(Model md, const int* __r
 // the test tiles of one row panel: consecutive workgroups of a pair share i) and writes X; a
 // stored P^T was re-read from HBM once per row panel (~8.5 x its size at n_s = 2000).
 // !GEN (Matern): P^T from k_pred_PT (its Bessel tables are too heavy to inline per element).
+// Cost-balanced XCD maps: row panel i costs i + 1 K-chunks of 128 (W lower-triangular), and
+// xcd_map's contiguous split of the (pair, panel, tile) items cut pairs at arbitrary panels whenever
+// the count of listed pairs was not a multiple of 8 -- the XCD holding a pair's late panels then set
+// the launch's length (configs[4]'s tiled replay refreshes ~12 pairs per launch: 1.16 x the mean
+// XCD load).
+//  * many test tiles (ntt >= 64, the tiled replay): XCD x takes test tiles [x q, x q + q), q =
+//    ntt / 8 rounded up, of every panel of every pair -- exactly an eighth of every panel's cost
+//    (each XCD reads every W panel into its own L2: 8 x W's bytes, small beside P^T's);
+//  * few (the fused path, ntt = n_test / 128, ~100 pairs per launch at configs[2]): xcd_map's
+//    contiguous split, which keeps a pair's panels on one XCD so its P^T is read into one L2 (1.6 %
+//    above the mean XCD load at 107 pairs; rotating the panels over the XCDs measured 0.7 % slower).
+int pv_grid(int max_entries, int nt, int ntt) {
+  return ntt >= 64 ? 8 * max_entries * nt * ((ntt + 7) / 8) : xcd_grid(max_entries, nt * ntt);
+}
+
 template <bool GEN>
 __global__ __launch_bounds__(256, 2) void k_pred_var(Model md, MatSet ms, const int* __restrict__ list,
                                                   const int* __restrict__ count) {
   extern __shared__ __attribute__((aligned(16))) double lds[];   // MK_GD_LDS_BYTES
   __shared__ double red[2][MK_NB];
-  const int per = ms.nt * md.ntt;
-  int e, t_;
-  if (!xcd_map(*count, per, &e, &t_)) return;
-  // row-panel-major raster: the ~64 workgroups an XCD holds at once share one W row panel (L2);
-  // grouped rasters that share P^T blocks instead measured slower
-  const int i = t_ / md.ntt, tb = t_ % md.ntt;
+  // block b runs on XCD b % 8 (xcd_map); within an XCD pair-major, then panels (largest first),
+  // then test tiles: the workgroups an XCD holds at once share one W row panel (L2); grouped rasters
+  // that share P^T blocks instead measured slower
+  const int x = blockIdx.x & 7, jx = blockIdx.x >> 3;
+  int e, i, tb;
+  if (md.ntt >= 64) {
+    const int qt = (md.ntt + 7) / 8, per_x = ms.nt * qt;
+    e = jx / per_x;
+    const int rr = jx % per_x;
+    i = ms.nt - 1 - rr / qt;
+    tb = x * qt + rr % qt;
+    if (tb >= md.ntt) return;
+  } else {
+    int t_;
+    if (!xcd_map(*count, ms.nt * md.ntt, &e, &t_)) return;
+    i = t_ / md.ntt;
+    tb = t_ % md.ntt;
+  }
+  if (e >= *count) return;
   const int sh = list[e];
   const int s = sh / md.q;
   const int ns = md.n_s[s];
