@@ -302,7 +302,7 @@ def node_end_to_end(a, world):
     cmd = [sys.executable, os.path.abspath(__file__), "--e2e-only", "--n", str(a.n), "--subsets", str(a.subsets),
            "--n-test", str(a.n_test), "--e2e-devices", ",".join(str(i) for i in range(world))]
     try:
-        r = subprocess.run(cmd, stdout=subprocess.PIPE, text=True, timeout=1500)   # stderr: progress lines
+        r = subprocess.run(cmd, stdout=subprocess.PIPE, text=True, timeout=600)   # stderr: progress lines; ~20 s expected on 8 GPUs
         if r.returncode != 0:
             return {"error": f"exit {r.returncode}", "stdout_tail": r.stdout[-500:]}
         return json.loads(r.stdout.strip().splitlines()[-1])
