@@ -418,7 +418,7 @@ struct mk_session {
                                   // hardware queue, GPU_MAX_HW_QUEUES = 4, and slows the split Cholesky)
   hipStream_t la_k = nullptr;     // kept iterations' kriging refresh beside the sweep (MK_LA_KRIG)
   std::vector<hipEvent_t> la_ev;  // [nt] panel k final | decided (or adapted) | join | W ready | kriged
-  hipError_t launch_err = hipSuccess;   // first failed hipLaunchKernel / cooperative launch of a run
+  hipError_t launch_err = hipSuccess;   // first failed kernel launch of a run
   const char* poisoned = nullptr;       // set when a run left the chain in a state that is not the sampler's
   std::vector<int> n_part;
   std::vector<void*> allocs;
@@ -845,9 +845,9 @@ static void launch_pred_refresh(mk_session* s, Group& g, hipStream_t st = nullpt
                      g.d_plist, g.d_pcount);
 }
 
-// The latent-w sweep: the cooperative multi-workgroup kernel when the session chose it (small
-// shard; g is then the whole-shard view), else one workgroup per subset; both give the same bits
-// (mk_mcmc.hip).
+// The latent-w sweep: the multi-workgroup kernel when the session chose it (small shard; g is then
+// the whole-shard view), else the site sweep or one workgroup per subset; the block sweeps give the
+// same bits (mk_mcmc.hip).
 // Default schedule: lookahead for shards of up to 224 (subset, outcome) pairs, where the chains
 // leave the chip room to overlap (measured vs sequential: 32 subsets 5,427 -> 6,972, 63 6,174 ->
 // 7,719, 125 7,486 -> 8,303, 188 8,071 -> 8,486 subset-iters/s); at 250 subsets both saturate the
@@ -1055,7 +1055,7 @@ static void run_iteration_la(mk_session* s, int it) {
 // One iteration of the shard.  Each group (stream) runs its own chain of launches; with the
 // multi-workgroup sweep and several groups, the groups join for one whole-shard sweep on the
 // session stream and fork again (the groups' Cholesky chains overlap each other's latency-bound
-// diagonal steps; the sweep is one cooperative launch).  Same kernels, same operands, same bits.
+// diagonal steps; the sweep is one multi-workgroup launch).  Same kernels, same operands, same bits.
 static void run_iteration(mk_session* s, int it) {
   if (s->la) {
     run_iteration_la(s, it);

@@ -306,7 +306,7 @@ __global__ __launch_bounds__(256) void k_dirty_list(Model md, int force, int* li
 // Two kernels, bit-identical by construction (the chains do not depend on which one runs):
 //   k_sweep     one 1024-thread workgroup per subset, W panels streamed twice (dots, update):
 //               large shards (every CU already has a subset);
-//   k_sweep_mg  one 256-thread workgroup per (subset, 128-row tile) in a cooperative grid: the
+//   k_sweep_mg  one 256-thread workgroup per (subset, 128-row tile), behind an admission consensus: the
 //               workgroup keeps its tile's 128 x 64 panel of W in registers from the dots to
 //               the update (one pass over W), the tiles' partial dots meet through a per-subset
 //               counter barrier and every workgroup runs the block's MH steps itself: small

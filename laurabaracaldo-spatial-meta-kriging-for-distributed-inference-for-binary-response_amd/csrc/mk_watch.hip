@@ -10,8 +10,9 @@
 // appended to that file (a test runner that captures stderr still leaves it on disk).
 //
 // Off by default (the bench and the R package run without it): with it on, every launch costs a
-// second dispatch.  The device-side waits that exist (the opt-in cooperative sweep) have their own
-// bounded spins and error flag (mk_mcmc.hip); this names the launch when a stream stops moving.
+// second dispatch.  The device-side waits that exist (the multi-workgroup sweep, after its admission
+// consensus) have their own bounded spins and error flag (mk_mcmc.hip); this names the launch when a
+// stream stops moving.
 #include <hip/hip_runtime.h>
 #include <atomic>
 #include <chrono>
