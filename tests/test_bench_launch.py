@@ -88,3 +88,13 @@ def test_process_group_setup_output_stays_off_stdout(capfd):
     print('{"metric": 1}')
     out, err = capfd.readouterr()
     assert out == '{"metric": 1}\n' and "[Gloo]" in err
+
+
+def test_roofline_traffic_profile_matches_the_dominant_kernel():
+    """roofline.traffic comes from the committed PMC passes (profiles/pmc_chol_update.json): they must
+    be of the kernel the line names (the fused column update) and hold a positive byte count."""
+    import json
+    m = _bench()
+    doc = json.load(open(os.path.join(ROOT, "profiles", "pmc_chol_update.json")))
+    assert any(k.startswith("mk::k_chol_update_trsm") for k in doc["instances"])
+    assert m._pmc_traffic() == doc["hbm_bytes_per_launch"] > 0
