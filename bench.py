@@ -250,6 +250,21 @@ def hbm_subphases(kern, n_post, n_s):
     return out
 
 
+def inverse_roofline(k):
+    """k_inv_level's rate over the post-window pass: algorithmic flops (per level the full-by-
+    triangular and triangular-by-full products over each accepted factor's extent n_s; with the
+    diagonal tiles' inverses inside k_chol_diag they sum to n_s^3 / 3 per factor) over the summed
+    launch durations (one stream: the launches do not overlap)."""
+    if k["ms"] <= 0:
+        return None
+    tf = k["flops"] / (k["ms"] * 1e-3) / 1e12
+    return {"kernel": "k_inv_level (recursive-doubling W = L^-1 of the accepted factors)", "bound": "mfma",
+            "achieved": tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": tf / FP64_PEAK_TFLOPS,
+            "launches": k["launches"], "avg_launch_ms": k["ms"] / max(1, k["launches"]),
+            "algorithmic_flops_per_launch": k["flops"] / max(1, k["launches"]),
+            "source": "untimed post-window pass, every kernel kind evented"}
+
+
 def end_to_end(mk, d, K, devices=(0,)):
     """The whole reference script on this GPU (metakriging.reference_flow -> mk_meta_fit):
     partition (R's stream) -> glm -> 5,000 amcmc iterations of every subset with spPredict on the
@@ -466,7 +481,9 @@ def main():
     before = {name: ses.kernel_stats(i) for name, i in kinds}
     ses.profile(True)
     ses.run(n_post)
-    kern = {name: {"ms": ses.kernel_stats(i)["ms"] - before[name]["ms"]} for name, i in kinds}
+    kern = {name: {"ms": ses.kernel_stats(i)["ms"] - before[name]["ms"],
+                   "flops": ses.kernel_stats(i)["flops"] - before[name]["flops"],
+                   "launches": ses.kernel_stats(i)["launches"] - before[name]["launches"]} for name, i in kinds}
     dev_window = ses.outputs(quantiles=False, samples=True)["samples"][:n_cpu] if n_cpu else []
     ses.close()
     legs = {}
@@ -535,8 +552,15 @@ def main():
                    "subsets_per_gpu": per, "total_subsets": K_job, "streams_per_gpu": a.streams or 1,
                    "parallelism": f"subset-sharded x{world}"},
         "roofline": {"bound": "mfma", "kernel": "the column-update launches of the left-looking Cholesky (fp64 MFMA): "
-                               "k_chol_update_trsm (update + panel solve fused, 128-tiles) and k_chol_update "
-                               "(diagonal corrections; 128-tile and 64/32-sub-tile instances) together",
+                               "k_chol_update_trsm (column k's update of tiles k+1.. with the panel solve fused in "
+                               "its epilogue, plus the next diagonal tile's update by panels < k) and, on the unfused "
+                               "and split schedules, k_chol_update (128-tile and 64/32-sub-tile instances). The "
+                               "fused schedule's rank-128 diagonal correction runs inside k_chol_diag (KS_CHOL_DIAG, "
+                               "outside this union)",
+                     "flops_definition": "algorithmic: off-diagonal tile updates 2*rows*cols*depth, the diagonal "
+                                         "tile's update as a SYRK cols*(cols+1)*depth, the panel solve as a "
+                                         "triangular solve rows*cols^2, every factor clipped to its valid extent "
+                                         "n_s+1 (the kernels execute more: whole MFMA blocks of the triangles)",
                      "sub_tile_launch_share": sub_share,
                      "busy_ms_union": st["ms"], "launch_ms_summed": summed_ms,
                      "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
@@ -551,6 +575,8 @@ def main():
                                      "shared with those kernels, so frac understates the kernel's own rate"
                                      if la else "update launches run alone on the stream (sequential schedule)")},
         "sweep_fallbacks": sweep_fallbacks,   # multi-workgroup sweep only: subsets refused admission
+        # the second MFMA kernel: W = L^-1 of the accepted factors (k_inv_level), from the post-window pass
+        "roofline_inverse": inverse_roofline(kern["inverse"]),
         "kernels_ms_per_step": {k: v["ms"] / n_post for k, v in kern.items()},
         "kernels_ms_per_step_note": f"untimed post-window pass of {n_post} iterations, every kernel kind evented",
         # the HBM-bound sub-phases in GB/s, on algorithmic bytes per subset-iteration --

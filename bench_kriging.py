@@ -33,7 +33,8 @@ PKG = "laurabaracaldo-spatial-meta-kriging-for-distributed-inference-for-binary-
 FP64_PEAK_TFLOPS = 78.6
 
 
-def kriging_leg(mk, subs, coords_test, beta0, bt, kept=6, burn=14, tile=65536, kernel_events=True, subset_base=0):
+def kriging_leg(mk, subs, coords_test, beta0, bt, kept=6, burn=14, tile=65536, kernel_events=True, subset_base=0,
+                fit_chunk=0):
     """Tiled spPredict of `coords_test` from the subsets `subs` (n_s each): burn + kept iterations with
     the kept states recorded, then the replay over test-site tiles, timed.  Returns the result dict
     (draws/s, k_pred_var roofline, the configs[4] extrapolation).  bench.py runs it on the per-GPU
@@ -46,7 +47,11 @@ def kriging_leg(mk, subs, coords_test, beta0, bt, kept=6, burn=14, tile=65536, k
                            predict_tile=tile)
     with mk.Session(subs, cfg, coords_test=coords_test, subset_base=subset_base) as ses:
         t0 = time.perf_counter()
-        ses.run(n_samples)
+        if fit_chunk > 0:   # the fit in pieces of fit_chunk iterations (each mk_session_run ends with the device idle)
+            for i in range(0, n_samples, fit_chunk):
+                ses.run(min(fit_chunk, n_samples - i))
+        else:
+            ses.run(n_samples)
         t1 = time.perf_counter()
         if kernel_events:   # HIP events around every k_pred_var launch (the kriging GEMM)
             ses.profile(True, kinds=[mk.session.KS_PRED_VAR])
@@ -115,9 +120,17 @@ def main():
     ap.add_argument("--burn", type=int, default=14)
     ap.add_argument("--tile", type=int, default=65536)
     ap.add_argument("--kernel-events", type=int, default=1, help="HIP events around k_pred_var (0: off)")
+    ap.add_argument("--fit-chunk", type=int, default=0,
+                    help="run the fit in pieces of this many iterations, each ending with the device idle (0: one "
+                         "call). Under rocprofv3 --pmc (kernels serialised) one 16-iteration call queues more "
+                         "launches than the profiler's packet intercept survives (DESIGN.md 6)")
     ap.add_argument("--phi-window", type=int, default=1,
                     help="price the configs[4] extrapolation from a full 5,000-iteration fit's kept window (0: off)")
     a = ap.parse_args()
+    if os.environ.get("MK_SEGV_DIAG"):
+        # diagnostic (tools/segv_diag.c): a host SIGSEGV appends its PC, frames and the process maps here
+        import ctypes
+        ctypes.CDLL(os.path.join(ROOT, "tools", "segv_diag.so")).segv_diag_install(os.environ["MK_SEGV_DIAG"].encode())
     mk = importlib.import_module(PKG)
     S, ns = a.subsets, a.n_sub
     d = mk.synthetic.generate(S * ns, q=1, n_test=a.n_test, seed=20250114)
@@ -125,7 +138,7 @@ def main():
     subs = [dict(coords=d["coords"][i * ns:(i + 1) * ns], y=d["y"][i * ns:(i + 1) * ns], weights=np.ones(ns),
                  x=d["x"][i * ns:(i + 1) * ns]) for i in range(S)]
     res = kriging_leg(mk, subs, d["coords_test"], beta0, bt, kept=a.kept, burn=a.burn, tile=a.tile,
-                      kernel_events=bool(a.kernel_events))
+                      kernel_events=bool(a.kernel_events), fit_chunk=a.fit_chunk)
     if a.phi_window:
         # price the full job from the phi sequence of a full 1,251-sample kept window (the sample above
         # holds only a few kept states, the first always a refresh)

@@ -148,12 +148,19 @@ int mk_session_grids(mk_session* s, int32_t which, double* out, int32_t device_o
  * grids of all 1M sites never coexist. */
 int mk_session_tile_grids(mk_session* s, int32_t t0, double* out, int32_t device_out);
 /* Per-kernel timing (HIP events on the launching streams): launches, total ms and
- * algorithmic flops per kernel kind (0 Cholesky panel update, 128-tiles; 1 diagonal tile;
- * 2 panel trsm; 3 latent sweep; 4 R^-1 diagonal tiles; 5 whole iterations; 6 inverse levels;
- * 7 panel update, 64/32-sub-tiles; 8 kinds 0 + 7 with overlapping launches counted once;
- * 9 kriging GEMM k_pred_var; 10 candidate covariance assembly; 11 latent sweeps the multi-workgroup
- * kernel refused admission and its fallback ran -- launches = (subset, iteration) count, no timing).  mk_session_profile(s, enable) before mk_session_run:
- * enable 0 = off, 1 = every kind, otherwise a mask with bit (1 + kind) per kind
+ * algorithmic flops per kernel kind.  0: the 128-tile column-update launches -- k_chol_update_trsm
+ * (column k's update of tiles k+1.. with the panel solve fused in its epilogue, plus the next diagonal
+ * tile's update by panels < k; the default schedule) and k_chol_update<128> (unfused and split
+ * schedules); 1 diagonal tile k_chol_diag (in the fused schedule it also applies the rank-128
+ * diagonal correction by panel k-1, priced here); 2 panel trsm k_chol_trsm (panel 0, and the unfused
+ * schedules); 3 latent sweep; 4 R^-1 diagonal tiles; 5 whole iterations; 6 inverse levels
+ * k_inv_level (flops per level over the accepted factors, n_s^3/3 per factor with kind 1's diagonal
+ * inverses); 7 kind 0's 64/32-sub-tile instances; 8 kinds 0 + 7 with overlapping launches counted
+ * once; 9 kriging GEMM k_pred_var; 10 candidate covariance assembly; 11 latent sweeps the
+ * multi-workgroup kernel refused admission and its fallback ran -- launches = (subset, iteration)
+ * count, no timing).  Flops are algorithmic, not executed: GEMM tiles 2 m n k, the diagonal tile's
+ * update as a SYRK, solves and inverse products over their triangles.  mk_session_profile(s, enable)
+ * before mk_session_run: enable 0 = off, 1 = every kind, otherwise a mask with bit (1 + kind) per kind
  * bracketed (e.g. 2 << 0 = the panel update only; fewer events, less overhead). */
 int mk_session_profile(mk_session* s, int32_t enable);
 int mk_session_kernel_stats(const mk_session* s, int32_t which, int64_t* launches, double* total_ms, double* flops);

@@ -113,6 +113,7 @@ struct Timed {
   int which;
   hipEvent_t a, b;
   double flops;
+  int cnt = -1;   // >= 0: flops are per listed factor, times the device-side count copied to inv_cnt[cnt]
 };
 
 // One stream's share of the shard: views of the shard arrays starting at subset s0.
@@ -425,6 +426,11 @@ struct mk_session {
   bool prof = false;
   uint32_t prof_kinds = ~0u;   // kernel kinds bracketed by events while prof (bit per KS_ kind)
   std::vector<Timed> pending;
+  // KS_INV timing: the inverse's work list length lives on the device, so each timed inverse copies
+  // its count into a pinned slot in stream order; drain_timers prices the launches with it
+  static constexpr int INV_CNT_CAP = 65536;
+  int* inv_cnt = nullptr;
+  int inv_cnt_used = 0;
   Stat stats[NKSTAT];
 
   // Free one buffer allocated by alloc().
@@ -458,6 +464,7 @@ struct mk_session {
     if (device >= 0) hipSetDevice(device);
     for (auto& o : owned) hipStreamSynchronize(o.second);
     for (auto& t : pending) { hipEventDestroy(t.a); hipEventDestroy(t.b); }
+    if (inv_cnt) hipHostFree(inv_cnt);
     for (auto& g : groups) {
       if (g.done) hipEventDestroy(g.done);
       for (hipEvent_t e : g.ev) hipEventDestroy(e);
@@ -478,12 +485,12 @@ static hipEvent_t ev_new() {
 
 // Launch helper that optionally brackets a kernel with events on its stream.
 template <typename F>
-static void timed(mk_session* s, hipStream_t st, int which, double flops, F&& launch) {
+static void timed(mk_session* s, hipStream_t st, int which, double flops, F&& launch, int cnt = -1) {
   if (!s->prof || !((s->prof_kinds >> which) & 1u)) {
     launch();
     return;
   }
-  Timed t{which, ev_new(), ev_new(), flops};
+  Timed t{which, ev_new(), ev_new(), flops, cnt};
   hipEventRecord(t.a, st);
   launch();
   hipEventRecord(t.b, st);
@@ -496,6 +503,7 @@ static void drain_timers(mk_session* s) {
     hipEventSynchronize(t.b);
     float ms = 0.f;
     hipEventElapsedTime(&ms, t.a, t.b);
+    if (t.cnt >= 0) t.flops *= (double)s->inv_cnt[t.cnt];
     s->stats[t.which].launches += 1;
     s->stats[t.which].ms += ms;
     s->stats[t.which].flops += t.flops;
@@ -525,6 +533,7 @@ static void drain_timers(mk_session* s) {
     hipEventDestroy(t.b);
   }
   s->pending.clear();
+  s->inv_cnt_used = 0;
 }
 
 static inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
@@ -664,19 +673,42 @@ static void chol_diag(mk_session* s, Group& g, hipStream_t st, int h0, int hc, i
 // Algorithmic flops of the column-k update over panels [j0, j1) (trsm: of panel k) of tiles
 // [ia, ib): every (subset, outcome) factor counted over its own valid extent n_s + 1 (the
 // bordered row; padding excluded), so ragged subsets (MK.R:18: the last takes the remainder) are
-// priced exactly.  With a subset list (tiled kriging replay) the active subsets live on the device:
-// the count is then an upper bound (every subset).
+// priced exactly.  Algorithmic, not executed: an off-diagonal tile's update is a GEMM,
+// 2 rows cols depth; the diagonal tile's (tile k of column k) a SYRK, cols (cols + 1) depth; the
+// panel solve L(i,k) = C(i,k) L(k,k)^-T a triangular solve, rows cols^2 (the kernels skip most of the
+// triangle's zero MFMA blocks but not all of them: what they execute is more than this).  With a
+// subset list (tiled kriging replay) the active subsets live on the device: the count is then an
+// upper bound (every subset).
 static double panel_flops(mk_session* s, Group& g, int hc, int k, int ia, int ib, bool trsm, int j0 = 0, int j1 = -1) {
   if (j1 < 0) j1 = k;
   double fl = 0.0;
   for (int i = g.s0; i < g.s0 + g.S; ++i) {
     const double nv = (double)s->n_part[i] + 1.0;
-    const double rows = std::fmax(0.0, std::fmin(nv, (double)ib * MK_NB) - (double)ia * MK_NB);
     const double cols = std::fmin((double)MK_NB, std::fmax(0.0, nv - (double)k * MK_NB));
     const double depth = std::fmax(0.0, std::fmin((double)j1 * MK_NB, nv) - (double)j0 * MK_NB);
-    fl += trsm ? 2.0 * rows * MK_NB * MK_NB : 2.0 * rows * cols * depth;
+    const bool diag = ia <= k && k < ib;   // tile k of column k is in [ia, ib)
+    const double lo = (double)(diag ? k + 1 : ia) * MK_NB;
+    const double rows = std::fmax(0.0, std::fmin(nv, (double)ib * MK_NB) - lo);   // off-diagonal rows
+    if (trsm)
+      fl += rows * cols * cols;
+    else
+      fl += 2.0 * rows * cols * depth + (diag ? cols * (cols + 1.0) * depth : 0.0);
   }
   return fl * hc;
+}
+
+// Algorithmic flops of one factor's inverse level (k_inv_level, level sz, phase): over the pairs of
+// blocks T = tiles [T0, T0+sz), B = [T0+sz, T0+2sz) clipped to the extent n, phase 0 Y = L_BT W_TT is
+// a full-by-triangular product (|B| |T|^2), phase 1 W_BT = -W_BB Y a triangular-by-full one (|B|^2 |T|).
+// Summed over the levels with the diagonal tiles' inverses (k_chol_diag's) this is n^3 / 3.
+static double inv_level_flops(int n, int nt, int sz, int phase) {
+  double fl = 0.0;
+  for (int T0 = 0; T0 < nt; T0 += 2 * sz) {
+    const double t0 = (double)T0 * MK_NB, b0 = (double)(T0 + sz) * MK_NB, b1 = (double)(T0 + 2 * sz) * MK_NB;
+    const double bt = std::fmax(0.0, std::fmin((double)n, b0) - t0), bb = std::fmax(0.0, std::fmin((double)n, b1) - b0);
+    fl += phase == 0 ? bb * bt * bt : bb * bb * bt;
+  }
+  return fl;
 }
 
 // Cholesky of all candidates of outcomes h0 .. h0+hc-1 (candidate tiles in the free slot), left-
@@ -779,14 +811,33 @@ static void launch_cholesky(mk_session* s, Group& g, int h0, int hc, const int* 
 static void launch_trinv(mk_session* s, Group& g, int max_entries, const int* list, const int* count) {
   const int nt = s->nt;
   MK_LAUNCH(k_inv_copydiag, dim3(max_entries * nt * MK_CD_SPLIT), dim3(256), 0, g.stream, g.ms, list, count);
+  // profiled: the listed count in stream order into a pinned slot (drain_timers multiplies the
+  // per-factor flops below by it); no slot left -> the launches run untimed
+  int cnt = -1;
+  if (s->prof && ((s->prof_kinds >> KS_INV) & 1u)) {
+    if (!s->inv_cnt && hipHostMalloc((void**)&s->inv_cnt, mk_session::INV_CNT_CAP * sizeof(int)) != hipSuccess) {
+      (void)hipGetLastError();
+      s->inv_cnt = nullptr;
+    }
+    if (s->inv_cnt && s->inv_cnt_used < mk_session::INV_CNT_CAP) {
+      cnt = s->inv_cnt_used++;
+      hipMemcpyAsync(s->inv_cnt + cnt, count, sizeof(int), hipMemcpyDeviceToHost, g.stream);
+    }
+  }
   for (int sz = 1; sz < nt; sz *= 2) {
     const int npairs = (nt + 2 * sz - 1) / (2 * sz);
     // the grid is sized for every pair, but only the accepted candidates' factors are in the
     // list (about 40% at the amcmc target rate) and the level's K ranges are uneven: price the
     // launch at an eighth of its 128-tile grid (measured: 32 subsets 1.33 -> 1.16 ms per iteration)
     const int tm = tile_size((long)max_entries * npairs * sz * sz / 8);
-    for (int phase = 0; phase < 2; ++phase)
-      timed(s, g.stream, KS_INV, 0.0, [&] {
+    for (int phase = 0; phase < 2; ++phase) {
+      // per listed factor: the mean over the group's subsets (exact for equal subset sizes)
+      double per = 0.0;
+      if (cnt >= 0) {
+        for (int i = g.s0; i < g.s0 + g.S; ++i) per += inv_level_flops(s->n_part[i], nt, sz, phase);
+        per /= std::max(1, g.S);
+      }
+      auto launch = [&] {
         if (tm == 32)
           MK_LAUNCH(k_inv_level<32>, dim3(xcd_grid_h(max_entries, npairs * sz * sz * 16)), dim3(256), LDS_32,
                              g.stream, g.ms, list, count, sz, phase);
@@ -796,7 +847,12 @@ static void launch_trinv(mk_session* s, Group& g, int max_entries, const int* li
         else
           MK_LAUNCH(k_inv_level<128>, dim3(xcd_grid_h(max_entries, npairs * sz * sz)), dim3(256), LDS_128,
                              g.stream, g.ms, list, count, sz, phase);
-      });
+      };
+      if (cnt >= 0)
+        timed(s, g.stream, KS_INV, per, launch, cnt);
+      else
+        launch();     // not profiled, or no count slot (untimed: the stats' ms and flops stay paired)
+    }
   }
 }
 

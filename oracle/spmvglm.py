@@ -178,8 +178,12 @@ class Config:
                  phi_starting=None, phi_tuning=None, phi_unif=None,
                  A_starting=None, A_tuning=None, w_starting=0.0, w_tuning=0.5,
                  nu_starting=None, nu_tuning=None, nu_unif=None,
-                 K_IW_df=None, K_IW_S=None, burn_in=None, seed=20250114, link=LINK_LOGIT):
+                 K_IW_df=None, K_IW_S=None, burn_in=None, seed=20250114, link=LINK_LOGIT, beta_prior=None):
         self.q, self.p = q, p
+        # TEST-ONLY (tests/test_geweke.py): a proper N(mean, sd^2) prior per beta_j as (mean, sd) arrays.
+        # None is the reference's beta.Flat (MK.R:63) -- the sampler the device implements.
+        self.beta_prior = None if beta_prior is None else (np.asarray(beta_prior[0], float),
+                                                           np.asarray(beta_prior[1], float))
         self.link = int(link)
         self.cov_model = cov_model
         self.n_batch, self.batch_length = n_batch, batch_length
@@ -226,6 +230,13 @@ class Config:
 
 
 # ----------------------------------------------------------------- the sampler
+def beta_logprior(b, j, cfg):
+    """log N(b; mean_j, sd_j^2) up to a constant, for Config.beta_prior (test-only: the reference's beta
+    prior is flat, MK.R:63, and contributes nothing to the ratio)."""
+    mu, sd = cfg.beta_prior
+    return -0.5 * ((b - mu[j]) / sd[j]) ** 2
+
+
 _SWEEP_LIB = None
 
 
@@ -365,11 +376,13 @@ def fit_subset(coords, y, wt, X, cfg, subset=0, coords_test=None, record_w=False
         zs = philox.proposal_normal(key, js, s)
         logus = philox.accept_log_uniform(key, js, s)
 
-        # ---------------- 1. beta_j (flat prior): likelihood only
+        # ---------------- 1. beta_j (flat prior, MK.R:63): likelihood only
         for j in range(p):
             delta = np.exp(tune[o_beta + j]) * zs[o_beta + j]
             eta_c = eta + delta * X[:, j]
             ratio = np.sum(loglik_terms(y, wt, eta_c, cfg.link) - loglik_terms(y, wt, eta, cfg.link))
+            if cfg.beta_prior is not None:      # test-only proper prior (Geweke test)
+                ratio += beta_logprior(beta[j] + delta, j, cfg) - beta_logprior(beta[j], j, cfg)
             if logus[o_beta + j] <= ratio:
                 beta[j] += delta
                 eta = eta_c

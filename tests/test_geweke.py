@@ -23,15 +23,19 @@ K_21 / sqrt(K_11 K_22), phi_h and nu_h (Matern) with their squared distances fro
 midpoint (a Jacobian error piles mass at both edges of the support), the standardised latent field
 mean(w_h) / sqrt(K_hh) and mean(w_h^2) / K_hh, and mean(y).  Every |z| <= 4.5.
 
-Proper priors are required, so: beta is held at its true value (MK.R:63's beta.Flat is improper;
-its step is the likelihood-only ratio the w step also uses, and literal.py pins it), and the IW
+Proper priors are required, so: beta is held at its true value in the covariance cases (MK.R:63's
+beta.Flat is improper), and the case exp_q1_beta moves it under a TEST-ONLY proper prior
+beta_j ~ N(0, 1) (oracle Config.beta_prior: the flat-prior step -- the likelihood ratio over eta,
+the code the device replays -- plus the prior's log ratio); the IW
 hyperparameters are K.IW = (q + 5, 4 I) -- the same IW code as the reference's (q, 0.1 I), whose
 q = 1 form (inverse-gamma(0.5, 0.05): log K has sd 2.2, w's scale spans orders of magnitude) mixes
 too slowly for a test of this length.  No adaptation (one batch longer than the run): adaptation
 changes the proposal scale, not the target.
 
 Power: the same test with the phi Jacobian or the IW Jacobian's A -> K terms deleted from the
-oracle (monkeypatched inside the workers) must fail (max |z| > 6): the negative controls below.
+oracle (monkeypatched inside the workers), or with the beta prior's term dropped from the beta step
+(the chain then samples beta under a flat prior while the marginal-conditional side draws it from
+N(0, 1)), must fail (max |z| > 6): the negative controls below.
 """
 import multiprocessing as mp
 import os
@@ -51,6 +55,7 @@ CASES = {
     "exp_q1": dict(q=1, cov_model=0),
     "matern_q1": dict(q=1, cov_model=1),
     "lmc_q2": dict(q=2, cov_model=0),
+    "exp_q1_beta": dict(q=1, cov_model=0, beta=True),
 }
 
 
@@ -68,15 +73,18 @@ def _setup(case):
         X[a::q, 2 * a] = 1.0
         X[a::q, 2 * a + 1] = rng.normal(size=N_SITES)
     beta = np.array([0.3, -0.5, -0.2, 0.4][:p])
-    cfg = om.Config(q, p, beta, np.ones(p), cov_model=cov, n_batch=1, batch_length=10 ** 7, burn_in=10 ** 7,
-                    K_IW_df=q + 5.0, K_IW_S=4.0 * np.eye(q))
+    cfg = om.Config(q, p, beta, np.full(p, 0.5), cov_model=cov, n_batch=1, batch_length=10 ** 7, burn_in=10 ** 7,
+                    K_IW_df=q + 5.0, K_IW_S=4.0 * np.eye(q),
+                    beta_prior=(np.zeros(p), np.ones(p)) if c.get("beta") else None)
     return om, coords, X, beta, cfg
 
 
 def _joint(om, rng, coords, X, beta, cfg):
-    """One marginal-conditional draw: (A, phi, nu, w, y)."""
+    """One marginal-conditional draw: (beta, A, phi, nu, w, y); beta from its prior when it moves."""
     from scipy.stats import invwishart
     q = cfg.q
+    if cfg.beta_prior is not None:
+        beta = rng.normal(cfg.beta_prior[0], cfg.beta_prior[1])
     K = np.atleast_2d(invwishart.rvs(cfg.K_IW_df, cfg.K_IW_S, random_state=rng))
     A = np.linalg.cholesky(K)
     phi = rng.uniform(cfg.phi_a, cfg.phi_b)
@@ -84,12 +92,15 @@ def _joint(om, rng, coords, X, beta, cfg):
     C = om.lmc_covariance(coords, A, phi, nu, cfg.cov_model)
     w = np.linalg.cholesky(C + 1e-12 * np.eye(C.shape[0])) @ rng.normal(size=C.shape[0])
     y = rng.binomial(1, 1.0 / (1.0 + np.exp(-(X @ beta + w)))).astype(float)
-    return A, phi, nu, w, y
+    return beta, A, phi, nu, w, y
 
 
-def _features(A, phi, nu, w, y, q, cfg):
+def _features(beta, A, phi, nu, w, y, q, cfg):
     K = A @ A.T
     f = []
+    if cfg.beta_prior is not None:
+        for b in beta:
+            f += [b, b * b]
     for h in range(q):
         lk = np.log(K[h, h])
         # phi and nu: the mean and the spread about the prior's midpoint (a Jacobian error moves mass
@@ -107,8 +118,10 @@ def _features(A, phi, nu, w, y, q, cfg):
     return np.array(f)
 
 
-def _feature_names(q, matern):
+def _feature_names(q, matern, beta_p=0):
     names = []
+    for j in range(beta_p):
+        names += [f"beta{j}", f"beta{j}^2"]
     for h in range(q):
         names += [f"logK{h}", f"logK{h}^2", f"phi{h}", f"(phi{h}-mid)^2"]
         if matern:
@@ -133,6 +146,8 @@ def _bug(om, which):
             Kinv = Ainv.T @ Ainv
             return -0.5 * (df + q + 1.0) * logdetK - 0.5 * np.sum(S * Kinv.T), logdetK
         om.iw_logprior_A = iw_no_jac
+    elif which == "beta_prior":
+        om.beta_logprior = lambda b, j, cfg: 0.0
 
 
 def _chain(args):
@@ -145,9 +160,10 @@ def _chain(args):
         _bug(om, bug)
     q, matern = cfg.q, cfg.cov_model == om.COV_MATERN
     rng = np.random.default_rng([7, k, len(bug or "")])
-    A, phi, nu, w, y = _joint(om, rng, coords, X, beta, cfg)
+    beta, A, phi, nu, w, y = _joint(om, rng, coords, X, beta, cfg)
     n_mh = cfg.p + cfg.n_theta + N_SITES * q
-    tune = np.concatenate([np.full(cfg.p, -np.inf),                  # beta held (proposal sd 0)
+    moves = cfg.beta_prior is not None
+    tune = np.concatenate([np.log(np.sqrt(cfg.beta_tuning)) if moves else np.full(cfg.p, -np.inf),  # held: sd 0
                            np.log(np.sqrt(cfg.A_tuning)), np.log(np.sqrt(cfg.phi_tuning)),
                            np.log(np.sqrt(cfg.nu_tuning)) if matern else np.zeros(0),
                            np.full(N_SITES * q, np.log(np.sqrt(cfg.w_tuning)))])
@@ -156,7 +172,7 @@ def _chain(args):
         theta.append(om.logit(nu, cfg.nu_a, cfg.nu_b))
     state = dict(iteration=0, beta=beta.copy(), theta=np.concatenate(theta), w=w, tune=tune, accept=np.zeros(n_mh))
     ntri = q * (q + 1) // 2
-    acc = np.zeros_like(_features(A, phi, nu, w, y, q, cfg))
+    acc = np.zeros_like(_features(beta, A, phi, nu, w, y, q, cfg))
     for s in range(ITERS):
         r = om.fit_subset(coords, y, np.ones(N_SITES * q), X, cfg, subset=k, start=state, max_iter=s + 1,
                           quantiles=False)
@@ -166,8 +182,9 @@ def _chain(args):
         phi = om.logit_inv(th[ntri:ntri + q], cfg.phi_a, cfg.phi_b)
         nu = om.logit_inv(th[ntri + q:ntri + 2 * q], cfg.nu_a, cfg.nu_b) if matern else None
         w = state["w"]
+        beta = state["beta"]
         y = rng.binomial(1, 1.0 / (1.0 + np.exp(-(X @ beta + w)))).astype(float)
-        acc += _features(A, phi, nu, w, y, q, cfg)
+        acc += _features(beta, A, phi, nu, w, y, q, cfg)
     return acc / ITERS
 
 
@@ -189,7 +206,8 @@ def _z(case, bug=None):
 @pytest.mark.parametrize("case", sorted(CASES))
 def test_geweke_successive_conditional_matches_marginal_conditional(case):
     z, m_sc, m_mc = _z(case)
-    names = _feature_names(CASES[case]["q"], CASES[case]["cov_model"] == 1)
+    c = CASES[case]
+    names = _feature_names(c["q"], c["cov_model"] == 1, 2 * c["q"] if c.get("beta") else 0)
     report = {n: (round(float(a), 4), round(float(b), 4), round(float(c), 2)) for n, a, b, c in zip(names, m_sc, m_mc, z)}
     assert np.all(np.abs(z) <= 4.5), report
 
@@ -198,3 +216,8 @@ def test_geweke_successive_conditional_matches_marginal_conditional(case):
 def test_geweke_detects_a_deleted_jacobian(bug):
     z, _, _ = _z("exp_q1", bug)
     assert np.max(np.abs(z)) > 6.0, (bug, np.round(z, 2))
+
+
+def test_geweke_detects_a_dropped_beta_prior():
+    z, _, _ = _z("exp_q1_beta", "beta_prior")
+    assert np.max(np.abs(z)) > 6.0, np.round(z, 2)
