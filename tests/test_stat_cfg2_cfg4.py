@@ -17,11 +17,15 @@ replicate 0 runs the oracle fixture's Philox streams and replicates 1..15 are in
   * replicate 0 replays the oracle over all 1,000 iterations (adaptation across 20 batch ends, the
     K and nu chains' drift included): samples, per-subset grids and the combined grids within 1e-6;
   * Monte Carlo-error parity against INDEPENDENT oracle chains: tests/golden/stat/<case>_indep.npz
-    (tests/golden/stat/make_indep_replicates.py) holds 4 more oracle meta-fits of the same data on
-    global subsets 1,000 + rK .. -- streams no device replicate runs -- and their combined grids are
-    compared with the device's replicates 1..15 by a two-sample t statistic per (column, level),
-    t = (mean_oracle - mean_device) / (s_pooled sqrt(1/4 + 1/15)), 17 df: every parameter |t| <= 5;
-    over the w.predict (site, level) pairs at most 3 % with |t| > 3.5 and mean t^2 in [0.5, 2].
+    (tests/golden/stat/make_indep_replicates.py) holds R_O more oracle meta-fits of the same data on
+    global subsets 1,000 + rK .. -- streams no device replicate runs; R_O = 12 for cfg3_exp and
+    cfg4_lmc, 4 for cfg2_matern -- and their combined grids are compared with the device's replicates
+    1..15 by a two-sample t statistic per (column, level),
+    t = (mean_oracle - mean_device) / (s_pooled sqrt(1/R_O + 1/15)), R_O + 13 df: every parameter
+    |t| <= 5; over the w.predict (site, level) pairs at most 3 % with |t| > 3.5 and mean t^2 in
+    [0.5, 2].  Detectable shift: |t| > 5 needs a mean shift of 5 sqrt(1/12 + 1/15) = 1.94 replicate
+    standard deviations at R_O = 12 (2.9 at R_O = 4); a negative control (phi.Unif's upper bound
+    12 -> 10 on the device only) must fail the same criteria.
     (Round 4 compared the oracle's own fixture with replicates 1..15 -- but that fixture IS replicate
     0's chain, so the test measured the device's spread against itself.)
 CPU: the fixtures' own consistency (inputs regenerate, the combine is the sequential mean, the
@@ -42,6 +46,7 @@ PKG = "laurabaracaldo-spatial-meta-kriging-for-distributed-inference-for-binary-
 CASES = ("cfg2_matern", "cfg3_exp", "cfg4_lmc")
 LEVELS3 = (4, 99, 194)
 R_REP = 16
+NEG_CONTROL = ("phi_b", 10.0)     # the negative control's perturbed target (_perturbed)
 
 
 def _load(case):
@@ -98,22 +103,37 @@ def test_fixture_combine_is_the_sequential_mean(case):
 _cache = {}
 
 
-def _device_replicates(mk, case):
-    if case in _cache:
-        return _cache[case]
+def _perturbed(q, which):
+    """SamplerConfig overrides of a perturbed target (negative controls): phi.Unif's upper bound
+    (MK.R:63's 3/0.25 = 12) -> b, or K.IW's scale matrix (MK.R:64's 0.1 I) -> s I."""
+    kind, v = which
+    if kind == "phi_b":
+        return {"phi_unif": (np.full(q, 3.0 / 0.75), np.full(q, float(v)))}
+    if kind == "iw_s":
+        return {"K_IW_S": float(v) * np.eye(q)}
+    raise ValueError(kind)
+
+
+def _device_replicates(mk, case, perturb=None):
+    """R_REP device meta-fits of the case in one session; perturb = (kind, value) samples another
+    target (negative controls only, _perturbed)."""
+    key = (case, perturb)
+    if key in _cache:
+        return _cache[key]
     g = _load(case)
     subs = _subsets(g)
     K, q = int(g["K"]), int(g["q"])
+    kw = {} if perturb is None else _perturbed(q, perturb)
     cfg = mk.SamplerConfig(q, 2 * q, g["beta_starting"], g["beta_tuning"],
                            cov_model="matern" if int(g["cov_model"]) == 1 else "exponential",
-                           n_batch=int(g["n_batch"]), batch_length=int(g["batch_length"]), seed=int(g["seed"]))
+                           n_batch=int(g["n_batch"]), batch_length=int(g["batch_length"]), seed=int(g["seed"]), **kw)
     with mk.Session(subs * R_REP, cfg, coords_test=g["coords_test"]) as ses:
         ses.run(cfg.n_samples)
         out = ses.outputs(samples=True)
     res = np.stack([mk.combine(out["parameters"][r * K:(r + 1) * K]) for r in range(R_REP)])
     res2 = np.stack([mk.combine(out["w_predict"][r * K:(r + 1) * K]) for r in range(R_REP)])
-    _cache[case] = (g, out, res, res2)
-    return _cache[case]
+    _cache[key] = (g, out, res, res2)
+    return _cache[key]
 
 
 @pytest.mark.gpu
@@ -157,14 +177,33 @@ def _t2(a, b):
     return (a.mean(axis=0) - b.mean(axis=0)) / np.where(se > 0, se, np.inf)
 
 
+def _mc_criteria(ind, res, res2):
+    """The MC-error criteria on the device's replicates 1..15 against the independent oracle
+    replicates: (every parameter |t| <= 5, share of w.predict |t| > 3.5 <= 3 %, mean t^2 in [0.5, 2]),
+    each as a bool, plus the statistics."""
+    L = list(LEVELS3)
+    tp = _t2(ind["result"][:, L], res[1:, L])            # 3 levels x P parameters
+    tw = _t2(ind["result2_3"], res2[1:, L])              # 3 levels x q n_test columns
+    frac, mt2 = float(np.mean(np.abs(tw) > 3.5)), float(np.mean(tw ** 2))
+    return (bool(np.all(np.abs(tp) <= 5.0)), frac <= 0.03, 0.5 <= mt2 <= 2.0), (tp, frac, mt2)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", CASES)
 def test_independent_oracle_chains_within_mc_error_of_device(mk, case):
     g, _, res, res2 = _device_replicates(mk, case)
-    ind = _load_indep(case)
-    L = list(LEVELS3)
-    tp = _t2(ind["result"][:, L], res[1:, L])            # 3 levels x P parameters
-    assert np.all(np.abs(tp) <= 5.0), tp
-    tw = _t2(ind["result2_3"], res2[1:, L])              # 3 levels x q n_test columns
-    assert np.mean(np.abs(tw) > 3.5) <= 0.03, np.mean(np.abs(tw) > 3.5)
-    assert 0.5 <= np.mean(tw ** 2) <= 2.0, np.mean(tw ** 2)
+    ok, (tp, frac, mt2) = _mc_criteria(_load_indep(case), res, res2)
+    assert ok[0], tp
+    assert ok[1], frac
+    assert ok[2], mt2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["cfg3_exp", "cfg4_lmc"])
+def test_mc_parity_detects_a_perturbed_phi_prior(mk, case):
+    """Negative control: the same criteria must FAIL when the device samples
+    another target -- phi.Unif's upper bound 12 -> 10 (MK.R:63) -- against the unperturbed oracle
+    replicates (12 of them for these cases)."""
+    _, _, res, res2 = _device_replicates(mk, case, perturb=NEG_CONTROL)
+    ok, (tp, frac, mt2) = _mc_criteria(_load_indep(case), res, res2)
+    assert not all(ok), (np.round(tp, 2), frac, mt2)
