@@ -1481,10 +1481,6 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
       for (int i = 0; i < S; ++i) all_even = all_even && (s->n_part[i] % 2 == 0);
       s->sweep_lean = q == 1 ? (all_even ? 2 : 1) : 0;
       s->sweep_site_lds = sweep_site_lds_bytes(nmax, q, s->sweep_lean);
-      // MK_SWEEP_LDS_MIN (KB, experiment): reserve at least that much LDS per sweep workgroup, so no
-      // tile-GEMM workgroup (64 KB) shares its CU
-      const size_t lds_min = (size_t)std::max(0, std::min(156, tile_env("MK_SWEEP_LDS_MIN", 0))) * 1024;
-      s->sweep_site_lds = std::max(s->sweep_site_lds, lds_min);
       HIPCHK(hipFuncSetAttribute(sweep_site_kernel(q, s->sweep_site, s->sweep_lean),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)s->sweep_site_lds));
     }

@@ -46,7 +46,12 @@ PKG = "laurabaracaldo-spatial-meta-kriging-for-distributed-inference-for-binary-
 CASES = ("cfg2_matern", "cfg3_exp", "cfg4_lmc")
 LEVELS3 = (4, 99, 194)
 R_REP = 16
-NEG_CONTROL = ("phi_b", 10.0)     # the negative control's perturbed target (_perturbed)
+# the negative controls' perturbed targets (_perturbed): phi.Unif's upper bound 12 -> 8 (cfg4_lmc) or
+# -> 6.5 (cfg3_exp; the starting value 6 must stay inside).  tools/mc_power.py (profiles/r06/mc_power_*.jsonl) measured the criteria's power:
+# phi -> 10 and K.IW's scale x 2 pass at both geometries; cfg4_lmc also fails phi -> 8 (max |t| 8.9)
+# and K.IW x 10 (w.predict mean t^2 3.1); cfg3_exp passes phi -> 8 and K.IW x 10 -- its 1,000-
+# iteration chains of a weakly identified phi spread too widely between replicates
+NEG_CONTROL = {"cfg3_exp": ("phi_b", 6.5), "cfg4_lmc": ("phi_b", 8.0)}
 
 
 def _load(case):
@@ -202,8 +207,8 @@ def test_independent_oracle_chains_within_mc_error_of_device(mk, case):
 @pytest.mark.parametrize("case", ["cfg3_exp", "cfg4_lmc"])
 def test_mc_parity_detects_a_perturbed_phi_prior(mk, case):
     """Negative control: the same criteria must FAIL when the device samples
-    another target -- phi.Unif's upper bound 12 -> 10 (MK.R:63) -- against the unperturbed oracle
-    replicates (12 of them for these cases)."""
-    _, _, res, res2 = _device_replicates(mk, case, perturb=NEG_CONTROL)
+    another target -- phi.Unif's upper bound 12 -> NEG_CONTROL[case] (MK.R:63) -- against the
+    unperturbed oracle replicates (12 of them for these cases)."""
+    _, _, res, res2 = _device_replicates(mk, case, perturb=NEG_CONTROL[case])
     ok, (tp, frac, mt2) = _mc_criteria(_load_indep(case), res, res2)
     assert not all(ok), (np.round(tp, 2), frac, mt2)

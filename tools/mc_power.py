@@ -18,7 +18,10 @@ mk = importlib.import_module(t.PKG)
 out = []
 for case in ("cfg3_exp", "cfg4_lmc"):
     ind = t._load_indep(case)
-    for pert in (None, ("phi_b", 10.0), ("phi_b", 8.0), ("iw_s", 0.2), ("iw_s", 1.0)):
+    perts = [None, ("phi_b", 10.0), ("phi_b", 8.0), ("iw_s", 0.2), ("iw_s", 1.0)]
+    if len(sys.argv) > 1:   # e.g. phi_b:6,phi_b:7
+        perts = [None] + [(k, float(v)) for k, v in (x.split(":") for x in sys.argv[1].split(","))]
+    for pert in perts:
         _, _, res, res2 = t._device_replicates(mk, case, perturb=pert)
         ok, (tp, frac, mt2) = t._mc_criteria(ind, res, res2)
         rec = {"case": case, "perturb": pert, "criteria_pass": ok, "max_abs_t_param": float(np.max(np.abs(tp))),

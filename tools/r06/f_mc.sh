@@ -5,7 +5,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/r06f
 mkdir -p $O
-timeout -k 10 300 python -u tools/mc_power.py > $O/mc_power.jsonl 2> $O/mc_power.err || { echo "power probe failed"; tail -20 $O/mc_power.err; exit 1; }
+timeout -k 10 300 python -u tools/mc_power.py phi_b:6.5,phi_b:7,iw_s:10 > $O/mc_power.jsonl 2> $O/mc_power.err || { echo "power probe failed"; tail -20 $O/mc_power.err; exit 1; }
 python -c "
 import json
 for l in open('$O/mc_power.jsonl'):
