@@ -167,7 +167,8 @@ def window_leg(mk, d, idx, S, q, cov, beta0, bt, adapt_batches, warmup, steps):
             "window": f"{n_burn} burn-in + {steps - n_burn} kept iterations at {W + 1}-{W + steps} (after {A} "
                       f"adaptation + {W - A} warmup iterations)",
             "schedule": "lookahead" if la else "sequential",
-            "roofline": {"kernel": "k_chol_update (union of its launch intervals)", "achieved": tf,
+            "roofline": {"kernel": "column-update launches: k_chol_update_trsm / k_chol_update (union of their launch "
+                                   "intervals; algorithmic flops as the headline roofline's)", "achieved": tf,
                          "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": tf / FP64_PEAK_TFLOPS,
                          "note": "lookahead schedule: update launches share the chip with the main stream, so "
                                  "the fraction understates the kernel's own rate" if la else
@@ -446,7 +447,7 @@ def main():
     # the CPU baseline resumes the first chains from here: the state at the window's first iteration
     n_cpu = min(host["usable"], hi - lo) if want_cpu else 0
     cpu_states = [ses.chain_state(i) for i in range(n_cpu)]
-    # timed window: HIP events bracket only the roofline kernel (k_chol_update) on its stream
+    # timed window: HIP events bracket only the roofline kernel (the column-update launches) on its stream
     upd_kinds = [mk.session.KS_CHOL_UPDATE, mk.session.KS_CHOL_UPDATE_SUB]   # k_chol_update<128> + <64>/<32>
     ses.profile(not a.no_kernel_events, kinds=upd_kinds)
 

@@ -1466,8 +1466,13 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, s->sweep_mg_lds));
     HIPCHK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, c->device));
     const int mode = tile_env("MK_SWEEP", 0);
-    // the whole grid fits the chip at once (else admission would mostly fall back)
-    const bool coop_fits = (long)xcd_grid(S, nt) <= (long)per_cu * n_cu && nt <= 32;
+    // the whole grid fits at once (else admission would mostly fall back) -- on the CUs the sweep's
+    // stream may use: a one-group session can run the lookahead schedule, whose main stream leaves
+    // MK_LA_MASK CUs (default 32 with 8 hardware queues) to the candidates' chain
+    const bool one_group = (c->n_streams > 0 ? std::min((int)c->n_streams, S) : 1) <= 1;
+    const int mask_env = tile_env("MK_LA_MASK", -1);
+    const int la_mask = one_group ? (mask_env >= 0 ? mask_env : (hw_queues() >= 8 ? 32 : 0)) : 0;
+    const bool coop_fits = (long)xcd_grid(S, nt) <= (long)per_cu * std::max(1, n_cu - la_mask) && nt <= 32;
     const bool small_multi = q >= 2 && S <= 16;
     const bool site_fits = sweep_site_kernel(q, n_pad <= 8 * MK_SS_T ? 1 : 2) != nullptr && n_pad <= 16 * MK_SS_T &&
                            sweep_site_lds_bytes(nmax, q, q == 1) <= 156 * 1024;
