@@ -163,6 +163,10 @@ int mk_session_tile_grids(mk_session* s, int32_t t0, double* out, int32_t device
  * before mk_session_run: enable 0 = off, 1 = every kind, otherwise a mask with bit (1 + kind) per kind
  * bracketed (e.g. 2 << 0 = the panel update only; fewer events, less overhead). */
 int mk_session_profile(mk_session* s, int32_t enable);
+/* Bracket only the launches of every `every`-th iteration (iteration index % every == 0; default 1:
+ * all).  At small shards per-launch events cost measurably (32 subsets: ~4 % of the rate, 250: 0.5 %);
+ * a sample keeps the per-launch averages and costs a fraction of that. */
+int mk_session_profile_every(mk_session* s, int32_t every);
 int mk_session_kernel_stats(const mk_session* s, int32_t which, int64_t* launches, double* total_ms, double* flops);
 void mk_session_destroy(mk_session* s);
 /* Sessions alive in this process (a failed mk_session_create leaves none behind). */

@@ -88,6 +88,7 @@ EXPORTS = {
     "mk_session_tile_grids": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32]),
     "mk_session_set_kept_window": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32]),
     "mk_session_profile": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32]),
+    "mk_session_profile_every": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32]),
     "mk_session_kernel_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64),
                                                _dp, _dp]),
     "mk_session_destroy": (None, [ctypes.c_void_p]),

@@ -425,6 +425,8 @@ struct mk_session {
   std::vector<void*> allocs;
   bool prof = false;
   uint32_t prof_kinds = ~0u;   // kernel kinds bracketed by events while prof (bit per KS_ kind)
+  int prof_every = 1;          // bracket the launches of every prof_every-th iteration only
+  bool prof_iter = true;       // this iteration's launches are bracketed (mk_session_run)
   std::vector<Timed> pending;
   // KS_INV timing: the inverse's work list length lives on the device, so each timed inverse copies
   // its count into a pinned slot in stream order; drain_timers prices the launches with it
@@ -486,7 +488,7 @@ static hipEvent_t ev_new() {
 // Launch helper that optionally brackets a kernel with events on its stream.
 template <typename F>
 static void timed(mk_session* s, hipStream_t st, int which, double flops, F&& launch, int cnt = -1) {
-  if (!s->prof || !((s->prof_kinds >> which) & 1u)) {
+  if (!s->prof || !s->prof_iter || !((s->prof_kinds >> which) & 1u)) {
     launch();
     return;
   }
@@ -814,7 +816,7 @@ static void launch_trinv(mk_session* s, Group& g, int max_entries, const int* li
   // profiled: the listed count in stream order into a pinned slot (drain_timers multiplies the
   // per-factor flops below by it); no slot left -> the launches run untimed
   int cnt = -1;
-  if (s->prof && ((s->prof_kinds >> KS_INV) & 1u)) {
+  if (s->prof && s->prof_iter && ((s->prof_kinds >> KS_INV) & 1u)) {
     if (!s->inv_cnt && hipHostMalloc((void**)&s->inv_cnt, mk_session::INV_CNT_CAP * sizeof(int)) != hipSuccess) {
       (void)hipGetLastError();
       s->inv_cnt = nullptr;
@@ -1706,12 +1708,14 @@ extern "C" int mk_session_run(mk_session* s, int32_t n_iter) {
   s->launch_err = hipSuccess;
   hipError_t le = hipSuccess;
   for (int i = 0; i < n_iter; ++i) {
+    s->prof_iter = s->prof_every <= 1 || s->iter % s->prof_every == 0;
     run_iteration(s, s->iter);
     s->iter++;
     le = hipGetLastError();
     if (le == hipSuccess) le = s->launch_err;
     if (le != hipSuccess) break;
   }
+  s->prof_iter = true;   // launches outside the iterations (the tiled replay) follow prof alone
   if (swap_m) s->groups[0].stream = s->stream;
   // every stream is drained before an error returns: nothing of this run is left queued
   if (le != hipSuccess) {
@@ -1789,6 +1793,13 @@ extern "C" int mk_session_profile(mk_session* s, int32_t enable) {
   if (!s) return set_err(MK_E_ARG, "null session");
   s->prof = enable != 0;
   s->prof_kinds = (enable == 1) ? ~0u : ((uint32_t)enable >> 1);
+  return 0;
+}
+
+extern "C" int mk_session_profile_every(mk_session* s, int32_t every) {
+  if (!s) return set_err(MK_E_ARG, "null session");
+  if (every < 1) return set_err(MK_E_ARG, "every must be >= 1");
+  s->prof_every = every;
   return 0;
 }
 
