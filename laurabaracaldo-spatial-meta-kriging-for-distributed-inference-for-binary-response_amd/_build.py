@@ -21,15 +21,19 @@ def _stale():
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
-def build(force=False, verbose=False):
-    if not force and not _stale():
+def build(force=False, verbose=False, out=None, defines=()):
+    """libmk.so in-tree; out / defines (e.g. ["MK_TRI_SKIP=0"]): an A/B variant elsewhere, loaded
+    through MK_LIB (tools only -- the package always loads the in-tree library by default)."""
+    lib_path = out or LIB_PATH
+    if out is None and not force and not _stale():
         return LIB_PATH
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     objs = []
     procs = []
+    tag = "" if out is None else ".variant"
     for src in SOURCES:
-        obj = os.path.join(CSRC, os.path.splitext(src)[0] + ".o")
-        cmd = [hipcc] + FLAGS + ["-c", os.path.join(CSRC, src), "-o", obj]
+        obj = os.path.join(CSRC, os.path.splitext(src)[0] + tag + ".o")
+        cmd = [hipcc] + FLAGS + ["-D" + d for d in defines] + ["-c", os.path.join(CSRC, src), "-o", obj]
         procs.append((cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
         objs.append(obj)
     for cmd, p in procs:
@@ -39,13 +43,13 @@ def build(force=False, verbose=False):
             raise RuntimeError("hipcc failed: " + " ".join(cmd))
         if verbose and out:
             sys.stderr.write(out.decode(errors="replace"))
-    tmp = LIB_PATH + ".tmp"
+    tmp = lib_path + ".tmp"
     cmd = [hipcc, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", tmp] + objs + ["-ldl"]
     subprocess.check_call(cmd)
-    os.replace(tmp, LIB_PATH)
+    os.replace(tmp, lib_path)
     for o in objs:
         os.remove(o)
-    return LIB_PATH
+    return lib_path
 
 
 if __name__ == "__main__":

@@ -111,7 +111,14 @@ __device__ inline double frag(const double* img, int m, int k) {
 //               diagonal (column block > row block) are never read   (flag = tile is diagonal)
 //   SKIP_TRI_B  op(B) lower-triangular in (n, k) over one 128-deep K: chunk c only touches
 //               output column blocks >= c                             (flag = chunk index c)
-enum { SKIP_NONE = 0, SKIP_UPPER = 1, SKIP_TRI_B = 2 };
+//   SKIP_TRI_A  op(A) lower-triangular in (m, k) over the 128-deep K block starting at diag_tile
+//               (gemm_tile): chunk c' of that block only touches output row blocks >= c'
+//               (flag = c' inside the block, -1 elsewhere)
+//   SKIP_TRI_BL op(B) lower-triangular in (k, n) over the 128-deep K block starting at diag_tile:
+//               chunk c' of that block only touches output column blocks <= c'
+//               (flag = c' inside the block, SKIP_FLAG_NONE elsewhere)
+enum { SKIP_NONE = 0, SKIP_UPPER = 1, SKIP_TRI_B = 2, SKIP_TRI_A = 3, SKIP_TRI_BL = 4 };
+constexpr int SKIP_FLAG_NONE = 1 << 20;
 
 // MASK: fragments with chunk-relative k >= kvalid read as zero.
 template <int TM, int TN, bool NEG, bool A_MU, bool B_NU, int SKIP, bool MASK>
@@ -139,6 +146,8 @@ __device__ inline void mma_chunk(const double* As, const double* Bs, AccT<TM / 3
       for (int bn = 0; bn < BN; ++bn) {
         if (SKIP == SKIP_UPPER && flag && cb0 + wn * BN + bn > rb0 + wm * BM + bm) continue;
         if (SKIP == SKIP_TRI_B && flag > cb0 + wn * BN + bn) continue;
+        if (SKIP == SKIP_TRI_A && flag > rb0 + wm * BM + bm) continue;
+        if (SKIP == SKIP_TRI_BL && flag < cb0 + wn * BN + bn) continue;
         acc.v[bm][bn] = __builtin_amdgcn_mfma_f64_16x16x4f64(xb[bn], ya[bm], acc.v[bm][bn], 0, 0, 0);
       }
   }
@@ -150,7 +159,8 @@ __device__ inline void mma_chunk(const double* As, const double* Bs, AccT<TM / 3
 // (triangular operands) then stream the same chunks at the same time, so an XCD's L2
 // serves the shared panels once.  SAME: op(B) = op(A)^T read from the same memory (A'A
 // products, TM == TN): one DMA and one LDS image serve both fragments.
-// SKIP (see mma_chunk): SKIP_UPPER with diag_tile != 0; SKIP_TRI_B for K = 128.
+// SKIP (see mma_chunk): SKIP_UPPER with diag_tile != 0; SKIP_TRI_B for K = 128; SKIP_TRI_A /
+// SKIP_TRI_BL with diag_tile = the K offset of the triangular 128-deep block.
 // lds: gb_lds_bytes(TM, TN) of dynamic LDS.  Ends with a barrier (the caller may reuse the LDS).
 template <int TM, int TN, bool A_MU, bool B_NU, bool NEG = false, bool REV = false, bool SAME = false,
           int SKIP = SKIP_NONE, bool MASK = false>
@@ -175,8 +185,14 @@ __device__ inline void gemm_tile(const double* __restrict__ A, long sA, const do
     // the stage chunk c+1 overwrites was last read in iteration c-1, which every wave has left
     if (c + 1 < nch) issue(c + 1);
     const int k0 = k_of(c);
-    mma_chunk<TM, TN, NEG, A_MU, B_NU, SKIP, MASK>(st, SAME ? st : st + gb_img(TM), acc,
-                                                   SKIP == SKIP_TRI_B ? k0 / GB_K : diag_tile, kvalid_total - k0,
+    int flag = diag_tile;
+    if (SKIP == SKIP_TRI_B) {
+      flag = k0 / GB_K;
+    } else if (SKIP == SKIP_TRI_A || SKIP == SKIP_TRI_BL) {
+      const int rel = k0 - diag_tile;
+      flag = (rel >= 0 && rel < 128) ? rel / GB_K : (SKIP == SKIP_TRI_A ? -1 : SKIP_FLAG_NONE);
+    }
+    mma_chunk<TM, TN, NEG, A_MU, B_NU, SKIP, MASK>(st, SAME ? st : st + gb_img(TM), acc, flag, kvalid_total - k0,
                                                    rb0, cb0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();

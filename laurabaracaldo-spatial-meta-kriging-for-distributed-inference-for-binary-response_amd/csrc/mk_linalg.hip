@@ -979,6 +979,13 @@ __global__ __launch_bounds__(256) void k_chol_diag(MatSet ms, const int* __restr
 }
 
 // ---------------------------------------------------------------- inverse (W = L^-1, persistent)
+// MK_TRI_SKIP (compile time, default 1): the inverse levels skip the MFMA blocks of their diagonal W
+// tiles' zero triangles (SKIP_TRI_A / SKIP_TRI_BL, mk_gemm.hpp: ~15 % of the top level's MFMAs);
+// measured 0.570 -> 0.581 of peak over the inverse (profiles/r06/tri_skip).  0 builds the dense form
+// (A/B builds only: the same results, the skipped products are exact zeros).
+#ifndef MK_TRI_SKIP
+#define MK_TRI_SKIP 1
+#endif
 __device__ inline double* wmat(const MatSet& ms, int sh) { return ms.W + (long)sh * mat_elems(ms); }
 
 // Eight workgroups per 128-tile, each copying one eighth of it (16 rows' worth: 2,048
@@ -1043,13 +1050,17 @@ __global__ __launch_bounds__(256, 2) void k_inv_level(MatSet ms, const int* __re
     const double* Lm = mat_slot(ms, sh, cur);
     const int K = (B0 - j) * MK_NB;
     // K ranges [j, B0) share their end: descending chunks keep the tiles of a subset in step (L2 reuse)
-    gemm_tile<TM, TM, true, false, false, true>(Lm + i * MK_NB + ro + (long)j * MK_NB * ld, ld,
-                                                Wm + j * MK_NB + (long)j * MK_NB * ld + co, ld, K, K, acc, lds);
+    // W_TT's first K tile is W_jj, lower-triangular in (k, n): its chunk c' feeds column blocks <= c'
+    gemm_tile<TM, TM, true, false, false, true, false, MK_TRI_SKIP ? SKIP_TRI_BL : SKIP_NONE>(
+        Lm + i * MK_NB + ro + (long)j * MK_NB * ld, ld, Wm + j * MK_NB + (long)j * MK_NB * ld + co, ld, K, K, acc, lds,
+        0, ro / 16, sc * TM / 16);
     store_tile(Y + i * MK_NB + ro + (long)j * MK_NB * ld + co, ld, acc);
   } else {
     const int K = (i - B0 + 1) * MK_NB;
-    gemm_tile<TM, TM, true, false, true>(Wm + i * MK_NB + ro + (long)B0 * MK_NB * ld, ld,
-                                         Y + B0 * MK_NB + (long)j * MK_NB * ld + co, ld, K, K, acc, lds);
+    // W_BB's last K tile is W_ii, lower-triangular in (m, k): its chunk c' feeds row blocks >= c'
+    gemm_tile<TM, TM, true, false, true, false, false, MK_TRI_SKIP ? SKIP_TRI_A : SKIP_NONE>(
+        Wm + i * MK_NB + ro + (long)B0 * MK_NB * ld, ld, Y + B0 * MK_NB + (long)j * MK_NB * ld + co, ld, K, K, acc, lds,
+        K - MK_NB, ro / 16, sc * TM / 16);
     store_tile(Wm + i * MK_NB + ro + (long)j * MK_NB * ld + co, ld, acc);
   }
 }
@@ -1551,6 +1562,8 @@ __global__ __launch_bounds__(256, 2) void k_pred_var(Model md, MatSet ms, const 
     });
   } else {
     const double* PT = md.PT + (long)sh * md.n_pad * md.n_test_pad + tb * MK_NB;
+    // dense: skipping W_ii's zero triangle (SKIP_TRI_A, 5 % of the MFMAs) measured slower here, 0.736 vs
+    // 0.758 of peak (profiles/r06/tri_skip), unlike in the inverse levels
     gemm_128<true, true>(Wm + i * MK_NB, ld, PT, md.n_test_pad, K, K, acc, lds);
   }
   double* XK = md.XK + (long)sh * md.n_test_pad * md.n_pad + (long)tb * MK_NB * md.n_pad + i * MK_NB;
