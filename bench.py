@@ -504,7 +504,8 @@ def main():
         legs["configs[3]_lmc_share7"] = config_leg(mk, 3, a.adapt_batches, a.warmup, ls, subsets=7)
     e2e = None
     if world == 1 and not a.no_e2e:
-        e2e = end_to_end(mk, d, K, tuple(int(x) for x in a.e2e_devices.split(",")))
+        with _stdout_to_stderr():    # RCCL prints its version banner on stdout at communicator set-up
+            e2e = end_to_end(mk, d, K, tuple(int(x) for x in a.e2e_devices.split(",")))
     if world == 1 and not a.no_legs:
         # the 1M-site kriging leg in a fresh process (bench_kriging.py: the same kriging_leg on 32
         # subsets of n_s = 2,000 from the same generator): sessions that follow one another in a process

@@ -413,6 +413,12 @@ struct mk_session {
   bool la_ok = false;             // eligible (buffers allocated)
   bool la = false;                // in use
   int la_next = -1;               // iteration whose candidates are queued on la_c (-1: none)
+  // Sequential schedule, one group (MK_EARLY_COV, default on): iteration t+1's phi candidates are
+  // assembled (without the bordered row) on cov_st beside iteration t's sweep; iteration t+1 writes
+  // the row once its A step has produced u (k_cand_border) and factors as usual -- the same matrices.
+  int cov_pre = -1;               // iteration whose candidates cov_st has assembled (-1: none)
+  hipStream_t cov_st = nullptr;
+  hipEvent_t cov_ev[2] = {nullptr, nullptr};   // [0] main stream ready for it, [1] assembled
   int la_enq = 0;                 // panels of those candidates enqueued so far
   hipStream_t la_m = nullptr;     // MK_LA_MASK: CU-masked main stream of the lookahead iterations
   hipStream_t la_c = nullptr;     // created at the first lookahead run (an unused stream still takes a
@@ -472,6 +478,8 @@ struct mk_session {
       for (hipEvent_t e : g.ev) hipEventDestroy(e);
     }
     if (swept) hipEventDestroy(swept);
+    for (hipEvent_t e : cov_ev)
+      if (e) hipEventDestroy(e);
     for (hipEvent_t e : la_ev) hipEventDestroy(e);
     pool_return(owned);   // drained above; their waits on the destroyed events are satisfied
     for (void* p_ : allocs) hipFree(p_);
@@ -989,7 +997,13 @@ static void iteration_pre_sweep(mk_session* s, Group& g, int it) {
   const int nkinds = s->matern ? 2 : 1;
   // the q outcomes' (phi_h, nu_h) steps are independent given u: one batched pass per kind
   for (int which = 0; which < nkinds; ++which) {
-    timed(s, st, KS_COV, 0.0, [&] { launch_candidates(md, g.ms, st, S * q, 0, q, which, it); });
+    if (which == 0 && s->cov_pre == it) {   // assembled beside the previous sweep: the bordered row now
+      hipStreamWaitEvent(st, s->cov_ev[1], 0);
+      MK_LAUNCH(k_cand_border, dim3(S * q * ((s->n_pad + 255) / 256)), dim3(256), 0, st, md, g.ms, 0, q);
+      s->cov_pre = -1;
+    } else {
+      timed(s, st, KS_COV, 0.0, [&] { launch_candidates(md, g.ms, st, S * q, 0, q, which, it); });
+    }
     launch_cholesky(s, g, 0, q);
     MK_LAUNCH(k_theta_mh, dim3((S * q + 63) / 64), dim3(64), 0, st, md, g.ms, 0, q, which, it);
   }
@@ -997,6 +1011,18 @@ static void iteration_pre_sweep(mk_session* s, Group& g, int it) {
                      g.d_plist, g.d_pcount);
   launch_inverse(s, g);
   if (kept && !s->tiled) launch_pred_refresh(s, g);
+  // the next iteration's phi candidates depend only on this iteration's decisions (and on the proposal
+  // scale, which adapts after a batch's last iteration): assemble them beside the sweep -- a
+  // store-bound kernel beside a VALU-bound one -- into the free factor slots, which nothing reads
+  // from here to the next iteration's Cholesky (the inverse's scratch is Y)
+  if (s->cov_st && it + 1 < md.n_samples && (it + 1) % md.batch_length != 0) {
+    hipEventRecord(s->cov_ev[0], st);
+    hipStreamWaitEvent(s->cov_st, s->cov_ev[0], 0);
+    timed(s, s->cov_st, KS_COV, 0.0,
+          [&] { launch_candidates(md, g.ms, s->cov_st, S * q, 0, q, MK_CAND_NOBORDER, it + 1); });
+    hipEventRecord(s->cov_ev[1], s->cov_st);
+    s->cov_pre = it + 1;
+  }
 }
 
 static void iteration_post_sweep(mk_session* s, Group& g, int it) {
@@ -1698,6 +1724,12 @@ extern "C" int mk_session_run(mk_session* s, int32_t n_iter) {
         return set_err(MK_E_HIP, "lookahead main stream");
     }
   }
+  static const int early_cov = tile_env("MK_EARLY_COV", 1);
+  if (early_cov && !s->la && s->groups.size() == 1 && !s->cov_st) {
+    if (pool_stream(s->owned, &s->cov_st, s->device, SK_PLAIN) != hipSuccess) return set_err(MK_E_HIP, "covariance stream");
+    for (auto& e : s->cov_ev)
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return set_err(MK_E_HIP, "covariance event");
+  }
   const bool swap_m = s->la && s->la_m;
   if (swap_m) {   // the iterations' main-stream work on la_m, after everything queued on the session stream
     hipEventRecord(s->la_ev[s->nt + 1], s->stream);
@@ -1853,6 +1885,7 @@ static int predict_tile(mk_session* s, int t0, double* dq, mk_outputs* o) {
   hipStream_t st = s->stream;
   Group g = s->all;
   s->la_next = -1;   // the replay factors into the free slots: a lookahead candidate is gone
+  s->cov_pre = -1;   // and so is an early-assembled one
   HIPCHK(hipMemsetAsync((void*)md.coords_test, 0, (size_t)2 * T_pad * 8, st));
   HIPCHK(hipMemcpyAsync((void*)md.coords_test, s->d_ct_all + t0, (size_t)Tc * 8, hipMemcpyDeviceToDevice, st));
   HIPCHK(hipMemcpyAsync((void*)(md.coords_test + T_pad), s->d_ct_all + s->n_test_pad_all + t0, (size_t)Tc * 8,

@@ -31,6 +31,7 @@ __global__ void k_inv_level(MatSet ms, const int* list, const int* count, int sz
 __global__ void k_lauum(MatSet ms, const int* n_s, const int* list, const int* count);
 __global__ void k_qblocks(MatSet ms, const int* n_s, const int* list, const int* count);
 __global__ void k_take_border(Model md, MatSet ms, const int* list, const int* count, const double* zc);
+__global__ void k_cand_border(Model md, MatSet ms, int h0, int hc);
 __global__ void k_border_step(Model md, MatSet ms, int k);
 __global__ void k_nu_border(Model md, MatSet ms);
 __global__ void k_border_quad(Model md);

@@ -274,6 +274,20 @@ __global__ __launch_bounds__(256) void k_cov_candidate(Model md, MatSet ms, int 
 template __global__ void k_cov_candidate<MK_COV_EXPONENTIAL>(Model, MatSet, int, int, int, int, const int*, const int*);
 template __global__ void k_cov_candidate<MK_COV_MATERN>(Model, MatSet, int, int, int, int, const int*, const int*);
 
+// The bordered row of candidates assembled without it (MK_CAND_NOBORDER): R[n_s][C] = u_h[C], C < n_s,
+// the values k_cov_candidate writes with u known -- the sequential schedule assembles the next
+// iteration's candidates early, before the A step has produced u (run_iteration, cov_pre).
+__global__ __launch_bounds__(256) void k_cand_border(Model md, MatSet ms, int h0, int hc) {
+  const int per = (md.n_pad + 255) / 256;
+  const int e = blockIdx.x / per, C = (blockIdx.x % per) * 256 + threadIdx.x;
+  const int s = e / hc, h = h0 + e % hc;
+  if (s >= md.S) return;
+  const int ns = md.n_s[s];
+  if (C >= ns) return;
+  const int sh = s * md.q + h;
+  mat_slot(ms, sh, 1 - ms.cur[sh])[ns + (long)C * ms.ld] = md.u[(long)sh * md.n_pad + C];
+}
+
 // Plain matrix (no border) loaded by the host for the standalone Cholesky test path.
 
 // ---------------------------------------------------------------- Cholesky

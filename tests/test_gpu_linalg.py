@@ -153,7 +153,8 @@ def test_sub_tile_gemm_split_cholesky_and_multi_wg_sweep_are_bit_identical(tmp_p
     rank-128d correction on the critical stream; the accumulator passes through fp64 memory) at
     depths 1-3, the 64-site-block sweeps -- one workgroup per subset (MK_SWEEP=1, k_sweep), the
     fused column update + panel solve (k_chol_update_trsm, 128- and 64-row forms, the unsplit
-    factorisation; MK_CHOL_FUSED=0 the separate U, D, T launches), the split launches (3: k_sweep_step, one launch per block) and the
+    factorisation; MK_CHOL_FUSED=0 the separate U, D, T launches), the sequential schedule's next
+    candidates assembled beside the sweep (MK_EARLY_COV=0: in-line), the split launches (3: k_sweep_step, one launch per block) and the
     multi-workgroup kernel (2:
     k_sweep_mg behind its admission consensus, on both schedules; MK_ADM_SPINS=0 refuses the subsets
     whose workgroups do not arrive together, -1 every subset, and the k_sweep fallback queued behind
@@ -186,7 +187,9 @@ def test_sub_tile_gemm_split_cholesky_and_multi_wg_sweep_are_bit_identical(tmp_p
                                               (("128", "2", "0", "0", "2", "1"), {"MK_ADM_SPINS": "-1"}),
                                               (("128", "1", "0", "0", "2", "0"), {"MK_CHOL_FUSED": "0"}),
                                               (("128", "1", "0", "0", "2", "1"), {"MK_CHOL_FUSED": "0"}),
-                                              (("64", "1", "0", "0", "2", "1"), {"MK_CHOL_FUSED": "0"})]
+                                              (("64", "1", "0", "0", "2", "1"), {"MK_CHOL_FUSED": "0"}),
+                                              (("128", "1", "0", "0", "2", "0"), {"MK_EARLY_COV": "0"}),
+                                              (("128", "3", "1", "0", "3", "0"), {"MK_EARLY_COV": "0"})]
     for cfg, extra in runs:
         tile, sweep, split, gen, depth, la = cfg
         key = cfg + tuple(k_[3:] + v for k_, v in extra.items())
