@@ -1012,9 +1012,12 @@ static void iteration_pre_sweep(mk_session* s, Group& g, int it) {
   launch_inverse(s, g);
   if (kept && !s->tiled) launch_pred_refresh(s, g);
   // the next iteration's phi candidates depend only on this iteration's decisions (and on the proposal
-  // scale, which adapts after a batch's last iteration): assemble them beside the sweep -- a
-  // store-bound kernel beside a VALU-bound one -- into the free factor slots, which nothing reads
-  // from here to the next iteration's Cholesky (the inverse's scratch is Y)
+  // scale, which adapts after a batch's last iteration): assemble them on cov_st beside the sweep into
+  // the free factor slots, which nothing reads from here to the next iteration's Cholesky (the
+  // inverse's scratch is Y).  250 subsets, 40-step windows interleaved: 11,075-11,120 vs 11,034-11,063
+  // in line (profiles/r06/earlycov; both VALU-heavy, the sweep slows 0.95 -> 1.2 ms, the assembly
+  // stretches to 1.9 ms beside it); started at the decision instead, beside the inverse, 11,011-11,029
+  // (the inverse 4.65 -> 5.69 ms).
   if (s->cov_st && it + 1 < md.n_samples && (it + 1) % md.batch_length != 0) {
     hipEventRecord(s->cov_ev[0], st);
     hipStreamWaitEvent(s->cov_st, s->cov_ev[0], 0);
@@ -1725,7 +1728,8 @@ extern "C" int mk_session_run(mk_session* s, int32_t n_iter) {
     }
   }
   static const int early_cov = tile_env("MK_EARLY_COV", 1);
-  if (early_cov && !s->la && s->groups.size() == 1 && !s->cov_st) {
+  // (the inverse must have its own scratch Y: without it, it works in the free factor slots)
+  if (early_cov && !s->la && s->groups.size() == 1 && s->ms.Y && !s->cov_st) {
     if (pool_stream(s->owned, &s->cov_st, s->device, SK_PLAIN) != hipSuccess) return set_err(MK_E_HIP, "covariance stream");
     for (auto& e : s->cov_ev)
       if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return set_err(MK_E_HIP, "covariance event");
