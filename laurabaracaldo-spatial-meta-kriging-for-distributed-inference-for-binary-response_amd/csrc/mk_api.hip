@@ -384,6 +384,7 @@ struct mk_session {
   std::vector<double> bbox;       // [S][4] xmin xmax ymin ymax of each subset's sites (Matern table ranges)
   double* d_ct_all = nullptr;     // all test sites [2][n_test_pad_all] (tiled mode)
   int* d_slist = nullptr;         // tiled replay: per-outcome subset lists [q][S] + counts [q]
+  int* d_run_start = nullptr;     // tiled replay, q = 1: first window state of each subset's pending draws
   int* d_scount = nullptr;
   std::vector<Group> groups;      // the run-time split, one stream each
   // The latent sweep (launch_sweep).  sweep_site: the one-pass site sweep (default; row pairs per
@@ -1900,6 +1901,16 @@ static int predict_tile(mk_session* s, int t0, double* dq, mk_outputs* o) {
   mt.t_off = t0;
   mt.ntt = (Tc + MK_NB - 1) / MK_NB;   // a short last tile: only its valid 128-site column blocks
                                         // (strides stay those of the full tile, n_test_pad)
+  // q = 1 (MK_DRAW_RUNS, default on): a subset's draws wait until its X is about to change, and the
+  // states of one phi run then read X once per 4 (k_pred_draw_runs; the same bits as per state)
+  static const int runs_env = tile_env("MK_DRAW_RUNS", 1);
+  const bool runs = q == 1 && runs_env;
+  const int per = (Tc + 3) / 4;
+  if (runs) {
+    int rc;
+    if (!s->d_run_start && (rc = s->alloc(&s->d_run_start, (size_t)S))) return rc;
+    HIPCHK(hipMemsetAsync(s->d_run_start, 0, (size_t)S * sizeof(int), st));
+  }
   for (int j = 0; j < n_kept; ++j) {
     const int k = k_lo + j;   // kept state k = iteration kept0 + k
     mt.theta = md.kth + (long)k * S * md.n_theta;
@@ -1908,6 +1919,11 @@ static int predict_tile(mk_session* s, int t0, double* dq, mk_outputs* o) {
     const double* prev = j ? md.kth + (long)(k - 1) * S * md.n_theta : nullptr;
     MK_LAUNCH(k_kept_dirty, dim3(1), dim3(256), 0, st, mt, prev, s->d_slist, s->d_scount, g.d_plist,
                        g.d_pcount);
+    if (runs && j > 0) {   // the listed subsets' X changes now: their pending states first
+      MK_LAUNCH(k_pred_draw_runs, dim3(S * per), dim3(256), 0, st, mt, md.kz, md.kA, k_lo, g.d_plist, g.d_pcount,
+                s->d_run_start, j);
+      MK_LAUNCH(k_run_start, dim3((S + 255) / 256), dim3(256), 0, st, g.d_plist, g.d_pcount, s->d_run_start, j);
+    }
     for (int h = 0; h < q; ++h) {
       launch_candidates(mt, g.ms, st, S, h, 1, 2, 0, s->d_slist + h * S, s->d_scount + h);
       launch_cholesky(s, g, h, 1, s->d_slist + h * S, s->d_scount + h);
@@ -1916,8 +1932,12 @@ static int predict_tile(mk_session* s, int t0, double* dq, mk_outputs* o) {
     launch_trinv(s, g, S * q, g.d_plist, g.d_pcount);
     g.md = mt;
     launch_pred_refresh(s, g);
-    const int per = (Tc + 3) / 4;
-    MK_LAUNCH(k_pred_draw, dim3(S * per), dim3(256), 0, st, mt, md.kept0 + k, j);
+    if (!runs) MK_LAUNCH(k_pred_draw, dim3(S * per), dim3(256), 0, st, mt, md.kept0 + k, j);
+    HIPCHK(hipGetLastError());
+  }
+  if (runs && n_kept > 0) {   // every subset's last run
+    MK_LAUNCH(k_pred_draw_runs, dim3(S * per), dim3(256), 0, st, mt, md.kz, md.kA, k_lo, (const int*)nullptr,
+              (const int*)nullptr, s->d_run_start, n_kept);
     HIPCHK(hipGetLastError());
   }
   if (dq) {

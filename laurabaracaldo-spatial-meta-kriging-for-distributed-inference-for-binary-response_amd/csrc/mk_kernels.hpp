@@ -32,6 +32,9 @@ __global__ void k_lauum(MatSet ms, const int* n_s, const int* list, const int* c
 __global__ void k_qblocks(MatSet ms, const int* n_s, const int* list, const int* count);
 __global__ void k_take_border(Model md, MatSet ms, const int* list, const int* count, const double* zc);
 __global__ void k_cand_border(Model md, MatSet ms, int h0, int hc);
+__global__ void k_pred_draw_runs(Model md, const double* kz, const double* kA, int k_lo, const int* plist,
+                                 const int* pcount, const int* run_start, int j_end);
+__global__ void k_run_start(const int* plist, const int* pcount, int* run_start, int j);
 __global__ void k_border_step(Model md, MatSet ms, int k);
 __global__ void k_nu_border(Model md, MatSet ms);
 __global__ void k_border_quad(Model md);

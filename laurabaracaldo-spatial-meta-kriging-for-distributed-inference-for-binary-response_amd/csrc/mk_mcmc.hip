@@ -1498,6 +1498,84 @@ __global__ __launch_bounds__(256) void k_pred_draw(Model md, int iter, int kidx)
   }
 }
 
+// Tiled replay, q = 1: the draws of kept states [run_start[s], j_end) of the listed subsets (plist;
+// nullptr: every subset) from X as it stands -- the states of one phi run share X, so it is read once
+// per 4 states instead of once per state.  State j is window state j (iteration kept0 + k_lo + j);
+// its z and A are the recorded ones (kz, kA).  The per-state arithmetic is k_pred_draw's -- the same
+// loads, the same order of the two products per row pair, the same reduction -- so the same bits.
+__global__ __launch_bounds__(256) void k_pred_draw_runs(Model md, const double* __restrict__ kz,
+                                                        const double* __restrict__ kA, int k_lo,
+                                                        const int* __restrict__ plist, const int* __restrict__ pcount,
+                                                        const int* __restrict__ run_start, int j_end) {
+  const int per = (md.n_test + 3) / 4;
+  const int e = blockIdx.x / per;
+  if (e >= (plist ? *pcount : md.S)) return;
+  const int s = plist ? plist[e] : e;   // q = 1: the pair is the subset
+  const int t = (blockIdx.x % per) * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int j0 = run_start[s];
+  if (t >= md.n_test || j0 >= j_end) return;
+  const int ns = md.n_s[s];
+  const double* xk = md.XK + ((long)s * md.n_test_pad + t) * md.n_pad;
+  const double sd = sqrt(fmax(1.0 - md.s_pred[(long)s * md.n_test_pad + t], 0.0));
+  const int np2 = md.n_pad >> 1;
+  const Key key = subset_key(md, s);
+  for (int jg = j0; jg < j_end; jg += 4) {
+    const int nr = min(4, j_end - jg);
+    double a[4][4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) a[r][u] = 0.0;
+    for (int base = 0; base < ns; base += 512) {
+      d2 xv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int pr = min((base >> 1) + u * 64 + lane, np2 - 1);
+        xv[u] = *reinterpret_cast<const d2*>(xk + 2 * pr);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (r >= nr) break;
+        const double* zh = kz + ((long)(k_lo + jg + r) * md.S + s) * md.n_pad;
+        d2 zv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int pr = min((base >> 1) + u * 64 + lane, np2 - 1);
+          zv[u] = *reinterpret_cast<const d2*>(zh + 2 * pr);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int row = base + 2 * (u * 64 + lane);
+          a[r][u] += (row < ns) ? xv[u].x * zv[u].x : 0.0;
+          a[r][u] += (row + 1 < ns) ? xv[u].y * zv[u].y : 0.0;
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (r >= nr) break;
+      double acc = (a[r][0] + a[r][1]) + (a[r][2] + a[r][3]);
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+      if (lane == 0) {
+        const int j = jg + r, k = k_lo + j;
+        const double v = acc + sd * predict_normal(key, md.t_off + t, md.kept0 + k);
+        double o = 0.0;
+        o += v * kA[(long)k * md.S + s];
+        md.w_pred[((long)s * md.n_kept + j) * md.n_test + t] = o;
+      }
+    }
+  }
+}
+
+// run_start[s] = j for the listed subsets (their X is refreshed at window state j).
+__global__ __launch_bounds__(256) void k_run_start(const int* __restrict__ plist, const int* __restrict__ pcount,
+                                                   int* run_start, int j) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e < *pcount) run_start[plist[e]] = j;
+}
+
 // ---------------------------------------------------------------- 8. type-7 quantiles (MK.R:88-89)
 // One workgroup per (subset, column): bitonic sort of the kept values in LDS (dynamic: the next
 // power of two >= n_rows doubles, at most MK_QUANT_MAX = 128 KB), then R's quantile.default type 7:

@@ -154,7 +154,8 @@ def test_sub_tile_gemm_split_cholesky_and_multi_wg_sweep_are_bit_identical(tmp_p
     depths 1-3, the 64-site-block sweeps -- one workgroup per subset (MK_SWEEP=1, k_sweep), the
     fused column update + panel solve (k_chol_update_trsm, 128- and 64-row forms, the unsplit
     factorisation; MK_CHOL_FUSED=0 the separate U, D, T launches), the sequential schedule's next
-    candidates assembled beside the sweep (MK_EARLY_COV=0: in-line), the split launches (3: k_sweep_step, one launch per block) and the
+    candidates assembled beside the sweep (MK_EARLY_COV=0: in-line), the tiled replay's draws per
+    phi run (MK_DRAW_RUNS=0: per kept state), the split launches (3: k_sweep_step, one launch per block) and the
     multi-workgroup kernel (2:
     k_sweep_mg behind its admission consensus, on both schedules; MK_ADM_SPINS=0 refuses the subsets
     whose workgroups do not arrive together, -1 every subset, and the k_sweep fallback queued behind
@@ -189,7 +190,8 @@ def test_sub_tile_gemm_split_cholesky_and_multi_wg_sweep_are_bit_identical(tmp_p
                                               (("128", "1", "0", "0", "2", "1"), {"MK_CHOL_FUSED": "0"}),
                                               (("64", "1", "0", "0", "2", "1"), {"MK_CHOL_FUSED": "0"}),
                                               (("128", "1", "0", "0", "2", "0"), {"MK_EARLY_COV": "0"}),
-                                              (("128", "3", "1", "0", "3", "0"), {"MK_EARLY_COV": "0"})]
+                                              (("128", "3", "1", "0", "3", "0"), {"MK_EARLY_COV": "0"}),
+                                              (("128", "1", "0", "0", "2", "1"), {"MK_DRAW_RUNS": "0"})]
     for cfg, extra in runs:
         tile, sweep, split, gen, depth, la = cfg
         key = cfg + tuple(k_[3:] + v for k_, v in extra.items())
