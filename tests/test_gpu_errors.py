@@ -47,3 +47,27 @@ def test_bad_config_after_device_checks_frees_session(mk):
     with pytest.raises(mk.MkError):
         mk.Session([sub], cfg)
     assert lib.mk_session_count() == base
+
+
+def test_profile_every_samples_iterations_and_keeps_the_chain(mk):
+    """mk_session_profile_every (bench.py's sampled roofline events): bracketing the launches of every
+    k-th iteration only times a subset of the launches -- in proportion -- and, like any profiling, leaves
+    the chain unchanged; the inverse's flops follow the device-side count of accepted factors."""
+    d = mk.synthetic.generate(900, q=1, n_test=0, seed=4)
+    cfg = mk.SamplerConfig(1, 2, [0.0, 0.0], [0.05, 0.05], n_batch=1, batch_length=12, seed=8)
+    subs = [dict(coords=d["coords"][i * 300:(i + 1) * 300], y=d["y"][i * 300:(i + 1) * 300], weights=np.ones(300),
+                 x=d["x"][i * 300:(i + 1) * 300]) for i in range(3)]
+    res = {}
+    for every in (0, 1, 4):
+        with mk.Session(subs, cfg, lookahead=False) as ses:
+            if every:
+                ses.profile(True, every=every)
+            ses.run(cfg.n_samples)
+            res[every] = (ses.kernel_stats(mk.session.KS_CHOL_DIAG)["launches"], ses.kernel_stats(mk.session.KS_INV),
+                          ses.outputs(quantiles=False, samples=True)["samples"])
+    assert np.array_equal(res[1][2], res[0][2]) and np.array_equal(res[4][2], res[0][2])
+    assert res[0][0] == 0
+    # iterations 0, 4, 8 of 12: a quarter of the diagonal launches
+    assert res[4][0] * 4 == res[1][0]
+    inv = res[1][1]
+    assert inv["launches"] > 0 and inv["flops"] > 0 and inv["ms"] > 0
