@@ -110,6 +110,10 @@ int mk_session_create(const mk_problem* prob, const mk_config* cfg, mk_session**
 int mk_session_run(mk_session* s, int32_t n_iter);
 /* Iterations done so far. */
 int32_t mk_session_iteration(const mk_session* s);
+/* Test sites per kriging tile in use (0: fused kriging).  A tiled session takes the configured
+ * predict_tile, or the largest tile (halved in 256-site steps) whose kriging buffers fit in HBM;
+ * hosts replaying tile by tile (mk_session_tile_grids) step by this value. */
+int32_t mk_session_predict_tile(const mk_session* s);
 /* One subset's chain state after the iterations done so far, in spMvGLM's MH parameter order:
  * beta [p]; theta [n_theta] (A lower-tri col-major with log diagonal | logit phi | logit nu);
  * w [n_s q] location-major; tune [p + n_theta + n_s q] log proposal sds; accept [same] accept counts

@@ -79,6 +79,7 @@ EXPORTS = {
     "mk_session_create": (ctypes.c_int, [ctypes.POINTER(Problem), ctypes.POINTER(Config), ctypes.POINTER(ctypes.c_void_p)]),
     "mk_session_run": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32]),
     "mk_session_iteration": (ctypes.c_int32, [ctypes.c_void_p]),
+    "mk_session_predict_tile": (ctypes.c_int32, [ctypes.c_void_p]),
     "mk_session_chain_state": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, _dp, _dp, _dp, _dp, _dp]),
     "mk_session_set_lookahead": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32]),
     "mk_session_lookahead": (ctypes.c_int32, [ctypes.c_void_p]),

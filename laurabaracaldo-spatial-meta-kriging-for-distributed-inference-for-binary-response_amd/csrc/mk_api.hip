@@ -1278,22 +1278,52 @@ static int kriging_buffers(mk_session* s, int n_test_all, const double* coords_t
   s->n_test_all = n_test_all;
   s->n_test_pad_all = round_up(std::max(n_test_all, 1), 256);
   s->pred_tile = s->tiled ? std::min(s->tile_req, std::max(n_test_all, 1)) : n_test_all;
-  const int n_test = n_test_all > 0 ? s->pred_tile : 0;
-  const int n_test_pad = round_up(std::max(n_test, 1), 256);
-  md.n_test = n_test;
-  md.n_test_pad = n_test_pad;
-  md.ntt = n_test_pad / MK_NB;
   double* d_ct = nullptr;
   double* d_spt = nullptr;
   int rc;
-  if ((rc = s->alloc(&d_ct, (size_t)2 * n_test_pad)) || (rc = s->alloc(&s->d_ct_all, (size_t)2 * s->n_test_pad_all)) ||
-      (rc = s->alloc(&d_spt, (size_t)S)) ||
-      (rc = s->alloc(&md.s_pred, (size_t)S * q * n_test_pad)) ||
-      (rc = s->alloc(&md.s_part, (size_t)S * q * nt * n_test_pad)) ||
-      (n_test > 0 && !s->pred_gen && (rc = s->alloc(&md.PT, (size_t)S * q * n_pad * n_test_pad))) ||
-      (n_test > 0 && (rc = s->alloc(&md.XK, (size_t)S * q * n_pad * n_test_pad))) ||
-      (rc = s->alloc(&md.w_pred, (size_t)S * md.n_kept * q * std::max(n_test, 1))))
-    return rc;
+  // Tiled sessions whose buffers for the requested tile do not fit in HBM (X and P^T are n_pad x tile
+  // per pair, the draws n_kept x tile per subset: configs[4]'s 250 subsets at 65,536 sites on one GPU
+  // would need ~700 GB) take the largest tile that fits, halving it (in 256-site steps) until the
+  // allocations succeed.  The draws do not depend on the tile (keyed by the global site index);
+  // mk_session_predict_tile reports the tile in use.
+  // MK_KRIG_MEM_GB (optional): a budget for the tile's kriging buffers (tests; hosts sharing the GPU)
+  const char* cap_env = std::getenv("MK_KRIG_MEM_GB");
+  const double cap = (cap_env && *cap_env) ? std::atof(cap_env) * 1e9 : 0.0;
+  for (;;) {
+    const int n_test = n_test_all > 0 ? s->pred_tile : 0;
+    const int n_test_pad = round_up(std::max(n_test, 1), 256);
+    const double bytes = 8.0 * ((double)S * q * n_test_pad * (1.0 + nt + (n_test > 0 ? (s->pred_gen ? 1 : 2) * n_pad : 0)) +
+                                (double)S * md.n_kept * q * std::max(n_test, 1));
+    if (cap > 0.0 && bytes > cap && s->tiled && s->pred_tile > 256) {
+      s->pred_tile = std::max(256, round_up(s->pred_tile / 2, 256));
+      continue;
+    }
+    md.n_test = n_test;
+    md.n_test_pad = n_test_pad;
+    md.ntt = n_test_pad / MK_NB;
+    d_ct = d_spt = nullptr;
+    md.PT = md.XK = md.s_pred = md.s_part = md.w_pred = nullptr;
+    s->d_ct_all = nullptr;
+    if ((rc = s->alloc(&d_ct, (size_t)2 * n_test_pad)) || (rc = s->alloc(&s->d_ct_all, (size_t)2 * s->n_test_pad_all)) ||
+        (rc = s->alloc(&d_spt, (size_t)S)) ||
+        (rc = s->alloc(&md.s_pred, (size_t)S * q * n_test_pad)) ||
+        (rc = s->alloc(&md.s_part, (size_t)S * q * nt * n_test_pad)) ||
+        (n_test > 0 && !s->pred_gen && (rc = s->alloc(&md.PT, (size_t)S * q * n_pad * n_test_pad))) ||
+        (n_test > 0 && (rc = s->alloc(&md.XK, (size_t)S * q * n_pad * n_test_pad))) ||
+        (rc = s->alloc(&md.w_pred, (size_t)S * md.n_kept * q * std::max(n_test, 1)))) {
+      for (void* b : {(void*)d_ct, (void*)s->d_ct_all, (void*)d_spt, (void*)md.s_pred, (void*)md.s_part, (void*)md.PT,
+                      (void*)md.XK, (void*)md.w_pred})
+        s->release(b);
+      md.PT = md.XK = md.s_pred = md.s_part = md.w_pred = nullptr;
+      s->d_ct_all = nullptr;
+      if (rc == MK_E_NOMEM && s->tiled && s->pred_tile > 256) {
+        s->pred_tile = std::max(256, round_up(s->pred_tile / 2, 256));
+        continue;
+      }
+      return rc;
+    }
+    break;
+  }
   md.coords_test = d_ct;
   s->kbufs = {d_ct, s->d_ct_all, md.s_pred, md.s_part, md.PT, md.XK, md.w_pred, d_spt};
   {   // Matern kriging tables (k_pred_PT_matern): a bound on every subset-site to test-site distance
@@ -1315,7 +1345,7 @@ static int kriging_buffers(mk_session* s, int n_test_all, const double* coords_t
     HIPCHK(hipMemcpy(d_spt, hs.data(), (size_t)S * 8, hipMemcpyHostToDevice));
     md.span_pt = d_spt;
   }
-  HIPCHK(hipMemset(md.s_pred, 0, (size_t)S * q * n_test_pad * 8));
+  HIPCHK(hipMemset(md.s_pred, 0, (size_t)S * q * md.n_test_pad * 8));
   const int npa = s->n_test_pad_all;
   std::vector<double> hct((size_t)2 * npa, 0.0);
   for (int t = 0; t < n_test_all; ++t) {
@@ -1789,6 +1819,8 @@ extern "C" int mk_session_run(mk_session* s, int32_t n_iter) {
 }
 
 extern "C" int32_t mk_session_iteration(const mk_session* s) { return s ? s->iter : -1; }
+
+extern "C" int32_t mk_session_predict_tile(const mk_session* s) { return (s && s->tiled) ? s->pred_tile : 0; }
 
 // The chain state of one subset after the iterations run so far, in spMvGLM's MH order: beta (p),
 // theta (n_theta: A lower-tri col-major with log diagonal | logit phi | logit nu), w (n_s q,

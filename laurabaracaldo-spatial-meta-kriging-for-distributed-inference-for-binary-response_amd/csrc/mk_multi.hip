@@ -536,6 +536,17 @@ extern "C" int mk_meta_fit(const mk_problem* pr, const mk_config* c, const int32
       if ((rc = exchange_combine(nd, C, comb, h_comb, h_sum))) return rc;
     } else if (want_w) {
       const int T = info0.pred_tile;
+      // every shard replays the same tiles (the exchange combines tile by tile): a shard whose HBM
+      // made it take a smaller kriging tile than the others (mk_session_predict_tile) cannot follow
+      for (auto& x : nd.b)
+        if (x->ses) {
+          ShardInfo in{};
+          session_info(x->ses, &in);
+          if (in.pred_tile != T)
+            return fail(MK_E_NOMEM, "the shards took different kriging tiles (" + std::to_string(T) + " and " +
+                                           std::to_string(in.pred_tile) +
+                                           " test sites: HBM limits differ); pass predict_tile <= the smaller");
+        }
       for (int t0 = 0; t0 < n_test; t0 += T) {
         const long Ct = (long)q * std::min(T, n_test - t0);
         rc = nd.pool->run([&](int r) -> int {

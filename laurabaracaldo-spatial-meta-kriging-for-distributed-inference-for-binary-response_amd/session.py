@@ -204,7 +204,7 @@ class Session:
     def tile_grids(self, t0):
         """Tiled session (predict_tile > 0), after the run: (S, 200, q*Tc) w.predict grids of test
         sites [t0, t0 + Tc) -- one tile's kriging replay only (configs[4]'s per-tile combine)."""
-        T = self.cfg.predict_tile
+        T = self.predict_tile
         Tc = min(T, self.n_test - int(t0))
         out = np.zeros((self.S, self.q * Tc, _lib.N_LEVELS))
         check(self._lib.mk_session_tile_grids(self._h, int(t0), out.ctypes.data_as(ctypes.c_void_p), 0))
@@ -228,6 +228,12 @@ class Session:
     @property
     def iteration(self):
         return self._lib.mk_session_iteration(self._h)
+
+    @property
+    def predict_tile(self):
+        """Test sites per kriging tile in use (0: fused): cfg.predict_tile, or smaller where the tile's
+        kriging buffers would not fit in HBM (the draws do not depend on it)."""
+        return int(self._lib.mk_session_predict_tile(self._h))
 
     def profile(self, on=True, kinds=None, every=1):
         """Per-kernel HIP-event timing from the next run on: every kind, or only `kinds`

@@ -119,7 +119,7 @@ def main():
 
     t4 = time.perf_counter()
     par = np.stack(out["parameters"]) if out["parameters"] else np.zeros((0, 200, P))
-    tile = cfg.predict_tile
+    tile = ses.predict_tile if ses is not None else cfg.predict_tile   # the tile in use (HBM may shrink it)
 
     def tile_grids(t0):                           # this shard's grids of one test-site tile (kriging replay)
         tc = min(tile, c["n_test"] - t0)
@@ -136,6 +136,12 @@ def main():
             return g.transpose(1, 2)
 
         result = dmod.combine_sharded(shard_grids(0, P), K, dist, method=a.combine, device=dev, gpu=local)   # MK.R:123-127
+        if big:   # the exchange runs tile by tile: every rank must replay the same tiles
+            tl = torch.tensor([tile, -tile], dtype=torch.int64, device=dev)
+            dist.all_reduce(tl, op=dist.ReduceOp.MIN)
+            if int(tl[0]) != -int(tl[1]):
+                raise SystemExit(f"ranks took different kriging tiles ({int(tl[0])} .. {-int(tl[1])} test sites: HBM "
+                                 f"limits differ); pass --predict-tile {int(tl[0])} or less")
         if not big:
             result2 = dmod.combine_sharded(shard_grids(1, C), K, dist, method=a.combine, device=dev, gpu=local)
         else:

@@ -45,3 +45,39 @@ def test_cfg5_tiled_kriging_matches_oracle_on_sampled_sites(mk):
     np.testing.assert_allclose(dev["w_predict_sum"][:, sites], grid_sum, rtol=0, atol=TOL)
     # the sum over the two subsets is the sequential one (MK.R:129-132), over every site
     assert np.array_equal(dev["w_predict_sum"], dev["w_predict"][0] + dev["w_predict"][1])
+
+
+def test_kriging_tile_shrinks_to_fit_and_draws_do_not_change(mk, monkeypatch):
+    """A tiled session whose requested tile's kriging buffers do not fit (here a budget,
+    MK_KRIG_MEM_GB; in production HBM itself: configs[4]'s 250 subsets at 65,536 sites would need
+    ~700 GB on one GPU) takes the largest tile that fits, halving in 256-site steps, and reports it
+    (mk_session_predict_tile).  The draws are keyed by the global site index, so they equal a session
+    given that tile outright and the fused path, bit for bit; the grids likewise."""
+    n, n_test, S = 200, 20_000, 3
+    d = mk.synthetic.generate(S * n, q=1, n_test=n_test, seed=77, cov_model=0)
+    kw = dict(n_batch=2, batch_length=3, burn_in=4, seed=5)      # 6 iterations, 3 kept
+    subs = [dict(coords=d["coords"][s * n:(s + 1) * n], y=d["y"][s * n:(s + 1) * n], weights=np.ones(n),
+                 x=d["x"][s * n:(s + 1) * n]) for s in range(S)]
+
+    def run(tile, budget=None):
+        if budget is not None:
+            monkeypatch.setenv("MK_KRIG_MEM_GB", str(budget))
+        else:
+            monkeypatch.delenv("MK_KRIG_MEM_GB", raising=False)
+        cfg = mk.SamplerConfig(1, 2, np.zeros(2), np.full(2, 0.05), predict_tile=tile, **kw)
+        with mk.Session(subs, cfg, coords_test=d["coords_test"]) as ses:
+            t = ses.predict_tile
+            ses.run(cfg.n_samples)
+            out = ses.outputs(w_pred_samples=True)
+        monkeypatch.delenv("MK_KRIG_MEM_GB", raising=False)
+        return t, out
+
+    # 16,384 sites need 3 x 16,384 x (1 + 2 + 2 x 256) doubles + the draws = 0.2 GB; 0.06 GB allows 4,096
+    t_small, small = run(16384, budget=0.06)
+    assert t_small < 16384 and t_small % 256 == 0
+    t_ref, ref = run(t_small)
+    assert t_ref == t_small
+    _, fused = run(0)
+    for k in ("w_pred_samples", "w_predict"):
+        assert np.array_equal(small[k], ref[k]), k
+        assert np.array_equal(small[k], fused[k]), k

@@ -53,11 +53,12 @@ def main():
     subs = [mk.subset_data(d["y"], d["x"], 1.0, d["coords"], 1, idx[i]) for i in range(lo, hi)]
     cfg = mk.SamplerConfig(1, 2, beta0, bt, n_batch=100, batch_length=50, seed=20250114, predict_tile=a.tile)
     t["setup_s"] = time.perf_counter() - t1
-    ntiles = (a.n_test + a.tile - 1) // a.tile
     ta, tb = (int(x) for x in a.tiles.split(":"))
-    tb = min(tb, ntiles)
     per_tile = []
     with mk.Session(subs, cfg, coords_test=d["coords_test"], subset_base=lo) as ses:
+        tile = ses.predict_tile                      # the tile in use (HBM may shrink the request)
+        ntiles = (a.n_test + tile - 1) // tile
+        tb = min(tb, ntiles)
         t2 = time.perf_counter()
         for b in range(cfg.n_batch):                                               # MK.R:80-84
             ses.run(cfg.batch_length)
@@ -72,7 +73,7 @@ def main():
         refreshes = int(sum(1 + np.count_nonzero(np.diff(r)) for r in kept_phi))
         for ti in range(ta, tb):
             t4 = time.perf_counter()
-            g = ses.tile_grids(ti * a.tile)          # (S, 200, Tc): the replay of 1,251 kept states, MK.R:87-89
+            g = ses.tile_grids(ti * tile)            # (S, 200, Tc): the replay of 1,251 kept states, MK.R:87-89
             t5 = time.perf_counter()
             comb = mk.combine(g)                     # the shard's sequential mean of this tile (MK.R:127-133)
             t6 = time.perf_counter()
@@ -87,7 +88,7 @@ def main():
     sites = sum(p["sites"] for p in per_tile)
     draws = len(subs) * sites * cfg.kept
     rec = {"workload": f"configs[4] per-GPU share: rank {a.rank} of {a.gpus} (subsets {lo}..{hi - 1}, {hi - lo} of "
-                       f"K={a.K}, n_s={len(subs[0]['coords'])}), n={a.n}, {a.n_test} test sites in tiles of {a.tile}, "
+                       f"K={a.K}, n_s={len(subs[0]['coords'])}), n={a.n}, {a.n_test} test sites in tiles of {tile}, "
                        f"100 x 50 amcmc iterations, burn.in {cfg.burn_in}, {cfg.kept} kept states",
            "tiles": [ta, tb], "n_tiles": ntiles, "phases_s": t, "per_tile": per_tile,
            "x_refreshes_per_kept_sample": refreshes / kept_phi.size,
