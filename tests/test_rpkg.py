@@ -1,8 +1,13 @@
 """The R package skeleton (mkgpu/) stays consistent with include/mk.h.  R is not installed in
-this image, so the glue is never compiled or run here; these checks catch drift between the
-C-ABI, the .Call glue (mkgpu/src/mk_r.c) and the R wrappers (mkgpu/R/mkgpu.R) statically."""
+this image, so the glue is never linked or run here; these checks catch drift between the
+C-ABI, the .Call glue (mkgpu/src/mk_r.c) and the R wrappers (mkgpu/R/mkgpu.R) statically, and
+type-check the glue against mk.h with gcc over stub declarations of the R API (tests/rstub/)."""
 import os
 import re
+import shutil
+import subprocess
+
+import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -117,3 +122,18 @@ def test_onload_passes_the_queue_count_hip_started_with():
     assert 'reg.finalizer(.mk_exit, function(e) .Call("mk_r_shutdown"), onexit = TRUE)' in body
     assert '.Call("mk_r_shutdown")' in r[r.index(".onUnload"):]
     assert "mk_hip_initialized()" in c and "mk_shutdown();" in c
+
+
+@pytest.mark.skipif(shutil.which("gcc") is None, reason="gcc not on PATH")
+def test_glue_type_checks_against_the_c_abi():
+    """gcc -fsyntax-only over mk_r.c with tests/rstub/ standing in for R's headers (declarations of
+    the R entry points the glue uses, with R's signatures): every mk_* call, struct field and
+    pointer type the glue hands to include/mk.h is checked by the compiler.  Linking against R
+    and running under R stay untested (no R in the image)."""
+    cmd = ["gcc", "-fsyntax-only", "-std=c99", "-Wall", "-Werror=implicit-function-declaration",
+           "-Werror=incompatible-pointer-types", "-Werror=int-conversion", "-Werror=return-type",
+           "-I", os.path.join(ROOT, "tests", "rstub"), "-I", os.path.join(ROOT, "include"),
+           os.path.join(ROOT, "mkgpu", "src", "mk_r.c")]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    assert "warning" not in r.stderr, r.stderr
