@@ -91,7 +91,7 @@ extern "C" int mk_device_memory(int32_t device, int64_t* free_bytes, int64_t* to
 
 namespace {
 
-constexpr int NKSTAT = 12;
+constexpr int NKSTAT = 14;
 // KS_CHOL_UPDATE: the 128-tile panel-update launches (k_chol_update<128>); KS_CHOL_UPDATE_SUB:
 // the 64- / 32-sub-tile ones (small grids).  Together: the roofline kernel k_chol_update.
 // KS_UPDATE_BUSY: both, with the time of launches that overlap (the split schedule's bulk and
@@ -100,7 +100,11 @@ constexpr int NKSTAT = 12;
 // bound: only the pairs whose factor changed are in the list -- bench_kriging counts exactly).
 // KS_COV: the candidates' covariance assembly (k_cov_candidate, with k_matern_table for Matern).
 enum { KS_CHOL_UPDATE = 0, KS_CHOL_DIAG, KS_CHOL_TRSM, KS_SWEEP, KS_LAUUM, KS_ITER, KS_INV, KS_CHOL_UPDATE_SUB,
-       KS_UPDATE_BUSY, KS_PRED_VAR, KS_COV, KS_SWEEP_FALLBACK };
+       KS_UPDATE_BUSY, KS_PRED_VAR, KS_COV, KS_SWEEP_FALLBACK, KS_KRIG_CHEB, KS_KRIG_FALLBACK };
+// KS_KRIG_CHEB: tiles kriged by phi interpolation (predict_tile_cheb): launches = tiles, flops = exact
+// s evaluations ((subset, node or check point) pairs), total_ms = the largest check difference seen
+// (not a time).  KS_KRIG_FALLBACK: tiles whose check failed and were replayed exactly (launches), and
+// total_ms the largest failing difference.
 // KS_SWEEP_FALLBACK: launches = (subset, iteration) sweeps k_sweep_mg refused admission and its
 // k_sweep fallback ran (counted on the device, read at the end of every mk_session_run; no timing).
 
@@ -380,6 +384,13 @@ struct mk_session {
   int pred_tile = 0, n_test_all = 0, n_test_pad_all = 0;
   int tile_req = 0;               // predict_tile as configured
   int win_lo = 0, win_n = -1;     // tiled kriging: kept states [win_lo, win_lo + win_n) (-1: all)
+  // phi-interpolated tiled kriging (predict_tile_cheb): the window's g_k = W_k' z_k and phi_k, kept
+  // across tiles (made at the first tile after a run or a window change)
+  double* cg_G = nullptr;         // [win][S][n_pad]
+  double* cg_phi = nullptr;       // [win][S]
+  std::vector<double> cg_phi_h;
+  int cg_iter = -1, cg_lo = -1, cg_n = -1;
+  std::vector<double> span_pt_h;  // [S] bound on the subset-site to test-site distances (host copy)
   std::vector<void*> kbufs;       // the kriging buffers (re-sized by mk_session_set_test_sites)
   std::vector<double> bbox;       // [S][4] xmin xmax ymin ymax of each subset's sites (Matern table ranges)
   double* d_ct_all = nullptr;     // all test sites [2][n_test_pad_all] (tiled mode)
@@ -1344,6 +1355,7 @@ static int kriging_buffers(mk_session* s, int n_test_all, const double* coords_t
     }
     HIPCHK(hipMemcpy(d_spt, hs.data(), (size_t)S * 8, hipMemcpyHostToDevice));
     md.span_pt = d_spt;
+    s->span_pt_h = hs;
   }
   HIPCHK(hipMemset(md.s_pred, 0, (size_t)S * q * md.n_test_pad * 8));
   const int npa = s->n_test_pad_all;
@@ -1902,6 +1914,224 @@ struct DevBufs {
 
 }  // namespace
 
+// A tile's draws are in md.w_pred ([S][n_kept][Ct]): its 200-level grids into dq and, if
+// o->w_pred_samples, the draws to the host.  Returns after the stream is idle.
+static int tile_outputs(mk_session* s, int t0, double* dq, mk_outputs* o, int n_kept, int Ct) {
+  Model& md = s->md;
+  const int S = s->S, q = s->q;
+  const long C = (long)q * s->n_test_all;
+  hipStream_t st = s->stream;
+  if (dq) {
+    const int rq = launch_quantiles(S * Ct, st, md.w_pred, (long)n_kept * Ct, (long)Ct, n_kept, Ct, s->d_probs,
+                                    MK_N_LEVELS, dq);
+    if (rq) return rq;
+  }
+  if (o && o->w_pred_samples)   // per subset (C x kept) column-major
+    for (int i = 0; i < S; ++i)
+      HIPCHK(hipMemcpy2DAsync(o->w_pred_samples + (size_t)i * n_kept * C + (size_t)t0 * q, (size_t)C * 8,
+                              md.w_pred + (size_t)i * n_kept * Ct, (size_t)Ct * 8, (size_t)Ct * 8, n_kept,
+                              hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  return 0;
+}
+
+// Tile [t0, t0 + Tc) by phi interpolation (exponential, q = 1; mk_mcmc.hip section 11).  The kriging
+// variance s(t; phi) = rho_t' R(phi)^-1 rho_t is analytic in phi: it is computed exactly (the replay's
+// own kernels: candidate, Cholesky, inverse, X = W P^T) at nc Chebyshev nodes of each subset's kept
+// phi range and interpolated at every kept state's phi, instead of at every phi the chain visited
+// (0.39 refreshes per kept state at configs[4], i.e. ~490 per subset against nc = 12..21 here).  nc
+// grows with the range's width in units of the correlation decay over the largest distance involved,
+// (phi_hi - phi_lo) * d_max: 8 + ceil of it, at least 12 (measured in float64 on 2,000-site subsets
+// with clustered sites and test sites 1e-6 from a site: |error| <= 1e-14 over phi in [3.3, 11.8] with
+// 20 nodes, [6, 8] with 10).  Every tile also computes s exactly at the range's two ends and its
+// middle and compares the interpolant there over all its sites and subsets; a difference above
+// MK_KRIG_CHEB_TOL (default 1e-10) sends the tile to the exact replay (KS_KRIG_FALLBACK).  The mean
+// uses m_k(t) = rho_t(phi_k)' g_k, g_k = W_k' z_k, made once per kept window.  Against the exact
+// replay the draws agree to rounding and the interpolation's difference (tests/test_gpu_cfg5.py);
+// MK_KRIG_CHEB: 1 (default) where the nodes and checks cost fewer exact evaluations than the exact
+// replay's refreshes, -1 always, n > 1 always with n nodes, 0 never (the exact replay).
+// Returns 0 when the tile is done, -1 when the exact replay must run (not applicable, scratch
+// memory short, check failed), > 0 on an error.
+static int predict_tile_cheb(mk_session* s, int t0, double* dq, mk_outputs* o) {
+  Model& md = s->md;
+  const char* env = std::getenv("MK_KRIG_CHEB");
+  const int force_n = (env && *env) ? std::atoi(env) : 1;   // 0 exact, 1 auto, -1 always, n > 1 always, n nodes
+  if (force_n == 0 || s->q != 1 || md.cov_model != MK_COV_EXPONENTIAL) return -1;
+  const int S = s->S, nth = md.n_theta, n_pad = md.n_pad;
+  const int k_lo = s->win_lo, n_kept = s->win_n < 0 ? md.n_kept : s->win_n;
+  if (n_kept < 1 || (int)s->span_pt_h.size() != S) return -1;
+  const int T_pad = md.n_test_pad, Tc = std::min(s->pred_tile, s->n_test_all - t0);
+  hipStream_t st = s->stream;
+  Group g = s->all;
+  s->la_next = -1;   // the replay factors into the free slots
+  s->cov_pre = -1;
+  // 1. phi_k of the window's kept states (once per window)
+  if (s->cg_iter != s->iter || s->cg_lo != k_lo || s->cg_n != n_kept) {
+    s->release(s->cg_G);
+    s->release(s->cg_phi);
+    s->cg_G = s->cg_phi = nullptr;
+    s->cg_iter = -1;
+    if (s->alloc(&s->cg_phi, (size_t)n_kept * S)) return -1;
+    MK_LAUNCH(k_kept_phi, dim3((unsigned)(((long)n_kept * S + 255) / 256)), dim3(256), 0, st, md,
+              md.kth + (long)k_lo * S * nth, n_kept, s->cg_phi);
+    s->cg_phi_h.assign((size_t)n_kept * S, 0.0);
+    HIPCHK(hipMemcpyAsync(s->cg_phi_h.data(), s->cg_phi, (size_t)n_kept * S * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    s->cg_iter = s->iter;
+    s->cg_lo = k_lo;
+    s->cg_n = n_kept;
+  }
+  // 2. per subset: nodes over its kept phi range, then the three check points
+  const double pa = md.phi_a[0], pb = md.phi_b[0];
+  std::vector<int> nc(S);
+  std::vector<double> wts((size_t)S * MK_CHEB_MAX, 0.0);
+  std::vector<std::vector<double>> sphi(S);
+  int E = 0;
+  long evals = 0, refreshes = 0;
+  for (int i = 0; i < S; ++i) {
+    double lo = s->cg_phi_h[i], hi = lo;
+    refreshes += 1;
+    for (int j = 1; j < n_kept; ++j) {
+      const double v = s->cg_phi_h[(size_t)j * S + i];
+      refreshes += v != s->cg_phi_h[(size_t)(j - 1) * S + i];
+      lo = std::fmin(lo, v);
+      hi = std::fmax(hi, v);
+    }
+    const double mag = std::fmax(1.0, std::fabs(lo));
+    if (hi - lo < 1e-6 * mag) {   // a (nearly) fixed phi: a short interval around it
+      const double c = 0.5 * (lo + hi);
+      lo = c - 5e-7 * mag;
+      hi = c + 5e-7 * mag;
+    }
+    const double eps = (pb - pa) * 1e-9;
+    lo = std::fmax(lo, pa + eps);
+    hi = std::fmin(hi, pb - eps);
+    const double* bb = s->bbox.data() + 4 * i;
+    const double dmax = std::fmax(s->span_pt_h[i], std::hypot(bb[1] - bb[0], bb[3] - bb[2]));
+    const int n = force_n > 1 ? std::min(force_n, MK_CHEB_MAX)
+                              : std::max(12, std::min(MK_CHEB_MAX, 8 + (int)std::ceil((hi - lo) * dmax)));
+    nc[i] = n;
+    const double c = 0.5 * (lo + hi), h = 0.5 * (hi - lo);
+    for (int m = 0; m < n; ++m) {
+      const double ang = M_PI * (2.0 * m + 1.0) / (2.0 * n);
+      sphi[i].push_back(c + h * std::cos(ang));
+      wts[(size_t)i * MK_CHEB_MAX + m] = ((m & 1) ? -1.0 : 1.0) * std::sin(ang);
+    }
+    sphi[i].push_back(lo);
+    sphi[i].push_back(hi);
+    sphi[i].push_back(c);
+    E = std::max(E, n + MK_CHEB_CHECKS);
+    evals += n + MK_CHEB_CHECKS;
+  }
+  // auto (MK_KRIG_CHEB unset or 1): only where it saves exact evaluations -- the exact replay
+  // refreshes X at each subset's first state and wherever phi changed (a short window, e.g. the
+  // bench's 6-state kriging sample, refreshes less often than a range needs nodes)
+  if (force_n == 1 && evals >= refreshes) return -1;
+  // 3. g_k = W_k' z_k of the window's kept states (once per window): the exact replay's
+  //    factorisations where phi changed, then one W' z per state
+  if (!s->cg_G) {
+    if (s->alloc(&s->cg_G, (size_t)n_kept * S * n_pad)) return -1;
+    Model mt = md;
+    for (int j = 0; j < n_kept; ++j) {
+      const int k = k_lo + j;
+      mt.theta = md.kth + (long)k * S * nth;
+      const double* prev = j ? md.kth + (long)(k - 1) * S * nth : nullptr;
+      MK_LAUNCH(k_kept_dirty, dim3(1), dim3(256), 0, st, mt, prev, s->d_slist, s->d_scount, g.d_plist, g.d_pcount);
+      launch_candidates(mt, g.ms, st, S, 0, 1, 2, 0, s->d_slist, s->d_scount);
+      launch_cholesky(s, g, 0, 1, s->d_slist, s->d_scount);
+      MK_LAUNCH(k_flip_pairs, dim3((S + 255) / 256), dim3(256), 0, st, g.ms, g.d_plist, g.d_pcount);
+      launch_trinv(s, g, S, g.d_plist, g.d_pcount);
+      MK_LAUNCH(k_krig_g, dim3(S * (n_pad / 4)), dim3(256), 0, st, mt, g.ms, md.kz + (long)k * S * n_pad,
+                s->cg_G + (long)j * S * n_pad);
+      HIPCHK(hipGetLastError());
+    }
+  }
+  // slot e's theta (phi in the candidate's logit form; the device's phi of it is what counts) and
+  // its subset list (the subsets with that many slots)
+  std::vector<double> thn((size_t)E * S * nth, 0.0);
+  std::vector<int> lists((size_t)E * (S + 1), 0);
+  for (int e = 0; e < E; ++e) {
+    int cnt = 0;
+    for (int i = 0; i < S; ++i) {
+      const double ph = e < (int)sphi[i].size() ? sphi[i][e] : sphi[i][0];
+      thn[((size_t)e * S + i) * nth + md.ntri] = std::log((ph - pa) / (pb - ph));
+      if (e < (int)sphi[i].size()) lists[(size_t)e * (S + 1) + cnt++] = i;
+    }
+    lists[(size_t)e * (S + 1) + S] = cnt;
+  }
+  DevBufs scratch;
+  double* d_thn = scratch.get<double>(thn.size());
+  double* d_nphi = scratch.get<double>((size_t)E * S);
+  double* d_wts = scratch.get<double>(wts.size());
+  int* d_nc = scratch.get<int>((size_t)S);
+  int* d_lists = scratch.get<int>(lists.size());
+  double* d_Sn = scratch.get<double>((size_t)E * S * T_pad);
+  unsigned long long* d_err = scratch.get<unsigned long long>(1);
+  if (!d_thn || !d_nphi || !d_wts || !d_nc || !d_lists || !d_Sn || !d_err) return -1;
+  HIPCHK(hipMemcpyAsync(d_thn, thn.data(), thn.size() * 8, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(d_wts, wts.data(), wts.size() * 8, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(d_nc, nc.data(), (size_t)S * sizeof(int), hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(d_lists, lists.data(), lists.size() * sizeof(int), hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemsetAsync(d_Sn, 0, (size_t)E * S * T_pad * 8, st));
+  HIPCHK(hipMemsetAsync(d_err, 0, 8, st));
+  // 4. the tile's sites (as predict_tile), the slots' phi, exact s at every slot
+  HIPCHK(hipMemsetAsync((void*)md.coords_test, 0, (size_t)2 * T_pad * 8, st));
+  HIPCHK(hipMemcpyAsync((void*)md.coords_test, s->d_ct_all + t0, (size_t)Tc * 8, hipMemcpyDeviceToDevice, st));
+  HIPCHK(hipMemcpyAsync((void*)(md.coords_test + T_pad), s->d_ct_all + s->n_test_pad_all + t0, (size_t)Tc * 8,
+                        hipMemcpyDeviceToDevice, st));
+  Model mt = md;
+  mt.n_kept = n_kept;
+  mt.n_test = Tc;
+  mt.t_off = t0;
+  mt.ntt = (Tc + MK_NB - 1) / MK_NB;
+  MK_LAUNCH(k_kept_phi, dim3((unsigned)(((long)E * S + 255) / 256)), dim3(256), 0, st, md, d_thn, E, d_nphi);
+  for (int e = 0; e < E; ++e) {
+    int* L = d_lists + (size_t)e * (S + 1);
+    int* C = L + S;
+    mt.theta = d_thn + (size_t)e * S * nth;
+    mt.s_pred = d_Sn + (size_t)e * S * T_pad;
+    launch_candidates(mt, g.ms, st, S, 0, 1, 2, 0, L, C);
+    launch_cholesky(s, g, 0, 1, L, C);
+    MK_LAUNCH(k_flip_pairs, dim3((S + 255) / 256), dim3(256), 0, st, g.ms, L, C);
+    launch_trinv(s, g, S, L, C);
+    Group gp = g;
+    gp.md = mt;
+    gp.d_plist = L;
+    gp.d_pcount = C;
+    launch_pred_refresh(s, gp);
+    HIPCHK(hipGetLastError());
+  }
+  // 5. the check, then the draws
+  ChebK ck;
+  ck.Sn = d_Sn;
+  ck.nphi = d_nphi;
+  ck.wts = d_wts;
+  ck.nc = d_nc;
+  ck.T_pad = T_pad;
+  const int nb = (Tc + 255) / 256;
+  MK_LAUNCH(k_cheb_check, dim3(S * nb), dim3(256), 0, st, mt, ck, d_err);
+  unsigned long long eb = 0;
+  HIPCHK(hipMemcpyAsync(&eb, d_err, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  double emax;
+  std::memcpy(&emax, &eb, 8);
+  const char* tenv = std::getenv("MK_KRIG_CHEB_TOL");
+  const double tol = (tenv && *tenv) ? std::atof(tenv) : 1e-10;
+  if (!(emax <= tol)) {
+    Stat& f = s->stats[KS_KRIG_FALLBACK];
+    f.launches += 1;
+    f.ms = std::fmax(f.ms, std::isfinite(emax) ? emax : 1e300);
+    return -1;
+  }
+  MK_LAUNCH(k_pred_cheb_draw, dim3(S * nb), dim3(256), 0, st, mt, ck, s->cg_G, s->cg_phi, md.kA, k_lo);
+  HIPCHK(hipGetLastError());
+  Stat& c = s->stats[KS_KRIG_CHEB];
+  c.launches += 1;
+  c.flops += (double)evals;
+  c.ms = std::fmax(c.ms, emax);
+  return tile_outputs(s, t0, dq, o, n_kept, s->q * Tc);
+}
+
 // spPredict after the fit (MK.R:87-89) over test-site tiles: replays the kriging of every kept
 // iteration from the recorded chain states (z, theta, A).  A factor is recomputed only where
 // (phi, nu) changed since the previous kept sample, with the same kernels and inputs as in the
@@ -1912,6 +2142,8 @@ struct DevBufs {
 // HBM, on s->stream) and, if o->w_pred_samples, its draws to the host.  Returns after the stream
 // is idle.
 static int predict_tile(mk_session* s, int t0, double* dq, mk_outputs* o) {
+  const int rc_cheb = predict_tile_cheb(s, t0, dq, o);
+  if (rc_cheb >= 0) return rc_cheb;
   Model& md = s->md;
   const int S = s->S, q = s->q;
   const int k_lo = s->win_lo, n_kept = s->win_n < 0 ? md.n_kept : s->win_n;   // kept states replayed
@@ -1972,18 +2204,7 @@ static int predict_tile(mk_session* s, int t0, double* dq, mk_outputs* o) {
               (const int*)nullptr, s->d_run_start, n_kept);
     HIPCHK(hipGetLastError());
   }
-  if (dq) {
-    const int rq = launch_quantiles(S * Ct, st, md.w_pred, (long)n_kept * Ct, (long)Ct, n_kept, Ct, s->d_probs,
-                                    MK_N_LEVELS, dq);
-    if (rq) return rq;
-  }
-  if (o && o->w_pred_samples)   // per subset (C x kept) column-major
-    for (int i = 0; i < S; ++i)
-      HIPCHK(hipMemcpy2DAsync(o->w_pred_samples + (size_t)i * n_kept * C + (size_t)t0 * q, (size_t)C * 8,
-                              md.w_pred + (size_t)i * n_kept * Ct, (size_t)Ct * 8, (size_t)Ct * 8, n_kept,
-                              hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
-  return 0;
+  return tile_outputs(s, t0, dq, o, n_kept, Ct);
 }
 
 static int predict_tiled(mk_session* s, mk_outputs* o) {

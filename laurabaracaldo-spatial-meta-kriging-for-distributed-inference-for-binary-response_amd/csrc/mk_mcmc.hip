@@ -1691,4 +1691,141 @@ __global__ __launch_bounds__(256) void k_flip_pairs(MatSet ms, const int* __rest
   if (e < *pcount) ms.cur[plist[e]] ^= 1;
 }
 
+// ---------------------------------------------------------------- 11. phi-interpolated tiled kriging
+// (exponential, q = 1; mk_api.hip predict_tile_cheb).  spPredict's draw for kept state k at test site t
+// is w*_k(t) = A_k (m_k(t) + sqrt(1 - s(t; phi_k)) e), with m_k(t) = rho_t(phi_k)' R(phi_k)^-1 u_k and
+// s(t; phi) = rho_t(phi)' R(phi)^-1 rho_t(phi).  The exact replay recomputes X = W P^T, i.e. s at every
+// phi the chain visited (0.39 refreshes per kept state at configs[4]).  s is an analytic function of
+// phi on the kept range: it is interpolated instead from exact values at Chebyshev nodes of that range
+// (barycentric form, nodes of the first kind), and every tile checks the interpolant against exact
+// values at the range's two ends and its middle before any draw uses it.  The mean needs no X:
+// m_k(t) = rho_t(phi_k)' g_k with g_k = W_k' z_k (z_k recorded, W_k the state's inverse factor).
+
+// phis[j][s] = phi of record j (th: [n][S][n_theta] records): the candidate assembly's formula
+// (candidate_theta, which = 2), so a record's phi here is bit for bit the one its factor used.
+__global__ __launch_bounds__(256) void k_kept_phi(Model md, const double* __restrict__ th, int n,
+                                                  double* __restrict__ phis) {
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (long)n * md.S) return;
+  phis[e] = logit_inv(th[e * md.n_theta + md.ntri], md.phi_a[0], md.phi_b[0]);
+}
+
+// g = W' z for every subset (q = 1): g_i = sum_{i <= r < n_s} W[r, i] z_r, one wave per column i
+// (W column-major: the wave's loads are contiguous); g_i = 0 for i >= n_s.
+__global__ __launch_bounds__(256) void k_krig_g(Model md, MatSet ms, const double* __restrict__ z,
+                                                double* __restrict__ g) {
+  const int per = md.n_pad / 4;
+  const int s = blockIdx.x / per;
+  const int i = (blockIdx.x % per) * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int ns = md.n_s[s];
+  const long ld = ms.ld;
+  const double* Wc = ms.W + (long)s * ld * ld + (long)i * ld;
+  const double* zs = z + (long)s * md.n_pad;
+  double a0 = 0.0, a1 = 0.0;
+  if (i < ns) {
+    for (int r = i + lane; r < ns; r += 128) {
+      a0 += Wc[r] * zs[r];
+      if (r + 64 < ns) a1 += Wc[r + 64] * zs[r + 64];
+    }
+  }
+  double acc = a0 + a1;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if (lane == 0) g[(long)s * md.n_pad + i] = (i < ns) ? acc : 0.0;
+}
+
+// s(t; phi) of subset s from its nodes (slots 0 .. nc-1): barycentric interpolation of the second
+// kind with the Chebyshev weights (-1)^i sin((2i + 1) pi / (2 nc)) (wts[s][i]); a node's own value
+// at its phi.
+__device__ inline double cheb_s(const ChebK& c, int S, int s, long t, double phi) {
+  const int nc = c.nc[s];
+  const double* w = c.wts + (long)s * MK_CHEB_MAX;
+  double num = 0.0, den = 0.0;
+  for (int i = 0; i < nc; ++i) {
+    const double f = c.Sn[((long)i * S + s) * c.T_pad + t];
+    const double d = phi - c.nphi[(long)i * S + s];
+    if (d == 0.0) return f;
+    const double ci = w[i] / d;
+    num += ci * f;
+    den += ci;
+  }
+  return num / den;
+}
+
+// The interpolant against the exact values at the check slots nc .. nc+2 (the range's ends and its
+// middle): the largest |difference| over the tile's sites and subsets into *err (bit pattern of a
+// non-negative double; a NaN counts as +inf).
+__global__ __launch_bounds__(256) void k_cheb_check(Model md, ChebK c, unsigned long long* err) {
+  __shared__ double red[4];
+  const int nb = (md.n_test + 255) / 256;
+  const int s = blockIdx.x / nb;
+  const int t = (blockIdx.x % nb) * 256 + threadIdx.x;
+  double e = 0.0;
+  if (t < md.n_test) {
+    const int nc = c.nc[s];
+    for (int k = 0; k < MK_CHEB_CHECKS; ++k) {
+      const int slot = nc + k;
+      const double phi = c.nphi[(long)slot * md.S + s];
+      const double ex = c.Sn[((long)slot * md.S + s) * c.T_pad + t];
+      const double d = fabs(cheb_s(c, md.S, s, t, phi) - ex);
+      if (!(d <= e)) e = (d != d) ? INFINITY : d;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) e = fmax(e, __shfl_xor(e, o, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = e;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const double m = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+    atomicMax(err, (unsigned long long)__double_as_longlong(m));
+  }
+}
+
+// The draws of the window's kept states j = 0 .. md.n_kept-1 (state k = k_lo + j; G, phis: window
+// records) at the tile's sites, one thread per (subset, site).  States of one phi share rho_t(phi):
+// up to 4 of them per pass over the subset's sites.  The normal, the A factor and the output layout
+// are k_pred_draw_runs' (q = 1).
+__global__ __launch_bounds__(256) void k_pred_cheb_draw(Model md, ChebK c, const double* __restrict__ G,
+                                                        const double* __restrict__ phis,
+                                                        const double* __restrict__ kA, int k_lo) {
+  const int nb = (md.n_test + 255) / 256;
+  const int s = blockIdx.x / nb;
+  const int t0 = (blockIdx.x % nb) * 256 + threadIdx.x;
+  const bool act = t0 < md.n_test;
+  const int t = act ? t0 : md.n_test - 1;
+  const int S = md.S, n = md.n_kept, ns = md.n_s[s], np = md.n_pad;
+  const double xt = md.coords_test[t], yt = md.coords_test[md.n_test_pad + t];
+  const double* cx = md.coords + (long)s * 2 * np;
+  const double* cy = cx + np;
+  const Key key = subset_key(md, s);
+  const long gs = (long)S * np;   // G stride between states
+  for (int j = 0; j < n;) {
+    const double phi = phis[(long)j * S + s];
+    int r = 1;
+    while (r < 4 && j + r < n && phis[(long)(j + r) * S + s] == phi) ++r;
+    const double* g0 = G + (long)j * gs + (long)s * np;
+    double a[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll 2
+    for (int i = 0; i < ns; ++i) {
+      const double e = exp(-phi * dist2d(cx[i], cy[i], xt, yt));
+      a[0] += e * g0[i];
+      if (r > 1) a[1] += e * g0[gs + i];
+      if (r > 2) a[2] += e * g0[2 * gs + i];
+      if (r > 3) a[3] += e * g0[3 * gs + i];
+    }
+    const double sd = sqrt(fmax(1.0 - cheb_s(c, S, s, t, phi), 0.0));
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      if (rr >= r) break;
+      const int k = k_lo + j + rr;
+      const double v = a[rr] + sd * predict_normal(key, md.t_off + t, md.kept0 + k);
+      double o = 0.0;
+      o += v * kA[(long)k * S + s];
+      if (act) md.w_pred[((long)s * n + j + rr) * md.n_test + t] = o;
+    }
+    j += r;
+  }
+}
+
 }  // namespace mk

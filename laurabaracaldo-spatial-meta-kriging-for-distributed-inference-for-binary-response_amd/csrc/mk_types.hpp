@@ -106,6 +106,17 @@ struct MatSet {
   int ld, nt, q;
 };
 
+// phi-interpolated tiled kriging (mk_mcmc.hip section 11, mk_api.hip predict_tile_cheb)
+#define MK_CHEB_MAX 32      // Chebyshev nodes per subset at most
+#define MK_CHEB_CHECKS 3    // exact check values per subset and tile: the kept range's ends and middle
+struct ChebK {
+  const double* Sn;     // [slot][S][T_pad]  exact s at the nodes (slots < nc[s]) and the check points
+  const double* nphi;   // [slot][S]         the slots' phi (as the candidate assembly computed it)
+  const double* wts;    // [S][MK_CHEB_MAX]  barycentric weights
+  const int* nc;        // [S]               nodes
+  long T_pad;
+};
+
 __device__ inline long mat_elems(const MatSet& m) { return (long)m.ld * m.ld; }
 __device__ inline double* mat_slot(const MatSet& m, int sh, int slot) {
   return m.L + ((long)sh * 2 + slot) * mat_elems(m);

@@ -16,7 +16,7 @@ LINKS = {"logit": _lib.MK_LINK_LOGIT, "probit": _lib.MK_LINK_PROBIT}
 
 # kernel-stat ids (mk_api.hip)
 (KS_CHOL_UPDATE, KS_CHOL_DIAG, KS_CHOL_TRSM, KS_SWEEP, KS_LAUUM, KS_ITER, KS_INV, KS_CHOL_UPDATE_SUB, KS_UPDATE_BUSY,
- KS_PRED_VAR, KS_COV, KS_SWEEP_FALLBACK) = range(12)
+ KS_PRED_VAR, KS_COV, KS_SWEEP_FALLBACK, KS_KRIG_CHEB, KS_KRIG_FALLBACK) = range(14)
 
 
 def _f64(a):

@@ -6,6 +6,8 @@ run's chains), with the reference's sampler as written -- 100 x 50 amcmc iterati
 1,251 kept states (MK.R:57-59, 83, 85) -- through the tiled replay (predict_tile = 65,536): per test
 tile, the replay of all 1,251 kept states (X = W P^T re-run where phi changed), the 200-level grids
 of every subset and their sequential mean over the shard (the shard's share of the combine, MK.R:123-133).
+Since round 6 the replay interpolates the kriging variance in phi (MK_KRIG_CHEB, mk_api.hip
+predict_tile_cheb); MK_KRIG_CHEB=0 runs the exact replay.
 
 Wall clock by phase.  One gpurun command may run at most 20 minutes, so the 16 test tiles can be
 split over calls (--tiles a:b); the fit is deterministic (Philox streams keyed by the global subset
@@ -82,6 +84,8 @@ def main():
             print(f"cfg5 share: tile {ti} replay+grids {t5 - t4:.1f}s combine {t6 - t5:.2f}s", file=sys.stderr,
                   flush=True)
             del g, comb
+        cheb = ses.kernel_stats(mk.session.KS_KRIG_CHEB)          # tiles kriged by phi interpolation
+        fallback = ses.kernel_stats(mk.session.KS_KRIG_FALLBACK)  # tiles whose check sent them to the exact replay
     t["tiles_replay_grids_s"] = sum(p["replay_grids_s"] for p in per_tile)
     t["tiles_combine_s"] = sum(p["combine_s"] for p in per_tile)
     t["process_s"] = time.perf_counter() - t0
@@ -92,7 +96,10 @@ def main():
                        f"100 x 50 amcmc iterations, burn.in {cfg.burn_in}, {cfg.kept} kept states",
            "tiles": [ta, tb], "n_tiles": ntiles, "phases_s": t, "per_tile": per_tile,
            "x_refreshes_per_kept_sample": refreshes / kept_phi.size,
-           "draws": draws, "draws_per_s_replay": draws / max(t["tiles_replay_grids_s"], 1e-9)}
+           "draws": draws, "draws_per_s_replay": draws / max(t["tiles_replay_grids_s"], 1e-9),
+           "krig_mode": os.environ.get("MK_KRIG_CHEB", "1"),
+           "interpolated_tiles": cheb["launches"], "exact_evaluations": cheb["flops"],
+           "max_check_difference": cheb["ms"], "fallback_tiles": fallback["launches"]}
     print(json.dumps(rec), flush=True)
 
 
