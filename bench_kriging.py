@@ -94,21 +94,47 @@ def kriging_leg(mk, subs, coords_test, beta0, bt, kept=6, burn=14, tile=65536, k
     return res
 
 
-def kept_window_runs(mk, subs, beta0, bt, subset_base=0):
-    """The configs[4] replay's refresh count from a real kept window: the fit of MK.R:83 as written
-    (100 x 50 amcmc iterations, burn.in 3,750 -> 1,251 kept, MK.R:85) on `subs`, no test sites (the
-    fit alone, minutes-cheap), and the phi sequence of every subset's kept window.  The tiled replay
-    re-runs X = W P^T for a subset at its first kept state and wherever phi changed since the
-    previous one.  Returns (refreshes per kept sample, fit seconds)."""
-    cfg = mk.SamplerConfig(1, 2, beta0, bt, n_batch=100, batch_length=50, seed=20250114)
-    t0 = time.perf_counter()
-    with mk.Session(subs, cfg, subset_base=subset_base) as ses:
+def interpolated_share(mk, subs, coords_test, beta0, bt, tile=65536, subset_base=0):
+    """configs[4] through the phi-interpolated replay (mk_api.hip predict_tile_cheb), measured on a real
+    kept window: the fit of MK.R:83 as written (100 x 50 amcmc iterations, burn.in 3,750 -> 1,251 kept)
+    on `subs` with the test sites, then the first two test tiles' replay + 200-level grids (the first
+    also makes every kept state's g = W' z, once per window).  Returns the measured phases, the
+    per-tile rate (draws/s), the exact-path refresh count of the same window, and the per-GPU share
+    of the full job priced from them (fit + g pass + tiles x the second tile's time)."""
+    S = len(subs)
+    n_test = int(np.asarray(coords_test).shape[0])
+    cfg = mk.SamplerConfig(1, 2, beta0, bt, n_batch=100, batch_length=50, seed=20250114, predict_tile=tile)
+    with mk.Session(subs, cfg, coords_test=coords_test, subset_base=subset_base) as ses:
+        tile = ses.predict_tile
+        t0 = time.perf_counter()
         ses.run(cfg.n_samples)
-        out = ses.outputs(quantiles=False, samples=True)
-    fit_s = time.perf_counter() - t0
-    kept = np.stack([smp[cfg.burn_in - 1:, 3] for smp in out["samples"]])     # phi, iterations 3,750..5,000
+        t1 = time.perf_counter()
+        out = ses.outputs(quantiles=False, samples=True, w_predict=False)
+        times, sites = [], []
+        for ti in range(min(2, (n_test + tile - 1) // tile)):
+            ta = time.perf_counter()
+            g = ses.tile_grids(ti * tile)
+            times.append(time.perf_counter() - ta)
+            sites.append(int(g.shape[2]))
+            finite = bool(np.isfinite(g).all())
+            del g
+        cheb = ses.kernel_stats(mk.session.KS_KRIG_CHEB)
+        fb = ses.kernel_stats(mk.session.KS_KRIG_FALLBACK)
+    kept = np.stack([smp[cfg.burn_in - 1:, 3] for smp in out["samples"]])
     runs = int(sum(1 + np.count_nonzero(np.diff(r)) for r in kept))
-    return runs / kept.size, fit_s, kept.shape[1]
+    n_tiles = (1_000_000 + tile - 1) // tile
+    per_tile = times[-1]
+    g_pass = times[0] - times[-1] if len(times) > 1 else 0.0
+    return {"workload": f"{S} subsets, {n_test} test sites, 100 x 50 amcmc iterations, burn.in {cfg.burn_in} "
+                        f"({cfg.kept} kept), tiles of {tile}: the first {len(times)} replayed",
+            "fit_seconds": t1 - t0, "tile_seconds": times, "tile_sites": sites, "g_pass_seconds": g_pass,
+            "draws_per_s": S * sites[-1] * cfg.kept / per_tile, "interpolated_tiles": cheb["launches"],
+            "fallback_tiles": fb["launches"], "exact_evaluations_per_subset_tile": cheb["flops"] / max(1, S * cheb["launches"]),
+            "max_check_difference": cheb["ms"], "grids_finite": finite,
+            "exact_refreshes_per_subset": runs / S, "refreshes_per_kept_sample": runs / kept.size,
+            "cfg5_share_seconds_estimate": (t1 - t0) + g_pass + n_tiles * per_tile,
+            "estimate_note": f"fit + g pass + {n_tiles} tiles x the second tile's replay + grids (the host combine of "
+                             f"the grids not included); tools/cfg5_share.py measures the whole share"}
 
 
 def main():
@@ -141,8 +167,11 @@ def main():
                       kernel_events=bool(a.kernel_events), fit_chunk=a.fit_chunk)
     if a.phi_window:
         # price the full job from the phi sequence of a full 1,251-sample kept window (the sample above
-        # holds only a few kept states, the first always a refresh)
-        frac, fit_s, n_kept = kept_window_runs(mk, subs, beta0, bt)
+        # holds only a few kept states, the first always a refresh); the same window through the
+        # phi-interpolated replay, two tiles measured
+        inter = interpolated_share(mk, subs, d["coords_test"], beta0, bt, tile=a.tile)
+        res["interpolated"] = inter
+        frac, fit_s, n_kept = inter["refreshes_per_kept_sample"], inter["fit_seconds"], 1251
         ex = res["cfg5_extrapolation"]
         rate_tf = res["roofline"]["achieved"]
         cfg5_flops = 250 * 1251 * frac * ns * ns * 1_000_000
@@ -150,6 +179,8 @@ def main():
         res["cfg5_extrapolation"] = {
             "flops": cfg5_flops, "seconds_1gpu": cfg5_flops / (rate_tf * 1e12),
             "seconds_8gpu": cfg5_flops / (rate_tf * 1e12) / 8,
+            "path": "exact replay (MK_KRIG_CHEB=0; the 6-state sample above runs it: its window is too short "
+                    "for the interpolation to pay)",
             "refreshes_per_kept_sample": frac,
             "assumes": f"X = W P^T refreshes per kept sample {frac:.3f}, measured on these {S} subsets' full kept "
                        f"window ({n_kept} kept of 100 x 50 amcmc iterations, burn.in 3,750; fit {fit_s:.1f} s) at "

@@ -162,7 +162,10 @@ int mk_session_tile_grids(mk_session* s, int32_t t0, double* out, int32_t device
  * inverses); 7 kind 0's 64/32-sub-tile instances; 8 kinds 0 + 7 with overlapping launches counted
  * once; 9 kriging GEMM k_pred_var; 10 candidate covariance assembly; 11 latent sweeps the
  * multi-workgroup kernel refused admission and its fallback ran -- launches = (subset, iteration)
- * count, no timing).  Flops are algorithmic, not executed: GEMM tiles 2 m n k, the diagonal tile's
+ * count, no timing; 12 tiles of a tiled session kriged by phi interpolation -- launches = tiles, flops
+ * = exact kriging-variance evaluations, total_ms = the largest per-tile check difference (not a time);
+ * 13 tiles whose check failed and were replayed exactly -- launches, total_ms = the largest failing
+ * difference).  Flops are algorithmic, not executed: GEMM tiles 2 m n k, the diagonal tile's
  * update as a SYRK, solves and inverse products over their triangles.  mk_session_profile(s, enable)
  * before mk_session_run: enable 0 = off, 1 = every kind, otherwise a mask with bit (1 + kind) per kind
  * bracketed (e.g. 2 << 0 = the panel update only; fewer events, less overhead). */

@@ -386,8 +386,9 @@ struct mk_session {
   int win_lo = 0, win_n = -1;     // tiled kriging: kept states [win_lo, win_lo + win_n) (-1: all)
   // phi-interpolated tiled kriging (predict_tile_cheb): the window's g_k = W_k' z_k and phi_k, kept
   // across tiles (made at the first tile after a run or a window change)
-  double* cg_G = nullptr;         // [win][S][n_pad]
+  double* cg_G = nullptr;         // [S][n_pad][nkp]: g of the window's states (nkp = window rounded up to 8)
   double* cg_phi = nullptr;       // [win][S]
+  double* cg_phit = nullptr;      // [S][nkp]: phi per state, padded with the last
   std::vector<double> cg_phi_h;
   int cg_iter = -1, cg_lo = -1, cg_n = -1;
   std::vector<double> span_pt_h;  // [S] bound on the subset-site to test-site distances (host copy)
@@ -1969,7 +1970,8 @@ static int predict_tile_cheb(mk_session* s, int t0, double* dq, mk_outputs* o) {
   if (s->cg_iter != s->iter || s->cg_lo != k_lo || s->cg_n != n_kept) {
     s->release(s->cg_G);
     s->release(s->cg_phi);
-    s->cg_G = s->cg_phi = nullptr;
+    s->release(s->cg_phit);
+    s->cg_G = s->cg_phi = s->cg_phit = nullptr;
     s->cg_iter = -1;
     if (s->alloc(&s->cg_phi, (size_t)n_kept * S)) return -1;
     MK_LAUNCH(k_kept_phi, dim3((unsigned)(((long)n_kept * S + 255) / 256)), dim3(256), 0, st, md,
@@ -2029,8 +2031,19 @@ static int predict_tile_cheb(mk_session* s, int t0, double* dq, mk_outputs* o) {
   if (force_n == 1 && evals >= refreshes) return -1;
   // 3. g_k = W_k' z_k of the window's kept states (once per window): the exact replay's
   //    factorisations where phi changed, then one W' z per state
+  const int nkp = (n_kept + 7) / 8 * 8;
   if (!s->cg_G) {
-    if (s->alloc(&s->cg_G, (size_t)n_kept * S * n_pad)) return -1;
+    if (s->alloc(&s->cg_G, (size_t)S * n_pad * nkp)) return -1;
+    if (s->alloc(&s->cg_phit, (size_t)S * nkp)) {
+      s->release(s->cg_G);
+      s->cg_G = nullptr;
+      return -1;
+    }
+    std::vector<double> pt((size_t)S * nkp);
+    for (int i = 0; i < S; ++i)
+      for (int j = 0; j < nkp; ++j) pt[(size_t)i * nkp + j] = s->cg_phi_h[(size_t)std::min(j, n_kept - 1) * S + i];
+    HIPCHK(hipMemcpyAsync(s->cg_phit, pt.data(), pt.size() * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemsetAsync(s->cg_G, 0, (size_t)S * n_pad * nkp * 8, st));
     Model mt = md;
     for (int j = 0; j < n_kept; ++j) {
       const int k = k_lo + j;
@@ -2041,9 +2054,12 @@ static int predict_tile_cheb(mk_session* s, int t0, double* dq, mk_outputs* o) {
       launch_cholesky(s, g, 0, 1, s->d_slist, s->d_scount);
       MK_LAUNCH(k_flip_pairs, dim3((S + 255) / 256), dim3(256), 0, st, g.ms, g.d_plist, g.d_pcount);
       launch_trinv(s, g, S, g.d_plist, g.d_pcount);
-      MK_LAUNCH(k_krig_g, dim3(S * (n_pad / 4)), dim3(256), 0, st, mt, g.ms, md.kz + (long)k * S * n_pad,
-                s->cg_G + (long)j * S * n_pad);
+      MK_LAUNCH(k_krig_g, dim3(S * (n_pad / 4)), dim3(256), 0, st, mt, g.ms, md.kz + (long)k * S * n_pad, s->cg_G,
+                j, nkp);
       HIPCHK(hipGetLastError());
+      // the host stays at most 32 states (~2,000 launches) ahead: rocprofv3's queue intercept read
+      // past its packet buffer with tens of thousands queued
+      if (j % 32 == 31) HIPCHK(hipStreamSynchronize(st));
     }
   }
   // slot e's theta (phi in the candidate's logit form; the device's phi of it is what counts) and
@@ -2100,6 +2116,7 @@ static int predict_tile_cheb(mk_session* s, int t0, double* dq, mk_outputs* o) {
     gp.d_pcount = C;
     launch_pred_refresh(s, gp);
     HIPCHK(hipGetLastError());
+    if (e % 4 == 3) HIPCHK(hipStreamSynchronize(st));   // (as above; four slots are ~0.6 s of GEMMs)
   }
   // 5. the check, then the draws
   ChebK ck;
@@ -2123,7 +2140,8 @@ static int predict_tile_cheb(mk_session* s, int t0, double* dq, mk_outputs* o) {
     f.ms = std::fmax(f.ms, std::isfinite(emax) ? emax : 1e300);
     return -1;
   }
-  MK_LAUNCH(k_pred_cheb_draw, dim3(S * nb), dim3(256), 0, st, mt, ck, s->cg_G, s->cg_phi, md.kA, k_lo);
+  MK_LAUNCH(k_pred_cheb_draw, dim3(S * nb), dim3(256), 0, st, mt, ck, s->cg_G, s->cg_phit, md.coords, md.kA, k_lo,
+            nkp);
   HIPCHK(hipGetLastError());
   Stat& c = s->stats[KS_KRIG_CHEB];
   c.launches += 1;

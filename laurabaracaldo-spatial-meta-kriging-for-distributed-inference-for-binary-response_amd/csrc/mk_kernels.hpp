@@ -111,9 +111,10 @@ __global__ void k_record_kept(Model md, int kidx);
 __global__ void k_kept_dirty(Model md, const double* th_prev, int* slist, int* scount, int* plist, int* pcount);
 __global__ void k_flip_pairs(MatSet ms, const int* plist, const int* pcount);
 __global__ void k_kept_phi(Model md, const double* th, int n, double* phis);
-__global__ void k_krig_g(Model md, MatSet ms, const double* z, double* g);
+__global__ void k_krig_g(Model md, MatSet ms, const double* z, double* Gt, int j, int nkp);
 __global__ void k_cheb_check(Model md, ChebK c, unsigned long long* err);
-__global__ void k_pred_cheb_draw(Model md, ChebK c, const double* G, const double* phis, const double* kA, int k_lo);
+__global__ void k_pred_cheb_draw(Model md, ChebK c, const double* Gt, const double* phit, const double* coords,
+                                 const double* kA, int k_lo, int nkp);
 // mk_post.hip
 __global__ void k_weiszfeld(const double* grids, int K, int L, long C, int max_iter, double tol, double* out, int* iters);
 __global__ void k_post_index(uint64_t seed, int samplesize, int n_levels, int* idx);

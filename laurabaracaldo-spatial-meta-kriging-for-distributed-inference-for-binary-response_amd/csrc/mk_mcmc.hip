@@ -1711,9 +1711,10 @@ __global__ __launch_bounds__(256) void k_kept_phi(Model md, const double* __rest
 }
 
 // g = W' z for every subset (q = 1): g_i = sum_{i <= r < n_s} W[r, i] z_r, one wave per column i
-// (W column-major: the wave's loads are contiguous); g_i = 0 for i >= n_s.
+// (W column-major: the wave's loads are contiguous); g_i = 0 for i >= n_s.  Stored state-minor,
+// Gt[s][i][j] (j: the window state, nkp per row), so a pass over 8 states reads 64 contiguous bytes.
 __global__ __launch_bounds__(256) void k_krig_g(Model md, MatSet ms, const double* __restrict__ z,
-                                                double* __restrict__ g) {
+                                                double* __restrict__ Gt, int j, int nkp) {
   const int per = md.n_pad / 4;
   const int s = blockIdx.x / per;
   const int i = (blockIdx.x % per) * 4 + (threadIdx.x >> 6);
@@ -1732,7 +1733,7 @@ __global__ __launch_bounds__(256) void k_krig_g(Model md, MatSet ms, const doubl
   double acc = a0 + a1;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
-  if (lane == 0) g[(long)s * md.n_pad + i] = (i < ns) ? acc : 0.0;
+  if (lane == 0) Gt[((long)s * md.n_pad + i) * nkp + j] = (i < ns) ? acc : 0.0;
 }
 
 // s(t; phi) of subset s from its nodes (slots 0 .. nc-1): barycentric interpolation of the second
@@ -1782,13 +1783,17 @@ __global__ __launch_bounds__(256) void k_cheb_check(Model md, ChebK c, unsigned 
   }
 }
 
-// The draws of the window's kept states j = 0 .. md.n_kept-1 (state k = k_lo + j; G, phis: window
-// records) at the tile's sites, one thread per (subset, site).  States of one phi share rho_t(phi):
-// up to 4 of them per pass over the subset's sites.  The normal, the A factor and the output layout
-// are k_pred_draw_runs' (q = 1).
-__global__ __launch_bounds__(256) void k_pred_cheb_draw(Model md, ChebK c, const double* __restrict__ G,
-                                                        const double* __restrict__ phis,
-                                                        const double* __restrict__ kA, int k_lo) {
+// The draws of the window's kept states j = 0 .. md.n_kept-1 (state k = k_lo + j) at the tile's sites,
+// one thread per (subset, site), 8 states per pass over the subset's sites: the distance once per
+// site and pass, rho_t(phi) = exp(-phi d) once per distinct phi among the 8 (consecutive states share
+// phi while the chain stays), m_k(t) = sum_i rho_i g_k,i in site order.  Gt [S][n_pad][nkp] and phit
+// [S][nkp] are zero / last-phi padded to nkp (a multiple of 8), and with the coordinates they are read
+// through scalar loads (uniform addresses).  The normal, the A factor and the output layout are
+// k_pred_draw_runs' (q = 1).
+__global__ __launch_bounds__(256) void k_pred_cheb_draw(Model md, ChebK c, const double* __restrict__ Gt,
+                                                        const double* __restrict__ phit,
+                                                        const double* __restrict__ coords,
+                                                        const double* __restrict__ kA, int k_lo, int nkp) {
   const int nb = (md.n_test + 255) / 256;
   const int s = blockIdx.x / nb;
   const int t0 = (blockIdx.x % nb) * 256 + threadIdx.x;
@@ -1796,35 +1801,41 @@ __global__ __launch_bounds__(256) void k_pred_cheb_draw(Model md, ChebK c, const
   const int t = act ? t0 : md.n_test - 1;
   const int S = md.S, n = md.n_kept, ns = md.n_s[s], np = md.n_pad;
   const double xt = md.coords_test[t], yt = md.coords_test[md.n_test_pad + t];
-  const double* cx = md.coords + (long)s * 2 * np;
+  const double* cx = coords + (long)s * 2 * np;
   const double* cy = cx + np;
+  const double* ph = phit + (long)s * nkp;
+  const double* gs = Gt + (long)s * np * nkp;
   const Key key = subset_key(md, s);
-  const long gs = (long)S * np;   // G stride between states
-  for (int j = 0; j < n;) {
-    const double phi = phis[(long)j * S + s];
-    int r = 1;
-    while (r < 4 && j + r < n && phis[(long)(j + r) * S + s] == phi) ++r;
-    const double* g0 = G + (long)j * gs + (long)s * np;
-    double a[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int j0 = 0; j0 < n; j0 += 8) {
+    double p[8];
+#pragma unroll
+    for (int b = 0; b < 8; ++b) p[b] = ph[j0 + b];
+    double a[8];
+#pragma unroll
+    for (int b = 0; b < 8; ++b) a[b] = 0.0;
 #pragma unroll 2
     for (int i = 0; i < ns; ++i) {
-      const double e = exp(-phi * dist2d(cx[i], cy[i], xt, yt));
-      a[0] += e * g0[i];
-      if (r > 1) a[1] += e * g0[gs + i];
-      if (r > 2) a[2] += e * g0[2 * gs + i];
-      if (r > 3) a[3] += e * g0[3 * gs + i];
-    }
-    const double sd = sqrt(fmax(1.0 - cheb_s(c, S, s, t, phi), 0.0));
+      const double d = dist2d(cx[i], cy[i], xt, yt);
+      const double* gi = gs + (long)i * nkp + j0;
+      double e = exp(-p[0] * d);
+      a[0] += e * gi[0];
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      if (rr >= r) break;
-      const int k = k_lo + j + rr;
-      const double v = a[rr] + sd * predict_normal(key, md.t_off + t, md.kept0 + k);
+      for (int b = 1; b < 8; ++b) {
+        if (p[b] != p[b - 1]) e = exp(-p[b] * d);
+        a[b] += e * gi[b];
+      }
+    }
+    double sd = 0.0;
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      if (j0 + b >= n) break;
+      if (b == 0 || p[b] != p[b - 1]) sd = sqrt(fmax(1.0 - cheb_s(c, S, s, t, p[b]), 0.0));
+      const int k = k_lo + j0 + b;
+      const double v = a[b] + sd * predict_normal(key, md.t_off + t, md.kept0 + k);
       double o = 0.0;
       o += v * kA[(long)k * S + s];
-      if (act) md.w_pred[((long)s * n + j + rr) * md.n_test + t] = o;
+      if (act) md.w_pred[((long)s * n + j0 + b) * md.n_test + t] = o;
     }
-    j += r;
   }
 }
 

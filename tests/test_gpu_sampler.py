@@ -332,12 +332,16 @@ def test_sppredict_reuses_the_fit_without_refitting(mk, q, cov):
     assert np.array_equal(part, sub)
 
 
-def test_sppredict_at_the_reference_amcmc_length(mk):
+@pytest.mark.parametrize("krig", ["0", "1"])
+def test_sppredict_at_the_reference_amcmc_length(mk, monkeypatch, krig):
     """MK.R:83-87 as written: amcmc n.batch = 100 x batch.length = 50 (5,000 samples, every one of
     them recorded by spMvGLM for spPredict), then spPredict(start = burn.in = 3,750, end = 5,000):
-    1,251 kept draws per site, equal to a session that fused the kriging into those iterations.
+    1,251 kept draws per site, equal to a session that fused the kriging into those iterations --
+    bit for bit through the exact replay (MK_KRIG_CHEB=0), to 1e-8 through the default
+    phi-interpolated replay, which a window this long takes (tests/test_gpu_krig_cheb.py).
     The fit's quantile grid of the 5,000 recorded samples is not needed, so no 2,048-sample cap
     applies to the recording (the quantile sort takes up to 16,384)."""
+    monkeypatch.setenv("MK_KRIG_CHEB", krig)
     n, n_test = 40, 6
     d = mk.synthetic.generate(n, q=1, n_test=n_test, seed=88)
     formula = [(d["y"], d["x"])]
@@ -360,6 +364,9 @@ def test_sppredict_at_the_reference_amcmc_length(mk):
         ses.run(cfg.n_samples)
         ref = ses.outputs(samples=True, w_pred_samples=True)
     assert np.array_equal(fit["p.beta.theta.samples"], ref["samples"][0])
-    assert np.array_equal(pred, ref["w_pred_samples"][0])
+    if krig == "0":
+        assert np.array_equal(pred, ref["w_pred_samples"][0])
+    else:
+        np.testing.assert_allclose(pred, ref["w_pred_samples"][0], rtol=0, atol=1e-8)
     # the 1,250-sample quantile grid of the reference workflow (MK.R:88-89)
-    assert np.array_equal(ref["w_predict"][0], r_quantile7(pred.T, PROBS200, axis=0))
+    assert np.array_equal(ref["w_predict"][0], r_quantile7(ref["w_pred_samples"][0].T, PROBS200, axis=0))

@@ -3,7 +3,7 @@
 # tiles of configs[4]'s per-GPU share
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/r06x
+O=gpurun_out/${OUT:-r06x}
 mkdir -p $O
 timeout -k 10 600 python -u -m pytest -x -v --timeout 240 --timeout-method thread tests/test_gpu_krig_cheb.py \
   tests/test_gpu_cfg5.py "tests/test_gpu_sampler.py::test_tiled_kriging_is_bit_identical_to_fused" \
