@@ -226,6 +226,7 @@ static bool g_pool_closed = false;   // mk_shutdown ran: returned streams are de
 static std::vector<int> g_pool_count;   // streams of the pool in existence per device (idle or owned)
 static int hw_queues();
 static int tile_env(const char* name, int dflt);
+static int krig_tables(mk_session* s);
 
 static int& pool_count(int device) {   // g_pool_mu held
   if ((int)g_pool_count.size() <= device) g_pool_count.resize(device + 1, 0);
@@ -392,6 +393,13 @@ struct mk_session {
   std::vector<double> cg_phi_h;
   int cg_iter = -1, cg_lo = -1, cg_n = -1;
   std::vector<double> span_pt_h;  // [S] bound on the subset-site to test-site distances (host copy)
+  // fused kriging from phi tables (krig_tables; exponential, q = 1, one group): s(t; phi) at Chebyshev
+  // nodes of the prior's phi range, made at session creation; kept iterations interpolate them
+  bool kt_on = false;
+  int kt_fail = 0;                // set-up checks that failed (the session then refreshes X exactly)
+  double kt_check = 0.0, kt_evals = 0.0;
+  ChebK kt{};
+  double* kt_g = nullptr;         // [S][n_pad] g = W' z of the current kept iteration
   std::vector<void*> kbufs;       // the kriging buffers (re-sized by mk_session_set_test_sites)
   std::vector<double> bbox;       // [S][4] xmin xmax ymin ymax of each subset's sites (Matern table ranges)
   double* d_ct_all = nullptr;     // all test sites [2][n_test_pad_all] (tiled mode)
@@ -1023,7 +1031,7 @@ static void iteration_pre_sweep(mk_session* s, Group& g, int it) {
   MK_LAUNCH(k_dirty_list, dim3(1), dim3(256), 0, st, md, (int)(it == md.kept0), g.d_list, g.d_count,
                      g.d_plist, g.d_pcount);
   launch_inverse(s, g);
-  if (kept && !s->tiled) launch_pred_refresh(s, g);
+  if (kept && !s->tiled && !s->kt_on) launch_pred_refresh(s, g);
   // the next iteration's phi candidates depend only on this iteration's decisions (and on the proposal
   // scale, which adapts after a batch's last iteration): assemble them on cov_st beside the sweep into
   // the free factor slots, which nothing reads from here to the next iteration's Cholesky (the
@@ -1048,7 +1056,12 @@ static void iteration_post_sweep(mk_session* s, Group& g, int it) {
   hipStream_t st = g.stream;
   if (s->record_samples) MK_LAUNCH(k_record, dim3((S + 63) / 64), dim3(64), 0, st, md, it);
   if (s->record_w) MK_LAUNCH(k_record_w, dim3((md.Np + 255) / 256, S), dim3(256), 0, st, md, it);
-  if (kept && md.n_test > 0 && !s->tiled) {
+  if (kept && md.n_test > 0 && !s->tiled && s->kt_on) {   // from the phi tables (krig_tables)
+    MK_LAUNCH(k_krig_g, dim3(S * (md.n_pad / 4)), dim3(256), 0, st, md, g.ms, (const double*)md.z, s->kt_g, 0, 1);
+    MK_LAUNCH(k_pred_tab_draw, dim3(S * ((md.n_test + 255) / 256)), dim3(256), 0, st, md, s->kt, s->kt_g,
+              md.coords, it, it - md.kept0);
+    s->stats[KS_KRIG_CHEB].launches += 1;
+  } else if (kept && md.n_test > 0 && !s->tiled) {
     const int per = (md.n_test + 3) / 4;
     MK_LAUNCH(k_pred_draw, dim3(S * per), dim3(256), 0, st, md, it, it - md.kept0);
   }
@@ -1132,13 +1145,13 @@ static void run_iteration_la(mk_session* s, int it) {
   const bool kept = it >= md.kept0;
   // kept iterations: the kriging refresh (X = W P^T of the changed pairs) only reads W, as the sweep
   // does, and the draws after the sweep are its only consumer -- it runs on la_k beside the sweep
-  const bool side = kept && !s->tiled && md.n_test > 0 && s->la_k;
+  const bool side = kept && !s->tiled && !s->kt_on && md.n_test > 0 && s->la_k;
   if (side) {
     hipEventRecord(evP[nt + 2], M);
     hipStreamWaitEvent(s->la_k, evP[nt + 2], 0);
     launch_pred_refresh(s, g, s->la_k);
     hipEventRecord(evP[nt + 3], s->la_k);
-  } else if (kept && !s->tiled) {
+  } else if (kept && !s->tiled && !s->kt_on) {
     launch_pred_refresh(s, g);
   }
   timed(s, M, KS_SWEEP, 0.0, [&] { launch_sweep(s, g, it); });
@@ -1711,6 +1724,13 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
   if (!set_gemm_lds()) return set_err(MK_E_HIP, "gemm lds attribute");
   HIPCHK(hipFuncSetAttribute(sweep_kernel(q, false), hipFuncAttributeMaxDynamicSharedMemorySize,
                              q * (64 * 64 + 2 * 64) * 8));
+  // fused kriging tables (before the initial factorisation: their evaluation uses the factor slots and
+  // W as scratch), then the slots, W and the diagonal inverses as the initial state expects them
+  if ((rc = krig_tables(s))) return rc;
+  HIPCHK(hipMemsetAsync(ms.cur, 0, (size_t)S * q * 4, s->stream));
+  HIPCHK(hipMemsetAsync(md.info, 0, (size_t)S * q * 4, s->stream));
+  HIPCHK(hipMemsetAsync(ms.W, 0, (size_t)S * q * n_pad * n_pad * 8, s->stream));
+  HIPCHK(hipMemsetAsync(ms.Winv, 0, (size_t)S * q * 2 * nt * MK_NB * MK_NB * 8, s->stream));
   // ---------------- initial state: eta, u, factor every R_h at the starting values, W, z (whole shard)
   Group& a = s->all;
   MK_LAUNCH(k_init_state, dim3(S), dim3(256), 0, s->stream, md);
@@ -1723,6 +1743,13 @@ extern "C" int mk_session_create(const mk_problem* pr, const mk_config* c, mk_se
   HIPCHK(hipStreamSynchronize(s->stream));
   drain_timers(s);
   for (auto& st : s->stats) st = Stat();
+  if (s->kt_on) {   // the tables: exact evaluations and the largest set-up check difference
+    s->stats[KS_KRIG_CHEB].flops = s->kt_evals;
+    s->stats[KS_KRIG_CHEB].ms = s->kt_check;
+  } else if (s->kt_fail) {
+    s->stats[KS_KRIG_FALLBACK].launches = s->kt_fail;
+    s->stats[KS_KRIG_FALLBACK].ms = s->kt_check;
+  }
   // default schedule: lookahead where eligible; MK_LOOKAHEAD=0 / 1 overrides (mk_session_set_lookahead too)
   static const int la_env = tile_env("MK_LOOKAHEAD", -1);
   s->la = s->la_ok && (la_env == 1 || (la_env < 0 && la_auto(s)));
@@ -1936,23 +1963,193 @@ static int tile_outputs(mk_session* s, int t0, double* dq, mk_outputs* o, int n_
   return 0;
 }
 
-// Tile [t0, t0 + Tc) by phi interpolation (exponential, q = 1; mk_mcmc.hip section 11).  The kriging
-// variance s(t; phi) = rho_t' R(phi)^-1 rho_t is analytic in phi: it is computed exactly (the replay's
-// own kernels: candidate, Cholesky, inverse, X = W P^T) at nc Chebyshev nodes of each subset's kept
-// phi range and interpolated at every kept state's phi, instead of at every phi the chain visited
-// (0.39 refreshes per kept state at configs[4], i.e. ~490 per subset against nc = 12..21 here).  nc
-// grows with the range's width in units of the correlation decay over the largest distance involved,
-// (phi_hi - phi_lo) * d_max: 8 + ceil of it, at least 12 (measured in float64 on 2,000-site subsets
-// with clustered sites and test sites 1e-6 from a site: |error| <= 1e-14 over phi in [3.3, 11.8] with
-// 20 nodes, [6, 8] with 10).  Every tile also computes s exactly at the range's two ends and its
-// middle and compares the interpolant there over all its sites and subsets; a difference above
-// MK_KRIG_CHEB_TOL (default 1e-10) sends the tile to the exact replay (KS_KRIG_FALLBACK).  The mean
-// uses m_k(t) = rho_t(phi_k)' g_k, g_k = W_k' z_k, made once per kept window.  Against the exact
-// replay the draws agree to rounding and the interpolation's difference (tests/test_gpu_cfg5.py);
-// MK_KRIG_CHEB: 1 (default) where the nodes and checks cost fewer exact evaluations than the exact
-// replay's refreshes, -1 always, n > 1 always with n nodes, 0 never (the exact replay).
-// Returns 0 when the tile is done, -1 when the exact replay must run (not applicable, scratch
-// memory short, check failed), > 0 on an error.
+// ------------------------------------------------------------------ kriging variance by phi interpolation
+// (exponential, q = 1; DESIGN.md 4.7, mk_mcmc.hip section 11).  s(t; phi) = rho_t' R(phi)^-1 rho_t is
+// analytic in phi: it is computed exactly (the replay's own kernels: candidate, Cholesky, inverse,
+// X = W P^T) at nc Chebyshev nodes (first kind) of a phi range per subset and interpolated (barycentric)
+// wherever a draw needs it.  nc = 8 + ceil((phi_hi - phi_lo) * d_max), at least 12, at most 32 (d_max:
+// the subset's largest site-to-site or site-to-test-site distance, so the rule counts the range in units
+// of the correlation decay; measured in float64 on 2,000-site subsets with clustered sites and test
+// sites 1e-6 from a site: |error| <= 1e-14 over phi in [3.3, 11.8] with 20 nodes, [6, 8] with 10).  The
+// exact values at nchk check points (the range's ends, then interior points) bound the interpolant's
+// error before any draw uses it.
+
+// Nodes of [lo, hi] for each subset: nc[i], the slots' phi (nodes, then nchk check points) and the
+// barycentric weights.  Returns the slot count E (the largest nc + nchk).
+static int cheb_plan(mk_session* s, const std::vector<double>& lo, const std::vector<double>& hi, int force_n, int nchk,
+                     std::vector<int>& nc, std::vector<std::vector<double>>& sphi, std::vector<double>& wts) {
+  const int S = s->S;
+  nc.assign(S, 0);
+  sphi.assign(S, {});
+  wts.assign((size_t)S * MK_CHEB_MAX, 0.0);
+  int E = 0;
+  for (int i = 0; i < S; ++i) {
+    const double* bb = s->bbox.data() + 4 * i;
+    const double dmax = std::fmax(s->span_pt_h[i], std::hypot(bb[1] - bb[0], bb[3] - bb[2]));
+    const int n = force_n > 1 ? std::min(force_n, MK_CHEB_MAX)
+                              : std::max(12, std::min(MK_CHEB_MAX, 8 + (int)std::ceil((hi[i] - lo[i]) * dmax)));
+    nc[i] = n;
+    const double c = 0.5 * (lo[i] + hi[i]), h = 0.5 * (hi[i] - lo[i]);
+    for (int m = 0; m < n; ++m) {
+      const double ang = M_PI * (2.0 * m + 1.0) / (2.0 * n);
+      sphi[i].push_back(c + h * std::cos(ang));
+      wts[(size_t)i * MK_CHEB_MAX + m] = ((m & 1) ? -1.0 : 1.0) * std::sin(ang);
+    }
+    static const double frac[5] = {0.0, 1.0, 0.5, 0.25, 0.75};
+    for (int k = 0; k < nchk; ++k) sphi[i].push_back(lo[i] + frac[k] * (hi[i] - lo[i]));
+    E = std::max(E, n + nchk);
+  }
+  return E;
+}
+
+// Exact s of every planned slot into Sn ([slot][S][n_test_pad] of mt's sites) and the slots' device phi
+// into nphi; then the interpolant against the check points (largest difference into *emax).  The factor
+// slots, cur and W serve as scratch: callers are the tiled replay (the chain is finished) and session
+// set-up (before the initial factorisation).  The host stays at most four slots ahead of the device.
+static int cheb_eval(mk_session* s, Model mt, const std::vector<int>& nc, const std::vector<std::vector<double>>& sphi,
+                     const std::vector<double>& wts, int E, int nchk, DevBufs& scratch, ChebK* ck, double* emax) {
+  Model& md = s->md;
+  const int S = s->S, nth = md.n_theta, T_pad = md.n_test_pad;
+  const double pa = md.phi_a[0], pb = md.phi_b[0];
+  hipStream_t st = s->stream;
+  Group g = s->all;
+  // slot e's theta (phi in the candidate's logit form; the device's phi of it is what counts) and its
+  // subset list (the subsets with that many slots)
+  std::vector<double> thn((size_t)E * S * nth, 0.0);
+  std::vector<int> lists((size_t)E * (S + 1), 0);
+  for (int e = 0; e < E; ++e) {
+    int cnt = 0;
+    for (int i = 0; i < S; ++i) {
+      const double ph = e < (int)sphi[i].size() ? sphi[i][e] : sphi[i][0];
+      thn[((size_t)e * S + i) * nth + md.ntri] = std::log((ph - pa) / (pb - ph));
+      if (e < (int)sphi[i].size()) lists[(size_t)e * (S + 1) + cnt++] = i;
+    }
+    lists[(size_t)e * (S + 1) + S] = cnt;
+  }
+  double* d_thn = scratch.get<double>(thn.size());
+  double* d_nphi = scratch.get<double>((size_t)E * S);
+  double* d_wts = scratch.get<double>(wts.size());
+  int* d_nc = scratch.get<int>((size_t)S);
+  int* d_lists = scratch.get<int>(lists.size());
+  double* d_Sn = scratch.get<double>((size_t)E * S * T_pad);
+  unsigned long long* d_err = scratch.get<unsigned long long>(1);
+  if (!d_thn || !d_nphi || !d_wts || !d_nc || !d_lists || !d_Sn || !d_err) return -1;
+  HIPCHK(hipMemcpyAsync(d_thn, thn.data(), thn.size() * 8, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(d_wts, wts.data(), wts.size() * 8, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(d_nc, nc.data(), (size_t)S * sizeof(int), hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(d_lists, lists.data(), lists.size() * sizeof(int), hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemsetAsync(d_Sn, 0, (size_t)E * S * T_pad * 8, st));
+  HIPCHK(hipMemsetAsync(d_err, 0, 8, st));
+  MK_LAUNCH(k_kept_phi, dim3((unsigned)(((long)E * S + 255) / 256)), dim3(256), 0, st, md, d_thn, E, d_nphi);
+  for (int e = 0; e < E; ++e) {
+    int* L = d_lists + (size_t)e * (S + 1);
+    int* C = L + S;
+    mt.theta = d_thn + (size_t)e * S * nth;
+    mt.s_pred = d_Sn + (size_t)e * S * T_pad;
+    launch_candidates(mt, g.ms, st, S, 0, 1, 2, 0, L, C);
+    launch_cholesky(s, g, 0, 1, L, C);
+    MK_LAUNCH(k_flip_pairs, dim3((S + 255) / 256), dim3(256), 0, st, g.ms, L, C);
+    launch_trinv(s, g, S, L, C);
+    Group gp = g;
+    gp.md = mt;
+    gp.d_plist = L;
+    gp.d_pcount = C;
+    launch_pred_refresh(s, gp);
+    HIPCHK(hipGetLastError());
+    if (e % 4 == 3) HIPCHK(hipStreamSynchronize(st));   // four slots are ~0.6 s of GEMMs at configs[4]
+  }
+  ck->Sn = d_Sn;
+  ck->nphi = d_nphi;
+  ck->wts = d_wts;
+  ck->nc = d_nc;
+  ck->nchk = nchk;
+  ck->T_pad = T_pad;
+  MK_LAUNCH(k_cheb_check, dim3(S * ((mt.n_test + 255) / 256)), dim3(256), 0, st, mt, *ck, d_err);
+  unsigned long long eb = 0;
+  HIPCHK(hipMemcpyAsync(&eb, d_err, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  std::memcpy(emax, &eb, 8);
+  return 0;
+}
+
+static double cheb_tol() {
+  const char* tenv = std::getenv("MK_KRIG_CHEB_TOL");
+  return (tenv && *tenv) ? std::atof(tenv) : 1e-10;
+}
+
+// Fused kriging by phi tables (called by mk_session_create before the initial factorisation; exponential,
+// q = 1, one group).  The fused path refreshes X = W P^T at every kept iteration for the pairs whose phi
+// changed (~0.4 of them at configs[2]: 6.9 ms of a kept iteration at 250 subsets).  Instead, s(t; phi)
+// is computed once over the prior's whole phi range [a, b] (MK.R:63 phi.Unif), so it holds wherever the
+// chain goes: Chebyshev nodes of [a, b] per subset, checked at a, b, the middle and the quarters (5
+// points); a difference above MK_KRIG_CHEB_TOL keeps the exact refresh for the session (KS_KRIG_FALLBACK).
+// Kept iterations then draw with g = W' z (one W pass) and the interpolated s (k_pred_tab_draw).
+// MK_KRIG_CHEB: 1 (default) where the kept window's expected refreshes (0.25 n_kept per subset, below
+// the amcmc target's 0.43) exceed the nodes and checks, -1 always, n > 1 always with n nodes, 0 never.
+static int krig_tables(mk_session* s) {
+  Model& md = s->md;
+  s->kt_on = false;
+  const char* env = std::getenv("MK_KRIG_CHEB");
+  const int force_n = (env && *env) ? std::atoi(env) : 1;
+  const int S = s->S;
+  if (force_n == 0 || s->tiled || md.n_test <= 0 || s->q != 1 || md.cov_model != MK_COV_EXPONENTIAL ||
+      s->groups.size() != 1 || (int)s->span_pt_h.size() != S)
+    return 0;
+  const double pa = md.phi_a[0], pb = md.phi_b[0], eps = (pb - pa) * 1e-9;
+  std::vector<double> lo(S, pa + eps), hi(S, pb - eps);
+  std::vector<int> nc;
+  std::vector<std::vector<double>> sphi;
+  std::vector<double> wts;
+  const int nchk = MK_CHEB_CHECKS_MAX;
+  const int E = cheb_plan(s, lo, hi, force_n, nchk, nc, sphi, wts);
+  double evals = 0.0;
+  for (int i = 0; i < S; ++i) evals += nc[i] + nchk;
+  if (force_n == 1 && 0.25 * md.n_kept * S <= evals) return 0;
+  Model mt = md;   // every test site (the fused path's buffers hold them all)
+  DevBufs scratch;
+  ChebK ck;
+  double emax = 0.0;
+  const int rc = cheb_eval(s, mt, nc, sphi, wts, E, nchk, scratch, &ck, &emax);
+  if (rc > 0) return rc;
+  s->kt_check = emax;
+  if (rc < 0 || !(emax <= cheb_tol())) {   // scratch memory short, or the check failed: exact refreshes
+    s->kt_fail += rc < 0 ? 0 : 1;
+    return 0;
+  }
+  // keep the node slots (the checks are not needed past this point)
+  int nmax = 0;
+  for (int i = 0; i < S; ++i) nmax = std::max(nmax, nc[i]);
+  const size_t sn = (size_t)nmax * S * md.n_test_pad;
+  double *Sn = nullptr, *nphi = nullptr, *w = nullptr;
+  int* n = nullptr;
+  if (s->alloc(&Sn, sn) || s->alloc(&nphi, (size_t)nmax * S) || s->alloc(&w, wts.size()) || s->alloc(&n, (size_t)S) ||
+      s->alloc(&s->kt_g, (size_t)S * md.n_pad))
+    return MK_E_NOMEM;
+  HIPCHK(hipMemcpyAsync(Sn, ck.Sn, sn * 8, hipMemcpyDeviceToDevice, s->stream));
+  HIPCHK(hipMemcpyAsync(nphi, ck.nphi, (size_t)nmax * S * 8, hipMemcpyDeviceToDevice, s->stream));
+  HIPCHK(hipMemcpyAsync(w, ck.wts, wts.size() * 8, hipMemcpyDeviceToDevice, s->stream));
+  HIPCHK(hipMemcpyAsync(n, ck.nc, (size_t)S * sizeof(int), hipMemcpyDeviceToDevice, s->stream));
+  HIPCHK(hipStreamSynchronize(s->stream));
+  s->kt.Sn = Sn;
+  s->kt.nphi = nphi;
+  s->kt.wts = w;
+  s->kt.nc = n;
+  s->kt.nchk = 0;
+  s->kt.T_pad = md.n_test_pad;
+  s->kt_evals = evals;
+  s->kt_on = true;
+  return 0;
+}
+
+// Tile [t0, t0 + Tc) of the tiled replay by phi interpolation: nodes over each subset's kept phi range,
+// checked at its ends and middle (a difference above MK_KRIG_CHEB_TOL, default 1e-10, sends the tile
+// to the exact replay: KS_KRIG_FALLBACK); the mean m_k(t) = rho_t(phi_k)' g_k with g_k = W_k' z_k made
+// once per kept window (the exact replay's factorisations where phi changed, one W' z per state).  At
+// configs[4]: ~490 X refreshes per subset and tile become 13-21 nodes + 3 checks.  MK_KRIG_CHEB: 1
+// (default) where the nodes and checks cost fewer exact evaluations than the exact replay's refreshes,
+// -1 always, n > 1 always with n nodes, 0 never (the exact replay); read at every tile.
+// Returns 0 when the tile is done, -1 when the exact replay must run (not applicable, scratch memory
+// short, check failed), > 0 on an error.
 static int predict_tile_cheb(mk_session* s, int t0, double* dq, mk_outputs* o) {
   Model& md = s->md;
   const char* env = std::getenv("MK_KRIG_CHEB");
@@ -1983,51 +2180,38 @@ static int predict_tile_cheb(mk_session* s, int t0, double* dq, mk_outputs* o) {
     s->cg_lo = k_lo;
     s->cg_n = n_kept;
   }
-  // 2. per subset: nodes over its kept phi range, then the three check points
+  // 2. per subset: nodes over its kept phi range (a nearly fixed phi: a short interval around it)
   const double pa = md.phi_a[0], pb = md.phi_b[0];
-  std::vector<int> nc(S);
-  std::vector<double> wts((size_t)S * MK_CHEB_MAX, 0.0);
-  std::vector<std::vector<double>> sphi(S);
-  int E = 0;
-  long evals = 0, refreshes = 0;
+  std::vector<double> lo(S), hi(S);
+  long refreshes = 0;
   for (int i = 0; i < S; ++i) {
-    double lo = s->cg_phi_h[i], hi = lo;
+    double l = s->cg_phi_h[i], h = l;
     refreshes += 1;
     for (int j = 1; j < n_kept; ++j) {
       const double v = s->cg_phi_h[(size_t)j * S + i];
       refreshes += v != s->cg_phi_h[(size_t)(j - 1) * S + i];
-      lo = std::fmin(lo, v);
-      hi = std::fmax(hi, v);
+      l = std::fmin(l, v);
+      h = std::fmax(h, v);
     }
-    const double mag = std::fmax(1.0, std::fabs(lo));
-    if (hi - lo < 1e-6 * mag) {   // a (nearly) fixed phi: a short interval around it
-      const double c = 0.5 * (lo + hi);
-      lo = c - 5e-7 * mag;
-      hi = c + 5e-7 * mag;
+    const double mag = std::fmax(1.0, std::fabs(l));
+    if (h - l < 1e-6 * mag) {
+      const double c = 0.5 * (l + h);
+      l = c - 5e-7 * mag;
+      h = c + 5e-7 * mag;
     }
     const double eps = (pb - pa) * 1e-9;
-    lo = std::fmax(lo, pa + eps);
-    hi = std::fmin(hi, pb - eps);
-    const double* bb = s->bbox.data() + 4 * i;
-    const double dmax = std::fmax(s->span_pt_h[i], std::hypot(bb[1] - bb[0], bb[3] - bb[2]));
-    const int n = force_n > 1 ? std::min(force_n, MK_CHEB_MAX)
-                              : std::max(12, std::min(MK_CHEB_MAX, 8 + (int)std::ceil((hi - lo) * dmax)));
-    nc[i] = n;
-    const double c = 0.5 * (lo + hi), h = 0.5 * (hi - lo);
-    for (int m = 0; m < n; ++m) {
-      const double ang = M_PI * (2.0 * m + 1.0) / (2.0 * n);
-      sphi[i].push_back(c + h * std::cos(ang));
-      wts[(size_t)i * MK_CHEB_MAX + m] = ((m & 1) ? -1.0 : 1.0) * std::sin(ang);
-    }
-    sphi[i].push_back(lo);
-    sphi[i].push_back(hi);
-    sphi[i].push_back(c);
-    E = std::max(E, n + MK_CHEB_CHECKS);
-    evals += n + MK_CHEB_CHECKS;
+    lo[i] = std::fmax(l, pa + eps);
+    hi[i] = std::fmin(h, pb - eps);
   }
-  // auto (MK_KRIG_CHEB unset or 1): only where it saves exact evaluations -- the exact replay
-  // refreshes X at each subset's first state and wherever phi changed (a short window, e.g. the
-  // bench's 6-state kriging sample, refreshes less often than a range needs nodes)
+  std::vector<int> nc;
+  std::vector<std::vector<double>> sphi;
+  std::vector<double> wts;
+  const int E = cheb_plan(s, lo, hi, force_n, MK_CHEB_CHECKS, nc, sphi, wts);
+  long evals = 0;
+  for (int i = 0; i < S; ++i) evals += nc[i] + MK_CHEB_CHECKS;
+  // auto: only where it saves exact evaluations -- the exact replay refreshes X at each subset's first
+  // state and wherever phi changed (a short window, e.g. the bench's 6-state kriging sample, refreshes
+  // less often than a range needs nodes)
   if (force_n == 1 && evals >= refreshes) return -1;
   // 3. g_k = W_k' z_k of the window's kept states (once per window): the exact replay's
   //    factorisations where phi changed, then one W' z per state
@@ -2062,35 +2246,7 @@ static int predict_tile_cheb(mk_session* s, int t0, double* dq, mk_outputs* o) {
       if (j % 32 == 31) HIPCHK(hipStreamSynchronize(st));
     }
   }
-  // slot e's theta (phi in the candidate's logit form; the device's phi of it is what counts) and
-  // its subset list (the subsets with that many slots)
-  std::vector<double> thn((size_t)E * S * nth, 0.0);
-  std::vector<int> lists((size_t)E * (S + 1), 0);
-  for (int e = 0; e < E; ++e) {
-    int cnt = 0;
-    for (int i = 0; i < S; ++i) {
-      const double ph = e < (int)sphi[i].size() ? sphi[i][e] : sphi[i][0];
-      thn[((size_t)e * S + i) * nth + md.ntri] = std::log((ph - pa) / (pb - ph));
-      if (e < (int)sphi[i].size()) lists[(size_t)e * (S + 1) + cnt++] = i;
-    }
-    lists[(size_t)e * (S + 1) + S] = cnt;
-  }
-  DevBufs scratch;
-  double* d_thn = scratch.get<double>(thn.size());
-  double* d_nphi = scratch.get<double>((size_t)E * S);
-  double* d_wts = scratch.get<double>(wts.size());
-  int* d_nc = scratch.get<int>((size_t)S);
-  int* d_lists = scratch.get<int>(lists.size());
-  double* d_Sn = scratch.get<double>((size_t)E * S * T_pad);
-  unsigned long long* d_err = scratch.get<unsigned long long>(1);
-  if (!d_thn || !d_nphi || !d_wts || !d_nc || !d_lists || !d_Sn || !d_err) return -1;
-  HIPCHK(hipMemcpyAsync(d_thn, thn.data(), thn.size() * 8, hipMemcpyHostToDevice, st));
-  HIPCHK(hipMemcpyAsync(d_wts, wts.data(), wts.size() * 8, hipMemcpyHostToDevice, st));
-  HIPCHK(hipMemcpyAsync(d_nc, nc.data(), (size_t)S * sizeof(int), hipMemcpyHostToDevice, st));
-  HIPCHK(hipMemcpyAsync(d_lists, lists.data(), lists.size() * sizeof(int), hipMemcpyHostToDevice, st));
-  HIPCHK(hipMemsetAsync(d_Sn, 0, (size_t)E * S * T_pad * 8, st));
-  HIPCHK(hipMemsetAsync(d_err, 0, 8, st));
-  // 4. the tile's sites (as predict_tile), the slots' phi, exact s at every slot
+  // 4. the tile's sites (as predict_tile), exact s at every slot, the check
   HIPCHK(hipMemsetAsync((void*)md.coords_test, 0, (size_t)2 * T_pad * 8, st));
   HIPCHK(hipMemcpyAsync((void*)md.coords_test, s->d_ct_all + t0, (size_t)Tc * 8, hipMemcpyDeviceToDevice, st));
   HIPCHK(hipMemcpyAsync((void*)(md.coords_test + T_pad), s->d_ct_all + s->n_test_pad_all + t0, (size_t)Tc * 8,
@@ -2100,48 +2256,20 @@ static int predict_tile_cheb(mk_session* s, int t0, double* dq, mk_outputs* o) {
   mt.n_test = Tc;
   mt.t_off = t0;
   mt.ntt = (Tc + MK_NB - 1) / MK_NB;
-  MK_LAUNCH(k_kept_phi, dim3((unsigned)(((long)E * S + 255) / 256)), dim3(256), 0, st, md, d_thn, E, d_nphi);
-  for (int e = 0; e < E; ++e) {
-    int* L = d_lists + (size_t)e * (S + 1);
-    int* C = L + S;
-    mt.theta = d_thn + (size_t)e * S * nth;
-    mt.s_pred = d_Sn + (size_t)e * S * T_pad;
-    launch_candidates(mt, g.ms, st, S, 0, 1, 2, 0, L, C);
-    launch_cholesky(s, g, 0, 1, L, C);
-    MK_LAUNCH(k_flip_pairs, dim3((S + 255) / 256), dim3(256), 0, st, g.ms, L, C);
-    launch_trinv(s, g, S, L, C);
-    Group gp = g;
-    gp.md = mt;
-    gp.d_plist = L;
-    gp.d_pcount = C;
-    launch_pred_refresh(s, gp);
-    HIPCHK(hipGetLastError());
-    if (e % 4 == 3) HIPCHK(hipStreamSynchronize(st));   // (as above; four slots are ~0.6 s of GEMMs)
-  }
-  // 5. the check, then the draws
+  DevBufs scratch;
   ChebK ck;
-  ck.Sn = d_Sn;
-  ck.nphi = d_nphi;
-  ck.wts = d_wts;
-  ck.nc = d_nc;
-  ck.T_pad = T_pad;
-  const int nb = (Tc + 255) / 256;
-  MK_LAUNCH(k_cheb_check, dim3(S * nb), dim3(256), 0, st, mt, ck, d_err);
-  unsigned long long eb = 0;
-  HIPCHK(hipMemcpyAsync(&eb, d_err, 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
-  double emax;
-  std::memcpy(&emax, &eb, 8);
-  const char* tenv = std::getenv("MK_KRIG_CHEB_TOL");
-  const double tol = (tenv && *tenv) ? std::atof(tenv) : 1e-10;
-  if (!(emax <= tol)) {
+  double emax = 0.0;
+  const int rc = cheb_eval(s, mt, nc, sphi, wts, E, MK_CHEB_CHECKS, scratch, &ck, &emax);
+  if (rc) return rc;
+  if (!(emax <= cheb_tol())) {
     Stat& f = s->stats[KS_KRIG_FALLBACK];
     f.launches += 1;
     f.ms = std::fmax(f.ms, std::isfinite(emax) ? emax : 1e300);
     return -1;
   }
-  MK_LAUNCH(k_pred_cheb_draw, dim3(S * nb), dim3(256), 0, st, mt, ck, s->cg_G, s->cg_phit, md.coords, md.kA, k_lo,
-            nkp);
+  // 5. the draws
+  MK_LAUNCH(k_pred_cheb_draw, dim3(S * ((Tc + 255) / 256)), dim3(256), 0, st, mt, ck, s->cg_G, s->cg_phit, md.coords,
+            md.kA, k_lo, nkp);
   HIPCHK(hipGetLastError());
   Stat& c = s->stats[KS_KRIG_CHEB];
   c.launches += 1;

@@ -1754,8 +1754,8 @@ __device__ inline double cheb_s(const ChebK& c, int S, int s, long t, double phi
   return num / den;
 }
 
-// The interpolant against the exact values at the check slots nc .. nc+2 (the range's ends and its
-// middle): the largest |difference| over the tile's sites and subsets into *err (bit pattern of a
+// The interpolant against the exact values at the check slots nc .. nc+nchk-1 (the range's ends, its
+// middle, its quarters): the largest |difference| over the tile's sites and subsets into *err (bit pattern of a
 // non-negative double; a NaN counts as +inf).
 __global__ __launch_bounds__(256) void k_cheb_check(Model md, ChebK c, unsigned long long* err) {
   __shared__ double red[4];
@@ -1765,7 +1765,7 @@ __global__ __launch_bounds__(256) void k_cheb_check(Model md, ChebK c, unsigned 
   double e = 0.0;
   if (t < md.n_test) {
     const int nc = c.nc[s];
-    for (int k = 0; k < MK_CHEB_CHECKS; ++k) {
+    for (int k = 0; k < c.nchk; ++k) {
       const int slot = nc + k;
       const double phi = c.nphi[(long)slot * md.S + s];
       const double ex = c.Sn[((long)slot * md.S + s) * c.T_pad + t];
@@ -1837,6 +1837,38 @@ __global__ __launch_bounds__(256) void k_pred_cheb_draw(Model md, ChebK c, const
       if (act) md.w_pred[((long)s * n + j0 + b) * md.n_test + t] = o;
     }
   }
+}
+
+// Fused kriging from the session's phi tables (mk_api.hip krig_tables; kept iteration `iter`, record
+// kidx, q = 1): k_pred_draw's draw with s(t; phi) interpolated from the tables and the mean
+// m(t) = rho_t(phi)' g, g = W' z of this iteration (k_krig_g), instead of X = W P^T refreshed wherever
+// phi changed.  One thread per (subset, site).
+__global__ __launch_bounds__(256) void k_pred_tab_draw(Model md, ChebK c, const double* __restrict__ g,
+                                                       const double* __restrict__ coords, int iter, int kidx) {
+  const int nb = (md.n_test + 255) / 256;
+  const int s = blockIdx.x / nb;
+  const int t0 = (blockIdx.x % nb) * 256 + threadIdx.x;
+  const bool act = t0 < md.n_test;
+  const int t = act ? t0 : md.n_test - 1;
+  const int ns = md.n_s[s], np = md.n_pad;
+  const double phi = logit_inv(md.theta[(long)s * md.n_theta + md.ntri], md.phi_a[0], md.phi_b[0]);
+  const double xt = md.coords_test[t], yt = md.coords_test[md.n_test_pad + t];
+  const double* cx = coords + (long)s * 2 * np;
+  const double* cy = cx + np;
+  const double* gs = g + (long)s * np;
+  double a0 = 0.0, a1 = 0.0;
+  int i = 0;
+  for (; i + 1 < ns; i += 2) {
+    a0 += exp(-phi * dist2d(cx[i], cy[i], xt, yt)) * gs[i];
+    a1 += exp(-phi * dist2d(cx[i + 1], cy[i + 1], xt, yt)) * gs[i + 1];
+  }
+  if (i < ns) a0 += exp(-phi * dist2d(cx[i], cy[i], xt, yt)) * gs[i];
+  const double sd = sqrt(fmax(1.0 - cheb_s(c, md.S, s, t, phi), 0.0));
+  const Key key = subset_key(md, s);
+  const double v = (a0 + a1) + sd * predict_normal(key, md.t_off + t, iter);   // q = 1: index (t_off + t) q + h
+  double o = 0.0;
+  o += v * md.A_full[s];
+  if (act) md.w_pred[((long)s * md.n_kept + kidx) * md.n_test + t] = o;
 }
 
 }  // namespace mk

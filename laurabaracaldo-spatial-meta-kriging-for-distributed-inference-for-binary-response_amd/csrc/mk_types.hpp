@@ -109,11 +109,13 @@ struct MatSet {
 // phi-interpolated tiled kriging (mk_mcmc.hip section 11, mk_api.hip predict_tile_cheb)
 #define MK_CHEB_MAX 32      // Chebyshev nodes per subset at most
 #define MK_CHEB_CHECKS 3    // exact check values per subset and tile: the kept range's ends and middle
+#define MK_CHEB_CHECKS_MAX 5
 struct ChebK {
   const double* Sn;     // [slot][S][T_pad]  exact s at the nodes (slots < nc[s]) and the check points
   const double* nphi;   // [slot][S]         the slots' phi (as the candidate assembly computed it)
   const double* wts;    // [S][MK_CHEB_MAX]  barycentric weights
   const int* nc;        // [S]               nodes
+  int nchk;             // check slots per subset (after the nodes)
   long T_pad;
 };
 

@@ -1,4 +1,5 @@
-"""phi-interpolated tiled kriging (spPredict after the fit, MK.R:87-89; mk_api.hip predict_tile_cheb).
+"""The kriging variance by phi interpolation (MK.R:87-89): the tiled replay
+(spPredict after the fit, mk_api.hip predict_tile_cheb) and the fused path's phi tables (krig_tables).
 
 The kriging variance s(t; phi) = rho_t(phi)' R(phi)^-1 rho_t(phi) is computed exactly at Chebyshev
 nodes of each subset's kept phi range and interpolated at every kept state's phi; the mean is
@@ -109,3 +110,69 @@ def test_interpolated_kriging_matches_the_oracle(mk, monkeypatch):
         np.testing.assert_allclose(dev["w_predict"][s][:, sites], ref["w_q"], rtol=0, atol=TOL)
         grid_sum = ref["w_q"] if grid_sum is None else grid_sum + ref["w_q"]
     np.testing.assert_allclose(dev["w_predict_sum"][:, sites], grid_sum, rtol=0, atol=2 * TOL)
+
+
+# ---- the fused path's phi tables (mk_api.hip krig_tables): s(t; phi) tabulated over the prior's phi
+# range at session creation; kept iterations draw with g = W' z and the interpolated s
+
+def _fused(mk, monkeypatch, subs, ct, cfg, mode, base=0, lookahead=-1):
+    monkeypatch.setenv("MK_KRIG_CHEB", mode)
+    with mk.Session(subs, cfg, coords_test=ct, subset_base=base) as ses:
+        ses.set_lookahead(lookahead)
+        assert lookahead == -1 or ses.lookahead == bool(lookahead)
+        ses.run(cfg.n_samples)
+        out = ses.outputs(samples=True, w_pred_samples=True, w_predict_sum=True)
+        out["cheb"] = ses.kernel_stats(mk.session.KS_KRIG_CHEB)
+        out["fallback"] = ses.kernel_stats(mk.session.KS_KRIG_FALLBACK)
+    monkeypatch.delenv("MK_KRIG_CHEB", raising=False)
+    return out
+
+
+@pytest.mark.parametrize("lookahead", [True, False])
+def test_fused_phi_tables_match_the_exact_refresh(mk, monkeypatch, lookahead):
+    """Fused kriging (draws inside the kept iterations, MK.R:87 fused into the fit) from the phi tables
+    against the exact X = W P^T refresh: the chain is untouched (samples bit for bit), the draws, grids
+    and their sum agree to 1e-8, every kept iteration drew from the tables, and the set-up check
+    (5 points of the prior's range) is at rounding level.  Both launch schedules."""
+    subs, ct = _problem(mk, [300, 257, 280], 700, seed=65)
+    cfg = mk.SamplerConfig(1, 2, np.zeros(2), np.full(2, 0.05), n_batch=4, batch_length=10, burn_in=10, seed=6)
+    exact = _fused(mk, monkeypatch, subs, ct, cfg, "0", lookahead=int(lookahead))
+    tab = _fused(mk, monkeypatch, subs, ct, cfg, "-1", lookahead=int(lookahead))
+    assert exact["cheb"]["launches"] == 0
+    assert tab["cheb"]["launches"] == cfg.kept and tab["fallback"]["launches"] == 0, (tab["cheb"], tab["fallback"])
+    assert 0 < tab["cheb"]["ms"] < 1e-11, tab["cheb"]
+    for s in range(3):
+        assert np.array_equal(tab["samples"][s], exact["samples"][s])
+        np.testing.assert_allclose(tab["w_pred_samples"][s], exact["w_pred_samples"][s], rtol=0, atol=TOL)
+        np.testing.assert_allclose(tab["w_predict"][s], exact["w_predict"][s], rtol=0, atol=TOL)
+    np.testing.assert_allclose(tab["w_predict_sum"], exact["w_predict_sum"], rtol=0, atol=3 * TOL)
+
+
+def test_fused_phi_tables_failed_check_keeps_the_exact_refresh(mk, monkeypatch):
+    """Two nodes over the prior's range fail the set-up check: the session keeps the exact refresh
+    (the same bits) and counts the failure."""
+    subs, ct = _problem(mk, [200, 220], 300, seed=66)
+    cfg = mk.SamplerConfig(1, 2, np.zeros(2), np.full(2, 0.05), n_batch=2, batch_length=6, burn_in=4, seed=3)
+    exact = _fused(mk, monkeypatch, subs, ct, cfg, "0")
+    forced = _fused(mk, monkeypatch, subs, ct, cfg, "2")
+    assert forced["cheb"]["launches"] == 0 and forced["fallback"]["launches"] == 1
+    assert forced["fallback"]["ms"] > 1e-10
+    for s in range(2):
+        assert np.array_equal(forced["w_pred_samples"][s], exact["w_pred_samples"][s])
+
+
+def test_fused_phi_tables_match_the_oracle(mk, monkeypatch):
+    """The fused path from the tables against the CPU oracle's exact spPredict (per kept iteration),
+    subset_base offset: samples, draws and grids to 1e-8."""
+    n, n_test, S, base = 500, 400, 2, 9
+    subs, ct = _problem(mk, [n] * S, n_test, seed=67)
+    kw = dict(n_batch=3, batch_length=6, burn_in=5, seed=17)
+    cfg = mk.SamplerConfig(1, 2, np.zeros(2), np.full(2, 0.05), **kw)
+    dev = _fused(mk, monkeypatch, subs, ct, cfg, "-1", base=base)
+    assert dev["cheb"]["launches"] == cfg.kept
+    ocfg = om.Config(1, 2, beta_starting=np.zeros(2), beta_tuning=np.full(2, 0.05), cov_model=0, **kw)
+    for s, sb in enumerate(subs):
+        ref = om.fit_subset(sb["coords"], sb["y"], sb["weights"], sb["x"], ocfg, subset=base + s, coords_test=ct)
+        np.testing.assert_allclose(dev["samples"][s], ref["samples"], rtol=0, atol=TOL)
+        np.testing.assert_allclose(dev["w_pred_samples"][s].T, ref["w_pred"], rtol=0, atol=TOL)
+        np.testing.assert_allclose(dev["w_predict"][s], ref["w_q"], rtol=0, atol=TOL)
