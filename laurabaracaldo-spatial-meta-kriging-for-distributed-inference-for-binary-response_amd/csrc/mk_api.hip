@@ -227,6 +227,7 @@ static std::vector<int> g_pool_count;   // streams of the pool in existence per 
 static int hw_queues();
 static int tile_env(const char* name, int dflt);
 static int krig_tables(mk_session* s);
+static void kt_wait(mk_session* s, hipStream_t st);
 
 static int& pool_count(int device) {   // g_pool_mu held
   if ((int)g_pool_count.size() <= device) g_pool_count.resize(device + 1, 0);
@@ -400,6 +401,9 @@ struct mk_session {
   double kt_check = 0.0, kt_evals = 0.0;
   ChebK kt{};
   double* kt_g = nullptr;         // [S][n_pad] g = W' z of the current kept iteration
+  double* kt_z = nullptr;         // [S][n_pad + 2]: its z, then phi and A per subset (k_kt_snap)
+  hipEvent_t kt_ev[2] = {nullptr, nullptr};   // [0] snapshot taken, [1] draws done (side stream)
+  bool kt_pending = false;        // draws queued on the side stream, not yet waited for
   std::vector<void*> kbufs;       // the kriging buffers (re-sized by mk_session_set_test_sites)
   std::vector<double> bbox;       // [S][4] xmin xmax ymin ymax of each subset's sites (Matern table ranges)
   double* d_ct_all = nullptr;     // all test sites [2][n_test_pad_all] (tiled mode)
@@ -500,6 +504,8 @@ struct mk_session {
     }
     if (swept) hipEventDestroy(swept);
     for (hipEvent_t e : cov_ev)
+      if (e) hipEventDestroy(e);
+    for (hipEvent_t e : kt_ev)
       if (e) hipEventDestroy(e);
     for (hipEvent_t e : la_ev) hipEventDestroy(e);
     pool_return(owned);   // drained above; their waits on the destroyed events are satisfied
@@ -1006,6 +1012,13 @@ static void launch_sweep(mk_session* s, Group& g, int it) {
   if (e != hipSuccess && s->launch_err == hipSuccess) s->launch_err = e;
 }
 
+// The stream st waits for the table draws queued on the side stream (iteration_post_sweep).
+static void kt_wait(mk_session* s, hipStream_t st) {
+  if (!s->kt_pending) return;
+  hipStreamWaitEvent(st, s->kt_ev[1], 0);
+  s->kt_pending = false;
+}
+
 // One MCMC iteration of a group, in two halves around the latent sweep (run_iterations).
 static void iteration_pre_sweep(mk_session* s, Group& g, int it) {
   Model& md = g.md;
@@ -1030,6 +1043,7 @@ static void iteration_pre_sweep(mk_session* s, Group& g, int it) {
   }
   MK_LAUNCH(k_dirty_list, dim3(1), dim3(256), 0, st, md, (int)(it == md.kept0), g.d_list, g.d_count,
                      g.d_plist, g.d_pcount);
+  kt_wait(s, st);   // the previous kept iteration's draws read W
   launch_inverse(s, g);
   if (kept && !s->tiled && !s->kt_on) launch_pred_refresh(s, g);
   // the next iteration's phi candidates depend only on this iteration's decisions (and on the proposal
@@ -1056,10 +1070,27 @@ static void iteration_post_sweep(mk_session* s, Group& g, int it) {
   hipStream_t st = g.stream;
   if (s->record_samples) MK_LAUNCH(k_record, dim3((S + 63) / 64), dim3(64), 0, st, md, it);
   if (s->record_w) MK_LAUNCH(k_record_w, dim3((md.Np + 255) / 256, S), dim3(256), 0, st, md, it);
-  if (kept && md.n_test > 0 && !s->tiled && s->kt_on) {   // from the phi tables (krig_tables)
-    MK_LAUNCH(k_krig_g, dim3(S * (md.n_pad / 4)), dim3(256), 0, st, md, g.ms, (const double*)md.z, s->kt_g, 0, 1);
-    MK_LAUNCH(k_pred_tab_draw, dim3(S * ((md.n_test + 255) / 256)), dim3(256), 0, st, md, s->kt, s->kt_g,
-              md.coords, it, it - md.kept0);
+  if (kept && md.n_test > 0 && !s->tiled && s->kt_on) {
+    // from the phi tables (krig_tables): z, phi and A captured now, g = W' z and the draws on a side
+    // stream (the kriging stream of the lookahead schedule, else the early assembly's stream, after its
+    // assembly) beside the next iteration's beta, A and decision steps; W is rewritten only by the next
+    // inverse, which waits for them (kt_wait)
+    double* zs = s->kt_z;
+    double* ph = zs + (size_t)S * md.n_pad;
+    double* As = ph + S;
+    MK_LAUNCH(k_kt_snap, dim3(S), dim3(256), 0, st, md, zs, ph, As);
+    hipStream_t side = s->la_k ? s->la_k : (s->cov_st ? s->cov_st : st);
+    if (side != st) {
+      hipEventRecord(s->kt_ev[0], st);
+      hipStreamWaitEvent(side, s->kt_ev[0], 0);
+    }
+    MK_LAUNCH(k_krig_g, dim3(S * (md.n_pad / 4)), dim3(256), 0, side, md, g.ms, (const double*)zs, s->kt_g, 0, 1);
+    MK_LAUNCH(k_pred_tab_draw, dim3(S * ((md.n_test + 255) / 256)), dim3(256), 0, side, md, s->kt, s->kt_g,
+              md.coords, (const double*)ph, (const double*)As, it, it - md.kept0);
+    if (side != st) {
+      hipEventRecord(s->kt_ev[1], side);
+      s->kt_pending = true;
+    }
     s->stats[KS_KRIG_CHEB].launches += 1;
   } else if (kept && md.n_test > 0 && !s->tiled) {
     const int per = (md.n_test + 3) / 4;
@@ -1141,6 +1172,7 @@ static void run_iteration_la(mk_session* s, int it) {
   }
   MK_LAUNCH(k_dirty_list, dim3(1), dim3(256), 0, M, md, (int)(it == md.kept0), g.d_list, g.d_count, g.d_plist,
                      g.d_pcount);
+  kt_wait(s, M);   // the previous kept iteration's draws read W
   launch_inverse(s, g, true);
   const bool kept = it >= md.kept0;
   // kept iterations: the kriging refresh (X = W P^T of the changed pairs) only reads W, as the sweep
@@ -1826,7 +1858,8 @@ extern "C" int mk_session_run(mk_session* s, int32_t n_iter) {
   if (swap_m) s->groups[0].stream = s->stream;
   // every stream is drained before an error returns: nothing of this run is left queued
   if (le != hipSuccess) {
-    for (hipStream_t st : {s->la_m, s->la_c, s->la_k}) if (st) (void)hipStreamSynchronize(st);
+    for (hipStream_t st : {s->la_m, s->la_c, s->la_k, s->cov_st}) if (st) (void)hipStreamSynchronize(st);
+    s->kt_pending = false;
     for (auto& g : s->groups) (void)hipStreamSynchronize(g.stream);
     return set_err(MK_E_HIP, std::string("kernel launch in iteration ") + std::to_string(s->iter - 1) + ": " +
                                  hipGetErrorString(le));
@@ -1835,6 +1868,10 @@ extern "C" int mk_session_run(mk_session* s, int32_t n_iter) {
   for (auto& g : s->groups) HIPCHK(hipStreamSynchronize(g.stream));
   if (s->la_c) HIPCHK(hipStreamSynchronize(s->la_c));   // the next iteration's candidates
   if (s->la_k) HIPCHK(hipStreamSynchronize(s->la_k));
+  if (s->kt_pending) {   // the last kept iteration's table draws (side stream)
+    HIPCHK(hipEventSynchronize(s->kt_ev[1]));
+    s->kt_pending = false;
+  }
   if (s->sweep_coop) {
     // the multi-workgroup sweep's barrier time-out (after admission every wait completes: this is the
     // net under that argument): its chain state is then not the sampler's -- the session is
@@ -2123,8 +2160,10 @@ static int krig_tables(mk_session* s) {
   double *Sn = nullptr, *nphi = nullptr, *w = nullptr;
   int* n = nullptr;
   if (s->alloc(&Sn, sn) || s->alloc(&nphi, (size_t)nmax * S) || s->alloc(&w, wts.size()) || s->alloc(&n, (size_t)S) ||
-      s->alloc(&s->kt_g, (size_t)S * md.n_pad))
+      s->alloc(&s->kt_g, (size_t)S * md.n_pad) || s->alloc(&s->kt_z, (size_t)S * (md.n_pad + 2)))
     return MK_E_NOMEM;
+  for (auto& e : s->kt_ev)
+    if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return set_err(MK_E_HIP, "table event");
   HIPCHK(hipMemcpyAsync(Sn, ck.Sn, sn * 8, hipMemcpyDeviceToDevice, s->stream));
   HIPCHK(hipMemcpyAsync(nphi, ck.nphi, (size_t)nmax * S * 8, hipMemcpyDeviceToDevice, s->stream));
   HIPCHK(hipMemcpyAsync(w, ck.wts, wts.size() * 8, hipMemcpyDeviceToDevice, s->stream));

@@ -113,7 +113,9 @@ __global__ void k_flip_pairs(MatSet ms, const int* plist, const int* pcount);
 __global__ void k_kept_phi(Model md, const double* th, int n, double* phis);
 __global__ void k_krig_g(Model md, MatSet ms, const double* z, double* Gt, int j, int nkp);
 __global__ void k_cheb_check(Model md, ChebK c, unsigned long long* err);
-__global__ void k_pred_tab_draw(Model md, ChebK c, const double* g, const double* coords, int iter, int kidx);
+__global__ void k_kt_snap(Model md, double* zs, double* phis, double* As);
+__global__ void k_pred_tab_draw(Model md, ChebK c, const double* g, const double* coords, const double* phis,
+                                const double* As, int iter, int kidx);
 __global__ void k_pred_cheb_draw(Model md, ChebK c, const double* Gt, const double* phit, const double* coords,
                                  const double* kA, int k_lo, int nkp);
 // mk_post.hip

@@ -1839,19 +1839,33 @@ __global__ __launch_bounds__(256) void k_pred_cheb_draw(Model md, ChebK c, const
   }
 }
 
-// Fused kriging from the session's phi tables (mk_api.hip krig_tables; kept iteration `iter`, record
-// kidx, q = 1): k_pred_draw's draw with s(t; phi) interpolated from the tables and the mean
-// m(t) = rho_t(phi)' g, g = W' z of this iteration (k_krig_g), instead of X = W P^T refreshed wherever
-// phi changed.  One thread per (subset, site).
+// Fused kriging from the session's phi tables (mk_api.hip krig_tables; q = 1): what a kept iteration's
+// draws read, captured after its sweep (z, phi, A), so they can run on a side stream while the next
+// iteration's A step, decision and inverse move on.
+__global__ __launch_bounds__(256) void k_kt_snap(Model md, double* __restrict__ zs, double* __restrict__ phis,
+                                                 double* __restrict__ As) {
+  const int s = blockIdx.x;
+  for (int i = threadIdx.x; i < md.n_pad; i += 256) zs[(long)s * md.n_pad + i] = md.z[(long)s * md.n_pad + i];
+  if (threadIdx.x == 0) {
+    phis[s] = logit_inv(md.theta[(long)s * md.n_theta + md.ntri], md.phi_a[0], md.phi_b[0]);
+    As[s] = md.A_full[s];
+  }
+}
+
+// k_pred_draw's draw (kept iteration `iter`, record kidx) with s(t; phi) interpolated from the tables and
+// the mean m(t) = rho_t(phi)' g, g = W' z (k_krig_g over the snapshot), instead of X = W P^T refreshed
+// wherever phi changed.  One thread per (subset, site).
 __global__ __launch_bounds__(256) void k_pred_tab_draw(Model md, ChebK c, const double* __restrict__ g,
-                                                       const double* __restrict__ coords, int iter, int kidx) {
+                                                       const double* __restrict__ coords,
+                                                       const double* __restrict__ phis,
+                                                       const double* __restrict__ As, int iter, int kidx) {
   const int nb = (md.n_test + 255) / 256;
   const int s = blockIdx.x / nb;
   const int t0 = (blockIdx.x % nb) * 256 + threadIdx.x;
   const bool act = t0 < md.n_test;
   const int t = act ? t0 : md.n_test - 1;
   const int ns = md.n_s[s], np = md.n_pad;
-  const double phi = logit_inv(md.theta[(long)s * md.n_theta + md.ntri], md.phi_a[0], md.phi_b[0]);
+  const double phi = phis[s];
   const double xt = md.coords_test[t], yt = md.coords_test[md.n_test_pad + t];
   const double* cx = coords + (long)s * 2 * np;
   const double* cy = cx + np;
@@ -1867,7 +1881,7 @@ __global__ __launch_bounds__(256) void k_pred_tab_draw(Model md, ChebK c, const 
   const Key key = subset_key(md, s);
   const double v = (a0 + a1) + sd * predict_normal(key, md.t_off + t, iter);   // q = 1: index (t_off + t) q + h
   double o = 0.0;
-  o += v * md.A_full[s];
+  o += v * As[s];
   if (act) md.w_pred[((long)s * md.n_kept + kidx) * md.n_test + t] = o;
 }
 
