@@ -2011,6 +2011,10 @@ static int tile_outputs(mk_session* s, int t0, double* dq, mk_outputs* o, int n_
 // exact values at nchk check points (the range's ends, then interior points) bound the interpolant's
 // error before any draw uses it.
 
+// The φ-interpolated paths return 0 when done, this when the exact path must run instead (not
+// applicable, scratch memory short, a check failed), and an MK_E_* code (< 0) on an error.
+constexpr int MK_CHEB_EXACT = 1;
+
 // Nodes of [lo, hi] for each subset: nc[i], the slots' phi (nodes, then nchk check points) and the
 // barycentric weights.  Returns the slot count E (the largest nc + nchk).
 static int cheb_plan(mk_session* s, const std::vector<double>& lo, const std::vector<double>& hi, int force_n, int nchk,
@@ -2070,7 +2074,7 @@ static int cheb_eval(mk_session* s, Model mt, const std::vector<int>& nc, const 
   int* d_lists = scratch.get<int>(lists.size());
   double* d_Sn = scratch.get<double>((size_t)E * S * T_pad);
   unsigned long long* d_err = scratch.get<unsigned long long>(1);
-  if (!d_thn || !d_nphi || !d_wts || !d_nc || !d_lists || !d_Sn || !d_err) return -1;
+  if (!d_thn || !d_nphi || !d_wts || !d_nc || !d_lists || !d_Sn || !d_err) return MK_CHEB_EXACT;
   HIPCHK(hipMemcpyAsync(d_thn, thn.data(), thn.size() * 8, hipMemcpyHostToDevice, st));
   HIPCHK(hipMemcpyAsync(d_wts, wts.data(), wts.size() * 8, hipMemcpyHostToDevice, st));
   HIPCHK(hipMemcpyAsync(d_nc, nc.data(), (size_t)S * sizeof(int), hipMemcpyHostToDevice, st));
@@ -2147,10 +2151,11 @@ static int krig_tables(mk_session* s) {
   ChebK ck;
   double emax = 0.0;
   const int rc = cheb_eval(s, mt, nc, sphi, wts, E, nchk, scratch, &ck, &emax);
-  if (rc > 0) return rc;
+  if (rc < 0) return rc;
+  if (rc == MK_CHEB_EXACT) return 0;   // scratch memory short: exact refreshes
   s->kt_check = emax;
-  if (rc < 0 || !(emax <= cheb_tol())) {   // scratch memory short, or the check failed: exact refreshes
-    s->kt_fail += rc < 0 ? 0 : 1;
+  if (!(emax <= cheb_tol())) {          // the check failed: exact refreshes
+    s->kt_fail += 1;
     return 0;
   }
   // keep the node slots (the checks are not needed past this point)
@@ -2160,8 +2165,13 @@ static int krig_tables(mk_session* s) {
   double *Sn = nullptr, *nphi = nullptr, *w = nullptr;
   int* n = nullptr;
   if (s->alloc(&Sn, sn) || s->alloc(&nphi, (size_t)nmax * S) || s->alloc(&w, wts.size()) || s->alloc(&n, (size_t)S) ||
-      s->alloc(&s->kt_g, (size_t)S * md.n_pad) || s->alloc(&s->kt_z, (size_t)S * (md.n_pad + 2)))
-    return MK_E_NOMEM;
+      s->alloc(&s->kt_g, (size_t)S * md.n_pad) || s->alloc(&s->kt_z, (size_t)S * (md.n_pad + 2))) {
+    // HBM short: the session keeps the exact refresh (the tables are an optimisation, not a requirement)
+    for (void* b : {(void*)Sn, (void*)nphi, (void*)w, (void*)n, (void*)s->kt_g, (void*)s->kt_z}) s->release(b);
+    s->kt_g = s->kt_z = nullptr;
+    set_err(0, "");
+    return 0;
+  }
   for (auto& e : s->kt_ev)
     if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return set_err(MK_E_HIP, "table event");
   HIPCHK(hipMemcpyAsync(Sn, ck.Sn, sn * 8, hipMemcpyDeviceToDevice, s->stream));
@@ -2187,16 +2197,15 @@ static int krig_tables(mk_session* s) {
 // configs[4]: ~490 X refreshes per subset and tile become 13-21 nodes + 3 checks.  MK_KRIG_CHEB: 1
 // (default) where the nodes and checks cost fewer exact evaluations than the exact replay's refreshes,
 // -1 always, n > 1 always with n nodes, 0 never (the exact replay); read at every tile.
-// Returns 0 when the tile is done, -1 when the exact replay must run (not applicable, scratch memory
-// short, check failed), > 0 on an error.
+// Returns 0, MK_CHEB_EXACT (the exact replay must run) or an error (< 0).
 static int predict_tile_cheb(mk_session* s, int t0, double* dq, mk_outputs* o) {
   Model& md = s->md;
   const char* env = std::getenv("MK_KRIG_CHEB");
   const int force_n = (env && *env) ? std::atoi(env) : 1;   // 0 exact, 1 auto, -1 always, n > 1 always, n nodes
-  if (force_n == 0 || s->q != 1 || md.cov_model != MK_COV_EXPONENTIAL) return -1;
+  if (force_n == 0 || s->q != 1 || md.cov_model != MK_COV_EXPONENTIAL) return MK_CHEB_EXACT;
   const int S = s->S, nth = md.n_theta, n_pad = md.n_pad;
   const int k_lo = s->win_lo, n_kept = s->win_n < 0 ? md.n_kept : s->win_n;
-  if (n_kept < 1 || (int)s->span_pt_h.size() != S) return -1;
+  if (n_kept < 1 || (int)s->span_pt_h.size() != S) return MK_CHEB_EXACT;
   const int T_pad = md.n_test_pad, Tc = std::min(s->pred_tile, s->n_test_all - t0);
   hipStream_t st = s->stream;
   Group g = s->all;
@@ -2209,7 +2218,7 @@ static int predict_tile_cheb(mk_session* s, int t0, double* dq, mk_outputs* o) {
     s->release(s->cg_phit);
     s->cg_G = s->cg_phi = s->cg_phit = nullptr;
     s->cg_iter = -1;
-    if (s->alloc(&s->cg_phi, (size_t)n_kept * S)) return -1;
+    if (s->alloc(&s->cg_phi, (size_t)n_kept * S)) return MK_CHEB_EXACT;
     MK_LAUNCH(k_kept_phi, dim3((unsigned)(((long)n_kept * S + 255) / 256)), dim3(256), 0, st, md,
               md.kth + (long)k_lo * S * nth, n_kept, s->cg_phi);
     s->cg_phi_h.assign((size_t)n_kept * S, 0.0);
@@ -2251,16 +2260,16 @@ static int predict_tile_cheb(mk_session* s, int t0, double* dq, mk_outputs* o) {
   // auto: only where it saves exact evaluations -- the exact replay refreshes X at each subset's first
   // state and wherever phi changed (a short window, e.g. the bench's 6-state kriging sample, refreshes
   // less often than a range needs nodes)
-  if (force_n == 1 && evals >= refreshes) return -1;
+  if (force_n == 1 && evals >= refreshes) return MK_CHEB_EXACT;
   // 3. g_k = W_k' z_k of the window's kept states (once per window): the exact replay's
   //    factorisations where phi changed, then one W' z per state
   const int nkp = (n_kept + 7) / 8 * 8;
   if (!s->cg_G) {
-    if (s->alloc(&s->cg_G, (size_t)S * n_pad * nkp)) return -1;
+    if (s->alloc(&s->cg_G, (size_t)S * n_pad * nkp)) return MK_CHEB_EXACT;
     if (s->alloc(&s->cg_phit, (size_t)S * nkp)) {
       s->release(s->cg_G);
       s->cg_G = nullptr;
-      return -1;
+      return MK_CHEB_EXACT;
     }
     std::vector<double> pt((size_t)S * nkp);
     for (int i = 0; i < S; ++i)
@@ -2304,7 +2313,7 @@ static int predict_tile_cheb(mk_session* s, int t0, double* dq, mk_outputs* o) {
     Stat& f = s->stats[KS_KRIG_FALLBACK];
     f.launches += 1;
     f.ms = std::fmax(f.ms, std::isfinite(emax) ? emax : 1e300);
-    return -1;
+    return MK_CHEB_EXACT;
   }
   // 5. the draws
   MK_LAUNCH(k_pred_cheb_draw, dim3(S * ((Tc + 255) / 256)), dim3(256), 0, st, mt, ck, s->cg_G, s->cg_phit, md.coords,
@@ -2328,7 +2337,7 @@ static int predict_tile_cheb(mk_session* s, int t0, double* dq, mk_outputs* o) {
 // is idle.
 static int predict_tile(mk_session* s, int t0, double* dq, mk_outputs* o) {
   const int rc_cheb = predict_tile_cheb(s, t0, dq, o);
-  if (rc_cheb >= 0) return rc_cheb;
+  if (rc_cheb != MK_CHEB_EXACT) return rc_cheb;
   Model& md = s->md;
   const int S = s->S, q = s->q;
   const int k_lo = s->win_lo, n_kept = s->win_n < 0 ? md.n_kept : s->win_n;   // kept states replayed

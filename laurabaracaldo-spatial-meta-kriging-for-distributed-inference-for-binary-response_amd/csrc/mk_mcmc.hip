@@ -1701,6 +1701,22 @@ __global__ __launch_bounds__(256) void k_flip_pairs(MatSet ms, const int* __rest
 // values at the range's two ends and its middle before any draw uses it.  The mean needs no X:
 // m_k(t) = rho_t(phi_k)' g_k with g_k = W_k' z_k (z_k recorded, W_k the state's inverse factor).
 
+// |s_i - t| for the interpolated draws' means: a square root from the hardware reciprocal square-root
+// estimate and one Newton-Raphson step (x r, then the residual correction, as the library's rounding
+// sequence does without its denormal scaling -- squared distances here are >= 1e-24 or 0); within an ulp
+// or two of the correctly rounded root, which only enters rho = exp(-phi d).
+__device__ inline double dist_fast(double x0, double y0, double x1, double y1) {
+  const double dx = x0 - x1, dy = y0 - y1;
+  const double x = fma(dx, dx, dy * dy);
+  const double r = __builtin_amdgcn_rsq(x);
+  double g = x * r, h = 0.5 * r;
+  const double e = fma(-g, h, 0.5);
+  g = fma(g, e, g);
+  h = fma(h, e, h);
+  g = fma(fma(-g, g, x), h, g);
+  return x > 0.0 ? g : 0.0;
+}
+
 // phis[j][s] = phi of record j (th: [n][S][n_theta] records): the candidate assembly's formula
 // (candidate_theta, which = 2), so a record's phi here is bit for bit the one its factor used.
 __global__ __launch_bounds__(256) void k_kept_phi(Model md, const double* __restrict__ th, int n,
@@ -1785,8 +1801,8 @@ __global__ __launch_bounds__(256) void k_cheb_check(Model md, ChebK c, unsigned 
 
 // The draws of the window's kept states j = 0 .. md.n_kept-1 (state k = k_lo + j) at the tile's sites,
 // one thread per (subset, site), 8 states per pass over the subset's sites: the distance once per
-// site and pass, rho_t(phi) = exp(-phi d) once per distinct phi among the 8 (consecutive states share
-// phi while the chain stays), m_k(t) = sum_i rho_i g_k,i in site order.  Gt [S][n_pad][nkp] and phit
+// site and pass (dist_fast), rho_t(phi) = exp(-phi d) once per distinct phi among the 8 (consecutive
+// states share phi while the chain stays), m_k(t) = sum_i rho_i g_k,i in site order (fma).  Gt [S][n_pad][nkp] and phit
 // [S][nkp] are zero / last-phi padded to nkp (a multiple of 8), and with the coordinates they are read
 // through scalar loads (uniform addresses).  The normal, the A factor and the output layout are
 // k_pred_draw_runs' (q = 1).
@@ -1815,14 +1831,14 @@ __global__ __launch_bounds__(256) void k_pred_cheb_draw(Model md, ChebK c, const
     for (int b = 0; b < 8; ++b) a[b] = 0.0;
 #pragma unroll 2
     for (int i = 0; i < ns; ++i) {
-      const double d = dist2d(cx[i], cy[i], xt, yt);
+      const double d = dist_fast(cx[i], cy[i], xt, yt);
       const double* gi = gs + (long)i * nkp + j0;
       double e = exp(-p[0] * d);
-      a[0] += e * gi[0];
+      a[0] = fma(e, gi[0], a[0]);
 #pragma unroll
       for (int b = 1; b < 8; ++b) {
         if (p[b] != p[b - 1]) e = exp(-p[b] * d);
-        a[b] += e * gi[b];
+        a[b] = fma(e, gi[b], a[b]);
       }
     }
     double sd = 0.0;
@@ -1873,10 +1889,10 @@ __global__ __launch_bounds__(256) void k_pred_tab_draw(Model md, ChebK c, const 
   double a0 = 0.0, a1 = 0.0;
   int i = 0;
   for (; i + 1 < ns; i += 2) {
-    a0 += exp(-phi * dist2d(cx[i], cy[i], xt, yt)) * gs[i];
-    a1 += exp(-phi * dist2d(cx[i + 1], cy[i + 1], xt, yt)) * gs[i + 1];
+    a0 = fma(exp(-phi * dist_fast(cx[i], cy[i], xt, yt)), gs[i], a0);
+    a1 = fma(exp(-phi * dist_fast(cx[i + 1], cy[i + 1], xt, yt)), gs[i + 1], a1);
   }
-  if (i < ns) a0 += exp(-phi * dist2d(cx[i], cy[i], xt, yt)) * gs[i];
+  if (i < ns) a0 = fma(exp(-phi * dist_fast(cx[i], cy[i], xt, yt)), gs[i], a0);
   const double sd = sqrt(fmax(1.0 - cheb_s(c, md.S, s, t, phi), 0.0));
   const Key key = subset_key(md, s);
   const double v = (a0 + a1) + sd * predict_normal(key, md.t_off + t, iter);   // q = 1: index (t_off + t) q + h
