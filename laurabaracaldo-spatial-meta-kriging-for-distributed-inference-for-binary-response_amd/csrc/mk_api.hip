@@ -2004,10 +2004,12 @@ static int tile_outputs(mk_session* s, int t0, double* dq, mk_outputs* o, int n_
 // (exponential, q = 1; DESIGN.md 4.7, mk_mcmc.hip section 11).  s(t; phi) = rho_t' R(phi)^-1 rho_t is
 // analytic in phi: it is computed exactly (the replay's own kernels: candidate, Cholesky, inverse,
 // X = W P^T) at nc Chebyshev nodes (first kind) of a phi range per subset and interpolated (barycentric)
-// wherever a draw needs it.  nc = 8 + ceil((phi_hi - phi_lo) * d_max), at least 12, at most 32 (d_max:
+// wherever a draw needs it.  nc = 6 + ceil((phi_hi - phi_lo) * d_max), at least 10, at most 32 (d_max:
 // the subset's largest site-to-site or site-to-test-site distance, so the rule counts the range in units
 // of the correlation decay; measured in float64 on 2,000-site subsets with clustered sites and test
-// sites 1e-6 from a site: |error| <= 1e-14 over phi in [3.3, 11.8] with 20 nodes, [6, 8] with 10).  The
+// sites 1e-6 from a site, d_max 1.41: |error| 2e-14 over phi in [3.3, 11.8] with the rule's 18 nodes,
+// 1e-14 over [4.5, 10.5] with 15, 1e-14 over [6, 8] with 10; on the GPU at configs[4] 4 + ceil(.), at
+// least 8, left 6.5e-12 and 8 + ceil(.), at least 12, 2.6e-14).  The
 // exact values at nchk check points (the range's ends, then interior points) bound the interpolant's
 // error before any draw uses it.
 
@@ -2028,7 +2030,7 @@ static int cheb_plan(mk_session* s, const std::vector<double>& lo, const std::ve
     const double* bb = s->bbox.data() + 4 * i;
     const double dmax = std::fmax(s->span_pt_h[i], std::hypot(bb[1] - bb[0], bb[3] - bb[2]));
     const int n = force_n > 1 ? std::min(force_n, MK_CHEB_MAX)
-                              : std::max(12, std::min(MK_CHEB_MAX, 8 + (int)std::ceil((hi[i] - lo[i]) * dmax)));
+                              : std::max(10, std::min(MK_CHEB_MAX, 6 + (int)std::ceil((hi[i] - lo[i]) * dmax)));
     nc[i] = n;
     const double c = 0.5 * (lo[i] + hi[i]), h = 0.5 * (hi[i] - lo[i]);
     for (int m = 0; m < n; ++m) {

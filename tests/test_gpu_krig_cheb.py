@@ -176,3 +176,25 @@ def test_fused_phi_tables_match_the_oracle(mk, monkeypatch):
         np.testing.assert_allclose(dev["samples"][s], ref["samples"], rtol=0, atol=TOL)
         np.testing.assert_allclose(dev["w_pred_samples"][s].T, ref["w_pred"], rtol=0, atol=TOL)
         np.testing.assert_allclose(dev["w_predict"][s], ref["w_q"], rtol=0, atol=TOL)
+
+
+@pytest.mark.parametrize("tile", [0, 700])
+def test_interpolated_kriging_is_shard_invariant(mk, monkeypatch, tile):
+    """mk_meta_fit over virtual blocks (each its own session of some of the subsets) gives what one
+    session gives, bit for bit, with the interpolation forced on both sides: a subset's nodes depend
+    only on its own phi range and distances, its node GEMMs and draws only on its own data (fused tables,
+    tile = 0; tiled replay exchanged tile by tile, tile = 700)."""
+    subs, ct = _problem(mk, [260, 300, 241], 1500, seed=68)
+    cfg = mk.SamplerConfig(1, 2, np.zeros(2), np.full(2, 0.05), n_batch=3, batch_length=8, burn_in=6, seed=7,
+                           predict_tile=tile)
+    monkeypatch.setenv("MK_KRIG_CHEB", "-1")
+    with mk.Session(subs, cfg, coords_test=ct, subset_base=4) as ses:
+        ses.run(cfg.n_samples)
+        ref = ses.outputs(w_pred_samples=True, w_predict_sum=True)
+        assert ses.kernel_stats(mk.session.KS_KRIG_CHEB)["launches"] > 0
+    got = mk.meta_fit_node(subs, cfg, coords_test=ct, devices=[0, 0], subset_base=4, w_pred_samples=True,
+                           w_predict_sum=True)
+    for s in range(3):
+        assert np.array_equal(got["w_pred_samples"][s], ref["w_pred_samples"][s]), s
+        assert np.array_equal(got["w_predict"][s], ref["w_predict"][s]), s
+    assert np.array_equal(got["w_predict_sum"], ref["w_predict_sum"])
