@@ -1071,15 +1071,20 @@ static void iteration_post_sweep(mk_session* s, Group& g, int it) {
   if (s->record_samples) MK_LAUNCH(k_record, dim3((S + 63) / 64), dim3(64), 0, st, md, it);
   if (s->record_w) MK_LAUNCH(k_record_w, dim3((md.Np + 255) / 256, S), dim3(256), 0, st, md, it);
   if (kept && md.n_test > 0 && !s->tiled && s->kt_on) {
-    // from the phi tables (krig_tables): z, phi and A captured now, g = W' z and the draws on a side
-    // stream (the kriging stream of the lookahead schedule, else the early assembly's stream, after its
-    // assembly) beside the next iteration's beta, A and decision steps; W is rewritten only by the next
-    // inverse, which waits for them (kt_wait)
+    // from the phi tables (krig_tables): z, phi and A captured now, then g = W' z and the draws on a
+    // side stream -- the lookahead schedule's kriging stream, else the early assembly's stream after its
+    // assembly -- beside the next iteration's beta, A and decision steps (W is rewritten only by the next
+    // inverse, which waits for them: kt_wait).  At 250 subsets they then overlap the next Cholesky's first
+    // columns and slow its diagonal launches (a kept iteration 22.0 ms against 20.0 for a burn-in one,
+    // profiles/r06/zg/), but in line costs as much: 40-step windows 11,971-11,988 vs 11,957-11,976, and
+    // 8,690-8,730 vs 8,601-8,642 at 32 subsets (profiles/r06/kside/).  MK_KT_SIDE=0: in line.
     double* zs = s->kt_z;
     double* ph = zs + (size_t)S * md.n_pad;
     double* As = ph + S;
     MK_LAUNCH(k_kt_snap, dim3(S), dim3(256), 0, st, md, zs, ph, As);
-    hipStream_t side = s->la_k ? s->la_k : (s->cov_st ? s->cov_st : st);
+    static const int side_env = tile_env("MK_KT_SIDE", 1);
+    hipStream_t side = st;
+    if (side_env) side = s->la_k ? s->la_k : (s->cov_st ? s->cov_st : st);
     if (side != st) {
       hipEventRecord(s->kt_ev[0], st);
       hipStreamWaitEvent(side, s->kt_ev[0], 0);
