@@ -4,7 +4,7 @@
 # GEMM, then a 32-subset kernel trace
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/r06fin
+O=gpurun_out/${OUT:-r06fin}
 mkdir -p $O
 for c in FETCH_SIZE WRITE_SIZE; do
   lc=$(echo $c | cut -d_ -f1 | tr A-Z a-z)
