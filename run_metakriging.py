@@ -160,6 +160,9 @@ def main():
             g = tile_grids(t0)
             result2[:, t0 * q:t0 * q + g.shape[2]] = mk.combine_results([{"parameters": x} for x in g], device=local,
                                                                         method=a.combine)[0]
+            del g
+            print(f"tile {t0 // tile + 1}/{(c['n_test'] + tile - 1) // tile}  {time.perf_counter() - t4:.1f}s",
+                  file=sys.stderr, flush=True)
     if ses is not None:
         ses.close()
     t["combine_s"] = time.perf_counter() - t4
